@@ -1,0 +1,293 @@
+"""Offline tokenizers.
+
+The reference tokenizes with ``tiktoken`` (GPT-2 BPE, build_components.py:278; Llama-3 BPE,
+Models/Llama/Llama3.py:14-51) and SentencePiece (Llama-2, Llama2.py:12-28), downloading the
+vocab files from the HF hub. Neither tiktoken nor the network is available here, so this
+module provides:
+
+* :class:`BPETokenizer` — a byte-level BPE that reads local vocab files in either format
+  (tiktoken ``*.tiktoken`` / Llama-3 ``tokenizer.model`` base64-rank files, or GPT-2
+  ``encoder.json`` + ``vocab.bpe``) with the GPT-2 / Llama-3 pre-tokenisation regexes and
+  tiktoken's ``allowed_special`` semantics;
+* :class:`Llama2Tokenizer` — SentencePiece wrapper whose ``encode`` accepts the
+  ``allowed_special`` kwarg the reference passes (fixes SURVEY §2.8 defect 1);
+* :class:`ByteTokenizer` — deterministic fallback (one id per UTF-8 byte, special tokens
+  mapped to the model's ids) so pretraining / finetuning / benchmarks run with no assets.
+"""
+from __future__ import annotations
+
+import base64
+import json
+import os
+from functools import lru_cache
+from typing import Dict, Iterable, List, Optional, Sequence, Set, Union
+
+import regex as re
+
+GPT2_PAT = r"""'s|'t|'re|'ve|'m|'ll|'d| ?\p{L}+| ?\p{N}+| ?[^\s\p{L}\p{N}]+|\s+(?!\S)|\s+"""
+LLAMA3_PAT = (r"(?i:'s|'t|'re|'ve|'m|'ll|'d)|[^\r\n\p{L}\p{N}]?\p{L}+|\p{N}{1,3}|"
+              r" ?[^\s\p{L}\p{N}]+[\r\n]*|\s*[\r\n]+|\s+(?!\S)|\s+")
+
+LLAMA3_SPECIAL = {
+    "<|begin_of_text|>": 128000,
+    "<|end_of_text|>": 128001,
+    "<|start_header_id|>": 128006,
+    "<|end_header_id|>": 128007,
+    "<|eot_id|>": 128009,
+}
+
+
+def llama3_special_tokens() -> Dict[str, int]:
+    sp = dict(LLAMA3_SPECIAL)
+    used = set(sp.values())
+    for i in range(256):
+        if 128002 + i not in used:
+            sp[f"<|reserved_{i}|>"] = 128002 + i
+    return sp
+
+
+def _bytes_to_unicode() -> Dict[int, str]:
+    """GPT-2's reversible byte<->unicode table used by encoder.json / vocab.bpe."""
+    bs = list(range(ord("!"), ord("~") + 1)) + list(range(ord("¡"), ord("¬") + 1)) + \
+        list(range(ord("®"), ord("ÿ") + 1))
+    cs = bs[:]
+    n = 0
+    for b in range(256):
+        if b not in bs:
+            bs.append(b)
+            cs.append(256 + n)
+            n += 1
+    return dict(zip(bs, (chr(c) for c in cs)))
+
+
+def _special_split(text: str, specials: Iterable[str]):
+    """Yield (is_special, piece) splitting ``text`` at any of the ``specials``."""
+    specials = sorted(set(specials), key=len, reverse=True)
+    if not specials:
+        yield False, text
+        return
+    pat = re.compile("|".join(re.escape(s) for s in specials))
+    pos = 0
+    for m in pat.finditer(text):
+        if m.start() > pos:
+            yield False, text[pos:m.start()]
+        yield True, m.group(0)
+        pos = m.end()
+    if pos < len(text):
+        yield False, text[pos:]
+
+
+class BPETokenizer:
+    """Byte-level BPE over mergeable ranks ``{bytes: rank}`` (tiktoken semantics)."""
+
+    def __init__(self, mergeable_ranks: Dict[bytes, int], pat_str: str,
+                 special_tokens: Optional[Dict[str, int]] = None, name: str = "bpe"):
+        self.name = name
+        self.ranks = mergeable_ranks
+        self.decoder = {v: k for k, v in mergeable_ranks.items()}
+        self.special_tokens = dict(special_tokens or {})
+        self.special_decoder = {v: k.encode("utf-8") for k, v in self.special_tokens.items()}
+        self.pat = re.compile(pat_str)
+        self.n_vocab = max(list(self.decoder) + list(self.special_decoder) + [0]) + 1
+        self._cache: Dict[bytes, List[int]] = {}
+
+    # ------------------------------------------------------------------ loaders
+    @classmethod
+    def from_tiktoken_file(cls, path: str, pat_str: str, special_tokens=None, name=None):
+        ranks = {}
+        with open(path, "rb") as f:
+            for line in f:
+                line = line.strip()
+                if not line:
+                    continue
+                tok, rank = line.split()
+                ranks[base64.b64decode(tok)] = int(rank)
+        return cls(ranks, pat_str, special_tokens, name or os.path.basename(path))
+
+    @classmethod
+    def from_gpt2_files(cls, encoder_json: str, vocab_bpe: Optional[str] = None):
+        with open(encoder_json, "r", encoding="utf-8") as f:
+            encoder = json.load(f)
+        byte_dec = {v: k for k, v in _bytes_to_unicode().items()}
+        ranks = {}
+        for tok, idx in encoder.items():
+            if tok == "<|endoftext|>":
+                continue
+            ranks[bytes(byte_dec[c] for c in tok)] = idx
+        return cls(ranks, GPT2_PAT, {"<|endoftext|>": encoder.get("<|endoftext|>", 50256)}, "gpt2")
+
+    # ------------------------------------------------------------------ core BPE
+    def _bpe(self, piece: bytes) -> List[int]:
+        hit = self._cache.get(piece)
+        if hit is not None:
+            return hit
+        r = self.ranks.get(piece)
+        if r is not None:
+            out = [r]
+        else:
+            parts = [piece[i:i + 1] for i in range(len(piece))]
+            while len(parts) > 1:
+                best, best_i = None, -1
+                for i in range(len(parts) - 1):
+                    rk = self.ranks.get(parts[i] + parts[i + 1])
+                    if rk is not None and (best is None or rk < best):
+                        best, best_i = rk, i
+                if best is None:
+                    break
+                parts[best_i:best_i + 2] = [parts[best_i] + parts[best_i + 1]]
+            out = [self.ranks[p] for p in parts]
+        if len(self._cache) < 500_000:
+            self._cache[piece] = out
+        return out
+
+    def encode_ordinary(self, text: str) -> List[int]:
+        ids: List[int] = []
+        for m in self.pat.finditer(text):
+            ids.extend(self._bpe(m.group(0).encode("utf-8")))
+        return ids
+
+    def encode(self, text: str, allowed_special: Union[str, Set[str]] = frozenset(),
+               disallowed_special: Union[str, Sequence[str]] = ()) -> List[int]:
+        if allowed_special == "all":
+            allowed = set(self.special_tokens)
+        else:
+            allowed = set(allowed_special) & set(self.special_tokens)
+        ids: List[int] = []
+        for is_sp, piece in _special_split(text, allowed):
+            if is_sp:
+                ids.append(self.special_tokens[piece])
+            else:
+                ids.extend(self.encode_ordinary(piece))
+        return ids
+
+    def decode(self, ids: Sequence[int]) -> str:
+        out = bytearray()
+        for i in ids:
+            b = self.decoder.get(i)
+            if b is None:
+                b = self.special_decoder.get(i, b"")
+            out += b
+        return out.decode("utf-8", errors="replace")
+
+
+class ByteTokenizer:
+    """Deterministic offline fallback: UTF-8 bytes -> ids 0..255; special tokens keep the
+    model's ids (e.g. ``<|endoftext|>`` -> 50256) so eos handling matches the reference."""
+
+    def __init__(self, special_tokens: Optional[Dict[str, int]] = None, name: str = "bytes"):
+        self.name = name
+        self.special_tokens = dict(special_tokens or {})
+        self.special_decoder = {v: k for k, v in self.special_tokens.items()}
+        self.n_vocab = max([256] + [v + 1 for v in self.special_tokens.values()])
+
+    def encode(self, text: str, allowed_special: Union[str, Set[str]] = frozenset(),
+               disallowed_special=(), bos: bool = False, eos: bool = False) -> List[int]:
+        allowed = set(self.special_tokens) if allowed_special == "all" else \
+            set(allowed_special) & set(self.special_tokens)
+        ids: List[int] = []
+        for is_sp, piece in _special_split(text, allowed):
+            if is_sp:
+                ids.append(self.special_tokens[piece])
+            else:
+                ids.extend(piece.encode("utf-8"))
+        return ids
+
+    def decode(self, ids: Sequence[int]) -> str:
+        out = bytearray()
+        parts: List[str] = []
+        for i in ids:
+            if i < 256:
+                out.append(i)
+            else:
+                parts.append(out.decode("utf-8", errors="replace"))
+                out = bytearray()
+                parts.append(self.special_decoder.get(i, ""))
+        parts.append(out.decode("utf-8", errors="replace"))
+        return "".join(parts)
+
+
+class Llama3Tokenizer:
+    """Llama-3 tokenizer (reference Llama3.py:14-51) on local ``tokenizer.model``."""
+
+    def __init__(self, model_path: str):
+        assert os.path.isfile(model_path), f"Model file {model_path} not found"
+        self.special_tokens = llama3_special_tokens()
+        self.model = BPETokenizer.from_tiktoken_file(model_path, LLAMA3_PAT, self.special_tokens)
+
+    def encode(self, text, bos=False, eos=False, allowed_special=frozenset(), disallowed_special=()):
+        ids = [self.special_tokens["<|begin_of_text|>"]] if bos else []
+        ids += self.model.encode(text, allowed_special=allowed_special)
+        if eos:
+            ids.append(self.special_tokens["<|end_of_text|>"])
+        return ids
+
+    def decode(self, ids):
+        return self.model.decode(ids)
+
+
+class Llama2Tokenizer:
+    """SentencePiece wrapper (reference Llama2.py:12-28) with an ``allowed_special`` kwarg:
+    ``</s>`` text maps to the eos id when allowed."""
+
+    def __init__(self, tokenizer_file: str):
+        import sentencepiece as spm
+        sp = spm.SentencePieceProcessor()
+        sp.load(tokenizer_file)
+        self.tokenizer = sp
+        self.special_tokens = {"</s>": sp.eos_id(), "<s>": sp.bos_id()}
+
+    def encode(self, text, allowed_special=frozenset(), **_):
+        allowed = set(allowed_special) & set(self.special_tokens)
+        ids: List[int] = []
+        for is_sp, piece in _special_split(text, allowed):
+            ids.extend([self.special_tokens[piece]] if is_sp else self.tokenizer.encode_as_ids(piece))
+        return ids
+
+    def decode(self, ids):
+        return self.tokenizer.decode_ids(list(ids))
+
+
+# ---------------------------------------------------------------------------
+_SEARCH_DIRS = ("tokenizers", "Llama-3-8B", "Llama-3.1-8B", "Llama-3.2-1B", "Llama-2-7b",
+                "hf_checkpoints", os.path.expanduser("~/.cache/bllm_tokenizers"))
+
+
+def _find(paths: Sequence[str]) -> Optional[str]:
+    for p in paths:
+        if p and os.path.isfile(p):
+            return p
+    return None
+
+
+def build_tokenizer(model: str, cfg, tokenizer_path: Optional[str] = None):
+    """Reference build_components.py:265-300 without downloads. Looks for local vocab files
+    (``--tokenizer_path`` or the reference's local_dir names); otherwise returns the
+    :class:`ByteTokenizer` fallback with the model's eos mapping."""
+    from ..logger import setup_logger
+    log = setup_logger("tokenizer")
+    eos_text, eos_id = cfg["eos_text"], cfg["eos_id"]
+    if model == "GPT2":
+        d = tokenizer_path if tokenizer_path and os.path.isdir(tokenizer_path) else None
+        enc = _find([os.path.join(x, "encoder.json") for x in ((d,) if d else ()) + _SEARCH_DIRS])
+        if tokenizer_path and tokenizer_path.endswith(".json") and os.path.isfile(tokenizer_path):
+            enc = tokenizer_path
+        if enc:
+            return BPETokenizer.from_gpt2_files(enc)
+        tk = _find([tokenizer_path] if tokenizer_path else [])
+        if tk:
+            return BPETokenizer.from_tiktoken_file(tk, GPT2_PAT, {"<|endoftext|>": 50256}, "gpt2")
+    elif model == "llama2":
+        f = _find([tokenizer_path] + [os.path.join(x, "tokenizer.model") for x in _SEARCH_DIRS])
+        if f:
+            return Llama2Tokenizer(f)
+    elif model.startswith("llama3"):
+        f = _find([tokenizer_path] + [os.path.join(x, "original", "tokenizer.model") for x in _SEARCH_DIRS]
+                  + [os.path.join(x, "tokenizer.model") for x in _SEARCH_DIRS])
+        if f:
+            return Llama3Tokenizer(f)
+    specials = {eos_text: eos_id}
+    if model.startswith("llama3"):
+        specials = llama3_special_tokens()
+    log.info(f"No local tokenizer files for {model}; using the offline byte-level tokenizer "
+             f"(eos '{eos_text}' -> {eos_id}).")
+    return ByteTokenizer(specials, name=f"bytes-{model}")

@@ -1,0 +1,321 @@
+"""Unit-structured language-model base.
+
+The reference runs every model as a plain ``nn.Module`` forward under autograd (one graph
+node per eager op, ``[B,H,T,T]`` scores materialised; reference GPT2.py:108-124,
+Llama3.py:196-204).  Here a model is an ordered list of *units* (embedding -> blocks ->
+final norm + head) and each unit is ONE autograd node whose forward/backward is written by
+hand (models/gpt2.py, models/llama.py) on top of the HIP kernels and hipBLASLt GEMMs.  That
+gives exact control over:
+
+  * what each block saves for backward (``actv_ckpt``: ``none`` | ``selective`` — recompute
+    norms/activations only | ``full`` — save the block input only, the reference's
+    ``checkpoint_sequential(segments=n_layers)`` semantics);
+  * where distributed hooks fire (``engine.pre_forward/post_forward/pre_backward/
+    post_backward`` per unit — FSDP gathers and reduce-scatters, DDP bucket all-reduce);
+  * fused head + cross-entropy: ``model(idx, targets)`` returns the mean loss without
+    keeping fp32 logits (``model(idx)`` still returns logits like the reference).
+"""
+from __future__ import annotations
+
+from typing import List, Optional
+
+import torch
+import torch.nn as nn
+
+from .flat import FlatUnit
+
+
+class LocalEngine:
+    """No-op distributed engine (single process)."""
+
+    world_size = 1
+    rank = 0
+
+    def pre_forward(self, unit):
+        pass
+
+    def post_forward(self, unit):
+        pass
+
+    def pre_backward(self, unit):
+        pass
+
+    def post_backward(self, unit):
+        pass
+
+    def finish_backward(self):
+        pass
+
+
+class RunCtx:
+    """Per-model mutable run state shared by all unit computes."""
+
+    def __init__(self, cfg, actv_ckpt: str = "none"):
+        self.cfg = cfg
+        self.actv_ckpt = actv_ckpt
+        self.training = True
+        self.engine = LocalEngine()
+        self.accumulate = False        # micro-batch gradient accumulation: add into grads
+        self.seed = 1234
+        self._offset = 0
+        self.rope = None               # (cos, sin) fp32 [T, hd/2] on device
+        self.B = 1
+        self.T = 1
+        self.profile_hook = None
+
+    def reserve_offsets(self, n: int) -> int:
+        base = self._offset
+        self._offset += (n + 255) // 256 * 256
+        return base
+
+    @property
+    def drop_p(self) -> float:
+        return float(self.cfg.drop_rate) if self.training else 0.0
+
+
+class UnitCompute:
+    """Hand-written forward/backward of one unit over a :class:`FlatUnit`."""
+
+    name = "unit"
+
+    def __init__(self, rctx: RunCtx):
+        self.rctx = rctx
+        self.unit: Optional[FlatUnit] = None
+
+    def layout(self) -> List[List[nn.Parameter]]:
+        raise NotImplementedError
+
+    def bind(self, unit: FlatUnit):
+        self.unit = unit
+
+    def forward(self, x, save: bool, replay=None):
+        raise NotImplementedError
+
+    def backward(self, dy, saved):
+        raise NotImplementedError
+
+
+# ---------------------------------------------------------------------------
+# autograd nodes
+# ---------------------------------------------------------------------------
+class _EmbedFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, idx, anchor, comp):
+        eng = comp.rctx.engine
+        eng.pre_forward(comp.unit)
+        x, saved = comp.forward(idx, save=True)
+        eng.post_forward(comp.unit)
+        ctx.comp, ctx.saved = comp, saved
+        return x
+
+    @staticmethod
+    def backward(ctx, dx):
+        comp = ctx.comp
+        eng = comp.rctx.engine
+        eng.pre_backward(comp.unit)
+        comp.backward(dx.contiguous(), ctx.saved)
+        ctx.saved = None
+        eng.post_backward(comp.unit)
+        eng.finish_backward()
+        return None, None, None
+
+
+class _BlockFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, comp):
+        eng = comp.rctx.engine
+        eng.pre_forward(comp.unit)
+        full = comp.rctx.actv_ckpt == "full"
+        y, saved = comp.forward(x, save=not full)
+        eng.post_forward(comp.unit)
+        ctx.comp = comp
+        ctx.saved = ("__recompute__", x, saved) if full else saved
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        comp = ctx.comp
+        eng = comp.rctx.engine
+        eng.pre_backward(comp.unit)
+        saved = ctx.saved
+        if isinstance(saved, tuple) and len(saved) == 3 and isinstance(saved[0], str) \
+                and saved[0] == "__recompute__":
+            _, x, replay = saved
+            _, saved = comp.forward(x, save=True, replay=replay)
+        dx = comp.backward(dy.contiguous(), saved)
+        ctx.saved = None
+        eng.post_backward(comp.unit)
+        return dx, None
+
+
+class _HeadLossFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, targets, comp):
+        eng = comp.rctx.engine
+        eng.pre_forward(comp.unit)
+        loss, saved = comp.forward_loss(x, targets, save=True)
+        eng.post_forward(comp.unit)
+        ctx.comp, ctx.saved = comp, saved
+        return loss
+
+    @staticmethod
+    def backward(ctx, dloss):
+        comp = ctx.comp
+        eng = comp.rctx.engine
+        eng.pre_backward(comp.unit)
+        dx = comp.backward_loss(dloss, ctx.saved)
+        ctx.saved = None
+        eng.post_backward(comp.unit)
+        return dx, None, None
+
+
+class _HeadLogitsFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, comp):
+        eng = comp.rctx.engine
+        eng.pre_forward(comp.unit)
+        logits, saved = comp.forward_logits(x, save=True)
+        eng.post_forward(comp.unit)
+        ctx.comp, ctx.saved = comp, saved
+        return logits
+
+    @staticmethod
+    def backward(ctx, dlogits):
+        comp = ctx.comp
+        eng = comp.rctx.engine
+        eng.pre_backward(comp.unit)
+        dx = comp.backward_logits(dlogits.contiguous(), ctx.saved)
+        ctx.saved = None
+        eng.post_backward(comp.unit)
+        return dx, None
+
+
+# ---------------------------------------------------------------------------
+class BaseLM(nn.Module):
+    """Common machinery for GPTModel / Llama models."""
+
+    def __init__(self, cfg, use_actv_ckpt=False):
+        super().__init__()
+        self.cfg = cfg
+        mode = use_actv_ckpt if isinstance(use_actv_ckpt, str) else ("full" if use_actv_ckpt else "none")
+        assert mode in ("none", "selective", "full"), mode
+        self.use_actv_ckpt = mode != "none"
+        object.__setattr__(self, "_rctx", RunCtx(cfg, mode))
+        object.__setattr__(self, "_comps", None)
+        object.__setattr__(self, "_anchor", None)
+
+    # -- to be provided by subclasses ------------------------------------------------
+    def build_computes(self) -> List[UnitCompute]:
+        raise NotImplementedError
+
+    # -- configuration -----------------------------------------------------------------
+    @property
+    def rctx(self) -> RunCtx:
+        return self._rctx
+
+    def set_actv_ckpt(self, mode: str):
+        assert mode in ("none", "selective", "full")
+        self._rctx.actv_ckpt = mode
+        self.use_actv_ckpt = mode != "none"
+
+    def set_engine(self, engine):
+        self._rctx.engine = engine
+
+    def train(self, mode: bool = True):
+        super().train(mode)
+        self._rctx.training = mode
+        return self
+
+    @property
+    def device(self):
+        return next(self.parameters()).device
+
+    @property
+    def units(self) -> List[FlatUnit]:
+        self._ensure_flat()
+        return [c.unit for c in self._comps]
+
+    @property
+    def computes(self) -> List[UnitCompute]:
+        self._ensure_flat()
+        return self._comps
+
+    # -- flat storage ------------------------------------------------------------------
+    def flatten(self, device=None, dtype=None, pad_to: int = 1, grad_dtype=None):
+        """(Re)build every unit's flat buffers from the current parameters (call after
+        LoRA replacement / weight loading; idempotent)."""
+        p0 = next(self.parameters())
+        device = torch.device(device) if device is not None else p0.device
+        dtype = dtype or p0.dtype
+        comps = self.build_computes()
+        for i, c in enumerate(comps):
+            u = FlatUnit(c.name, i)
+            u.flatten(c.layout(), device, dtype, pad_to=pad_to, grad_dtype=grad_dtype)
+            c.bind(u)
+        object.__setattr__(self, "_comps", comps)
+        object.__setattr__(self, "_anchor", torch.zeros((), device=device, requires_grad=True))
+        self._after_flatten(device)
+        return self
+
+    def _after_flatten(self, device):
+        pass
+
+    def _ensure_flat(self):
+        if self._comps is None:
+            self.flatten()
+
+    def _apply(self, fn, *args, **kwargs):
+        # .to()/.cuda() on a flattened model: move, then rebuild flats on the new device
+        was_flat = self._comps is not None
+        r = super()._apply(fn, *args, **kwargs)
+        if was_flat:
+            object.__setattr__(self, "_comps", None)
+            self.flatten()
+        return r
+
+    # -- forward -----------------------------------------------------------------------
+    def forward(self, in_idx: torch.Tensor, targets: Optional[torch.Tensor] = None,
+                last_only: bool = False):
+        self._ensure_flat()
+        comps = self._comps
+        rc = self._rctx
+        B, T = in_idx.shape
+        rc.B, rc.T = B, T
+        idx = in_idx.to(self._anchor.device, non_blocking=True)
+        grad = torch.is_grad_enabled()
+        emb, blocks, head = comps[0], comps[1:-1], comps[-1]
+        eng = rc.engine
+        if grad:
+            x = _EmbedFn.apply(idx, self._anchor, emb)
+            for c in blocks:
+                x = _BlockFn.apply(x, c)
+            if targets is not None:
+                tg = targets.to(self._anchor.device, non_blocking=True).reshape(-1)
+                return _HeadLossFn.apply(x, tg, head)
+            logits = _HeadLogitsFn.apply(x, head)
+            return logits.view(B, T, -1)
+        # inference path: no autograd nodes, nothing saved
+        with torch.no_grad():
+            for c in comps[:-1]:
+                eng.pre_forward(c.unit)
+                x, _ = c.forward(idx if c is emb else x, save=False)
+                eng.post_forward(c.unit)
+            eng.pre_forward(head.unit)
+            if targets is not None:
+                tg = targets.to(self._anchor.device, non_blocking=True).reshape(-1)
+                loss, _ = head.forward_loss(x, tg, save=False)
+                eng.post_forward(head.unit)
+                return loss
+            if last_only:
+                x = x.view(B, T, -1)[:, -1, :].contiguous()
+                logits, _ = head.forward_logits(x, save=False)
+                eng.post_forward(head.unit)
+                return logits.view(B, 1, -1)
+            logits, _ = head.forward_logits(x, save=False)
+            eng.post_forward(head.unit)
+            return logits.view(B, T, -1)
+
+    # -- parameter groups for optimizers -----------------------------------------------
+    def trainable_buffers(self):
+        self._ensure_flat()
+        return [c.unit.train for c in self._comps if c.unit.train is not None]

@@ -1,0 +1,251 @@
+"""GPT-2 (reference Models/GPT2/GPT2.py:6-124).
+
+Names / state dict: ``tok_emb``, ``pos_emb``, ``blocks.{i}.att.W_query|W_key|W_value|out_proj``
+(+ ``att.mask`` buffer), ``blocks.{i}.ff.layers.0|2``, ``blocks.{i}.norm1|norm2``, ``norm``,
+``output_head`` (untied).  Math: pre-LayerNorm, causal MHA with attention-probability
+dropout, residual dropout, embedding dropout (p = ``drop_rate`` = 0.1), exact-erf GELU MLP.
+
+Differences: parameters follow ``--data_type`` (the reference ignores it for GPT-2, SURVEY
+§2.8 defect 5); no per-forward debug print (defect 10).  Dropout masks come from a
+counter-based hash (seed, element offset) so backward and activation-checkpoint recompute
+regenerate them instead of storing them; GPU kernels and the CPU path produce identical masks.
+
+Execution per block: LayerNorm[HIP] -> QKV GEMM (+bias epilogue) -> flash attention with
+in-kernel dropout[HIP MFMA] -> out-proj GEMM (+bias) -> dropout+residual[HIP] -> LayerNorm
+-> fc GEMM (+bias) -> GELU[HIP] -> proj GEMM (+bias) -> dropout+residual[HIP].
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+
+from .. import ops
+from .base import BaseLM, UnitCompute
+from .linear import FusedLinear
+from .llama import HeadComputeMixin, _write_vec_grad
+
+
+class MultiHeadAttention(nn.Module):
+    def __init__(self, d_in, d_out, context_length, dropout, num_heads, qkv_bias=False, dtype=None, device=None):
+        super().__init__()
+        assert d_out % num_heads == 0, "Output dimension must be divisible by number of heads"
+        self.d_out = d_out
+        self.num_heads = num_heads
+        self.head_dim = d_out // num_heads
+        kw = dict(dtype=dtype, device=device)
+        self.W_query = nn.Linear(d_in, d_out, bias=qkv_bias, **kw)
+        self.W_key = nn.Linear(d_in, d_out, bias=qkv_bias, **kw)
+        self.W_value = nn.Linear(d_in, d_out, bias=qkv_bias, **kw)
+        self.out_proj = nn.Linear(d_out, d_out, **kw)
+        self.dropout = nn.Dropout(dropout)
+
+
+class FeedForward(nn.Module):
+    def __init__(self, cfg, device=None):
+        super().__init__()
+        d = cfg["emb_dim"]
+        kw = dict(dtype=cfg["dtype"], device=device)
+        self.layers = nn.Sequential(nn.Linear(d, 4 * d, **kw), nn.GELU(), nn.Linear(4 * d, d, **kw))
+
+
+class TransformerBlock(nn.Module):
+    def __init__(self, cfg, device=None):
+        super().__init__()
+        self.att = MultiHeadAttention(cfg["emb_dim"], cfg["emb_dim"], cfg["context_length"],
+                                      cfg["drop_rate"], cfg["n_heads"], cfg["qkv_bias"],
+                                      dtype=cfg["dtype"], device=device)
+        self.ff = FeedForward(cfg, device)
+        kw = dict(dtype=cfg["dtype"], device=device)
+        self.norm1 = nn.LayerNorm(cfg["emb_dim"], **kw)
+        self.norm2 = nn.LayerNorm(cfg["emb_dim"], **kw)
+        self.dropout = nn.Dropout(cfg["drop_rate"])
+
+
+# ---------------------------------------------------------------------------
+class GPTEmbedCompute(UnitCompute):
+    name = "embed"
+
+    def __init__(self, rctx, model):
+        super().__init__(rctx)
+        self.m = model
+
+    def layout(self):
+        return [[self.m.tok_emb.weight], [self.m.pos_emb.weight]]
+
+    def forward(self, idx, save, replay=None):
+        rc = self.rctx
+        p = rc.drop_p
+        off = rc.reserve_offsets(idx.numel() * self.rctx.cfg.emb_dim) if p > 0 else 0
+        x = ops.embedding_fwd(idx.reshape(-1), self.unit.data(self.m.tok_emb.weight),
+                              self.unit.data(self.m.pos_emb.weight), rc.T, p, rc.seed, off)
+        return x.view(rc.B, rc.T, -1), ((idx.reshape(-1), p, off) if save else None)
+
+    def backward(self, dx, saved):
+        idx, p, off = saved
+        rc = self.rctx
+        dx = ops.dropout_bwd(dx.view(-1, dx.shape[-1]), p, rc.seed, off)
+        ops.embedding_bwd(idx, dx, self.unit.grad(self.m.tok_emb.weight),
+                          self.unit.grad(self.m.pos_emb.weight), rc.T, rc.accumulate)
+        return None
+
+
+def _ln_grads(unit, norm, dw, db, acc):
+    _write_vec_grad(unit, norm.weight, dw, acc)
+    _write_vec_grad(unit, norm.bias, db, acc)
+
+
+class GPTBlockCompute(UnitCompute):
+    def __init__(self, rctx, block: TransformerBlock, i: int):
+        super().__init__(rctx)
+        self.block = block
+        self.name = f"blocks.{i}"
+        a, f = block.att, block.ff
+        self.qkv = FusedLinear([a.W_query, a.W_key, a.W_value])
+        self.o = FusedLinear([a.out_proj])
+        self.fc = FusedLinear([f.layers[0]])
+        self.proj = FusedLinear([f.layers[2]])
+
+    def layout(self):
+        b = self.block
+        return (self.qkv.layout() + self.o.layout() + self.fc.layout() + self.proj.layout()
+                + [[b.norm1.weight, b.norm1.bias], [b.norm2.weight, b.norm2.bias]])
+
+    def bind(self, unit):
+        super().bind(unit)
+        for fl in (self.qkv, self.o, self.fc, self.proj):
+            fl.bind(unit)
+
+    def _ln(self, x, norm):
+        u = self.unit
+        return ops.layernorm_fwd(x, u.data(norm.weight), u.data(norm.bias), 1e-5)
+
+    def forward(self, x, save, replay=None):
+        rc, cfg, b = self.rctx, self.rctx.cfg, self.block
+        B, T = rc.B, rc.T
+        N, d = B * T, cfg.emb_dim
+        H, hd = cfg.n_heads, cfg.head_dim
+        p = rc.drop_p
+        if replay is not None:
+            offs = replay
+        elif p > 0:
+            offs = (rc.reserve_offsets(B * H * T * T), rc.reserve_offsets(N * d), rc.reserve_offsets(N * d))
+        else:
+            offs = (0, 0, 0)
+        x2d = x.reshape(N, d)
+        h1, m1, r1 = self._ln(x2d, b.norm1)
+        qkv, xa_qkv = self.qkv.forward(h1)
+        o, lse = ops.flash_attn_fwd(qkv, B, T, H, H, hd, True, p, rc.seed, offs[0])
+        a, xa_o = self.o.forward(o)
+        x2 = ops.dropout_add(x2d, a, p, rc.seed, offs[1])
+        del a
+        h2, m2, r2 = self._ln(x2, b.norm2)
+        f, xa_fc = self.fc.forward(h2)
+        g = ops.gelu_fwd(f)
+        m, xa_pr = self.proj.forward(g)
+        x3 = ops.dropout_add(x2, m, p, rc.seed, offs[2])
+        if not save:
+            # full-recompute mode: _BlockFn keeps ``offs`` as the replay token so the
+            # recomputed forward regenerates identical dropout masks
+            return x3.view(B, T, d), offs
+        saved = dict(x=x2d, m1=m1, r1=r1, qkv=qkv, o=o, lse=lse, x2=x2, m2=m2, r2=r2, f=f,
+                     p=p, offs=offs, xa=(xa_qkv, xa_o, xa_fc, xa_pr))
+        if rc.actv_ckpt == "none":
+            saved.update(h1=h1, h2=h2, g=g)
+        return x3.view(B, T, d), saved
+
+    def backward(self, dy, s):
+        rc, cfg, u, b = self.rctx, self.rctx.cfg, self.unit, self.block
+        B, T = rc.B, rc.T
+        N, d = B * T, cfg.emb_dim
+        H, hd = cfg.n_heads, cfg.head_dim
+        acc, p, offs = rc.accumulate, s["p"], s["offs"]
+        xa_qkv, xa_o, xa_fc, xa_pr = s["xa"]
+        dy2 = dy.reshape(N, d)
+        # ---- MLP branch: x3 = x2 + drop(proj(gelu(fc(ln2(x2)))))
+        dm = ops.dropout_bwd(dy2, p, rc.seed, offs[2])
+        g = s["g"] if "g" in s else ops.gelu_fwd(s["f"])
+        dg = self.proj.backward(dm, g, xa_pr, accumulate=acc)
+        del dm, g
+        df = ops.gelu_bwd(s["f"], dg)
+        del dg
+        h2 = s["h2"] if "h2" in s else self._ln(s["x2"], b.norm2)[0]
+        dh2 = self.fc.backward(df, h2, xa_fc, accumulate=acc)
+        del df, h2
+        dx2, dw2, db2 = ops.layernorm_bwd(dh2, s["x2"], u.data(b.norm2.weight), s["m2"], s["r2"], dy2)
+        _ln_grads(u, b.norm2, dw2, db2, acc)
+        # ---- attention branch: x2 = x + drop(out_proj(attn(ln1(x))))
+        da = ops.dropout_bwd(dx2, p, rc.seed, offs[1])
+        d_o = self.o.backward(da, s["o"], xa_o, accumulate=acc)
+        del da
+        dqkv = ops.flash_attn_bwd(s["qkv"], s["o"], s["lse"], d_o, B, T, H, H, hd, True, p, rc.seed, offs[0])
+        del d_o
+        h1 = s["h1"] if "h1" in s else self._ln(s["x"], b.norm1)[0]
+        dh1 = self.qkv.backward(dqkv, h1, xa_qkv, accumulate=acc)
+        del dqkv, h1
+        dx, dw1, db1 = ops.layernorm_bwd(dh1, s["x"], u.data(b.norm1.weight), s["m1"], s["r1"], dx2)
+        _ln_grads(u, b.norm1, dw1, db1, acc)
+        return dx.view(B, T, d)
+
+
+class GPTHeadCompute(HeadComputeMixin, UnitCompute):
+    name = "final"
+
+    def __init__(self, rctx, model):
+        super().__init__(rctx)
+        self.m = model
+        self.head = FusedLinear([model.output_head])
+
+    def layout(self):
+        return [[self.m.norm.weight, self.m.norm.bias]] + self.head.layout()
+
+    def bind(self, unit):
+        super().bind(unit)
+        self.head.bind(unit)
+
+    def _norm_fwd(self, x2d):
+        u, n = self.unit, self.m.norm
+        h, mean, rstd = ops.layernorm_fwd(x2d, u.data(n.weight), u.data(n.bias), 1e-5)
+        return h, (mean, rstd)
+
+    def _norm_bwd(self, dh, ns):
+        x2d, mean, rstd = ns
+        u, n = self.unit, self.m.norm
+        dx, dw, db = ops.layernorm_bwd(dh, x2d, u.data(n.weight), mean, rstd, None)
+        _ln_grads(u, n, dw, db, self.rctx.accumulate)
+        return dx
+
+
+class GPTModel(BaseLM):
+    def __init__(self, cfg, use_actv_ckpt=False, device=None):
+        super().__init__(cfg, use_actv_ckpt)
+        kw = dict(dtype=cfg["dtype"], device=device)
+        self.tok_emb = nn.Embedding(cfg["vocab_size"], cfg["emb_dim"], **kw)
+        self.pos_emb = nn.Embedding(cfg["context_length"], cfg["emb_dim"], **kw)
+        self.drop_emb = nn.Dropout(cfg["drop_rate"])
+        self.blocks = nn.Sequential(*[TransformerBlock(cfg, device) for _ in range(cfg["n_layers"])])
+        self.norm = nn.LayerNorm(cfg["emb_dim"], **kw)
+        self.output_head = nn.Linear(cfg["emb_dim"], cfg["vocab_size"], bias=False, **kw)
+        self._register_state_dict_hook(_gpt_state_dict_hook)
+        self._register_load_state_dict_pre_hook(_gpt_load_pre_hook)
+        self.include_buffers_in_state_dict = True
+
+    def build_computes(self):
+        rc = self._rctx
+        return ([GPTEmbedCompute(rc, self)]
+                + [GPTBlockCompute(rc, b, i) for i, b in enumerate(self.blocks)]
+                + [GPTHeadCompute(rc, self)])
+
+
+def _gpt_state_dict_hook(module, state_dict, prefix, local_metadata):
+    if getattr(module, "include_buffers_in_state_dict", False):
+        T = module.cfg.context_length
+        mask = torch.triu(torch.ones(T, T), diagonal=1)
+        for i in range(module.cfg.n_layers):
+            state_dict[f"{prefix}blocks.{i}.att.mask"] = mask
+    return state_dict
+
+
+def _gpt_load_pre_hook(state_dict, prefix, *args, **kwargs):
+    for k in list(state_dict.keys()):
+        if k.startswith(prefix) and k.endswith(".att.mask"):
+            del state_dict[k]

@@ -1,0 +1,338 @@
+"""Llama-2 / Llama-3 / 3.1 / 3.2 (one GQA module; MHA is GQA with n_kv_groups == n_heads).
+
+Parity (reference, read-only):
+  * module / state-dict names: ``tok_emb``, ``trf_blocks.{i}.att.W_query|W_key|W_value|out_proj``,
+    ``trf_blocks.{i}.ff.fc1|fc2|fc3``, ``trf_blocks.{i}.norm1|norm2``, ``final_norm``, ``out_head``
+    plus the ``att.mask|cos|sin`` buffers (Llama3.py:108-204, Llama2.py:61-190);
+  * math: pre-RMSNorm (eps 1e-5, fp32 weight in checkpoints), rotate-half RoPE with the 3.1
+    by-parts smoothing, causal GQA, SwiGLU ``fc3(silu(fc1 x) * fc2 x)``, untied head
+    (common_components.py:6-124, Llama3.py:131-181).
+
+MI355X execution (per block, N = B*T rows, all bf16 with fp32 accumulation):
+  rmsnorm[HIP] -> QKV GEMM (fused [Wq;Wk;Wv], hipBLASLt) -> RoPE in place[HIP] ->
+  flash-attention fwd (GQA-native, no repeat_interleave)[HIP MFMA] -> out-proj GEMM with
+  the residual add in the epilogue (addmm beta=1) -> rmsnorm[HIP] -> gate/up GEMM (fused
+  [fc1;fc2]) -> SwiGLU[HIP] -> down GEMM + residual.  Backward mirrors it and writes all
+  weight gradients into the unit's flat gradient buffer.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+
+from .. import ops
+from .base import BaseLM, UnitCompute
+from .linear import FusedLinear
+
+
+# ---------------------------------------------------------------------------
+# reference-named containers (parameters become views into flat unit buffers)
+# ---------------------------------------------------------------------------
+class RMSNorm(nn.Module):
+    def __init__(self, emb_dim, eps=1e-5, dtype=None, device=None):
+        super().__init__()
+        self.eps = eps
+        self.emb_dim = emb_dim
+        self.weight = nn.Parameter(torch.ones(emb_dim, dtype=dtype, device=device))
+
+    def forward(self, x):  # reference-style eager path (used only by tests / users)
+        xf = x.float()
+        y = xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + self.eps)
+        return (y * self.weight.float()).to(x.dtype)
+
+
+class GroupedQueryAttention(nn.Module):
+    def __init__(self, d_in, d_out, context_length, num_heads, num_kv_groups, rope_base=10_000,
+                 rope_config=None, dtype=None, device=None):
+        super().__init__()
+        assert d_out % num_heads == 0 and num_heads % num_kv_groups == 0
+        self.d_out = d_out
+        self.num_heads = num_heads
+        self.head_dim = d_out // num_heads
+        self.num_kv_groups = num_kv_groups
+        self.group_size = num_heads // num_kv_groups
+        kw = dict(bias=False, dtype=dtype, device=device)
+        self.W_query = nn.Linear(d_in, d_out, **kw)
+        self.W_key = nn.Linear(d_in, num_kv_groups * self.head_dim, **kw)
+        self.W_value = nn.Linear(d_in, num_kv_groups * self.head_dim, **kw)
+        self.out_proj = nn.Linear(d_out, d_out, **kw)
+
+
+# reference Llama2.py names this MultiHeadAttention
+class MultiHeadAttention(GroupedQueryAttention):
+    def __init__(self, d_in, d_out, context_length, num_heads, dtype=None, device=None):
+        super().__init__(d_in, d_out, context_length, num_heads, num_heads, dtype=dtype, device=device)
+
+
+class FeedForward(nn.Module):
+    def __init__(self, cfg, device=None):
+        super().__init__()
+        kw = dict(bias=False, dtype=cfg["dtype"], device=device)
+        self.fc1 = nn.Linear(cfg["emb_dim"], cfg["hidden_dim"], **kw)
+        self.fc2 = nn.Linear(cfg["emb_dim"], cfg["hidden_dim"], **kw)
+        self.fc3 = nn.Linear(cfg["hidden_dim"], cfg["emb_dim"], **kw)
+
+
+class TransformerBlock(nn.Module):
+    def __init__(self, cfg, device=None):
+        super().__init__()
+        self.att = GroupedQueryAttention(cfg["emb_dim"], cfg["emb_dim"], cfg["context_length"],
+                                         cfg["n_heads"], cfg["n_kv_groups"], cfg["rope_base"],
+                                         cfg["rope_freq"], dtype=cfg["dtype"], device=device)
+        self.ff = FeedForward(cfg, device=device)
+        self.norm1 = RMSNorm(cfg["emb_dim"], eps=1e-5, dtype=cfg["dtype"], device=device)
+        self.norm2 = RMSNorm(cfg["emb_dim"], eps=1e-5, dtype=cfg["dtype"], device=device)
+
+
+# ---------------------------------------------------------------------------
+# unit computes
+# ---------------------------------------------------------------------------
+def _write_vec_grad(unit, p, g32, accumulate):
+    gv = unit.grad(p)
+    if gv is None:
+        return
+    if accumulate:
+        gv.add_(g32.to(gv.dtype))
+    else:
+        gv.copy_(g32)
+
+
+class LlamaEmbedCompute(UnitCompute):
+    name = "tok_emb"
+
+    def __init__(self, rctx, model):
+        super().__init__(rctx)
+        self.m = model
+
+    def layout(self):
+        return [[self.m.tok_emb.weight]]
+
+    def forward(self, idx, save, replay=None):
+        rc = self.rctx
+        W = self.unit.data(self.m.tok_emb.weight)
+        x = ops.embedding_fwd(idx.reshape(-1), W, None, rc.T)
+        return x.view(rc.B, rc.T, -1), (idx.reshape(-1) if save else None)
+
+    def backward(self, dx, saved):
+        g = self.unit.grad(self.m.tok_emb.weight)
+        if g is not None:
+            ops.embedding_bwd(saved, dx.view(-1, dx.shape[-1]), g, None, self.rctx.T, self.rctx.accumulate)
+        return None
+
+
+class LlamaBlockCompute(UnitCompute):
+    def __init__(self, rctx, block: TransformerBlock, i: int):
+        super().__init__(rctx)
+        self.block = block
+        self.name = f"trf_blocks.{i}"
+        a, f = block.att, block.ff
+        self.qkv = FusedLinear([a.W_query, a.W_key, a.W_value])
+        self.o = FusedLinear([a.out_proj])
+        self.gu = FusedLinear([f.fc1, f.fc2])
+        self.down = FusedLinear([f.fc3])
+
+    def layout(self):
+        b = self.block
+        return (self.qkv.layout() + self.o.layout() + self.gu.layout() + self.down.layout()
+                + [[b.norm1.weight], [b.norm2.weight]])
+
+    def bind(self, unit):
+        super().bind(unit)
+        for fl in (self.qkv, self.o, self.gu, self.down):
+            fl.bind(unit)
+
+    def forward(self, x, save, replay=None):
+        rc, cfg, u, b = self.rctx, self.rctx.cfg, self.unit, self.block
+        B, T = rc.B, rc.T
+        N, d = B * T, cfg.emb_dim
+        H, G, hd = cfg.n_heads, cfg.n_kv_groups, cfg.head_dim
+        eps = cfg.norm_eps
+        cos, sin = rc.rope
+        x2d = x.reshape(N, d)
+        h1, r1 = ops.rmsnorm_fwd(x2d, u.data(b.norm1.weight), eps)
+        qkv, xa_qkv = self.qkv.forward(h1)
+        ops.rope_(qkv, cos, sin, T, H, G, hd)
+        o, lse = ops.flash_attn_fwd(qkv, B, T, H, G, hd, causal=True)
+        x2, xa_o = self.o.forward(o, residual=x2d)
+        h2, r2 = ops.rmsnorm_fwd(x2, u.data(b.norm2.weight), eps)
+        gu, xa_gu = self.gu.forward(h2)
+        act = ops.swiglu_fwd(gu)
+        x3, xa_dn = self.down.forward(act, residual=x2)
+        saved = None
+        if save:
+            saved = dict(x=x2d, r1=r1, qkv=qkv, o=o, lse=lse, x2=x2, r2=r2, gu=gu,
+                         xa=(xa_qkv, xa_o, xa_gu, xa_dn))
+            if rc.actv_ckpt == "none":
+                saved.update(h1=h1, h2=h2, act=act)
+        return x3.view(B, T, d), saved
+
+    def backward(self, dy, s):
+        rc, cfg, u, b = self.rctx, self.rctx.cfg, self.unit, self.block
+        B, T = rc.B, rc.T
+        N, d = B * T, cfg.emb_dim
+        H, G, hd = cfg.n_heads, cfg.n_kv_groups, cfg.head_dim
+        eps, acc = cfg.norm_eps, rc.accumulate
+        cos, sin = rc.rope
+        xa_qkv, xa_o, xa_gu, xa_dn = s["xa"]
+        dy2 = dy.reshape(N, d)
+        w1, w2 = u.data(b.norm1.weight), u.data(b.norm2.weight)
+        # ---- MLP
+        act = s["act"] if "act" in s else ops.swiglu_fwd(s["gu"])
+        d_act = self.down.backward(dy2, act, xa_dn, accumulate=acc)
+        del act
+        d_gu = ops.swiglu_bwd(s["gu"], d_act)
+        del d_act
+        h2 = s["h2"] if "h2" in s else ops.rmsnorm_fwd(s["x2"], w2, eps)[0]
+        dh2 = self.gu.backward(d_gu, h2, xa_gu, accumulate=acc)
+        del d_gu, h2
+        dx2, dw2 = ops.rmsnorm_bwd(dh2, s["x2"], w2, s["r2"], dy2)
+        _write_vec_grad(u, b.norm2.weight, dw2, acc)
+        del dh2
+        # ---- attention
+        d_o = self.o.backward(dx2, s["o"], xa_o, accumulate=acc)
+        dqkv = ops.flash_attn_bwd(s["qkv"], s["o"], s["lse"], d_o, B, T, H, G, hd, causal=True)
+        del d_o
+        ops.rope_(dqkv, cos, sin, T, H, G, hd, inverse=True)
+        h1 = s["h1"] if "h1" in s else ops.rmsnorm_fwd(s["x"], w1, eps)[0]
+        dh1 = self.qkv.backward(dqkv, h1, xa_qkv, accumulate=acc)
+        del dqkv, h1
+        dx, dw1 = ops.rmsnorm_bwd(dh1, s["x"], w1, s["r1"], dx2)
+        _write_vec_grad(u, b.norm1.weight, dw1, acc)
+        return dx.view(B, T, d)
+
+
+class HeadComputeMixin:
+    """final norm + LM head + fused cross-entropy (reference train.py:88-92)."""
+
+    ignore_index = -100
+
+    def _norm_fwd(self, x):
+        raise NotImplementedError
+
+    def _norm_bwd(self, dh, ns, dx_acc=None):
+        raise NotImplementedError
+
+    def forward_logits(self, x, save):
+        x2d = x.reshape(-1, x.shape[-1])
+        h, ns = self._norm_fwd(x2d)
+        logits, xa = self.head.forward(h)
+        return logits, ((x2d, h, ns, xa) if save else None)
+
+    def backward_logits(self, dlogits, saved):
+        x2d, h, ns, xa = saved
+        dl = dlogits.reshape(-1, dlogits.shape[-1]).to(h.dtype)
+        dh = self.head.backward(dl, h, xa, accumulate=self.rctx.accumulate)
+        dx = self._norm_bwd(dh, (x2d,) + ns)
+        return dx.view(self.rctx.B, self.rctx.T, -1)
+
+    def forward_loss(self, x, targets, save):
+        x2d = x.reshape(-1, x.shape[-1])
+        h, ns = self._norm_fwd(x2d)
+        logits, xa = self.head.forward(h)
+        rows, lse = ops.ce_fwd(logits, targets, self.ignore_index)
+        nvalid = (targets != self.ignore_index).sum().to(torch.float32)
+        loss = rows.sum() / nvalid
+        if not save:
+            return loss, None
+        return loss, (x2d, h, ns, xa, logits, lse, targets, nvalid)
+
+    def backward_loss(self, dloss, saved):
+        x2d, h, ns, xa, logits, lse, targets, nvalid = saved
+        scale = (dloss.float() / nvalid).reshape(1)
+        dlogits = ops.ce_bwd_(logits, targets, lse, scale, self.ignore_index)  # in place
+        dh = self.head.backward(dlogits, h, xa, accumulate=self.rctx.accumulate)
+        del dlogits
+        dx = self._norm_bwd(dh, (x2d,) + ns)
+        return dx.view(self.rctx.B, self.rctx.T, -1)
+
+
+class LlamaHeadCompute(HeadComputeMixin, UnitCompute):
+    name = "final"
+
+    def __init__(self, rctx, model):
+        super().__init__(rctx)
+        self.m = model
+        self.head = FusedLinear([model.out_head])
+
+    def layout(self):
+        return [[self.m.final_norm.weight]] + self.head.layout()
+
+    def bind(self, unit):
+        super().bind(unit)
+        self.head.bind(unit)
+
+    def _norm_fwd(self, x2d):
+        h, r = ops.rmsnorm_fwd(x2d, self.unit.data(self.m.final_norm.weight), self.rctx.cfg.norm_eps)
+        return h, (r,)
+
+    def _norm_bwd(self, dh, ns):
+        x2d, r = ns
+        w = self.m.final_norm.weight
+        dx, dw = ops.rmsnorm_bwd(dh, x2d, self.unit.data(w), r, None)
+        _write_vec_grad(self.unit, w, dw, self.rctx.accumulate)
+        return dx
+
+
+# ---------------------------------------------------------------------------
+class LlamaModel(BaseLM):
+    """Llama-2 / 3 / 3.1 / 3.2 (reference Llama2Model, Llama3Model)."""
+
+    def __init__(self, cfg, use_actv_ckpt=False, device=None):
+        super().__init__(cfg, use_actv_ckpt)
+        dt = cfg["dtype"]
+        self.tok_emb = nn.Embedding(cfg["vocab_size"], cfg["emb_dim"], dtype=dt, device=device)
+        self.trf_blocks = nn.Sequential(*[TransformerBlock(cfg, device) for _ in range(cfg["n_layers"])])
+        self.final_norm = RMSNorm(cfg["emb_dim"], eps=1e-5, dtype=dt, device=device)
+        self.out_head = nn.Linear(cfg["emb_dim"], cfg["vocab_size"], bias=False, dtype=dt, device=device)
+        self._register_state_dict_hook(_llama_state_dict_hook)
+        self._register_load_state_dict_pre_hook(_llama_load_pre_hook)
+        self.include_buffers_in_state_dict = True
+
+    def build_computes(self):
+        rc = self._rctx
+        return ([LlamaEmbedCompute(rc, self)]
+                + [LlamaBlockCompute(rc, b, i) for i, b in enumerate(self.trf_blocks)]
+                + [LlamaHeadCompute(rc, self)])
+
+    def _after_flatten(self, device):
+        cfg = self.cfg
+        self._rctx.rope = ops.rope_tables(cfg.head_dim, cfg.context_length, cfg.rope_base,
+                                          cfg.rope_freq, device=device)
+
+
+Llama3Model = LlamaModel
+Llama2Model = LlamaModel
+
+
+def _llama_buffers(cfg):
+    """Reference per-block buffers: mask [T,T] fp32 (triu ones), cos/sin [T, hd] (halves
+    duplicated) — bf16 for Llama-3.x, fp32 for Llama-2 (Llama3.py:59-70, Llama2.py:83-88)."""
+    T, hd = cfg.context_length, cfg.head_dim
+    mask = torch.triu(torch.ones(T, T), diagonal=1)
+    c, s = ops.rope_tables(hd, T, cfg.rope_base, cfg.rope_freq)
+    cos = torch.cat([c, c], dim=1)
+    sin = torch.cat([s, s], dim=1)
+    if cfg.name != "llama2":
+        cos, sin = cos.to(cfg.dtype), sin.to(cfg.dtype)
+    return mask, cos, sin
+
+
+def _llama_state_dict_hook(module, state_dict, prefix, local_metadata):
+    # RMSNorm weights are fp32 in the reference's checkpoints
+    for k in list(state_dict.keys()):
+        if k.endswith("norm1.weight") or k.endswith("norm2.weight") or k.endswith("final_norm.weight"):
+            state_dict[k] = state_dict[k].float()
+    if getattr(module, "include_buffers_in_state_dict", False):
+        mask, cos, sin = _llama_buffers(module.cfg)
+        for i in range(module.cfg.n_layers):
+            p = f"{prefix}trf_blocks.{i}.att."
+            state_dict[p + "mask"] = mask
+            state_dict[p + "cos"] = cos
+            state_dict[p + "sin"] = sin
+    return state_dict
+
+
+def _llama_load_pre_hook(state_dict, prefix, *args, **kwargs):
+    for k in list(state_dict.keys()):
+        if k.startswith(prefix) and (k.endswith(".att.mask") or k.endswith(".att.cos") or k.endswith(".att.sin")):
+            del state_dict[k]

@@ -1,0 +1,178 @@
+"""Op dispatch: GPU tensors -> hand-written HIP kernels (``torch.ops.bllm.*`` from the
+in-tree ``_C.so``), CPU tensors -> ``ops.reference`` (plain PyTorch).
+
+There is deliberately NO silent fallback for GPU tensors: if the extension is not built,
+every op on a GPU tensor raises.  The single documented exception is fp32 *attention* on
+the GPU (the flash-attention kernels are bf16/fp16 MFMA kernels); fp32 GPU runs go through
+the reference attention math, which ``ops.attention_backend(dtype)`` reports.
+"""
+from __future__ import annotations
+
+from typing import List, Optional
+
+import torch
+
+from . import reference as ref
+from ._ext import ext_available, load_ext
+
+__all__ = [
+    "rmsnorm_fwd", "rmsnorm_bwd", "layernorm_fwd", "layernorm_bwd", "dropout_add", "dropout_bwd",
+    "rope_", "rope_tables", "flash_attn_fwd", "flash_attn_bwd", "swiglu_fwd", "swiglu_bwd",
+    "gelu_fwd", "gelu_bwd", "ce_fwd", "ce_bwd_", "embedding_fwd", "embedding_bwd",
+    "sq_norm_multi", "adamw_step_", "ext_available", "load_ext", "attention_backend",
+]
+
+rope_tables = ref.rope_tables
+
+
+def _hip(t: torch.Tensor) -> bool:
+    if t.device.type == "cuda":
+        load_ext(required=True)
+        return True
+    return False
+
+
+def _k():
+    return torch.ops.bllm
+
+
+# --------------------------------------------------------------------------- norms
+def rmsnorm_fwd(x, w, eps: float):
+    if _hip(x):
+        return _k().rmsnorm_fwd(x, w, eps)
+    return ref.rmsnorm_fwd(x, w, eps)
+
+
+def rmsnorm_bwd(dy, x, w, rstd, dx_acc: Optional[torch.Tensor] = None):
+    if _hip(x):
+        return _k().rmsnorm_bwd(dy, x, w, rstd, dx_acc)
+    return ref.rmsnorm_bwd(dy, x, w, rstd, dx_acc)
+
+
+def layernorm_fwd(x, w, b, eps: float):
+    if _hip(x):
+        return _k().layernorm_fwd(x, w, b, eps)
+    return ref.layernorm_fwd(x, w, b, eps)
+
+
+def layernorm_bwd(dy, x, w, mean, rstd, dx_acc: Optional[torch.Tensor] = None):
+    if _hip(x):
+        return _k().layernorm_bwd(dy, x, w, mean, rstd, dx_acc)
+    return ref.layernorm_bwd(dy, x, w, mean, rstd, dx_acc)
+
+
+def dropout_add(x, a, p: float, seed: int, offset: int):
+    if _hip(x):
+        return _k().dropout_add(x, a, float(p), int(seed), int(offset))
+    return ref.dropout_add(x, a, p, seed, offset)
+
+
+def dropout_bwd(dy, p: float, seed: int, offset: int):
+    if p <= 0.0:
+        return dy
+    if _hip(dy):
+        return _k().dropout_bwd(dy, float(p), int(seed), int(offset))
+    return ref.dropout_bwd(dy, p, seed, offset)
+
+
+# --------------------------------------------------------------------------- rope / attention
+def rope_(qkv, cos, sin, T: int, H: int, G: int, hd: int, inverse: bool = False, pos_offset: int = 0):
+    if _hip(qkv):
+        _k().rope_(qkv, cos, sin, T, H, G, hd, inverse, pos_offset)
+        return qkv
+    return ref.rope_(qkv, cos, sin, T, H, G, hd, inverse, pos_offset)
+
+
+def attention_backend(dtype: torch.dtype, device_type: str = "cuda") -> str:
+    if device_type != "cuda":
+        return "reference"
+    return "hip" if dtype in (torch.bfloat16, torch.float16) else "reference-fp32"
+
+
+def flash_attn_fwd(qkv, B, T, H, G, hd, causal=True, dropout_p=0.0, seed=0, offset=0):
+    if qkv.device.type == "cuda" and qkv.dtype in (torch.bfloat16, torch.float16):
+        load_ext(required=True)
+        return _k().flash_attn_fwd(qkv, B, T, H, G, hd, causal, float(dropout_p), int(seed), int(offset))
+    return ref.flash_attn_fwd(qkv, B, T, H, G, hd, causal, dropout_p, seed, offset)
+
+
+def flash_attn_bwd(qkv, o, lse, do, B, T, H, G, hd, causal=True, dropout_p=0.0, seed=0, offset=0):
+    if qkv.device.type == "cuda" and qkv.dtype in (torch.bfloat16, torch.float16):
+        load_ext(required=True)
+        return _k().flash_attn_bwd(qkv, o, lse, do, B, T, H, G, hd, causal, float(dropout_p),
+                                   int(seed), int(offset))
+    return ref.flash_attn_bwd(qkv, o, lse, do, B, T, H, G, hd, causal, dropout_p, seed, offset)
+
+
+# --------------------------------------------------------------------------- activations
+def swiglu_fwd(gu):
+    if _hip(gu):
+        return _k().swiglu_fwd(gu)
+    return ref.swiglu_fwd(gu)
+
+
+def swiglu_bwd(gu, dact):
+    if _hip(gu):
+        return _k().swiglu_bwd(gu, dact)
+    return ref.swiglu_bwd(gu, dact)
+
+
+def gelu_fwd(f):
+    if _hip(f):
+        return _k().gelu_fwd(f)
+    return ref.gelu_fwd(f)
+
+
+def gelu_bwd(f, dg):
+    if _hip(f):
+        return _k().gelu_bwd(f, dg)
+    return ref.gelu_bwd(f, dg)
+
+
+# --------------------------------------------------------------------------- loss
+def ce_fwd(logits, targets, ignore_index: int = -100):
+    if _hip(logits):
+        return _k().ce_fwd(logits, targets, ignore_index)
+    return ref.ce_fwd(logits, targets, ignore_index)
+
+
+def ce_bwd_(logits, targets, lse, scale, ignore_index: int = -100):
+    if _hip(logits):
+        _k().ce_bwd_(logits, targets, lse, scale, ignore_index)
+        return logits
+    return ref.ce_bwd_(logits, targets, lse, scale, ignore_index)
+
+
+# --------------------------------------------------------------------------- embedding
+def embedding_fwd(idx, wte, wpe, T: int, dropout_p: float = 0.0, seed: int = 0, offset: int = 0):
+    if _hip(wte):
+        return _k().embedding_fwd(idx, wte, wpe, T, float(dropout_p), int(seed), int(offset))
+    return ref.embedding_fwd(idx, wte, wpe, T, dropout_p, seed, offset)
+
+
+def embedding_bwd(idx, dx, grad_wte, grad_wpe, T: int, accumulate: bool = False):
+    if _hip(dx):
+        _k().embedding_bwd(idx, dx, grad_wte, grad_wpe, T, accumulate)
+        return
+    ref.embedding_bwd(idx, dx, grad_wte, grad_wpe, T, accumulate)
+
+
+# --------------------------------------------------------------------------- optimizer
+def sq_norm_multi(tensors: List[torch.Tensor]) -> torch.Tensor:
+    """Sum of squares over all tensors -> 1-element fp32 tensor (no host sync)."""
+    tensors = [t for t in tensors if t is not None and t.numel() > 0]
+    if not tensors:
+        return torch.zeros(1, dtype=torch.float32)
+    if _hip(tensors[0]):
+        return _k().sq_norm_multi(tensors)
+    return sum(ref.sq_norm(t) for t in tensors).reshape(1)
+
+
+def adamw_step_(param, master, grad, exp_avg, exp_avg_sq, lr, beta1, beta2, eps, weight_decay,
+                step, grad_scale=None):
+    if _hip(param):
+        _k().adamw_step_(param, master, grad, exp_avg, exp_avg_sq, float(lr), float(beta1),
+                         float(beta2), float(eps), float(weight_decay), int(step), grad_scale)
+        return
+    ref.adamw_step_(param, master, grad, exp_avg, exp_avg_sq, lr, beta1, beta2, eps, weight_decay,
+                    step, grad_scale)
