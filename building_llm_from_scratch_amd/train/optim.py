@@ -1,0 +1,91 @@
+"""Fused AdamW over flat unit buffers (+ on-device gradient clipping).
+
+Reference: ``torch.optim.AdamW(model.parameters(), lr, weight_decay=0.1)`` /
+``ZeroRedundancyOptimizer(AdamW)`` (build_components.py:243-258) and
+``clip_grad_norm_(max_norm=1.0)`` (train.py:114-120).
+
+Design: the optimizer steps *slots* — (param, grad) pairs of equal numel — supplied by the
+distributed engine: whole flat buffers for single-process / DDP, the local shard for ZeRO-1
+and FSDP.  Low-precision params get an fp32 master copy; exp_avg / exp_avg_sq are fp32.
+One fused HIP launch per slot (ops.adamw_step_).  ``clip_grad_norm_`` computes the global
+norm with one multi-tensor kernel (+ one all-reduce for sharded engines) and leaves the clip
+coefficient ON DEVICE; ``step`` multiplies it in, so clipping never syncs with the host.
+Weight decay applies to every parameter (the reference's single param group).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import List, Optional
+
+import torch
+
+from .. import ops
+
+
+@dataclass
+class OptSlot:
+    param: torch.Tensor      # updated in place (compute dtype)
+    grad: torch.Tensor       # same numel
+    name: str = ""
+
+
+def local_slots(model) -> List[OptSlot]:
+    return [OptSlot(fb.data, fb.grad, f"unit{i}") for i, fb in enumerate(model.trainable_buffers())]
+
+
+class FusedAdamW(torch.optim.Optimizer):
+    def __init__(self, model=None, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8,
+                 weight_decay: float = 0.01, slots: Optional[List[OptSlot]] = None, engine=None):
+        if slots is None:
+            eng = engine or (model.rctx.engine if model is not None else None)
+            slots = eng.optimizer_slots(model) if eng is not None and hasattr(eng, "optimizer_slots") \
+                else local_slots(model)
+        self.slots = slots
+        self.engine = engine or (model.rctx.engine if model is not None else None)
+        defaults = dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay)
+        super().__init__([s.param for s in slots], defaults)
+        for s in slots:
+            st = self.state[s.param]
+            st["step"] = 0
+            st["exp_avg"] = torch.zeros(s.param.numel(), dtype=torch.float32, device=s.param.device)
+            st["exp_avg_sq"] = torch.zeros_like(st["exp_avg"])
+            if s.param.dtype != torch.float32:
+                st["master"] = s.param.detach().reshape(-1).float().clone()
+        self._gscale: Optional[torch.Tensor] = None
+        self.last_grad_norm: Optional[torch.Tensor] = None
+
+    # torch's zero_grad would try to walk p.grad of the slot tensors; the unit backward
+    # OVERWRITES the flat gradients every step (accumulation is explicit), so this is a no-op
+    def zero_grad(self, set_to_none: bool = True):
+        self._gscale = None
+
+    def grad_sq_norm(self) -> torch.Tensor:
+        sq = ops.sq_norm_multi([s.grad.reshape(-1) for s in self.slots])
+        if self.engine is not None and hasattr(self.engine, "all_reduce_grad_sq_norm"):
+            sq = self.engine.all_reduce_grad_sq_norm(sq)
+        return sq
+
+    def clip_grad_norm_(self, max_norm: float = 1.0, extra_scale: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Global L2 norm; sets the on-device multiplier min(1, max_norm/(norm+1e-6))."""
+        sq = self.grad_sq_norm()
+        if extra_scale is not None:  # gradients carry a loss scale: norm of the unscaled grads
+            sq = sq * extra_scale.float() ** 2
+        norm = sq.sqrt()
+        coef = torch.clamp(max_norm / (norm + 1e-6), max=1.0)
+        self._gscale = coef if extra_scale is None else coef * extra_scale.float()
+        self.last_grad_norm = norm
+        return norm
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        g = self.param_groups[0]
+        lr, (b1, b2), eps, wd = g["lr"], g["betas"], g["eps"], g["weight_decay"]
+        for s in self.slots:
+            st = self.state[s.param]
+            st["step"] += 1
+            ops.adamw_step_(s.param.reshape(-1), st.get("master"), s.grad.reshape(-1), st["exp_avg"],
+                            st["exp_avg_sq"], lr, b1, b2, eps, wd, st["step"], self._gscale)
+        self._gscale = None
+        if self.engine is not None and hasattr(self.engine, "after_optimizer_step"):
+            self.engine.after_optimizer_step()
+        return None

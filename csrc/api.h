@@ -1,0 +1,68 @@
+// Host launch API of the kernel library (raw pointers + hipStream_t; no torch types so the
+// .hip translation units compile without PyTorch headers).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "common.h"
+
+namespace bllm {
+
+// norms.hip
+int norm_bwd_num_wg(int N);
+int norm_max_dim(DType dt);
+void rmsnorm_fwd(DType dt, const void* x, const void* w, void* y, float* rstd, int N, int d, float eps, hipStream_t s);
+void layernorm_fwd(DType dt, const void* x, const void* w, const void* b, void* y, float* mean, float* rstd, int N,
+                   int d, float eps, hipStream_t s);
+void rmsnorm_bwd(DType dt, const void* dy, const void* x, const void* w, const float* rstd, const void* dx_acc,
+                 void* dx, float* part, float* dw, int N, int d, int nwg, hipStream_t s);
+void layernorm_bwd(DType dt, const void* dy, const void* x, const void* w, const float* mean, const float* rstd,
+                   const void* dx_acc, void* dx, float* part_w, float* part_b, float* dw, float* db, int N, int d,
+                   int nwg, hipStream_t s);
+
+// elementwise.hip
+void swiglu_fwd(DType dt, const void* gu, void* act, long N, int F, hipStream_t s);
+void swiglu_bwd(DType dt, const void* gu, const void* dact, void* dgu, long N, int F, hipStream_t s);
+void gelu_fwd(DType dt, const void* f, void* g, long n, hipStream_t s);
+void gelu_bwd(DType dt, const void* f, const void* dg, void* df, long n, hipStream_t s);
+void dropout_add(DType dt, const void* x, const void* a, void* out, long n, float p, uint64_t seed, uint64_t offset,
+                 hipStream_t s);
+void rope(DType dt, void* qkv, const float* cosT, const float* sinT, long N, int T, int H, int G, int hd,
+          bool inverse, int pos_offset, hipStream_t s);
+
+// attention (attn_fwd.hip / attn_bwd.hip / attn_naive.hip)
+bool attn_supported_head_dim(int hd);
+void attn_fwd(DType dt, const void* qkv, void* o, float* lse, int B, int T, int H, int G, int hd, bool causal,
+              float p, uint64_t seed, uint64_t offset, hipStream_t s);
+void attn_bwd(DType dt, const void* qkv, const void* o, const float* lse, const void* dout, void* dqkv, float* delta,
+              float* dq_acc, int B, int T, int H, int G, int hd, bool causal, float p, uint64_t seed, uint64_t offset,
+              hipStream_t s);
+void attn_fwd_naive(DType dt, const void* qkv, void* o, float* lse, int B, int T, int H, int G, int hd, bool causal,
+                    float p, uint64_t seed, uint64_t offset, hipStream_t s);
+void attn_bwd_naive(DType dt, const void* qkv, const void* o, const float* lse, const void* dout, void* dqkv,
+                    float* delta, int B, int T, int H, int G, int hd, bool causal, float p, uint64_t seed,
+                    uint64_t offset, hipStream_t s);
+
+void attn_delta(DType dt, const void* o, const void* dout, float* delta, int B, int T, int H, int hd,
+                hipStream_t s);
+
+// loss.hip
+void ce_fwd(DType dt, const void* logits, const int64_t* tgt, float* loss, float* lse, long N, long V,
+            long ignore_index, hipStream_t s);
+void ce_bwd(DType dt, void* logits, const int64_t* tgt, const float* lse, const float* scale, long N, long V,
+            long ignore_index, hipStream_t s);
+
+// embedding.hip
+void embedding_fwd(DType dt, const int64_t* idx, const void* wte, const void* wpe, void* out, long N, int d, int T,
+                   float p, uint64_t seed, uint64_t offset, hipStream_t s);
+void embedding_bwd_tok(DType dt, const int64_t* sorted, const int64_t* perm, const void* dx, void* grad, long N, int d,
+                       bool accumulate, hipStream_t s);
+void embedding_bwd_pos(DType dt, const void* dx, void* grad, int B, int T, int d, bool accumulate, hipStream_t s);
+
+// optim.hip
+void adamw_step(DType pdt, DType gdt, void* param, float* master, const void* grad, float* m, float* v, long n,
+                float lr, float b1, float b2, float eps, float wd, int step, const float* gscale, hipStream_t s);
+int sqsum_slots(long n);
+void sqsum_partial(DType dt, const void* x, long n, float* part, int slots, hipStream_t s);
+void sum_partials(const float* part, int n, float* out, hipStream_t s);
+
+}  // namespace bllm

@@ -1,0 +1,383 @@
+// torch.ops.bllm.* registration for the gfx950 kernel library.
+//
+// Every op validates shapes/dtypes on the host before launching (a bad launch on the shared
+// GPU pool can reset the node), allocates outputs through the PyTorch HIP caching allocator
+// and launches on the current HIP stream, so ops compose with torch streams, events and
+// hipGraph capture.
+#include <ATen/ATen.h>
+#include <c10/hip/HIPStream.h>
+#include <c10/core/DeviceGuard.h>
+#include <torch/library.h>
+
+#include "common.h"
+#include "api.h"
+
+using at::Tensor;
+using c10::optional;
+using bllm::DType;
+
+namespace {
+
+DType dt_of(const Tensor& t) {
+  switch (t.scalar_type()) {
+    case at::kFloat: return DType::F32;
+    case at::kBFloat16: return DType::BF16;
+    case at::kHalf: return DType::F16;
+    default: TORCH_CHECK(false, "bllm: unsupported dtype ", t.scalar_type());
+  }
+  return DType::F32;
+}
+
+hipStream_t stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+void check_gpu(const Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), "bllm: ", name, " must be a GPU tensor");
+  TORCH_CHECK(t.is_contiguous(), "bllm: ", name, " must be contiguous");
+}
+
+void check_rows(const Tensor& x, int64_t vec_elems) {
+  TORCH_CHECK(x.dim() == 2, "bllm: expected a 2-D [rows, dim] tensor");
+  TORCH_CHECK(x.size(1) % vec_elems == 0, "bllm: row length ", x.size(1), " must be a multiple of ", vec_elems);
+}
+
+// ------------------------------------------------------------------ norms
+std::tuple<Tensor, Tensor> rmsnorm_fwd(const Tensor& x, const Tensor& w, double eps) {
+  check_gpu(x, "x"); check_gpu(w, "w");
+  c10::DeviceGuard g(x.device());
+  check_rows(x, 16 / x.element_size());
+  const int64_t N = x.size(0), d = x.size(1);
+  TORCH_CHECK(d <= bllm::norm_max_dim(dt_of(x)) && w.numel() == d && w.scalar_type() == x.scalar_type());
+  auto y = at::empty_like(x);
+  auto rstd = at::empty({N}, x.options().dtype(at::kFloat));
+  bllm::rmsnorm_fwd(dt_of(x), x.data_ptr(), w.data_ptr(), y.data_ptr(), rstd.data_ptr<float>(), N, d, (float)eps,
+                    stream());
+  return {y, rstd};
+}
+
+std::tuple<Tensor, Tensor> rmsnorm_bwd(const Tensor& dy, const Tensor& x, const Tensor& w, const Tensor& rstd,
+                                       const optional<Tensor>& dx_acc) {
+  check_gpu(dy, "dy"); check_gpu(x, "x"); check_gpu(w, "w"); check_gpu(rstd, "rstd");
+  c10::DeviceGuard g(x.device());
+  check_rows(x, 16 / x.element_size());
+  TORCH_CHECK(dy.sizes() == x.sizes() && dy.scalar_type() == x.scalar_type());
+  const int64_t N = x.size(0), d = x.size(1);
+  TORCH_CHECK(d <= bllm::norm_max_dim(dt_of(x)) && w.numel() == d);
+  const void* acc = nullptr;
+  if (dx_acc.has_value()) {
+    check_gpu(*dx_acc, "dx_acc");
+    TORCH_CHECK(dx_acc->sizes() == x.sizes() && dx_acc->scalar_type() == x.scalar_type());
+    acc = dx_acc->data_ptr();
+  }
+  auto dx = at::empty_like(x);
+  const int nwg = bllm::norm_bwd_num_wg(N);
+  auto part = at::empty({nwg, d}, x.options().dtype(at::kFloat));
+  auto dw = at::empty({d}, x.options().dtype(at::kFloat));
+  bllm::rmsnorm_bwd(dt_of(x), dy.data_ptr(), x.data_ptr(), w.data_ptr(), rstd.data_ptr<float>(), acc, dx.data_ptr(),
+                    part.data_ptr<float>(), dw.data_ptr<float>(), N, d, nwg, stream());
+  return {dx, dw};
+}
+
+std::tuple<Tensor, Tensor, Tensor> layernorm_fwd(const Tensor& x, const Tensor& w, const Tensor& b, double eps) {
+  check_gpu(x, "x"); check_gpu(w, "w"); check_gpu(b, "b");
+  c10::DeviceGuard g(x.device());
+  check_rows(x, 16 / x.element_size());
+  const int64_t N = x.size(0), d = x.size(1);
+  TORCH_CHECK(d <= bllm::norm_max_dim(dt_of(x)) && w.numel() == d && b.numel() == d);
+  auto y = at::empty_like(x);
+  auto mean = at::empty({N}, x.options().dtype(at::kFloat));
+  auto rstd = at::empty({N}, x.options().dtype(at::kFloat));
+  bllm::layernorm_fwd(dt_of(x), x.data_ptr(), w.data_ptr(), b.data_ptr(), y.data_ptr(), mean.data_ptr<float>(),
+                      rstd.data_ptr<float>(), N, d, (float)eps, stream());
+  return {y, mean, rstd};
+}
+
+std::tuple<Tensor, Tensor, Tensor> layernorm_bwd(const Tensor& dy, const Tensor& x, const Tensor& w,
+                                                 const Tensor& mean, const Tensor& rstd,
+                                                 const optional<Tensor>& dx_acc) {
+  check_gpu(dy, "dy"); check_gpu(x, "x"); check_gpu(w, "w");
+  c10::DeviceGuard g(x.device());
+  check_rows(x, 16 / x.element_size());
+  TORCH_CHECK(dy.sizes() == x.sizes() && dy.scalar_type() == x.scalar_type());
+  const int64_t N = x.size(0), d = x.size(1);
+  TORCH_CHECK(d <= bllm::norm_max_dim(dt_of(x)) && w.numel() == d);
+  const void* acc = nullptr;
+  if (dx_acc.has_value()) {
+    check_gpu(*dx_acc, "dx_acc");
+    TORCH_CHECK(dx_acc->sizes() == x.sizes() && dx_acc->scalar_type() == x.scalar_type());
+    acc = dx_acc->data_ptr();
+  }
+  auto dx = at::empty_like(x);
+  const int nwg = bllm::norm_bwd_num_wg(N);
+  auto pw = at::empty({nwg, d}, x.options().dtype(at::kFloat));
+  auto pb = at::empty({nwg, d}, x.options().dtype(at::kFloat));
+  auto dw = at::empty({d}, x.options().dtype(at::kFloat));
+  auto db = at::empty({d}, x.options().dtype(at::kFloat));
+  bllm::layernorm_bwd(dt_of(x), dy.data_ptr(), x.data_ptr(), w.data_ptr(), mean.data_ptr<float>(),
+                      rstd.data_ptr<float>(), acc, dx.data_ptr(), pw.data_ptr<float>(), pb.data_ptr<float>(),
+                      dw.data_ptr<float>(), db.data_ptr<float>(), N, d, nwg, stream());
+  return {dx, dw, db};
+}
+
+// ------------------------------------------------------------------ elementwise
+Tensor dropout_add(const Tensor& x, const Tensor& a, double p, int64_t seed, int64_t offset) {
+  check_gpu(x, "x"); check_gpu(a, "a");
+  c10::DeviceGuard g(x.device());
+  TORCH_CHECK(x.sizes() == a.sizes() && x.scalar_type() == a.scalar_type());
+  auto out = at::empty_like(x);
+  bllm::dropout_add(dt_of(x), x.data_ptr(), a.data_ptr(), out.data_ptr(), x.numel(), (float)p, (uint64_t)seed,
+                    (uint64_t)offset, stream());
+  return out;
+}
+
+Tensor dropout_bwd(const Tensor& dy, double p, int64_t seed, int64_t offset) {
+  check_gpu(dy, "dy");
+  c10::DeviceGuard g(dy.device());
+  auto out = at::empty_like(dy);
+  bllm::dropout_add(dt_of(dy), nullptr, dy.data_ptr(), out.data_ptr(), dy.numel(), (float)p, (uint64_t)seed,
+                    (uint64_t)offset, stream());
+  return out;
+}
+
+Tensor swiglu_fwd(const Tensor& gu) {
+  check_gpu(gu, "gu");
+  c10::DeviceGuard g(gu.device());
+  TORCH_CHECK(gu.dim() == 2 && gu.size(1) % 2 == 0);
+  const int64_t N = gu.size(0), F = gu.size(1) / 2;
+  auto act = at::empty({N, F}, gu.options());
+  bllm::swiglu_fwd(dt_of(gu), gu.data_ptr(), act.data_ptr(), N, F, stream());
+  return act;
+}
+
+Tensor swiglu_bwd(const Tensor& gu, const Tensor& dact) {
+  check_gpu(gu, "gu"); check_gpu(dact, "dact");
+  c10::DeviceGuard g(gu.device());
+  const int64_t N = gu.size(0), F = gu.size(1) / 2;
+  TORCH_CHECK(dact.size(0) == N && dact.size(1) == F && dact.scalar_type() == gu.scalar_type());
+  auto dgu = at::empty_like(gu);
+  bllm::swiglu_bwd(dt_of(gu), gu.data_ptr(), dact.data_ptr(), dgu.data_ptr(), N, F, stream());
+  return dgu;
+}
+
+Tensor gelu_fwd(const Tensor& f) {
+  check_gpu(f, "f");
+  c10::DeviceGuard g(f.device());
+  auto out = at::empty_like(f);
+  bllm::gelu_fwd(dt_of(f), f.data_ptr(), out.data_ptr(), f.numel(), stream());
+  return out;
+}
+
+Tensor gelu_bwd(const Tensor& f, const Tensor& dg) {
+  check_gpu(f, "f"); check_gpu(dg, "dg");
+  c10::DeviceGuard g(f.device());
+  TORCH_CHECK(f.sizes() == dg.sizes() && f.scalar_type() == dg.scalar_type());
+  auto out = at::empty_like(f);
+  bllm::gelu_bwd(dt_of(f), f.data_ptr(), dg.data_ptr(), out.data_ptr(), f.numel(), stream());
+  return out;
+}
+
+void rope_(Tensor& qkv, const Tensor& cos, const Tensor& sin, int64_t T, int64_t H, int64_t G, int64_t hd,
+           bool inverse, int64_t pos_offset) {
+  check_gpu(qkv, "qkv"); check_gpu(cos, "cos"); check_gpu(sin, "sin");
+  c10::DeviceGuard g(qkv.device());
+  TORCH_CHECK(qkv.dim() == 2 && qkv.size(1) == (H + 2 * G) * hd && hd % 2 == 0);
+  TORCH_CHECK(cos.scalar_type() == at::kFloat && sin.scalar_type() == at::kFloat);
+  TORCH_CHECK(cos.size(1) == hd / 2 && cos.size(0) >= T + pos_offset, "rope table too short");
+  bllm::rope(dt_of(qkv), qkv.data_ptr(), cos.data_ptr<float>(), sin.data_ptr<float>(), qkv.size(0), (int)T, (int)H,
+             (int)G, (int)hd, inverse, (int)pos_offset, stream());
+}
+
+// ------------------------------------------------------------------ attention
+std::tuple<Tensor, Tensor> flash_attn_fwd(const Tensor& qkv, int64_t B, int64_t T, int64_t H, int64_t G,
+                                          int64_t hd, bool causal, double p, int64_t seed, int64_t offset) {
+  check_gpu(qkv, "qkv");
+  c10::DeviceGuard g(qkv.device());
+  TORCH_CHECK(qkv.scalar_type() == at::kBFloat16 || qkv.scalar_type() == at::kHalf,
+              "flash_attn: bf16/fp16 only");
+  TORCH_CHECK(qkv.dim() == 2 && qkv.size(0) == B * T && qkv.size(1) == (H + 2 * G) * hd);
+  TORCH_CHECK(H % G == 0, "flash_attn: n_heads must be a multiple of n_kv_groups");
+  TORCH_CHECK(bllm::attn_supported_head_dim((int)hd), "flash_attn: unsupported head_dim ", hd);
+  auto o = at::empty({B * T, H * hd}, qkv.options());
+  auto lse = at::empty({B, H, T}, qkv.options().dtype(at::kFloat));
+  bllm::attn_fwd(dt_of(qkv), qkv.data_ptr(), o.data_ptr(), lse.data_ptr<float>(), (int)B, (int)T, (int)H, (int)G,
+                 (int)hd, causal, (float)p, (uint64_t)seed, (uint64_t)offset, stream());
+  return {o, lse};
+}
+
+Tensor flash_attn_bwd(const Tensor& qkv, const Tensor& o, const Tensor& lse, const Tensor& dout, int64_t B,
+                      int64_t T, int64_t H, int64_t G, int64_t hd, bool causal, double p, int64_t seed,
+                      int64_t offset) {
+  check_gpu(qkv, "qkv"); check_gpu(o, "o"); check_gpu(lse, "lse"); check_gpu(dout, "dout");
+  c10::DeviceGuard g(qkv.device());
+  TORCH_CHECK(qkv.scalar_type() == at::kBFloat16 || qkv.scalar_type() == at::kHalf);
+  TORCH_CHECK(qkv.dim() == 2 && qkv.size(0) == B * T && qkv.size(1) == (H + 2 * G) * hd);
+  TORCH_CHECK(o.sizes() == dout.sizes() && o.size(0) == B * T && o.size(1) == H * hd);
+  TORCH_CHECK(bllm::attn_supported_head_dim((int)hd), "flash_attn: unsupported head_dim ", hd);
+  auto dqkv = at::empty_like(qkv);
+  auto delta = at::empty({B, H, T}, qkv.options().dtype(at::kFloat));
+  auto dq_acc = at::zeros({B * T, H * hd}, qkv.options().dtype(at::kFloat));
+  bllm::attn_bwd(dt_of(qkv), qkv.data_ptr(), o.data_ptr(), lse.data_ptr<float>(), dout.data_ptr(), dqkv.data_ptr(),
+                 delta.data_ptr<float>(), dq_acc.data_ptr<float>(), (int)B, (int)T, (int)H, (int)G, (int)hd, causal,
+                 (float)p, (uint64_t)seed, (uint64_t)offset, stream());
+  return dqkv;
+}
+
+// ------------------------------------------------------------------ loss
+std::tuple<Tensor, Tensor> ce_fwd(const Tensor& logits, const Tensor& targets, int64_t ignore_index) {
+  check_gpu(logits, "logits"); check_gpu(targets, "targets");
+  c10::DeviceGuard g(logits.device());
+  TORCH_CHECK(logits.dim() == 2 && targets.dim() == 1 && targets.size(0) == logits.size(0));
+  TORCH_CHECK(targets.scalar_type() == at::kLong);
+  const int64_t N = logits.size(0), V = logits.size(1);
+  auto loss = at::empty({N}, logits.options().dtype(at::kFloat));
+  auto lse = at::empty({N}, logits.options().dtype(at::kFloat));
+  bllm::ce_fwd(dt_of(logits), logits.data_ptr(), targets.data_ptr<int64_t>(), loss.data_ptr<float>(),
+               lse.data_ptr<float>(), N, V, ignore_index, stream());
+  return {loss, lse};
+}
+
+void ce_bwd_(Tensor& logits, const Tensor& targets, const Tensor& lse, const Tensor& scale, int64_t ignore_index) {
+  check_gpu(logits, "logits"); check_gpu(targets, "targets"); check_gpu(lse, "lse"); check_gpu(scale, "scale");
+  c10::DeviceGuard g(logits.device());
+  TORCH_CHECK(scale.scalar_type() == at::kFloat && scale.numel() >= 1);
+  const int64_t N = logits.size(0), V = logits.size(1);
+  bllm::ce_bwd(dt_of(logits), logits.data_ptr(), targets.data_ptr<int64_t>(), lse.data_ptr<float>(),
+               scale.data_ptr<float>(), N, V, ignore_index, stream());
+}
+
+// ------------------------------------------------------------------ embedding
+Tensor embedding_fwd(const Tensor& idx, const Tensor& wte, const optional<Tensor>& wpe, int64_t T, double p,
+                     int64_t seed, int64_t offset) {
+  check_gpu(idx, "idx"); check_gpu(wte, "wte");
+  c10::DeviceGuard g(wte.device());
+  TORCH_CHECK(idx.scalar_type() == at::kLong);
+  const int64_t N = idx.numel(), d = wte.size(1);
+  const void* pe = nullptr;
+  if (wpe.has_value()) {
+    check_gpu(*wpe, "wpe");
+    TORCH_CHECK(wpe->size(1) == d && wpe->size(0) >= T && N % T == 0);
+    pe = wpe->data_ptr();
+  }
+  auto out = at::empty({N, d}, wte.options());
+  bllm::embedding_fwd(dt_of(wte), idx.data_ptr<int64_t>(), wte.data_ptr(), pe, out.data_ptr(), N, (int)d, (int)T,
+                      (float)p, (uint64_t)seed, (uint64_t)offset, stream());
+  return out;
+}
+
+void embedding_bwd(const Tensor& idx, const Tensor& dx, const optional<Tensor>& grad_wte,
+                   const optional<Tensor>& grad_wpe, int64_t T, bool accumulate) {
+  check_gpu(idx, "idx"); check_gpu(dx, "dx");
+  c10::DeviceGuard g(dx.device());
+  const int64_t N = idx.numel(), d = dx.size(1);
+  if (grad_wte.has_value()) {
+    Tensor gw = *grad_wte;
+    check_gpu(gw, "grad_wte");
+    TORCH_CHECK(gw.size(1) == d && gw.scalar_type() == dx.scalar_type());
+    if (!accumulate) gw.zero_();
+    auto sorted = at::sort(idx.reshape({-1}));
+    Tensor sid = std::get<0>(sorted).contiguous(), perm = std::get<1>(sorted).contiguous();
+    bllm::embedding_bwd_tok(dt_of(dx), sid.data_ptr<int64_t>(), perm.data_ptr<int64_t>(), dx.data_ptr(),
+                            gw.data_ptr(), N, (int)d, accumulate, stream());
+  }
+  if (grad_wpe.has_value()) {
+    Tensor gp = *grad_wpe;
+    check_gpu(gp, "grad_wpe");
+    TORCH_CHECK(N % T == 0 && gp.size(1) == d && gp.size(0) >= T);
+    if (!accumulate && gp.size(0) > T) gp.zero_();
+    bllm::embedding_bwd_pos(dt_of(dx), dx.data_ptr(), gp.data_ptr(), (int)(N / T), (int)T, (int)d, accumulate,
+                            stream());
+  }
+}
+
+// ------------------------------------------------------------------ optimizer
+Tensor sq_norm_multi(at::TensorList ts) {
+  TORCH_CHECK(!ts.empty());
+  c10::DeviceGuard g(ts[0].device());
+  std::vector<int> slots;
+  int total = 0;
+  for (auto& t : ts) {
+    check_gpu(t, "tensor");
+    slots.push_back(bllm::sqsum_slots(t.numel()));
+    total += slots.back();
+  }
+  auto part = at::empty({total}, ts[0].options().dtype(at::kFloat));
+  auto out = at::empty({1}, ts[0].options().dtype(at::kFloat));
+  int off = 0;
+  for (size_t i = 0; i < ts.size(); ++i) {
+    bllm::sqsum_partial(dt_of(ts[i]), ts[i].data_ptr(), ts[i].numel(), part.data_ptr<float>() + off, slots[i],
+                        stream());
+    off += slots[i];
+  }
+  bllm::sum_partials(part.data_ptr<float>(), total, out.data_ptr<float>(), stream());
+  return out;
+}
+
+void adamw_step_(Tensor& param, const optional<Tensor>& master, const Tensor& grad, Tensor& exp_avg,
+                 Tensor& exp_avg_sq, double lr, double b1, double b2, double eps, double wd, int64_t step,
+                 const optional<Tensor>& grad_scale) {
+  check_gpu(param, "param"); check_gpu(grad, "grad"); check_gpu(exp_avg, "exp_avg"); check_gpu(exp_avg_sq, "exp_avg_sq");
+  c10::DeviceGuard g(param.device());
+  const int64_t n = param.numel();
+  TORCH_CHECK(grad.numel() == n && exp_avg.numel() == n && exp_avg_sq.numel() == n);
+  TORCH_CHECK(exp_avg.scalar_type() == at::kFloat && exp_avg_sq.scalar_type() == at::kFloat);
+  float* mp = nullptr;
+  if (master.has_value()) {
+    check_gpu(*master, "master");
+    TORCH_CHECK(master->numel() == n && master->scalar_type() == at::kFloat);
+    mp = master->data_ptr<float>();
+  }
+  const float* gs = nullptr;
+  if (grad_scale.has_value()) {
+    check_gpu(*grad_scale, "grad_scale");
+    TORCH_CHECK(grad_scale->scalar_type() == at::kFloat);
+    gs = grad_scale->data_ptr<float>();
+  }
+  bllm::adamw_step(dt_of(param), dt_of(grad), param.data_ptr(), mp, grad.data_ptr(), exp_avg.data_ptr<float>(),
+                   exp_avg_sq.data_ptr<float>(), n, (float)lr, (float)b1, (float)b2, (float)eps, (float)wd,
+                   (int)step, gs, stream());
+}
+
+}  // namespace
+
+TORCH_LIBRARY(bllm, m) {
+  m.def("rmsnorm_fwd(Tensor x, Tensor w, float eps) -> (Tensor, Tensor)");
+  m.def("rmsnorm_bwd(Tensor dy, Tensor x, Tensor w, Tensor rstd, Tensor? dx_acc) -> (Tensor, Tensor)");
+  m.def("layernorm_fwd(Tensor x, Tensor w, Tensor b, float eps) -> (Tensor, Tensor, Tensor)");
+  m.def("layernorm_bwd(Tensor dy, Tensor x, Tensor w, Tensor mean, Tensor rstd, Tensor? dx_acc) -> (Tensor, Tensor, Tensor)");
+  m.def("dropout_add(Tensor x, Tensor a, float p, int seed, int offset) -> Tensor");
+  m.def("dropout_bwd(Tensor dy, float p, int seed, int offset) -> Tensor");
+  m.def("swiglu_fwd(Tensor gu) -> Tensor");
+  m.def("swiglu_bwd(Tensor gu, Tensor dact) -> Tensor");
+  m.def("gelu_fwd(Tensor f) -> Tensor");
+  m.def("gelu_bwd(Tensor f, Tensor dg) -> Tensor");
+  m.def("rope_(Tensor(a!) qkv, Tensor cos, Tensor sin, int T, int H, int G, int hd, bool inverse, int pos_offset) -> ()");
+  m.def("flash_attn_fwd(Tensor qkv, int B, int T, int H, int G, int hd, bool causal, float p, int seed, int offset) -> (Tensor, Tensor)");
+  m.def("flash_attn_bwd(Tensor qkv, Tensor o, Tensor lse, Tensor dout, int B, int T, int H, int G, int hd, bool causal, float p, int seed, int offset) -> Tensor");
+  m.def("ce_fwd(Tensor logits, Tensor targets, int ignore_index) -> (Tensor, Tensor)");
+  m.def("ce_bwd_(Tensor(a!) logits, Tensor targets, Tensor lse, Tensor scale, int ignore_index) -> ()");
+  m.def("embedding_fwd(Tensor idx, Tensor wte, Tensor? wpe, int T, float p, int seed, int offset) -> Tensor");
+  m.def("embedding_bwd(Tensor idx, Tensor dx, Tensor(a!)? grad_wte, Tensor(b!)? grad_wpe, int T, bool accumulate) -> ()");
+  m.def("sq_norm_multi(Tensor[] ts) -> Tensor");
+  m.def("adamw_step_(Tensor(a!) param, Tensor(b!)? master, Tensor grad, Tensor(c!) exp_avg, Tensor(d!) exp_avg_sq, float lr, float beta1, float beta2, float eps, float wd, int step, Tensor? grad_scale) -> ()");
+}
+
+TORCH_LIBRARY_IMPL(bllm, CUDA, m) {
+  m.impl("rmsnorm_fwd", &rmsnorm_fwd);
+  m.impl("rmsnorm_bwd", &rmsnorm_bwd);
+  m.impl("layernorm_fwd", &layernorm_fwd);
+  m.impl("layernorm_bwd", &layernorm_bwd);
+  m.impl("dropout_add", &dropout_add);
+  m.impl("dropout_bwd", &dropout_bwd);
+  m.impl("swiglu_fwd", &swiglu_fwd);
+  m.impl("swiglu_bwd", &swiglu_bwd);
+  m.impl("gelu_fwd", &gelu_fwd);
+  m.impl("gelu_bwd", &gelu_bwd);
+  m.impl("rope_", &rope_);
+  m.impl("flash_attn_fwd", &flash_attn_fwd);
+  m.impl("flash_attn_bwd", &flash_attn_bwd);
+  m.impl("ce_fwd", &ce_fwd);
+  m.impl("ce_bwd_", &ce_bwd_);
+  m.impl("embedding_fwd", &embedding_fwd);
+  m.impl("embedding_bwd", &embedding_bwd);
+  m.impl("sq_norm_multi", &sq_norm_multi);
+  m.impl("adamw_step_", &adamw_step_);
+}

@@ -1,0 +1,121 @@
+// Shared device helpers for the gfx950 (CDNA4, MI355X) kernel library.
+//
+// Conventions used by every kernel in csrc/:
+//  * wave64: all cross-lane reductions are over 64 lanes (__shfl_xor 32..1);
+//  * memory-bound kernels move 16 bytes per lane per access (8 x bf16/fp16, 4 x fp32),
+//    per the CDNA guide's "vectorize always" rule (scalar bf16 loads cost ~2x);
+//  * all math in fp32; storage type T in {float, __bf16, _Float16};
+//  * the dropout RNG is a stateless counter hash so masks are regenerated (never stored)
+//    in backward and in activation-checkpoint recompute — bit-identical to
+//    ops/reference.py::drop_keep_mask.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace bllm {
+
+enum class DType : int { F32 = 0, BF16 = 1, F16 = 2 };
+
+typedef __bf16 bf16_t;
+typedef _Float16 f16_t;
+
+template <typename T> __device__ __forceinline__ float to_f(T x) { return static_cast<float>(x); }
+template <typename T> __device__ __forceinline__ T from_f(float x) { return static_cast<T>(x); }
+
+// 16-byte vector of T
+template <typename T> struct Vec16 {
+  static constexpr int N = 16 / sizeof(T);
+  T v[N];
+};
+
+template <typename T>
+__device__ __forceinline__ Vec16<T> ld16(const T* p) {
+  Vec16<T> r;
+  *reinterpret_cast<uint4*>(&r) = *reinterpret_cast<const uint4*>(p);
+  return r;
+}
+template <typename T>
+__device__ __forceinline__ void st16(T* p, const Vec16<T>& r) {
+  *reinterpret_cast<uint4*>(p) = *reinterpret_cast<const uint4*>(&r);
+}
+
+// N-element vector of T (N*sizeof(T) bytes, naturally aligned loads when possible)
+template <typename T, int N> struct VecN { T v[N]; };
+// callers guarantee natural alignment of the whole vector (sizes are multiples of N)
+template <typename T, int N>
+__device__ __forceinline__ VecN<T, N> ldv(const T* p) {
+  VecN<T, N> r;
+  if constexpr (sizeof(r) == 16) *reinterpret_cast<uint4*>(&r) = *reinterpret_cast<const uint4*>(p);
+  else if constexpr (sizeof(r) == 8) *reinterpret_cast<uint2*>(&r) = *reinterpret_cast<const uint2*>(p);
+  else {
+#pragma unroll
+    for (int i = 0; i < N; ++i) r.v[i] = p[i];
+  }
+  return r;
+}
+template <typename T, int N>
+__device__ __forceinline__ void stv(T* p, const VecN<T, N>& r) {
+  if constexpr (sizeof(r) == 16) *reinterpret_cast<uint4*>(p) = *reinterpret_cast<const uint4*>(&r);
+  else if constexpr (sizeof(r) == 8) *reinterpret_cast<uint2*>(p) = *reinterpret_cast<const uint2*>(&r);
+  else {
+#pragma unroll
+    for (int i = 0; i < N; ++i) p[i] = r.v[i];
+  }
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// block-wide sum for blockDim.x == NT (multiple of 64); red must hold NT/64 floats
+template <int NT>
+__device__ __forceinline__ float block_sum(float v, float* red) {
+  v = wave_sum(v);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  __syncthreads();
+  if (l == 0) red[w] = v;
+  __syncthreads();
+  float t = 0.f;
+#pragma unroll
+  for (int i = 0; i < NT / 64; ++i) t += red[i];
+  return t;
+}
+
+// ---------------------------------------------------------------- dropout RNG
+__device__ __forceinline__ uint32_t mix32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7FEB352Du;
+  x ^= x >> 15;
+  x *= 0x846CA68Bu;
+  x ^= x >> 16;
+  return x;
+}
+// keep iff hash(seed, idx) >= thr,   thr = floor(p * 2^32)
+__device__ __forceinline__ uint32_t drop_hash(uint64_t seed, uint64_t idx) {
+  uint32_t lo = (uint32_t)idx, hi = (uint32_t)(idx >> 32);
+  uint32_t s = mix32((uint32_t)seed + hi * 0x9E3779B9u);
+  return mix32(lo ^ s);
+}
+inline uint32_t drop_threshold(float p) {
+  double t = (double)p * 4294967296.0;
+  if (t >= 4294967295.0) return 4294967295u;
+  return (uint32_t)t;
+}
+
+inline int ceil_div(long a, long b) { return (int)((a + b - 1) / b); }
+
+}  // namespace bllm
+
+#define BLLM_DISPATCH(dt, T, ...)                                  \
+  switch (dt) {                                                    \
+    case ::bllm::DType::F32: { typedef float T; __VA_ARGS__; break; }        \
+    case ::bllm::DType::BF16: { typedef ::bllm::bf16_t T; __VA_ARGS__; break; } \
+    case ::bllm::DType::F16: { typedef ::bllm::f16_t T; __VA_ARGS__; break; }   \
+  }

@@ -1,0 +1,230 @@
+// Elementwise kernels: SwiGLU, exact-erf GELU, dropout(+residual), RoPE.
+//
+// Replaces reference common_components.py:6-35 (RoPE), :78-124 (SiLU/SwiGLU),
+// GPT2.py:58-62 (nn.GELU, exact erf), and nn.Dropout.  All are HBM-bound: 16-byte
+// accesses per lane, grid-stride loops capped at 256 CUs x 8 workgroups.
+#include "common.h"
+
+namespace bllm {
+
+static inline int ew_grid(long nvec) {
+  long g = (nvec + 255) / 256;
+  return (int)(g < 2048 ? (g > 0 ? g : 1) : 2048);
+}
+
+// ---------------------------------------------------------------- SwiGLU
+// gu: [N, 2F] = [gate | up] per row (fused [fc1; fc2] GEMM output); act: [N, F]
+template <typename T, int VEC>
+__global__ __launch_bounds__(256) void swiglu_fwd_k(const T* __restrict__ gu, T* __restrict__ act, long N, int F) {
+  const int fv = F / VEC;
+  const long total = N * fv;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const long r = i / fv;
+    const int c = (int)(i - r * fv) * VEC;
+    VecN<T, VEC> g = ldv<T, VEC>(gu + r * 2 * F + c), u = ldv<T, VEC>(gu + r * 2 * F + F + c), o;
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) {
+      const float a = to_f(g.v[j]);
+      o.v[j] = from_f<T>(a / (1.f + __expf(-a)) * to_f(u.v[j]));
+    }
+    stv<T, VEC>(act + r * F + c, o);
+  }
+}
+
+template <typename T, int VEC>
+__global__ __launch_bounds__(256) void swiglu_bwd_k(const T* __restrict__ gu, const T* __restrict__ dact,
+                                                    T* __restrict__ dgu, long N, int F) {
+  const int fv = F / VEC;
+  const long total = N * fv;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const long r = i / fv;
+    const int c = (int)(i - r * fv) * VEC;
+    VecN<T, VEC> g = ldv<T, VEC>(gu + r * 2 * F + c), u = ldv<T, VEC>(gu + r * 2 * F + F + c), d = ldv<T, VEC>(dact + r * F + c);
+    VecN<T, VEC> dg, du;
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) {
+      const float a = to_f(g.v[j]), b = to_f(u.v[j]), dd = to_f(d.v[j]);
+      const float sg = 1.f / (1.f + __expf(-a));
+      dg.v[j] = from_f<T>(dd * b * sg * (1.f + a * (1.f - sg)));
+      du.v[j] = from_f<T>(dd * a * sg);
+    }
+    stv<T, VEC>(dgu + r * 2 * F + c, dg);
+    stv<T, VEC>(dgu + r * 2 * F + F + c, du);
+  }
+}
+
+// ---------------------------------------------------------------- GELU (erf)
+template <typename T, int VEC>
+__global__ __launch_bounds__(256) void gelu_fwd_k(const T* __restrict__ f, T* __restrict__ g, long nvec) {
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < nvec; i += (long)gridDim.x * 256) {
+    VecN<T, VEC> a = ldv<T, VEC>(f + i * VEC), o;
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) {
+      const float x = to_f(a.v[j]);
+      o.v[j] = from_f<T>(0.5f * x * (1.f + erff(x * 0.70710678118654752f)));
+    }
+    stv<T, VEC>(g + i * VEC, o);
+  }
+}
+
+template <typename T, int VEC>
+__global__ __launch_bounds__(256) void gelu_bwd_k(const T* __restrict__ f, const T* __restrict__ dg,
+                                                  T* __restrict__ df, long nvec) {
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < nvec; i += (long)gridDim.x * 256) {
+    VecN<T, VEC> a = ldv<T, VEC>(f + i * VEC), d = ldv<T, VEC>(dg + i * VEC), o;
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) {
+      const float x = to_f(a.v[j]);
+      const float cdf = 0.5f * (1.f + erff(x * 0.70710678118654752f));
+      const float pdf = __expf(-0.5f * x * x) * 0.39894228040143268f;
+      o.v[j] = from_f<T>(to_f(d.v[j]) * (cdf + x * pdf));
+    }
+    stv<T, VEC>(df + i * VEC, o);
+  }
+}
+
+// ---------------------------------------------------------------- dropout
+// out = x + a * keep / (1-p)    (x may be null -> out = dropout(a))
+template <typename T, int VEC>
+__global__ __launch_bounds__(256) void dropout_add_k(const T* __restrict__ x, const T* __restrict__ a,
+                                                     T* __restrict__ out, long nvec, uint64_t seed,
+                                                     uint64_t offset, uint32_t thr, float inv_keep) {
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < nvec; i += (long)gridDim.x * 256) {
+    VecN<T, VEC> av = ldv<T, VEC>(a + i * VEC), o;
+    VecN<T, VEC> xv;
+    if (x) xv = ldv<T, VEC>(x + i * VEC);
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) {
+      const uint64_t e = (uint64_t)(i * VEC + j);
+      const bool keep = drop_hash(seed, offset + e) >= thr;
+      float r = keep ? to_f(av.v[j]) * inv_keep : 0.f;
+      if (x) r += to_f(xv.v[j]);
+      o.v[j] = from_f<T>(r);
+    }
+    stv<T, VEC>(out + i * VEC, o);
+  }
+}
+
+// ---------------------------------------------------------------- RoPE in place
+// qkv [N, (H+2G)*hd]; rotates heads [0, H+G) of every row; position = row % T + pos_offset.
+// One thread = 8 consecutive pairs (x1[i..i+7], x2[i..i+7]); cos/sin fp32 [Tctx, hd/2].
+template <typename T>
+__global__ __launch_bounds__(256) void rope_k(T* __restrict__ qkv, const float* __restrict__ cosT,
+                                              const float* __restrict__ sinT, long N, int T_, int nh_rot,
+                                              int row_stride, int hd, int pos_offset, float sgn) {
+  const int half = hd / 2;
+  const int cpb = half / 8;  // chunks of 8 pairs per head
+  const long total = N * nh_rot * cpb;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const int ch = (int)(i % cpb);
+    const long t = i / cpb;
+    const int h = (int)(t % nh_rot);
+    const long r = t / nh_rot;
+    const int pos = (int)(r % T_) + pos_offset;
+    T* base = qkv + r * row_stride + (long)h * hd + ch * 8;
+    const float* cp = cosT + (long)pos * half + ch * 8;
+    const float* sp = sinT + (long)pos * half + ch * 8;
+    float x1[8], x2[8], c[8], s[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      x1[j] = to_f(base[j]);
+      x2[j] = to_f(base[half + j]);
+      c[j] = cp[j];
+      s[j] = sgn * sp[j];
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      base[j] = from_f<T>(x1[j] * c[j] - x2[j] * s[j]);
+      base[half + j] = from_f<T>(x2[j] * c[j] + x1[j] * s[j]);
+    }
+  }
+}
+
+// scalar fallback for head dims not multiple of 16
+template <typename T>
+__global__ __launch_bounds__(256) void rope_scalar_k(T* __restrict__ qkv, const float* __restrict__ cosT,
+                                                     const float* __restrict__ sinT, long N, int T_, int nh_rot,
+                                                     int row_stride, int hd, int pos_offset, float sgn) {
+  const int half = hd / 2;
+  const long total = N * nh_rot * half;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const int k = (int)(i % half);
+    const long t = i / half;
+    const int h = (int)(t % nh_rot);
+    const long r = t / nh_rot;
+    const int pos = (int)(r % T_) + pos_offset;
+    T* base = qkv + r * row_stride + (long)h * hd;
+    const float c = cosT[(long)pos * half + k], s = sgn * sinT[(long)pos * half + k];
+    const float a = to_f(base[k]), b = to_f(base[half + k]);
+    base[k] = from_f<T>(a * c - b * s);
+    base[half + k] = from_f<T>(b * c + a * s);
+  }
+}
+
+// ----------------------------------------------------------------------------- launchers
+// VEC = 16 bytes per lane when the sizes allow it, else 1 (tiny debug shapes)
+#define EW_VEC(T, cond, ...)                          \
+  if (cond) { constexpr int VEC = 16 / sizeof(T); __VA_ARGS__; } \
+  else { constexpr int VEC = 1; __VA_ARGS__; }
+
+void swiglu_fwd(DType dt, const void* gu, void* act, long N, int F, hipStream_t s) {
+  BLLM_DISPATCH(dt, T, {
+    EW_VEC(T, F % (16 / sizeof(T)) == 0, {
+      hipLaunchKernelGGL((swiglu_fwd_k<T, VEC>), dim3(ew_grid(N * F / VEC)), dim3(256), 0, s, (const T*)gu,
+                         (T*)act, N, F);
+    });
+  });
+}
+void swiglu_bwd(DType dt, const void* gu, const void* dact, void* dgu, long N, int F, hipStream_t s) {
+  BLLM_DISPATCH(dt, T, {
+    EW_VEC(T, F % (16 / sizeof(T)) == 0, {
+      hipLaunchKernelGGL((swiglu_bwd_k<T, VEC>), dim3(ew_grid(N * F / VEC)), dim3(256), 0, s, (const T*)gu,
+                         (const T*)dact, (T*)dgu, N, F);
+    });
+  });
+}
+void gelu_fwd(DType dt, const void* f, void* g, long n, hipStream_t s) {
+  BLLM_DISPATCH(dt, T, {
+    EW_VEC(T, n % (16 / sizeof(T)) == 0, {
+      hipLaunchKernelGGL((gelu_fwd_k<T, VEC>), dim3(ew_grid(n / VEC)), dim3(256), 0, s, (const T*)f, (T*)g,
+                         n / VEC);
+    });
+  });
+}
+void gelu_bwd(DType dt, const void* f, const void* dg, void* df, long n, hipStream_t s) {
+  BLLM_DISPATCH(dt, T, {
+    EW_VEC(T, n % (16 / sizeof(T)) == 0, {
+      hipLaunchKernelGGL((gelu_bwd_k<T, VEC>), dim3(ew_grid(n / VEC)), dim3(256), 0, s, (const T*)f,
+                         (const T*)dg, (T*)df, n / VEC);
+    });
+  });
+}
+void dropout_add(DType dt, const void* x, const void* a, void* out, long n, float p, uint64_t seed,
+                 uint64_t offset, hipStream_t s) {
+  const uint32_t thr = drop_threshold(p);
+  const float inv_keep = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  BLLM_DISPATCH(dt, T, {
+    EW_VEC(T, n % (16 / sizeof(T)) == 0, {
+      hipLaunchKernelGGL((dropout_add_k<T, VEC>), dim3(ew_grid(n / VEC)), dim3(256), 0, s, (const T*)x,
+                         (const T*)a, (T*)out, n / VEC, seed, offset, thr, inv_keep);
+    });
+  });
+}
+void rope(DType dt, void* qkv, const float* cosT, const float* sinT, long N, int T_, int H, int G, int hd,
+          bool inverse, int pos_offset, hipStream_t s) {
+  const int nh = H + G, stride = (H + 2 * G) * hd;
+  const float sgn = inverse ? -1.f : 1.f;
+  BLLM_DISPATCH(dt, T, {
+    if ((hd / 2) % 8 == 0) {
+      long tot = N * nh * (hd / 16);
+      hipLaunchKernelGGL(rope_k<T>, dim3(ew_grid(tot)), dim3(256), 0, s, (T*)qkv, cosT, sinT, N, T_, nh, stride,
+                         hd, pos_offset, sgn);
+    } else {
+      long tot = N * nh * (hd / 2);
+      hipLaunchKernelGGL(rope_scalar_k<T>, dim3(ew_grid(tot)), dim3(256), 0, s, (T*)qkv, cosT, sinT, N, T_, nh,
+                         stride, hd, pos_offset, sgn);
+    }
+  });
+}
+
+}  // namespace bllm

@@ -1,0 +1,244 @@
+// RMSNorm / LayerNorm forward + backward (fused residual-gradient add) for gfx950.
+//
+// Replaces reference Models/Llama/common_components.py:54-70 (RMSNorm) and nn.LayerNorm
+// (Models/GPT2/GPT2.py:79-80).  Memory-bound: one wave64 per row, the row held in VGPRs
+// (16-B loads, NV vectors per lane), fp32 statistics, one pass over x in forward and one
+// over (x, dy[, dx_acc]) in backward.  Weight/bias gradients: per-lane register
+// accumulators -> LDS float atomics across the 4 waves of a workgroup -> one fp32 partial
+// row per workgroup -> a column-reduction kernel (deterministic, no global atomics).
+#include "common.h"
+
+namespace bllm {
+
+constexpr int ROWS_PER_WG = 4;  // 4 waves x 1 row
+constexpr int MAX_BWD_WG = 512;
+
+template <typename T, int NV, bool LN>
+__global__ __launch_bounds__(256) void norm_fwd_k(const T* __restrict__ x, const T* __restrict__ w,
+                                                  const T* __restrict__ b, T* __restrict__ y,
+                                                  float* __restrict__ mean_out, float* __restrict__ rstd_out,
+                                                  int N, int d, float eps) {
+  constexpr int VEC = 16 / sizeof(T);
+  const int row = blockIdx.x * ROWS_PER_WG + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= N) return;
+  const int nvec = d / VEC;
+  const T* xr = x + (size_t)row * d;
+  float v[NV][VEC];
+  float s1 = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = lane + 64 * i;
+    if (c < nvec) {
+      Vec16<T> r = ld16(xr + c * VEC);
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) { v[i][j] = to_f(r.v[j]); s1 += LN ? v[i][j] : v[i][j] * v[i][j]; }
+    }
+  }
+  s1 = wave_sum(s1);
+  float mu = 0.f, rs;
+  if (LN) {
+    mu = s1 / d;
+    float s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int c = lane + 64 * i;
+      if (c < nvec) {
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) { float t = v[i][j] - mu; s2 += t * t; }
+      }
+    }
+    s2 = wave_sum(s2);
+    rs = rsqrtf(s2 / d + eps);
+  } else {
+    rs = rsqrtf(s1 / d + eps);
+  }
+  T* yr = y + (size_t)row * d;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = lane + 64 * i;
+    if (c < nvec) {
+      Vec16<T> wv = ld16(w + c * VEC), o;
+      if (LN) {
+        Vec16<T> bv = ld16(b + c * VEC);
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) o.v[j] = from_f<T>((v[i][j] - mu) * rs * to_f(wv.v[j]) + to_f(bv.v[j]));
+      } else {
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) o.v[j] = from_f<T>(v[i][j] * rs * to_f(wv.v[j]));
+      }
+      st16(yr + c * VEC, o);
+    }
+  }
+  if (lane == 0) {
+    rstd_out[row] = rs;
+    if (LN) mean_out[row] = mu;
+  }
+}
+
+// backward: dx = rs * (g - [LN: mean(g)] - xhat * mean(g * xhat)) (+ dx_acc), g = dy * w
+template <typename T, int NV, bool LN>
+__global__ __launch_bounds__(256) void norm_bwd_k(const T* __restrict__ dy, const T* __restrict__ x,
+                                                  const T* __restrict__ w, const float* __restrict__ mean,
+                                                  const float* __restrict__ rstd, const T* __restrict__ dx_acc,
+                                                  T* __restrict__ dx, float* __restrict__ part_w,
+                                                  float* __restrict__ part_b, int N, int d) {
+  constexpr int VEC = 16 / sizeof(T);
+  extern __shared__ __attribute__((aligned(16))) float lds[];  // [d] (+[d] for LN bias)
+  const int lane = threadIdx.x & 63;
+  const int nvec = d / VEC;
+  for (int i = threadIdx.x; i < d * (LN ? 2 : 1); i += blockDim.x) lds[i] = 0.f;
+  float aw[NV][VEC], ab[NV][VEC];
+#pragma unroll
+  for (int i = 0; i < NV; ++i)
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) { aw[i][j] = 0.f; ab[i][j] = 0.f; }
+  float wf[NV][VEC];
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = lane + 64 * i;
+    if (c < nvec) {
+      Vec16<T> wv = ld16(w + c * VEC);
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) wf[i][j] = to_f(wv.v[j]);
+    }
+  }
+  const int nw = gridDim.x * ROWS_PER_WG;
+  for (int row = blockIdx.x * ROWS_PER_WG + (threadIdx.x >> 6); row < N; row += nw) {
+    const T* xr = x + (size_t)row * d;
+    const T* dyr = dy + (size_t)row * d;
+    const float rs = rstd[row];
+    const float mu = LN ? mean[row] : 0.f;
+    float xh[NV][VEC], g[NV][VEC];
+    float sg = 0.f, sgx = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int c = lane + 64 * i;
+      if (c < nvec) {
+        Vec16<T> xv = ld16(xr + c * VEC), dv = ld16(dyr + c * VEC);
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) {
+          const float dd = to_f(dv.v[j]);
+          xh[i][j] = (to_f(xv.v[j]) - mu) * rs;
+          g[i][j] = dd * wf[i][j];
+          aw[i][j] += dd * xh[i][j];
+          if (LN) ab[i][j] += dd;
+          sg += g[i][j];
+          sgx += g[i][j] * xh[i][j];
+        }
+      }
+    }
+    sgx = wave_sum(sgx) / d;
+    if (LN) sg = wave_sum(sg) / d;
+    T* dxr = dx + (size_t)row * d;
+    const T* ar = dx_acc ? dx_acc + (size_t)row * d : nullptr;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int c = lane + 64 * i;
+      if (c < nvec) {
+        Vec16<T> o;
+        Vec16<T> av;
+        if (ar) av = ld16(ar + c * VEC);
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) {
+          float r = rs * (g[i][j] - (LN ? sg : 0.f) - xh[i][j] * sgx);
+          if (ar) r += to_f(av.v[j]);
+          o.v[j] = from_f<T>(r);
+        }
+        st16(dxr + c * VEC, o);
+      }
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = lane + 64 * i;
+    if (c < nvec) {
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) {
+        atomicAdd(&lds[c * VEC + j], aw[i][j]);
+        if (LN) atomicAdd(&lds[d + c * VEC + j], ab[i][j]);
+      }
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < d; i += blockDim.x) {
+    part_w[(size_t)blockIdx.x * d + i] = lds[i];
+    if (LN) part_b[(size_t)blockIdx.x * d + i] = lds[d + i];
+  }
+}
+
+// out[c] = sum_p part[p][c]   (64 columns x 4 row-groups per workgroup, fixed order)
+__global__ __launch_bounds__(256) void col_reduce_k(const float* __restrict__ part, float* __restrict__ out,
+                                                    int P, int d) {
+  __shared__ float red[4][64];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int g = threadIdx.x >> 6;
+  float s = 0.f;
+  if (c < d)
+    for (int p = g; p < P; p += 4) s += part[(size_t)p * d + c];
+  red[g][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (g == 0 && c < d) out[c] = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+}
+
+// ----------------------------------------------------------------------------- launchers
+template <typename T, bool LN>
+static void fwd_dispatch(const void* x, const void* w, const void* b, void* y, float* mean, float* rstd,
+                         int N, int d, float eps, hipStream_t s) {
+  constexpr int VEC = 16 / sizeof(T);
+  const int nvec = d / VEC;
+  const int nv = (nvec + 63) / 64;
+  dim3 grid(ceil_div(N, ROWS_PER_WG)), block(256);
+#define L(NVV) hipLaunchKernelGGL((norm_fwd_k<T, NVV, LN>), grid, block, 0, s, (const T*)x, (const T*)w, \
+                                  (const T*)b, (T*)y, mean, rstd, N, d, eps)
+  if (nv <= 1) L(1); else if (nv <= 2) L(2); else if (nv <= 4) L(4); else if (nv <= 8) L(8); else L(16);
+#undef L
+}
+
+template <typename T, bool LN>
+static void bwd_dispatch(const void* dy, const void* x, const void* w, const float* mean, const float* rstd,
+                         const void* dx_acc, void* dx, float* part_w, float* part_b, float* dw, float* db,
+                         int N, int d, int nwg, hipStream_t s) {
+  constexpr int VEC = 16 / sizeof(T);
+  const int nvec = d / VEC;
+  const int nv = (nvec + 63) / 64;
+  dim3 grid(nwg), block(256);
+  size_t lds = sizeof(float) * d * (LN ? 2 : 1);
+#define L(NVV) hipLaunchKernelGGL((norm_bwd_k<T, NVV, LN>), grid, block, lds, s, (const T*)dy, (const T*)x, \
+                                  (const T*)w, mean, rstd, (const T*)dx_acc, (T*)dx, part_w, part_b, N, d)
+  if (nv <= 1) L(1); else if (nv <= 2) L(2); else if (nv <= 4) L(4); else if (nv <= 8) L(8); else L(16);
+#undef L
+  hipLaunchKernelGGL(col_reduce_k, dim3(ceil_div(d, 64)), dim3(256), 0, s, part_w, dw, nwg, d);
+  if (LN) hipLaunchKernelGGL(col_reduce_k, dim3(ceil_div(d, 64)), dim3(256), 0, s, part_b, db, nwg, d);
+}
+
+int norm_bwd_num_wg(int N) {
+  int n = ceil_div(N, ROWS_PER_WG);
+  return n < MAX_BWD_WG ? n : MAX_BWD_WG;
+}
+
+// max supported row length per dtype (NV <= 16): 8192 (bf16/f16), 4096 (f32)
+int norm_max_dim(DType dt) { return dt == DType::F32 ? 4096 : 8192; }
+
+void rmsnorm_fwd(DType dt, const void* x, const void* w, void* y, float* rstd, int N, int d, float eps,
+                 hipStream_t s) {
+  BLLM_DISPATCH(dt, T, (fwd_dispatch<T, false>(x, w, nullptr, y, nullptr, rstd, N, d, eps, s)));
+}
+void layernorm_fwd(DType dt, const void* x, const void* w, const void* b, void* y, float* mean, float* rstd,
+                   int N, int d, float eps, hipStream_t s) {
+  BLLM_DISPATCH(dt, T, (fwd_dispatch<T, true>(x, w, b, y, mean, rstd, N, d, eps, s)));
+}
+void rmsnorm_bwd(DType dt, const void* dy, const void* x, const void* w, const float* rstd, const void* dx_acc,
+                 void* dx, float* part, float* dw, int N, int d, int nwg, hipStream_t s) {
+  BLLM_DISPATCH(dt, T, (bwd_dispatch<T, false>(dy, x, w, nullptr, rstd, dx_acc, dx, part, nullptr, dw,
+                                               nullptr, N, d, nwg, s)));
+}
+void layernorm_bwd(DType dt, const void* dy, const void* x, const void* w, const float* mean, const float* rstd,
+                   const void* dx_acc, void* dx, float* part_w, float* part_b, float* dw, float* db, int N, int d,
+                   int nwg, hipStream_t s) {
+  BLLM_DISPATCH(dt, T, (bwd_dispatch<T, true>(dy, x, w, mean, rstd, dx_acc, dx, part_w, part_b, dw, db, N,
+                                              d, nwg, s)));
+}
+
+}  // namespace bllm

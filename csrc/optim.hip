@@ -1,0 +1,118 @@
+// Fused AdamW over flat parameter buffers + multi-tensor squared L2 norm.
+//
+// Replaces torch.optim.AdamW(lr, weight_decay=0.1) (reference build_components.py:250-258)
+// and clip_grad_norm_(max_norm=1.0) (train.py:114-120).  One launch per flat unit buffer:
+// reads grad (bf16/f16/f32) + fp32 master/exp_avg/exp_avg_sq, writes them back plus the
+// low-precision param copy — 16-B vector accesses, pure HBM streaming.  The clip factor
+// (and the fp16 loss-scale inverse) arrive as a DEVICE scalar, so clipping never forces a
+// host sync.  The norm is two-level and order-fixed (deterministic).
+#include "common.h"
+
+namespace bllm {
+
+template <typename P, typename G, int VEC>
+__global__ __launch_bounds__(256) void adamw_k(P* __restrict__ param, float* __restrict__ master,
+                                               const G* __restrict__ grad, float* __restrict__ m,
+                                               float* __restrict__ v, long nvec, float lr, float b1, float b2,
+                                               float eps, float wd, float bc1, float bc2_sqrt,
+                                               const float* __restrict__ gscale) {
+  const float gs = gscale ? gscale[0] : 1.f;
+  const float decay = 1.f - lr * wd;
+  const float step = lr / bc1;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < nvec; i += (long)gridDim.x * 256) {
+    const long o = i * VEC;
+    VecN<G, VEC> gv = ldv<G, VEC>(grad + o);
+    VecN<float, VEC> mv = ldv<float, VEC>(m + o), vv = ldv<float, VEC>(v + o), pv;
+    if (master) pv = ldv<float, VEC>(master + o);
+    else {
+      VecN<P, VEC> pp = ldv<P, VEC>(param + o);
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) pv.v[j] = to_f(pp.v[j]);
+    }
+    VecN<P, VEC> po;
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) {
+      const float g = to_f(gv.v[j]) * gs;
+      mv.v[j] = b1 * mv.v[j] + (1.f - b1) * g;
+      vv.v[j] = b2 * vv.v[j] + (1.f - b2) * g * g;
+      float p = pv.v[j] * decay;
+      p -= step * mv.v[j] / (sqrtf(vv.v[j]) / bc2_sqrt + eps);
+      pv.v[j] = p;
+      po.v[j] = from_f<P>(p);
+    }
+    stv<float, VEC>(m + o, mv);
+    stv<float, VEC>(v + o, vv);
+    if (master) stv<float, VEC>(master + o, pv);
+    stv<P, VEC>(param + o, po);
+  }
+}
+
+template <typename T, int VEC>
+__global__ __launch_bounds__(256) void sqsum_partial_k(const T* __restrict__ x, long nvec, float* __restrict__ part) {
+  __shared__ float red[4];
+  float s = 0.f;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < nvec; i += (long)gridDim.x * 256) {
+    VecN<T, VEC> r = ldv<T, VEC>(x + i * VEC);
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) { const float f = to_f(r.v[j]); s += f * f; }
+  }
+  s = block_sum<256>(s, red);
+  if (threadIdx.x == 0) part[blockIdx.x] = s;
+}
+
+__global__ __launch_bounds__(256) void sum_k(const float* __restrict__ part, int n, float* __restrict__ out) {
+  __shared__ float red[4];
+  float s = 0.f;
+  for (int i = threadIdx.x; i < n; i += 256) s += part[i];
+  s = block_sum<256>(s, red);
+  if (threadIdx.x == 0) out[0] = s;
+}
+
+template <typename P, typename G>
+static void adamw_launch(void* param, float* master, const void* grad, float* m, float* v, long n, float lr,
+                         float b1, float b2, float eps, float wd, float bc1, float bc2s, const float* gscale,
+                         hipStream_t s) {
+  if (n % 4 == 0) {
+    long nv = n / 4;
+    int g = (int)((nv + 255) / 256 < 4096 ? (nv + 255) / 256 : 4096);
+    hipLaunchKernelGGL((adamw_k<P, G, 4>), dim3(g > 0 ? g : 1), dim3(256), 0, s, (P*)param, master,
+                       (const G*)grad, m, v, nv, lr, b1, b2, eps, wd, bc1, bc2s, gscale);
+  } else {
+    int g = (int)((n + 255) / 256 < 4096 ? (n + 255) / 256 : 4096);
+    hipLaunchKernelGGL((adamw_k<P, G, 1>), dim3(g > 0 ? g : 1), dim3(256), 0, s, (P*)param, master,
+                       (const G*)grad, m, v, n, lr, b1, b2, eps, wd, bc1, bc2s, gscale);
+  }
+}
+
+void adamw_step(DType pdt, DType gdt, void* param, float* master, const void* grad, float* m, float* v, long n,
+                float lr, float b1, float b2, float eps, float wd, int step, const float* gscale, hipStream_t s) {
+  const float bc1 = 1.f - powf(b1, (float)step);
+  const float bc2s = sqrtf(1.f - powf(b2, (float)step));
+  BLLM_DISPATCH(pdt, P, {
+    BLLM_DISPATCH(gdt, G, (adamw_launch<P, G>(param, master, grad, m, v, n, lr, b1, b2, eps, wd, bc1, bc2s,
+                                              gscale, s)));
+  });
+}
+
+// number of partial slots the launcher will use for a tensor of n elements
+int sqsum_slots(long n) {
+  long g = (n + 256L * 16 - 1) / (256L * 16);
+  return (int)(g < 512 ? (g > 0 ? g : 1) : 512);
+}
+
+void sqsum_partial(DType dt, const void* x, long n, float* part, int slots, hipStream_t s) {
+  BLLM_DISPATCH(dt, T, {
+    if (n % (16 / sizeof(T)) == 0) {
+      constexpr int VEC = 16 / sizeof(T);
+      hipLaunchKernelGGL((sqsum_partial_k<T, VEC>), dim3(slots), dim3(256), 0, s, (const T*)x, n / VEC, part);
+    } else {
+      hipLaunchKernelGGL((sqsum_partial_k<T, 1>), dim3(slots), dim3(256), 0, s, (const T*)x, n, part);
+    }
+  });
+}
+
+void sum_partials(const float* part, int n, float* out, hipStream_t s) {
+  hipLaunchKernelGGL(sum_k, dim3(1), dim3(256), 0, s, part, n, out);
+}
+
+}  // namespace bllm

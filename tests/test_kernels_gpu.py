@@ -1,0 +1,180 @@
+"""HIP kernels vs the plain-PyTorch fp32 reference (ops/reference.py).  GPU only."""
+import math
+
+import pytest
+import torch
+
+from building_llm_from_scratch_amd import ops
+from building_llm_from_scratch_amd.ops import reference as ref
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+DTYPES = [torch.bfloat16, torch.float16, torch.float32]
+TOL = {torch.bfloat16: 2e-2, torch.float16: 2e-3, torch.float32: 1e-5}
+
+
+def _close(a, b, dt, scale=1.0, name=""):
+    a, b = a.float().cpu(), b.float().cpu()
+    err = (a - b).abs().max().item()
+    ref_mag = b.abs().max().item() + 1e-6
+    assert err <= TOL[dt] * max(ref_mag, 1.0) * scale, f"{name}: max err {err} (ref mag {ref_mag})"
+
+
+@pytest.fixture(autouse=True)
+def _ext():
+    assert ops.load_ext(required=True)
+    torch.manual_seed(0)
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+@pytest.mark.parametrize("d", [32, 768, 1600, 4096])
+def test_rmsnorm(dt, d):
+    N = 67
+    x = torch.randn(N, d, device=DEV).to(dt)
+    w = (1 + 0.1 * torch.randn(d, device=DEV)).to(dt)
+    dy = torch.randn(N, d, device=DEV).to(dt)
+    acc = torch.randn(N, d, device=DEV).to(dt)
+    y, r = ops.rmsnorm_fwd(x, w, 1e-5)
+    y0, r0 = ref.rmsnorm_fwd(x.cpu().float(), w.cpu().float(), 1e-5)
+    _close(y, y0, dt, name="y")
+    _close(r, r0, torch.float32, 10, name="rstd")
+    dx, dw = ops.rmsnorm_bwd(dy, x, w, r, acc)
+    dx0, dw0 = ref.rmsnorm_bwd(dy.cpu().float(), x.cpu().float(), w.cpu().float(), r0, acc.cpu().float())
+    _close(dx, dx0, dt, 2, name="dx")
+    _close(dw, dw0, dt, 2, name="dw")
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+@pytest.mark.parametrize("d", [32, 768, 1280])
+def test_layernorm(dt, d):
+    N = 53
+    x = (torch.randn(N, d, device=DEV) + 0.5).to(dt)
+    w = (1 + 0.1 * torch.randn(d, device=DEV)).to(dt)
+    b = (0.1 * torch.randn(d, device=DEV)).to(dt)
+    dy = torch.randn(N, d, device=DEV).to(dt)
+    y, m, r = ops.layernorm_fwd(x, w, b, 1e-5)
+    y0, m0, r0 = ref.layernorm_fwd(x.cpu().float(), w.cpu().float(), b.cpu().float(), 1e-5)
+    _close(y, y0, dt, name="y")
+    dx, dw, db = ops.layernorm_bwd(dy, x, w, m, r, None)
+    dx0, dw0, db0 = ref.layernorm_bwd(dy.cpu().float(), x.cpu().float(), w.cpu().float(), m0, r0, None)
+    _close(dx, dx0, dt, 2, name="dx")
+    _close(dw, dw0, dt, 2, name="dw")
+    _close(db, db0, dt, 2, name="db")
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+@pytest.mark.parametrize("F", [10, 64, 1000])
+def test_swiglu_gelu(dt, F):
+    gu = torch.randn(33, 2 * F, device=DEV).to(dt)
+    da = torch.randn(33, F, device=DEV).to(dt)
+    _close(ops.swiglu_fwd(gu), ref.swiglu_fwd(gu.cpu().float()), dt, name="swiglu")
+    _close(ops.swiglu_bwd(gu, da), ref.swiglu_bwd(gu.cpu().float(), da.cpu().float()), dt, 2, name="swiglu_bwd")
+    f = torch.randn(33, F, device=DEV).to(dt)
+    _close(ops.gelu_fwd(f), ref.gelu_fwd(f.cpu().float()), dt, name="gelu")
+    _close(ops.gelu_bwd(f, da), ref.gelu_bwd(f.cpu().float(), da.cpu().float()), dt, name="gelu_bwd")
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+def test_dropout_bitexact_mask(dt):
+    x = torch.randn(37, 96, device=DEV).to(dt)
+    a = torch.randn(37, 96, device=DEV).to(dt)
+    out = ops.dropout_add(x, a, 0.1, 1234, 777)
+    out0 = ref.dropout_add(x.cpu().float(), a.cpu().float(), 0.1, 1234, 777)
+    _close(out, out0, dt, name="dropout_add")
+    keep_gpu = (ops.dropout_bwd(torch.ones(37, 96, device=DEV, dtype=dt), 0.1, 1234, 777) != 0).cpu()
+    keep_ref = ref.drop_keep_mask(1234, 777, 37 * 96, 0.1).view(37, 96)
+    assert torch.equal(keep_gpu, keep_ref)
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+@pytest.mark.parametrize("hd,H,G", [(64, 4, 4), (128, 8, 2), (2, 16, 8)])
+def test_rope(dt, hd, H, G):
+    B, T = 2, 17
+    cos, sin = ops.rope_tables(hd, 32, 500000.0, {"factor": 8.0, "low_freq_factor": 1.0, "high_freq_factor": 4.0,
+                                                  "original_context_length": 8192}, device=DEV)
+    qkv = torch.randn(B * T, (H + 2 * G) * hd, device=DEV).to(dt)
+    q0 = ref.rope_(qkv.cpu().float().clone(), cos.cpu(), sin.cpu(), T, H, G, hd)
+    q1 = ops.rope_(qkv.clone(), cos, sin, T, H, G, hd)
+    _close(q1, q0, dt, name="rope")
+    back = ops.rope_(q1.clone(), cos, sin, T, H, G, hd, inverse=True)
+    _close(back, qkv, dt, 2, name="rope inverse")
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+@pytest.mark.parametrize("V", [97, 50257, 128256])
+def test_cross_entropy(dt, V):
+    N = 24
+    logits = (3 * torch.randn(N, V, device=DEV)).to(dt)
+    tgt = torch.randint(0, V, (N,), device=DEV)
+    tgt[3] = -100
+    l, lse = ops.ce_fwd(logits, tgt)
+    l0, lse0 = ref.ce_fwd(logits.cpu().float(), tgt.cpu())
+    _close(l, l0, torch.float32, 100, name="loss")
+    _close(lse, lse0, torch.float32, 100, name="lse")
+    scale = torch.tensor([0.5], device=DEV)
+    g = ops.ce_bwd_(logits.clone(), tgt, lse, scale)
+    g0 = ref.ce_bwd_(logits.cpu().float().clone(), tgt.cpu(), lse0, scale.cpu())
+    _close(g, g0, dt, 2, name="dlogits")
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+@pytest.mark.parametrize("pos", [False, True])
+def test_embedding(dt, pos):
+    V, d, B, T = 300, 64, 3, 16
+    wte = torch.randn(V, d, device=DEV).to(dt)
+    wpe = torch.randn(T, d, device=DEV).to(dt) if pos else None
+    idx = torch.randint(0, 40, (B * T,), device=DEV)  # many duplicates
+    x = ops.embedding_fwd(idx, wte, wpe, T)
+    x0 = ref.embedding_fwd(idx.cpu(), wte.cpu().float(), None if wpe is None else wpe.cpu().float(), T)
+    _close(x, x0, dt, name="emb fwd")
+    dx = torch.randn(B * T, d, device=DEV).to(dt)
+    g = torch.full((V, d), 7.0, device=DEV, dtype=dt)
+    gp = torch.zeros(T, d, device=DEV, dtype=dt) if pos else None
+    ops.embedding_bwd(idx, dx, g, gp, T, accumulate=False)
+    g0 = torch.zeros(V, d)
+    gp0 = torch.zeros(T, d) if pos else None
+    ref.embedding_bwd(idx.cpu(), dx.cpu().float(), g0, gp0, T)
+    _close(g, g0, dt, 4, name="emb dW")
+    if pos:
+        _close(gp, gp0, dt, 4, name="pos dW")
+
+
+@pytest.mark.parametrize("pdt", [torch.bfloat16, torch.float32])
+def test_adamw_and_norm(pdt):
+    n = 4099
+    p32 = torch.randn(n, device=DEV)
+    g = torch.randn(n, device=DEV).to(pdt)
+    m = torch.randn(n, device=DEV).abs() * 0.1
+    v = torch.randn(n, device=DEV).abs() * 0.1
+    scale = torch.tensor([0.7], device=DEV)
+    master = p32.clone() if pdt != torch.float32 else None
+    param = p32.to(pdt)
+    args = dict(lr=1e-3, beta1=0.9, beta2=0.999, eps=1e-8, weight_decay=0.1, step=3)
+    refs = [t.cpu().clone() if t is not None else None for t in (param, master, g, m, v)]
+    ops.adamw_step_(param, master, g, m, v, grad_scale=scale, **args)
+    ref.adamw_step_(refs[0], refs[1], refs[2], refs[3], refs[4], grad_scale=scale.cpu(), **args)
+    _close(m, refs[3], torch.float32, 10, name="m")
+    _close(v, refs[4], torch.float32, 10, name="v")
+    if master is not None:
+        _close(master, refs[1], torch.float32, 10, name="master")
+    _close(param, refs[0], pdt, name="param")
+    ts = [torch.randn(1000, device=DEV).to(pdt), torch.randn(37, device=DEV), torch.randn(100003, device=DEV).to(pdt)]
+    sq = ops.sq_norm_multi(ts)
+    sq0 = sum(t.float().pow(2).sum() for t in ts)
+    assert math.isclose(sq.item(), sq0.item(), rel_tol=1e-4)
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("B,T,H,G,hd", [(2, 64, 4, 4, 64), (1, 200, 8, 2, 128), (2, 33, 4, 2, 64),
+                                         (1, 10, 16, 8, 2), (2, 256, 4, 1, 128)])
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_flash_attention(dt, B, T, H, G, hd, p):
+    qkv = torch.randn(B * T, (H + 2 * G) * hd, device=DEV).to(dt)
+    do = torch.randn(B * T, H * hd, device=DEV).to(dt)
+    o, lse = ops.flash_attn_fwd(qkv, B, T, H, G, hd, True, p, 99, 12345)
+    o0, lse0 = ref.flash_attn_fwd(qkv.cpu().float(), B, T, H, G, hd, True, p, 99, 12345)
+    _close(o, o0, dt, 2, name="o")
+    _close(lse, lse0, torch.float32, 1000, name="lse")
+    dqkv = ops.flash_attn_bwd(qkv, o, lse, do, B, T, H, G, hd, True, p, 99, 12345)
+    dqkv0 = ref.flash_attn_bwd(qkv.cpu().float(), o0, lse0, do.cpu().float(), B, T, H, G, hd, True, p, 99, 12345)
+    _close(dqkv, dqkv0, dt, 4, name="dqkv")
