@@ -1,0 +1,38 @@
+"""Distributed engines (one process per GPU, RCCL over xGMI via torch.distributed "nccl").
+
+* ``local``  — single process (no collectives).
+* ``ddp``    — replicated params, bucketed gradient all-reduce overlapped with backward
+               (reference: torch DDP, build_components.py:176).
+* ``zero1``  — DDP + optimizer-state sharding: reduce-scatter grads, shard-local AdamW,
+               all-gather params (reference: ZeroRedundancyOptimizer, :250-256).
+* ``fsdp``   — full sharding of params / grads / optimizer state per unit with prefetched
+               all-gathers and reduce-scatters on a comm stream (reference: FSDP FULL_SHARD,
+               :155-174).
+"""
+from __future__ import annotations
+
+import torch
+
+from ..models.base import LocalEngine
+
+
+def setup_engine(model, kind: str = "local", device=None, reduce_dtype=None, bucket_mb: float = 256.0,
+                 reshard_after_forward: bool = True, process_group=None):
+    """Flatten ``model`` onto ``device`` and attach the requested engine; returns it."""
+    device = torch.device(device) if device is not None else model.device
+    if kind in ("local", "single", "single_gpu"):
+        model.flatten(device=device)
+        eng = LocalEngine()
+        model.set_engine(eng)
+        return eng
+    if kind == "ddp":
+        from .ddp import DDPEngine
+        return DDPEngine(model, device, reduce_dtype=reduce_dtype, bucket_mb=bucket_mb, pg=process_group)
+    if kind == "zero1":
+        from .zero import ZeroEngine
+        return ZeroEngine(model, device, reduce_dtype=reduce_dtype, pg=process_group)
+    if kind == "fsdp":
+        from .fsdp import FSDPEngine
+        return FSDPEngine(model, device, reduce_dtype=reduce_dtype,
+                          reshard_after_forward=reshard_after_forward, pg=process_group)
+    raise ValueError(f"unknown parallel engine '{kind}'")

@@ -34,8 +34,9 @@ bool attn_supported_head_dim(int hd);
 void attn_fwd(DType dt, const void* qkv, void* o, float* lse, int B, int T, int H, int G, int hd, bool causal,
               float p, uint64_t seed, uint64_t offset, hipStream_t s);
 void attn_bwd(DType dt, const void* qkv, const void* o, const float* lse, const void* dout, void* dqkv, float* delta,
-              float* dq_acc, int B, int T, int H, int G, int hd, bool causal, float p, uint64_t seed, uint64_t offset,
-              hipStream_t s);
+              float* dq_acc, float* dkv_part, int B, int T, int H, int G, int hd, bool causal, float p, uint64_t seed,
+              uint64_t offset, hipStream_t s);
+bool attn_mfma_head_dim(int hd);
 void attn_fwd_naive(DType dt, const void* qkv, void* o, float* lse, int B, int T, int H, int G, int hd, bool causal,
                     float p, uint64_t seed, uint64_t offset, hipStream_t s);
 void attn_bwd_naive(DType dt, const void* qkv, const void* o, const float* lse, const void* dout, void* dqkv,

@@ -4,12 +4,11 @@
 
 namespace bllm {
 
-bool attn_mfma_head_dim(int hd);
 void attn_fwd_mfma(DType dt, const void* qkv, void* o, float* lse, int B, int T, int H, int G, int hd, bool causal,
                    float p, uint64_t seed, uint64_t offset, hipStream_t s);
 void attn_bwd_mfma(DType dt, const void* qkv, const void* o, const float* lse, const void* dout, void* dqkv,
-                   float* delta, float* dq_acc, int B, int T, int H, int G, int hd, bool causal, float p,
-                   uint64_t seed, uint64_t offset, hipStream_t s);
+                   float* delta, float* dq_acc, float* dkv_part, int B, int T, int H, int G, int hd, bool causal,
+                   float p, uint64_t seed, uint64_t offset, hipStream_t s);
 
 bool attn_supported_head_dim(int hd) { return hd > 0 && hd <= 256; }
 
@@ -22,10 +21,10 @@ void attn_fwd(DType dt, const void* qkv, void* o, float* lse, int B, int T, int 
 }
 
 void attn_bwd(DType dt, const void* qkv, const void* o, const float* lse, const void* dout, void* dqkv, float* delta,
-              float* dq_acc, int B, int T, int H, int G, int hd, bool causal, float p, uint64_t seed, uint64_t offset,
-              hipStream_t s) {
+              float* dq_acc, float* dkv_part, int B, int T, int H, int G, int hd, bool causal, float p, uint64_t seed,
+              uint64_t offset, hipStream_t s) {
   if (attn_mfma_head_dim(hd))
-    attn_bwd_mfma(dt, qkv, o, lse, dout, dqkv, delta, dq_acc, B, T, H, G, hd, causal, p, seed, offset, s);
+    attn_bwd_mfma(dt, qkv, o, lse, dout, dqkv, delta, dq_acc, dkv_part, B, T, H, G, hd, causal, p, seed, offset, s);
   else
     attn_bwd_naive(dt, qkv, o, lse, dout, dqkv, delta, B, T, H, G, hd, causal, p, seed, offset, s);
 }

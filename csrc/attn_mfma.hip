@@ -266,11 +266,4 @@ void attn_fwd_mfma(DType dt, const void* qkv, void* o, float* lse, int B, int T_
 #undef LAUNCH
 }
 
-// Backward: MFMA kernels land in attn_bwd_mfma.hip; until then the scalar kernels serve.
-void attn_bwd_mfma(DType dt, const void* qkv, const void* o, const float* lse, const void* dout, void* dqkv,
-                   float* delta, float* dq_acc, int B, int T_, int H, int G, int hd, bool causal, float p,
-                   uint64_t seed, uint64_t offset, hipStream_t s) {
-  attn_bwd_naive(dt, qkv, o, lse, dout, dqkv, delta, B, T_, H, G, hd, causal, p, seed, offset, s);
-}
-
 }  // namespace bllm
