@@ -1,0 +1,97 @@
+"""Component builder (reference build_components.py:50-323).
+
+build_config -> build_model (weights, LoRA, engine: local / DDP / ZeRO-1 / FSDP) ->
+build_optimizer (fused AdamW, wd 0.1; sharded slots under ZeRO-1 / FSDP) -> build_tokenizer.
+
+Differences: errors propagate instead of ``return None``; GPT-2 honours
+``--data_type``; Llama-2 builds (theta 10000, eos ``</s>``/2, activation checkpointing);
+``--mixed_precision`` maps to the FSDP compute/reduce dtype with fp32 master weights
+(the reference's import of non-existent ``fpSixteen``/``bfSixteen`` is defect 2).
+"""
+from __future__ import annotations
+
+import torch
+
+from .config import datatype_mapping, debug_config, get_config
+from .data.tokenizer import build_tokenizer as _build_tokenizer
+from .logger import setup_logger
+from .models import build_model as _build_model
+from .models.lora import replace_linear_with_lora
+from .models.weights import load_pretrained
+from .parallel import setup_engine
+from .train.optim import FusedAdamW
+from .utils import misc
+
+logger = setup_logger("build_components")
+
+
+def compute_dtype(args) -> torch.dtype:
+    if getattr(args, "mixed_precision", None):
+        return datatype_mapping[args.mixed_precision]
+    return datatype_mapping[args.data_type]
+
+
+def build_config(args):
+    cfg = get_config(args.model, args.num_params, context_length=getattr(args, "context_length", 1024) or 1024)
+    cfg = cfg.replace(dtype=compute_dtype(args))
+    if args.load_weights and args.model == "GPT2":
+        cfg = cfg.replace(qkv_bias=True)
+    if args.debug:
+        cfg = debug_config(cfg)
+    return cfg
+
+
+def engine_kind(args) -> str:
+    if args.run_type != "multi_gpu":
+        return "local"
+    if args.use_fsdp:
+        return "fsdp"
+    if args.use_zero_opt:
+        return "zero1"
+    return "ddp"
+
+
+def build_model(config, rank, device, args):
+    misc.start_memory_tracking()
+    ckpt = getattr(args, "actv_ckpt_mode", None) or ("full" if args.use_actv_ckpt else "none")
+    model = _build_model(config, use_actv_ckpt=ckpt, device=device)
+    if rank == 0:
+        logger.info(f"Total parameters: {misc.get_num_params(model):,}")
+        misc.model_memory_size(model, config.dtype)
+    if args.load_weights:
+        path = load_pretrained(model, args.model, args.num_params, getattr(args, "weights_path", None))
+        if rank == 0:
+            logger.info(f"Loaded pretrained weights from {path}")
+    if args.use_lora:
+        for p in model.parameters():
+            p.requires_grad = False
+        replace_linear_with_lora(model, rank=args.lora_rank, alpha=args.lora_alpha, dtype=config.dtype)
+        if rank == 0:
+            n = sum(p.numel() for p in model.parameters() if p.requires_grad)
+            logger.info(f"Total trainable LoRA parameters: {n:,}")
+    reduce = None
+    if getattr(args, "mixed_precision", None):
+        reduce = datatype_mapping[args.mixed_precision]
+    engine = setup_engine(model, engine_kind(args), device=device, reduce_dtype=reduce,
+                          reshard_after_forward=not getattr(args, "no_reshard_after_forward", False),
+                          bucket_mb=getattr(args, "bucket_mb", 256.0))
+    if rank == 0:
+        misc.print_memory_usage()
+    return model, engine
+
+
+def build_optimizer(args, model, engine):
+    return FusedAdamW(model, lr=args.lr, weight_decay=0.1, engine=engine)
+
+
+def build_tokenizer(rank, args, config):
+    return _build_tokenizer(args.model, config, getattr(args, "tokenizer_path", None))
+
+
+def build_components(rank: int, device, args):
+    """Returns (config, model, optimizer, tokenizer, engine)."""
+    config = build_config(args)
+    model, engine = build_model(config, rank, device, args)
+    optimizer = build_optimizer(args, model, engine)
+    tokenizer = build_tokenizer(rank, args, config)
+    return config, model, optimizer, tokenizer, engine

@@ -241,16 +241,20 @@ class BaseLM(nn.Module):
         return self._comps
 
     # -- flat storage ------------------------------------------------------------------
-    def flatten(self, device=None, dtype=None, pad_to: int = 1, grad_dtype=None):
+    def flatten(self, device=None, dtype=None, pad_to: int = 1, grad_dtype=None, arena=None):
         """(Re)build every unit's flat buffers from the current parameters (call after
-        LoRA replacement / weight loading; idempotent)."""
+        LoRA replacement / weight loading; idempotent).  ``arena`` (optional) maps a unit
+        index to ``(param_view, grad_view)`` slices of model-wide contiguous buffers that the
+        trainable flat must live in (DDP / ZeRO buckets)."""
         p0 = next(self.parameters())
         device = torch.device(device) if device is not None else p0.device
         dtype = dtype or p0.dtype
         comps = self.build_computes()
         for i, c in enumerate(comps):
             u = FlatUnit(c.name, i)
-            u.flatten(c.layout(), device, dtype, pad_to=pad_to, grad_dtype=grad_dtype)
+            ts, gs = (arena[i] if arena is not None and i in arena else (None, None))
+            u.flatten(c.layout(), device, dtype, pad_to=pad_to, grad_dtype=grad_dtype,
+                      train_storage=ts, train_grad_storage=gs)
             c.bind(u)
         object.__setattr__(self, "_comps", comps)
         object.__setattr__(self, "_anchor", torch.zeros((), device=device, requires_grad=True))

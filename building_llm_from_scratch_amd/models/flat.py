@@ -29,7 +29,8 @@ class FlatBuffer:
     """One contiguous buffer holding an ordered list of fused groups."""
 
     def __init__(self, groups: List[List[nn.Parameter]], dtype: torch.dtype, device,
-                 pad_to: int = 1):
+                 pad_to: int = 1, storage: Optional[torch.Tensor] = None,
+                 grad_storage: Optional[torch.Tensor] = None):
         self.groups = [g for g in groups if g]
         self.index: Dict[int, Tuple[int, torch.Size]] = {}
         off = 0
@@ -43,9 +44,24 @@ class FlatBuffer:
         self.numel = total
         self.dtype = dtype
         self.device = torch.device(device)
-        self.data = torch.zeros(total, dtype=dtype, device=device)
+        if storage is not None:
+            assert storage.numel() >= total and storage.dtype == dtype
+            self.data = storage[:total]
+        else:
+            self.data = torch.zeros(total, dtype=dtype, device=device)
         self.params: List[nn.Parameter] = [p for g in self.groups for p in g]
         self.grad: Optional[torch.Tensor] = None
+        self._grad_storage = grad_storage
+
+    @staticmethod
+    def size_of(groups: List[List[nn.Parameter]], pad_to: int = 1) -> int:
+        off = 0
+        for g in groups:
+            if not g:
+                continue
+            off = (off + ALIGN - 1) // ALIGN * ALIGN
+            off += sum(p.numel() for p in g)
+        return max((off + pad_to - 1) // pad_to * pad_to, pad_to)
 
     def view(self, buf: torch.Tensor, p: nn.Parameter) -> torch.Tensor:
         off, shape = self.index[id(p)]
@@ -73,7 +89,10 @@ class FlatBuffer:
                 p.grad = self.view(self.grad, p)
 
     def alloc_grad(self, dtype: Optional[torch.dtype] = None):
-        self.grad = torch.zeros(self.numel, dtype=dtype or self.dtype, device=self.device)
+        if self._grad_storage is not None:
+            self.grad = self._grad_storage[:self.numel]
+        else:
+            self.grad = torch.zeros(self.numel, dtype=dtype or self.dtype, device=self.device)
         for p in self.params:
             p.grad = self.view(self.grad, p)
 
@@ -92,7 +111,7 @@ class FlatUnit:
 
     # ------------------------------------------------------------------ build
     def flatten(self, layout: List[List[nn.Parameter]], device, dtype: torch.dtype, pad_to: int = 1,
-                grad_dtype: Optional[torch.dtype] = None):
+                grad_dtype: Optional[torch.dtype] = None, train_storage=None, train_grad_storage=None):
         seen = set()
         for g in layout:
             for p in g:
@@ -100,7 +119,7 @@ class FlatUnit:
                 seen.add(id(p))
         tr = [[p for p in g if p.requires_grad] for g in layout]
         fz = [[p for p in g if not p.requires_grad] for g in layout]
-        self.train = FlatBuffer(tr, dtype, device, pad_to) if any(tr) else None
+        self.train = FlatBuffer(tr, dtype, device, pad_to, train_storage, train_grad_storage) if any(tr) else None
         self.frozen = FlatBuffer(fz, dtype, device, pad_to) if any(fz) else None
         self._owner = {}
         for fb in (self.train, self.frozen):
@@ -144,3 +163,9 @@ class FlatUnit:
 
     def numel(self) -> int:
         return sum(fb.numel_used for fb in self.buffers())
+
+
+def split_layout(layout: List[List[nn.Parameter]]):
+    """(trainable groups, frozen groups) of a unit layout."""
+    return ([[p for p in g if p.requires_grad] for g in layout],
+            [[p for p in g if not p.requires_grad] for g in layout])

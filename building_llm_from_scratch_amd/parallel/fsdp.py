@@ -1,0 +1,211 @@
+"""Fully sharded data parallel (ZeRO-3) over units.
+
+Reference: ``FSDP(model, auto_wrap_policy=ModuleWrapPolicy({nn.Embedding, GPT2 TransformerBlock}),
+FULL_SHARD, BACKWARD_PRE, mixed_precision=<policy>)`` (build_components.py:155-174) — which
+for Llama wraps only the embedding, leaving the whole block stack in one root unit (SURVEY
+§2.8 defect 3), and crashes at import (defect 2).
+
+Here every unit (embedding, each transformer block, final norm + head) is an FSDP unit for
+every model family:
+  * each unit's flat buffers (trainable and frozen) are padded to a multiple of world size;
+    a rank keeps only its 1/world shard persistently (compute dtype) plus the optimizer's
+    fp32 master / moments for that shard;
+  * forward: ``all_gather_into_tensor`` of unit i+1 is issued asynchronously (RCCL's own HIP
+    stream) while unit i computes (prefetch); after its forward a unit is resharded (storage
+    freed) unless ``reshard_after_forward=False`` (ZeRO-2 style: keep until backward);
+  * backward: the gather of unit i-1 is prefetched while unit i runs its backward; unit i's
+    full gradient is reduce-scattered asynchronously into its gradient shard and freed;
+  * gradient clipping: shard-local sum of squares + one scalar all-reduce;
+  * checkpoint: full state dict gathered unit by unit to rank 0 with the reference key names.
+Mixed precision: the flats hold the compute dtype (``--mixed_precision`` or ``--data_type``),
+gradients are reduced in that dtype (reference bf16 policy), master weights stay fp32.
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional
+
+import torch
+import torch.distributed as dist
+
+from ..models.base import LocalEngine
+from ..models.flat import ALIGN
+from ..train.optim import OptSlot
+
+
+def _free(t: torch.Tensor):
+    st = t.untyped_storage()
+    if st.size() > 0:
+        st.resize_(0)
+
+
+def _alloc(t: torch.Tensor, nbytes: int):
+    st = t.untyped_storage()
+    if st.size() != nbytes:
+        st.resize_(nbytes)
+
+
+class FSDPEngine(LocalEngine):
+    def __init__(self, model, device, reduce_dtype: Optional[torch.dtype] = None,
+                 reshard_after_forward: bool = True, pg=None):
+        self.pg = pg
+        self.world_size = dist.get_world_size(pg)
+        self.rank = dist.get_rank(pg)
+        self.model = model
+        self.device = torch.device(device)
+        self.reshard_after_forward = reshard_after_forward
+        self.grad_prescale = 1.0 / self.world_size
+        self.is_cuda = self.device.type == "cuda"
+        dtype = next(model.parameters()).dtype
+        model.flatten(device=device, dtype=dtype, pad_to=self.world_size * ALIGN)
+        self.units = model.units
+        W, r = self.world_size, self.rank
+        for u in self.units:
+            st = u.state
+            st["bufs"] = []
+            for fb in u.buffers():
+                dist.broadcast(fb.data, src=0, group=pg)          # identical init on every rank
+                n = fb.numel // W
+                fb.shard = fb.data[r * n:(r + 1) * n].clone()
+                fb.nbytes = fb.data.untyped_storage().size()
+                if fb is u.train:
+                    fb.grad_shard = torch.zeros(n, dtype=fb.grad.dtype, device=device)
+                    fb.grad_nbytes = fb.grad.untyped_storage().size()
+                    fb.gaps = self._gaps(fb)
+                    _free(fb.grad)
+                _free(fb.data)
+                st["bufs"].append(fb)
+            st["gathered"] = False
+            st["gather_work"] = None
+        self._rs_works: List = []
+        self._in_backward = False
+        model.set_engine(self)
+
+    @staticmethod
+    def _gaps(fb):
+        """Element ranges of the flat NOT covered by parameters (alignment + tail padding):
+        zeroed after each full-gradient allocation so padding never carries garbage."""
+        spans = sorted((off, off + shape.numel()) for off, shape in fb.index.values())
+        gaps, cur = [], 0
+        for s, e in spans:
+            if s > cur:
+                gaps.append((cur, s))
+            cur = max(cur, e)
+        if cur < fb.numel:
+            gaps.append((cur, fb.numel))
+        return gaps
+
+    # ------------------------------------------------------------------ gather / reshard
+    def _issue_gather(self, u, async_op: bool):
+        st = u.state
+        if st["gathered"] or st["gather_work"] is not None:
+            return
+        works = []
+        for fb in st["bufs"]:
+            _alloc(fb.data, fb.nbytes)
+            works.append(dist.all_gather_into_tensor(fb.data, fb.shard, group=self.pg, async_op=async_op))
+        if async_op:
+            st["gather_work"] = works
+        else:
+            st["gathered"] = True
+
+    def _wait_gather(self, u):
+        st = u.state
+        if st["gather_work"] is not None:
+            for w in st["gather_work"]:
+                w.wait()
+            st["gather_work"] = None
+            st["gathered"] = True
+        if not st["gathered"]:
+            self._issue_gather(u, async_op=False)
+
+    def _reshard(self, u):
+        st = u.state
+        if st["gather_work"] is not None:
+            self._wait_gather(u)
+        for fb in st["bufs"]:
+            _free(fb.data)
+        st["gathered"] = False
+
+    # ------------------------------------------------------------------ hooks
+    def pre_forward(self, unit):
+        self._wait_gather(unit)
+        nxt = unit.index + 1
+        if nxt < len(self.units):
+            self._issue_gather(self.units[nxt], async_op=True)
+
+    def post_forward(self, unit):
+        last = unit.index == len(self.units) - 1
+        training = torch.is_grad_enabled() and self.model.training
+        if not training:
+            if not last or True:
+                self._reshard(unit)
+            return
+        if self.reshard_after_forward and not last:
+            self._reshard(unit)
+
+    def pre_backward(self, unit):
+        if not self._in_backward:
+            self._in_backward = True
+            self._rs_works = []
+        self._wait_gather(unit)
+        prv = unit.index - 1
+        if prv >= 0:
+            self._issue_gather(self.units[prv], async_op=True)
+        fb = unit.train
+        if fb is not None:
+            _alloc(fb.grad, fb.grad_nbytes)
+            for s, e in fb.gaps:
+                fb.grad[s:e].zero_()
+
+    def post_backward(self, unit):
+        fb = unit.train
+        if fb is not None:
+            w = dist.reduce_scatter_tensor(fb.grad_shard, fb.grad, group=self.pg, async_op=True)
+            if self.is_cuda:
+                # RCCL records fb.grad on its stream: releasing the storage now is stream-safe
+                self._rs_works.append((w, None))
+                _free(fb.grad)
+            else:
+                self._rs_works.append((w, fb))
+        self._reshard(unit)
+
+    def finish_backward(self):
+        for w, fb in self._rs_works:
+            w.wait()
+            if fb is not None:
+                _free(fb.grad)
+        self._rs_works = []
+        self._in_backward = False
+
+    # ------------------------------------------------------------------ optimizer
+    def optimizer_slots(self, model):
+        return [OptSlot(u.train.shard, u.train.grad_shard, u.name) for u in self.units if u.train is not None]
+
+    def all_reduce_grad_sq_norm(self, sq: torch.Tensor) -> torch.Tensor:
+        dist.all_reduce(sq, group=self.pg)
+        return sq
+
+    # ------------------------------------------------------------------ checkpoint
+    def full_state_dict(self) -> Optional[Dict[str, torch.Tensor]]:
+        """Gather unit by unit; rank 0 receives the reference-named CPU state dict."""
+        names = {id(p): n for n, p in self.model.named_parameters()}
+        sd: Dict[str, torch.Tensor] = {}
+        was_gathered = [u.state["gathered"] for u in self.units]
+        for u in self.units:
+            self._wait_gather(u)
+            if self.rank == 0:
+                for fb in u.state["bufs"]:
+                    for p in fb.params:
+                        sd[names[id(p)]] = fb.view(fb.data, p).detach().cpu().clone()
+            self._reshard(u)
+        for u, g in zip(self.units, was_gathered):
+            if g:
+                self._issue_gather(u, async_op=False)
+        if self.rank != 0:
+            return None
+        ordered = {k: sd[k] for k in (n for n, _ in self.model.named_parameters()) if k in sd}
+        for hook in self.model._state_dict_hooks.values():
+            r = hook(self.model, ordered, "", None)
+            if r is not None:
+                ordered = r
+        return ordered

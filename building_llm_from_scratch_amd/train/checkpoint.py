@@ -1,0 +1,76 @@
+"""Checkpoints with the reference's layout + optional resume state.
+
+* ``model_pg_{step}.pth`` / ``model_pg_{step}_interrupted.pth`` / ``model_pg_final.pth``:
+  ``torch.save`` of a plain, prefix-free ``state_dict`` (reference train.py:231-257) —
+  identical key names (incl. the ``att.mask|cos|sin`` buffers and fp32 RMSNorm weights).
+  Rank 0 writes; under FSDP the full state dict is gathered unit by unit to rank 0.
+* Extension (off unless ``--resume`` / ``save_resume_state``): ``trainer_state_{step}.pt``
+  with optimizer state (fp32 master, exp_avg, exp_avg_sq per flat slot), step, LR, RNG and
+  loss history.  The reference has no resume path at all.
+"""
+from __future__ import annotations
+
+import os
+import random
+from pathlib import Path
+from typing import Optional
+
+import numpy as np
+import torch
+
+
+def model_state_dict(model, engine=None) -> Optional[dict]:
+    """Full, unwrapped state dict on CPU (rank 0 only gets a dict under FSDP)."""
+    if engine is not None and hasattr(engine, "full_state_dict"):
+        return engine.full_state_dict()
+    return {k: v.detach().to("cpu") for k, v in model.state_dict().items()}
+
+
+def save_model(model, path, engine=None, rank: int = 0):
+    sd = model_state_dict(model, engine)
+    if rank == 0 and sd is not None:
+        tmp = str(path) + ".tmp"
+        torch.save(sd, tmp)
+        os.replace(tmp, path)
+
+
+def load_model(model, path, strict: bool = True):
+    sd = torch.load(path, map_location="cpu", weights_only=True)
+    return model.load_state_dict(sd, strict=strict)
+
+
+def save_resume_state(path, optimizer, trainer_state: dict, rank: int = 0, world: int = 1):
+    """Per-rank file (optimizer slots are rank-local under ZeRO / FSDP)."""
+    st = {
+        "trainer": trainer_state,
+        "optim": [{k: (v.detach().cpu() if torch.is_tensor(v) else v) for k, v in optimizer.state[s.param].items()}
+                  for s in optimizer.slots],
+        "lr": optimizer.param_groups[0]["lr"],
+        "rng": {"torch": torch.get_rng_state(), "numpy": np.random.get_state(), "python": random.getstate()},
+        "world": world,
+    }
+    p = Path(path)
+    if world > 1:
+        p = p.with_name(p.stem + f".rank{rank}" + p.suffix)
+    torch.save(st, p)
+
+
+def load_resume_state(path, optimizer, rank: int = 0, world: int = 1) -> dict:
+    p = Path(path)
+    if world > 1:
+        p = p.with_name(p.stem + f".rank{rank}" + p.suffix)
+    st = torch.load(p, map_location="cpu", weights_only=False)  # file written by this framework
+    assert st["world"] == world, "resume requires the same world size"
+    for s, saved in zip(optimizer.slots, st["optim"]):
+        cur = optimizer.state[s.param]
+        for k, v in saved.items():
+            if torch.is_tensor(v):
+                cur[k].copy_(v.to(cur[k].device))
+            else:
+                cur[k] = v
+        if "master" in cur:
+            s.param.reshape(-1).copy_(cur["master"].to(s.param.dtype))
+    torch.set_rng_state(st["rng"]["torch"])
+    np.random.set_state(st["rng"]["numpy"])
+    random.setstate(st["rng"]["python"])
+    return st["trainer"]

@@ -53,6 +53,9 @@ class FusedAdamW(torch.optim.Optimizer):
                 st["master"] = s.param.detach().reshape(-1).float().clone()
         self._gscale: Optional[torch.Tensor] = None
         self.last_grad_norm: Optional[torch.Tensor] = None
+        # data-parallel engines reduce with SUM; the 1/world average is folded in here
+        self.grad_prescale = float(getattr(self.engine, "grad_prescale", 1.0))
+        self._prescale_t: Optional[torch.Tensor] = None
 
     # torch's zero_grad would try to walk p.grad of the slot tensors; the unit backward
     # OVERWRITES the flat gradients every step (accumulation is explicit), so this is a no-op
@@ -68,11 +71,16 @@ class FusedAdamW(torch.optim.Optimizer):
     def clip_grad_norm_(self, max_norm: float = 1.0, extra_scale: Optional[torch.Tensor] = None) -> torch.Tensor:
         """Global L2 norm; sets the on-device multiplier min(1, max_norm/(norm+1e-6))."""
         sq = self.grad_sq_norm()
+        scale = None
+        if self.grad_prescale != 1.0:
+            scale = torch.full((1,), self.grad_prescale, dtype=torch.float32, device=sq.device)
         if extra_scale is not None:  # gradients carry a loss scale: norm of the unscaled grads
-            sq = sq * extra_scale.float() ** 2
+            scale = extra_scale.float() if scale is None else scale * extra_scale.float()
+        if scale is not None:
+            sq = sq * scale ** 2
         norm = sq.sqrt()
         coef = torch.clamp(max_norm / (norm + 1e-6), max=1.0)
-        self._gscale = coef if extra_scale is None else coef * extra_scale.float()
+        self._gscale = coef if scale is None else coef * scale
         self.last_grad_norm = norm
         return norm
 
@@ -80,6 +88,11 @@ class FusedAdamW(torch.optim.Optimizer):
     def step(self, closure=None):
         g = self.param_groups[0]
         lr, (b1, b2), eps, wd = g["lr"], g["betas"], g["eps"], g["weight_decay"]
+        if self._gscale is None and self.grad_prescale != 1.0:
+            if self._prescale_t is None:
+                self._prescale_t = torch.full((1,), self.grad_prescale, dtype=torch.float32,
+                                              device=self.slots[0].param.device)
+            self._gscale = self._prescale_t
         for s in self.slots:
             st = self.state[s.param]
             st["step"] += 1

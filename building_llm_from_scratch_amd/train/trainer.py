@@ -1,0 +1,287 @@
+"""Training runtime (reference train.py:43-276).
+
+Kept from the reference: constructor signature, ``train_model`` / ``finetune_model`` /
+``train_epoch`` / ``train_batch`` / ``evaluate_model`` / ``calc_loss_loader`` /
+``generate_and_print_sample`` / ``save_checkpoint``; linear warm-up ``initial_lr -> lr`` over
+``warmup_steps`` then cosine to ``min_lr`` over the whole run (train.py:99-107); eval every
+``eval_freq`` steps on ``eval_iter`` batches; a sample every ``print_sample_iter`` steps
+("Every effort moves you", top-k 5, temperature 1, 200 tokens); ``model_pg_{step}.pth`` every
+``save_ckpt_freq`` steps incl. step 0; ``model_pg_{step}_interrupted.pth`` on Ctrl-C; the same
+log line format; returned (train_losses, val_losses, tokens_seen, lrs).
+
+Changed on purpose: exceptions propagate (no log-and-continue), ``calc_loss_loader``
+stops after ``num_batches`` (defect 8), logged losses / tokens are all-reduced across ranks
+(defect 12), plus a tokens/s metric, JSONL metrics, fp16 dynamic loss scaling, a non-finite
+loss guard, optional ``max_steps`` and resume state.
+"""
+from __future__ import annotations
+
+import math
+import time
+from pathlib import Path
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+from ..logger import MetricsWriter, setup_logger
+from ..utils.misc import read_json_file, read_text_file, text_to_token_ids, token_ids_to_text
+from .checkpoint import save_model, save_resume_state
+from .generate import generate
+
+logger = setup_logger("train")
+
+ALPACA_CONTEXT = ("Below is an instruction that describes a task. Write a response that appropriately "
+                  "completes the request.\n\n### Instruction:\nWhat is an antonym of 'complicated'?")
+
+
+class DynamicLossScaler:
+    """fp16 loss scaling: grow x2 every ``interval`` clean steps, halve and skip on overflow."""
+
+    def __init__(self, init_scale=2.0 ** 16, interval=1000):
+        self.scale = float(init_scale)
+        self.interval = interval
+        self.clean = 0
+
+    def update(self, overflow: bool) -> bool:
+        if overflow:
+            self.scale = max(self.scale / 2.0, 1.0)
+            self.clean = 0
+            return False
+        self.clean += 1
+        if self.clean % self.interval == 0:
+            self.scale *= 2.0
+        return True
+
+
+class Trainer:
+    def __init__(self, model, optimizer, config, data_files, loaderObj, save_dir, warmup_steps=10,
+                 initial_lr=1e-5, min_lr=1e-6, device="cpu", rank=0, eval_freq=1, save_ckpt_freq=1,
+                 print_sample_iter=1, eval_iter=1, engine=None, max_grad_norm=1.0, metrics_file=None,
+                 loss_scaler: Optional[DynamicLossScaler] = None, max_steps: Optional[int] = None,
+                 sample_tokens: int = 200, save_resume: bool = False, world_size: int = 1):
+        self.config = config
+        self.model = model
+        self.optimizer = optimizer
+        self.data_files = data_files
+        self.loaderObj = loaderObj
+        self.save_dir = Path(save_dir)
+        self.device = device
+        self.rank = rank
+        self.world_size = world_size
+        self.engine = engine
+        self.warmup_steps = warmup_steps
+        self.initial_lr = initial_lr
+        self.min_lr = min_lr
+        self.eval_freq = eval_freq
+        self.save_ckpt_freq = save_ckpt_freq
+        self.print_sample_iter = print_sample_iter
+        self.eval_iter = eval_iter
+        self.max_grad_norm = max_grad_norm
+        self.loss_scaler = loss_scaler
+        self.max_steps = max_steps
+        self.sample_tokens = sample_tokens
+        self.save_resume = save_resume
+        self.global_step = -1
+        self.tokens_seen = 0
+        self.train_losses, self.val_losses, self.track_lrs, self.track_tokens_seen = [], [], [], []
+        self.metrics = MetricsWriter(metrics_file if rank == 0 else None)
+        self._t_last = None
+        self._tok_last = 0
+        self.peak_lr = optimizer.param_groups[0]["lr"]
+        self.total_training_steps = 1
+        self.lr_increment = 0.0
+        self.stop = False
+
+    # ------------------------------------------------------------------ helpers
+    def _dist(self) -> bool:
+        return self.world_size > 1 and dist.is_available() and dist.is_initialized()
+
+    def _allreduce_mean(self, x: float) -> float:
+        if not self._dist():
+            return x
+        t = torch.tensor([x], dtype=torch.float64, device=self.device)
+        dist.all_reduce(t)
+        return t.item() / self.world_size
+
+    def lr_at(self, step: int) -> float:
+        if step < self.warmup_steps:
+            return self.initial_lr + step * self.lr_increment
+        denom = max(1, self.total_training_steps - self.warmup_steps)
+        progress = min(1.0, (step - self.warmup_steps) / denom)
+        return self.min_lr + (self.peak_lr - self.min_lr) * 0.5 * (1 + math.cos(math.pi * progress))
+
+    # ------------------------------------------------------------------ steps
+    def calc_loss_batch(self, input_batch, target_batch):
+        input_batch = input_batch.to(self.device, non_blocking=True)
+        target_batch = target_batch.to(self.device, non_blocking=True)
+        return self.model(input_batch, target_batch)
+
+    def train_batch(self, input_batch, target_batch):
+        self.optimizer.zero_grad()
+        self.global_step += 1
+        lr = self.lr_at(self.global_step)
+        for g in self.optimizer.param_groups:
+            g["lr"] = lr
+        self.track_lrs.append(lr)
+        loss = self.calc_loss_batch(input_batch, target_batch)
+        if self.loss_scaler is not None:
+            (loss * self.loss_scaler.scale).backward()
+            inv = torch.tensor([1.0 / self.loss_scaler.scale], device=self.device)
+            norm = self.optimizer.clip_grad_norm_(self.max_grad_norm, extra_scale=inv)
+            overflow = not bool(torch.isfinite(norm).item())
+            if self.loss_scaler.update(overflow):
+                self.optimizer.step()
+            elif self.rank == 0:
+                logger.warning(f"fp16 overflow at step {self.global_step}; loss scale -> {self.loss_scaler.scale}")
+        else:
+            loss.backward()
+            self.optimizer.clip_grad_norm_(self.max_grad_norm)
+            self.optimizer.step()
+        self.tokens_seen += input_batch.numel() * self.world_size
+        return loss
+
+    def train_epoch(self, epoch_no, train_loader, val_loader, start_context="Every effort moves you"):
+        self.model.train()
+        for input_batch, target_batch in train_loader:
+            loss = self.train_batch(input_batch, target_batch)
+            if self.global_step % self.eval_freq == 0:
+                lv = float(loss.item())
+                if not math.isfinite(lv):
+                    raise FloatingPointError(f"non-finite training loss at step {self.global_step}")
+                train_loss, val_loss = self.evaluate_model(train_loader, val_loader, self.eval_iter)
+                self.train_losses.append(train_loss)
+                self.val_losses.append(val_loss)
+                self.track_tokens_seen.append(self.tokens_seen)
+                now = time.perf_counter()
+                tps = None
+                if self._t_last is not None:
+                    tps = (self.tokens_seen - self._tok_last) / max(now - self._t_last, 1e-9)
+                self._t_last, self._tok_last = now, self.tokens_seen
+                if self.rank == 0:
+                    logger.info(f"Epoch {epoch_no + 1} | Step {self.global_step} "
+                                f"| Train Loss: {train_loss:.3f} | Val Loss: {val_loss:.3f}"
+                                + (f" | {tps:,.0f} tok/s" if tps else ""))
+                    self.metrics.write(step=self.global_step, epoch=epoch_no, train_loss=train_loss,
+                                       val_loss=val_loss, lr=self.track_lrs[-1], tokens_seen=self.tokens_seen,
+                                       tokens_per_s=tps, batch_loss=lv,
+                                       max_mem_gb=(torch.cuda.max_memory_allocated() / 1e9
+                                                   if torch.cuda.is_available() else None))
+            if self.print_sample_iter and self.global_step % self.print_sample_iter == 0:
+                self.generate_and_print_sample(start_context)
+            if self.save_ckpt_freq and self.global_step % self.save_ckpt_freq == 0:
+                self.save_checkpoint(f"model_pg_{self.global_step}.pth")
+            if self.max_steps is not None and self.global_step + 1 >= self.max_steps:
+                self.stop = True
+                return
+
+    def _setup_schedule(self, n_epochs):
+        self.peak_lr = self.optimizer.param_groups[0]["lr"]
+        self.total_training_steps = max(1, self.loaderObj.get_total_steps_epoch(self.data_files) * n_epochs)
+        if self.max_steps is not None:
+            self.total_training_steps = min(self.total_training_steps, self.max_steps)
+        self.lr_increment = (self.peak_lr - self.initial_lr) / max(1, self.warmup_steps)
+
+    def _progress(self, total):
+        if self.rank != 0:
+            return None
+        try:
+            from tqdm import tqdm
+            return tqdm(total=total)
+        except Exception:  # pragma: no cover
+            return None
+
+    def train_model(self, n_epochs):
+        self._setup_schedule(n_epochs)
+        pbar = self._progress(n_epochs * len(self.data_files))
+        try:
+            for epoch in range(n_epochs):
+                for fp in self.data_files:
+                    raw = read_text_file(fp) + " " + self.config["eos_text"] + " "
+                    train_loader, val_loader = self.loaderObj.create_dataloaders(raw, num_workers=0)
+                    if hasattr(train_loader.sampler, "set_epoch"):
+                        train_loader.sampler.set_epoch(epoch)
+                    self.train_epoch(epoch, train_loader, val_loader)
+                    if pbar is not None:
+                        pbar.update(1)
+                    if self.stop:
+                        return self._results()
+        except KeyboardInterrupt:
+            self.save_checkpoint(f"model_pg_{self.global_step}_interrupted.pth")
+        return self._results()
+
+    def finetune_model(self, n_epochs):
+        self._setup_schedule(n_epochs)
+        pbar = self._progress(n_epochs * len(self.data_files))
+        try:
+            for epoch in range(n_epochs):
+                for fp in self.data_files:
+                    data = read_json_file(fp)
+                    train_loader, val_loader = self.loaderObj.create_dataloaders(data, num_workers=0)
+                    if hasattr(train_loader.sampler, "set_epoch"):
+                        train_loader.sampler.set_epoch(epoch)
+                    self.train_epoch(epoch, train_loader, val_loader, start_context=ALPACA_CONTEXT)
+                    if pbar is not None:
+                        pbar.update(1)
+                    if self.stop:
+                        return self._results()
+        except KeyboardInterrupt:
+            self.save_checkpoint(f"model_pg_{self.global_step}_interrupted.pth")
+        return self._results()
+
+    def _results(self):
+        return self.train_losses, self.val_losses, self.track_tokens_seen, self.track_lrs
+
+    # ------------------------------------------------------------------ eval / sample / ckpt
+    def generate_and_print_sample(self, start_context, temperature=1.0, top_k=5, memory_check=True,
+                                  max_new_tokens=None):
+        self.model.eval()
+        encoded = text_to_token_ids(start_context, self.loaderObj.tokenizer, self.config).to(self.device)
+        token_ids = generate(self.model, encoded, max_new_tokens or self.sample_tokens,
+                             self.config["context_length"], temperature=temperature, top_k=top_k,
+                             eos_id=self.config["eos_id"])
+        decoded = token_ids_to_text(token_ids.cpu(), self.loaderObj.tokenizer)
+        self.model.train()
+        if self.rank == 0 and memory_check:
+            logger.info(f"Generated Sample: {decoded.replace(chr(10), ' ')}")
+        return decoded
+
+    def save_checkpoint(self, file_name):
+        if self._dist():
+            dist.barrier()
+        path = self.save_dir / file_name
+        save_model(self.model, path, self.engine, self.rank)
+        if self.save_resume:
+            save_resume_state(self.save_dir / f"trainer_state_{self.global_step}.pt", self.optimizer,
+                              dict(global_step=self.global_step, tokens_seen=self.tokens_seen,
+                                   train_losses=self.train_losses, val_losses=self.val_losses,
+                                   track_lrs=self.track_lrs, track_tokens_seen=self.track_tokens_seen),
+                              self.rank, self.world_size)
+        if self.rank == 0:
+            logger.info(f"Checkpoint saved: {path}")
+        if self._dist():
+            dist.barrier()
+
+    def load_trainer_state(self, st: dict):
+        for k in ("global_step", "tokens_seen", "train_losses", "val_losses", "track_lrs", "track_tokens_seen"):
+            setattr(self, k, st[k])
+
+    @torch.no_grad()
+    def calc_loss_loader(self, data_loader, num_batches=None):
+        if len(data_loader) == 0:
+            return float("nan")
+        num_batches = min(num_batches or len(data_loader), len(data_loader))
+        total = 0.0
+        for i, (inp, tgt) in enumerate(data_loader):
+            if i >= num_batches:
+                break
+            total += float(self.calc_loss_batch(inp, tgt).item())
+        return self._allreduce_mean(total / num_batches)
+
+    def evaluate_model(self, train_loader, val_loader, eval_iter=5):
+        self.model.eval()
+        with torch.no_grad():
+            train_loss = self.calc_loss_loader(train_loader, eval_iter)
+            val_loss = self.calc_loss_loader(val_loader, eval_iter)
+        self.model.train()
+        return train_loss, val_loss

@@ -1,0 +1,114 @@
+"""DDP / ZeRO-1 / FSDP on CPU with gloo at world size 2 must match single-process training
+on the concatenated batch (fp32, several optimizer steps incl. clipping)."""
+import os
+import tempfile
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from building_llm_from_scratch_amd.config import get_config
+from building_llm_from_scratch_amd.models import build_model, replace_linear_with_lora
+from building_llm_from_scratch_amd.parallel import setup_engine
+from building_llm_from_scratch_amd.train.optim import FusedAdamW
+
+STEPS = 3
+
+
+def _cfg(family):
+    if family == "llama":
+        return get_config("llama3_2", "1B").replace(context_length=16, emb_dim=64, n_heads=4, n_kv_groups=2,
+                                                    hidden_dim=96, n_layers=3, vocab_size=97, dtype=torch.float32)
+    return get_config("GPT2", "124M").replace(context_length=16, emb_dim=64, n_heads=4, n_kv_groups=4,
+                                              hidden_dim=256, n_layers=3, vocab_size=97, dtype=torch.float32,
+                                              drop_rate=0.0)
+
+
+def _data(cfg):
+    g = torch.Generator().manual_seed(7)
+    return [torch.randint(0, cfg.vocab_size, (4, 17), generator=g) for _ in range(STEPS)]
+
+
+def _build(family, lora, ckpt="none"):
+    torch.manual_seed(0)
+    cfg = _cfg(family)
+    m = build_model(cfg, use_actv_ckpt=ckpt)
+    if lora:
+        for p in m.parameters():
+            p.requires_grad = False
+        replace_linear_with_lora(m, rank=4, alpha=8)
+        for mod in m.modules():
+            if hasattr(mod, "B") and isinstance(mod.B, torch.nn.Parameter):
+                torch.nn.init.normal_(mod.B, std=0.05)
+    return cfg, m
+
+
+def _train(m, opt, batches):
+    losses = []
+    for b in batches:
+        opt.zero_grad()
+        loss = m(b[:, :-1], b[:, 1:])
+        loss.backward()
+        opt.clip_grad_norm_(0.5)
+        opt.step()
+        losses.append(loss.item())
+    return losses
+
+
+def _reference(family, lora):
+    cfg, m = _build(family, lora)
+    setup_engine(m, "local", device="cpu")
+    opt = FusedAdamW(m, lr=1e-2, weight_decay=0.1)
+    losses = _train(m, opt, _data(cfg))
+    return {k: v.clone() for k, v in m.state_dict().items()}, losses
+
+
+def _worker(rank, world, kind, family, lora, ckpt, out, port):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        cfg, m = _build(family, lora, ckpt)
+        eng = setup_engine(m, kind, device="cpu", bucket_mb=0.05)
+        opt = FusedAdamW(m, lr=1e-2, weight_decay=0.1, engine=eng)
+        batches = [b[rank * 2:(rank + 1) * 2] for b in _data(cfg)]
+        losses = _train(m, opt, batches)
+        t = torch.tensor(losses)
+        dist.all_reduce(t)
+        sd = eng.full_state_dict() if hasattr(eng, "full_state_dict") else \
+            {k: v.detach().clone() for k, v in m.state_dict().items()}
+        if rank == 0:
+            torch.save({"sd": sd, "losses": (t / world).tolist()}, out)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("kind", ["ddp", "zero1", "fsdp"])
+@pytest.mark.parametrize("family,lora", [("llama", False), ("gpt2", False), ("llama", True)])
+def test_engine_matches_single_process(kind, family, lora):
+    ref_sd, ref_losses = _reference(family, lora)
+    with tempfile.TemporaryDirectory() as d:
+        out = os.path.join(d, "r.pt")
+        port = 29600 + hash((kind, family, lora)) % 300
+        mp.start_processes(_worker, args=(2, kind, family, lora, "none", out, port), nprocs=2, join=True,
+                           start_method="spawn")
+        res = torch.load(out, weights_only=True)
+    for a, b in zip(res["losses"], ref_losses):
+        assert abs(a - b) < 1e-4, (res["losses"], ref_losses)
+    sd = res["sd"]
+    assert set(sd) == set(ref_sd)
+    for k in ref_sd:
+        assert torch.allclose(sd[k].float(), ref_sd[k].float(), atol=1e-4, rtol=1e-4), \
+            (k, (sd[k].float() - ref_sd[k].float()).abs().max())
+
+
+def test_fsdp_full_ckpt_and_zero2_mode():
+    """FSDP with activation checkpointing ('full' recompute under re-gather)."""
+    ref_sd, _ = _reference("llama", False)
+    with tempfile.TemporaryDirectory() as d:
+        out = os.path.join(d, "r.pt")
+        mp.start_processes(_worker, args=(2, "fsdp", "llama", False, "full", out, 29950), nprocs=2, join=True,
+                           start_method="spawn")
+        sd = torch.load(out, weights_only=True)["sd"]
+    for k in ref_sd:
+        assert torch.allclose(sd[k].float(), ref_sd[k].float(), atol=1e-4, rtol=1e-4), k
