@@ -53,13 +53,15 @@ def main():
     from building_llm_from_scratch_amd.parallel import setup_engine
     from building_llm_from_scratch_amd.train.optim import FusedAdamW
 
+    launched = "WORLD_SIZE" in os.environ and "RANK" in os.environ  # torchrun
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     assert world == a.gpus, f"--gpus {a.gpus} but WORLD_SIZE={world} (launch with torchrun for N>1)"
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    distributed = launched or world > 1
+    if distributed:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("nccl", device_id=dev)
     ops.load_ext(required=True)
@@ -69,7 +71,7 @@ def main():
         cfg = cfg.replace(n_layers=a.layers)
     torch.manual_seed(123)
     model = build_model(cfg, use_actv_ckpt=a.actv_ckpt, device=dev)
-    engine = setup_engine(model, a.parallel if world > 1 else "local", device=dev,
+    engine = setup_engine(model, a.parallel if distributed else "local", device=dev,
                           reshard_after_forward=bool(a.reshard_after_forward))
     opt = FusedAdamW(model, lr=3e-4, weight_decay=0.1, engine=engine)
     B, T = a.batch_size, a.seq_len
@@ -89,19 +91,19 @@ def main():
     for i in range(a.warmup):
         loss = step(i)
     torch.cuda.synchronize()
-    if world > 1:
+    if distributed:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(a.steps):
         loss = step(i)
     torch.cuda.synchronize()
-    if world > 1:
+    if distributed:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     el = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-    if world > 1:
+    if distributed:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     elapsed = el.item()
     tokens = world * B * T * a.steps
@@ -133,7 +135,8 @@ def main():
                 "global_batch": world * B,
                 "micro_batch_per_gpu": B,
                 "seq_len": T,
-                "parallelism": f"{a.parallel if world > 1 else 'fsdp'}{world}",
+                "parallelism": f"{a.parallel}{world}",
+                "engine": type(engine).__name__,
                 "actv_ckpt": a.actv_ckpt,
                 "optimizer": "AdamW fp32 master, wd 0.1, clip 1.0",
             },
@@ -141,7 +144,7 @@ def main():
             "final_loss": round(float(loss.item()), 4),
         }
         print(json.dumps(out))
-    if world > 1:
+    if distributed:
         dist.destroy_process_group()
 
 
