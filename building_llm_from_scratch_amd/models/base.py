@@ -62,6 +62,18 @@ class RunCtx:
         self.B = 1
         self.T = 1
         self.profile_hook = None
+        # unit index -> HIP event recorded after that unit's optimizer update (the update
+        # runs on a side stream, overlapped with the next forward; see train/optim.py)
+        self.param_ready: dict = {}
+
+    def wait_param_ready(self, unit_index: int):
+        ev = self.param_ready.pop(unit_index, None)
+        if ev is not None:
+            torch.cuda.current_stream().wait_event(ev)
+
+    def sync_all_params(self):
+        for k in list(self.param_ready):
+            self.wait_param_ready(k)
 
     def reserve_offsets(self, n: int) -> int:
         base = self._offset
@@ -289,10 +301,14 @@ class BaseLM(nn.Module):
         grad = torch.is_grad_enabled()
         emb, blocks, head = comps[0], comps[1:-1], comps[-1]
         eng = rc.engine
+        wait = rc.wait_param_ready if rc.param_ready else (lambda i: None)
         if grad:
+            wait(emb.unit.index)
             x = _EmbedFn.apply(idx, self._anchor, emb)
             for c in blocks:
+                wait(c.unit.index)
                 x = _BlockFn.apply(x, c)
+            wait(head.unit.index)
             if targets is not None:
                 tg = targets.to(self._anchor.device, non_blocking=True).reshape(-1)
                 return _HeadLossFn.apply(x, tg, head)
@@ -301,9 +317,11 @@ class BaseLM(nn.Module):
         # inference path: no autograd nodes, nothing saved
         with torch.no_grad():
             for c in comps[:-1]:
+                wait(c.unit.index)
                 eng.pre_forward(c.unit)
                 x, _ = c.forward(idx if c is emb else x, save=False)
                 eng.post_forward(c.unit)
+            wait(head.unit.index)
             eng.pre_forward(head.unit)
             if targets is not None:
                 tg = targets.to(self._anchor.device, non_blocking=True).reshape(-1)
@@ -318,6 +336,17 @@ class BaseLM(nn.Module):
             logits, _ = head.forward_logits(x, save=False)
             eng.post_forward(head.unit)
             return logits.view(B, T, -1)
+
+    def sync_params(self):
+        """Make the current stream wait for every in-flight (overlapped) optimizer update."""
+        self._rctx.sync_all_params()
+        eng = self._rctx.engine
+        if hasattr(eng, "sync"):
+            eng.sync()
+
+    def state_dict(self, *args, **kwargs):
+        self.sync_params()
+        return super().state_dict(*args, **kwargs)
 
     # -- parameter groups for optimizers -----------------------------------------------
     def trainable_buffers(self):

@@ -85,5 +85,5 @@ class DDPEngine(LocalEngine):
 
     # ------------------------------------------------------------------ optimizer
     def optimizer_slots(self, model):
-        return [OptSlot(self.arena.bucket_param(b), self.arena.bucket_grad(b), f"bucket{b}")
-                for b in range(len(self.arena.buckets))]
+        return [OptSlot(self.arena.bucket_param(b), self.arena.bucket_grad(b), f"bucket{b}",
+                        tuple(self.arena.buckets[b])) for b in range(len(self.arena.buckets))]

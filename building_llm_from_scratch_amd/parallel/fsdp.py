@@ -100,6 +100,7 @@ class FSDPEngine(LocalEngine):
         if st["gathered"] or st["gather_work"] is not None:
             return
         works = []
+        self.model.rctx.wait_param_ready(u.index)  # its shard may still be in the optimizer stream
         for fb in st["bufs"]:
             _alloc(fb.data, fb.nbytes)
             works.append(dist.all_gather_into_tensor(fb.data, fb.shard, group=self.pg, async_op=async_op))
@@ -179,7 +180,8 @@ class FSDPEngine(LocalEngine):
 
     # ------------------------------------------------------------------ optimizer
     def optimizer_slots(self, model):
-        return [OptSlot(u.train.shard, u.train.grad_shard, u.name) for u in self.units if u.train is not None]
+        return [OptSlot(u.train.shard, u.train.grad_shard, u.name, (u.index,))
+                for u in self.units if u.train is not None]
 
     def all_reduce_grad_sq_norm(self, sq: torch.Tensor) -> torch.Tensor:
         dist.all_reduce(sq, group=self.pg)
@@ -188,6 +190,7 @@ class FSDPEngine(LocalEngine):
     # ------------------------------------------------------------------ checkpoint
     def full_state_dict(self) -> Optional[Dict[str, torch.Tensor]]:
         """Gather unit by unit; rank 0 receives the reference-named CPU state dict."""
+        self.model.rctx.sync_all_params()
         names = {id(p): n for n, p in self.model.named_parameters()}
         sd: Dict[str, torch.Tensor] = {}
         was_gathered = [u.state["gathered"] for u in self.units]

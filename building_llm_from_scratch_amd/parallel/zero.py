@@ -76,20 +76,21 @@ class ZeroEngine(LocalEngine):
         self._started = False
 
     def optimizer_slots(self, model):
-        return [OptSlot(self._shard(self.arena.bucket_param(b)), self.grad_shards[b], f"bucket{b}.shard")
-                for b in range(len(self.arena.buckets))]
+        return [OptSlot(self._shard(self.arena.bucket_param(b)), self.grad_shards[b], f"bucket{b}",
+                        tuple(self.arena.buckets[b])) for b in range(len(self.arena.buckets))]
 
     def all_reduce_grad_sq_norm(self, sq: torch.Tensor) -> torch.Tensor:
         dist.all_reduce(sq, group=self.pg)
         return sq
 
-    def after_optimizer_step(self):
-        # one all-gather per bucket, asynchronous: unit i's forward waits only for its bucket
-        for b in range(len(self.arena.buckets)):
-            full = self.arena.bucket_param(b)
-            shard = self._shard(full)
-            inp = shard if full.device.type == "cuda" else shard.clone()  # RCCL all-gathers in place
-            self._ag_works[b] = dist.all_gather_into_tensor(full, inp, group=self.pg, async_op=True)
+    def after_slot_update(self, slot):
+        # one all-gather per bucket, issued right behind that bucket's AdamW (on the optimizer
+        # stream when overlapped); unit i's next forward waits only for its own bucket
+        b = self.arena.bucket_of[slot.units[0]]
+        full = self.arena.bucket_param(b)
+        shard = self._shard(full)
+        inp = shard if full.device.type == "cuda" else shard.clone()  # RCCL all-gathers in place
+        self._ag_works[b] = dist.all_gather_into_tensor(full, inp, group=self.pg, async_op=True)
 
     def pre_forward(self, unit):
         b = self.arena.bucket_of.get(unit.index)
@@ -102,5 +103,6 @@ class ZeroEngine(LocalEngine):
         self._ag_works = {}
 
     def full_state_dict(self):
+        self.model.rctx.sync_all_params()
         self.sync()
         return {k: v.detach().cpu() for k, v in self.model.state_dict().items()} if self.rank == 0 else None

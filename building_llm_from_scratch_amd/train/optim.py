@@ -27,15 +27,18 @@ class OptSlot:
     param: torch.Tensor      # updated in place (compute dtype)
     grad: torch.Tensor       # same numel
     name: str = ""
+    units: tuple = ()        # unit indices whose parameters this slot updates
 
 
 def local_slots(model) -> List[OptSlot]:
-    return [OptSlot(fb.data, fb.grad, f"unit{i}") for i, fb in enumerate(model.trainable_buffers())]
+    return [OptSlot(c.unit.train.data, c.unit.train.grad, c.unit.name, (c.unit.index,))
+            for c in model.computes if c.unit.train is not None]
 
 
 class FusedAdamW(torch.optim.Optimizer):
     def __init__(self, model=None, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8,
-                 weight_decay: float = 0.01, slots: Optional[List[OptSlot]] = None, engine=None):
+                 weight_decay: float = 0.01, slots: Optional[List[OptSlot]] = None, engine=None,
+                 overlap: bool = True):
         if slots is None:
             eng = engine or (model.rctx.engine if model is not None else None)
             slots = eng.optimizer_slots(model) if eng is not None and hasattr(eng, "optimizer_slots") \
@@ -56,6 +59,14 @@ class FusedAdamW(torch.optim.Optimizer):
         # data-parallel engines reduce with SUM; the 1/world average is folded in here
         self.grad_prescale = float(getattr(self.engine, "grad_prescale", 1.0))
         self._prescale_t: Optional[torch.Tensor] = None
+        # Overlapped update: the (HBM-bound) AdamW of unit i runs on a side HIP stream and the
+        # next forward of unit i waits on its event only, so the update streams under the
+        # (MFMA-bound) forward GEMMs of the preceding units.
+        self.rctx = model.rctx if model is not None else None
+        dev = slots[0].param.device if slots else torch.device("cpu")
+        self.overlap = bool(overlap and dev.type == "cuda" and self.rctx is not None
+                            and all(s.units for s in slots))
+        self.opt_stream = torch.cuda.Stream(device=dev) if self.overlap else None
 
     # torch's zero_grad would try to walk p.grad of the slot tensors; the unit backward
     # OVERWRITES the flat gradients every step (accumulation is explicit), so this is a no-op
@@ -93,12 +104,36 @@ class FusedAdamW(torch.optim.Optimizer):
                 self._prescale_t = torch.full((1,), self.grad_prescale, dtype=torch.float32,
                                               device=self.slots[0].param.device)
             self._gscale = self._prescale_t
-        for s in self.slots:
-            st = self.state[s.param]
-            st["step"] += 1
-            ops.adamw_step_(s.param.reshape(-1), st.get("master"), s.grad.reshape(-1), st["exp_avg"],
-                            st["exp_avg_sq"], lr, b1, b2, eps, wd, st["step"], self._gscale)
+        if self.overlap:
+            cur = torch.cuda.current_stream()
+            self.opt_stream.wait_stream(cur)
+            if self._gscale is not None:
+                self._gscale.record_stream(self.opt_stream)
+            with torch.cuda.stream(self.opt_stream):
+                for s in self.slots:
+                    self._update(s, lr, b1, b2, eps, wd)
+                    if self.engine is not None and hasattr(self.engine, "after_slot_update"):
+                        self.engine.after_slot_update(s)
+                    ev = torch.cuda.Event()
+                    ev.record(self.opt_stream)
+                    for u in s.units:
+                        self.rctx.param_ready[u] = ev
+        else:
+            for s in self.slots:
+                self._update(s, lr, b1, b2, eps, wd)
+                if self.engine is not None and hasattr(self.engine, "after_slot_update"):
+                    self.engine.after_slot_update(s)
         self._gscale = None
-        if self.engine is not None and hasattr(self.engine, "after_optimizer_step"):
-            self.engine.after_optimizer_step()
         return None
+
+    def _update(self, s, lr, b1, b2, eps, wd):
+        st = self.state[s.param]
+        st["step"] += 1
+        ops.adamw_step_(s.param.reshape(-1), st.get("master"), s.grad.reshape(-1), st["exp_avg"],
+                        st["exp_avg_sq"], lr, b1, b2, eps, wd, st["step"], self._gscale)
+
+    def synchronize(self):
+        """Block the current stream until every overlapped update has been applied."""
+        if self.overlap:
+            torch.cuda.current_stream().wait_stream(self.opt_stream)
+            self.rctx.param_ready.clear()

@@ -3,22 +3,23 @@
 // Replaces autograd through the reference's materialised attention (GPT2.py:38-46,
 // Llama3.py:131-155) — no [B,H,T,T] tensor, P recomputed from the forward's LSE.
 //
-// Decomposition: one workgroup = 4 waves = 128 keys of ONE query head h (and its kv head
-// g = h / (H/G)).  Key on the MFMA lane: S = Q K^T and dP = dO V^T are computed with the
-// key as the accumulator column, so the dV^T += dO^T P and dK^T += Q^T dS products take P
-// and dS straight from the accumulator registers as their B operand (no LDS round trip),
-// and dK^T / dV^T for the wave's 32 keys stay in registers for the whole sweep over query
-// blocks.  Only dS crosses LDS, once, for dQ = dS K (32 queries x HD per step, summed over
-// the workgroup's 128 keys on chip, then ONE fp32 atomic per element per workgroup in
-// full 128-B row segments).  Per-head dK/dV partials are plain-stored in fp32 and summed
-// over the H/G heads of each kv group by a small reduction kernel (GQA without atomics).
-//
-// Rows are constants folded into the softmax: p = exp2(s*c - lse2), ds = p*(dp - delta);
-// delta = rowsum(dO * O) comes from a pre-pass (attn_naive.hip:attn_delta).  Q/dO tiles
-// arrive by global_load_lds DMA, double-buffered, each stored twice: a 16-B-chunk XOR image
-// for MFMA row reads (ds_read_b128) and a 64-B-chunk XOR image for hardware-transposed reads
-// (ds_read_b64_tr_b16).  Causal: a key block only visits query blocks at or below the
-// diagonal; grid order = heaviest key blocks first.
+// Two atomic-free kernels (dQ is bitwise deterministic):
+//  * dK/dV kernel — one workgroup = 4 waves = 128 keys of ONE query head h (kv head
+//    g = h / (H/G)).  Key on the MFMA lane: S = Q K^T and dP = dO V^T put the key in the
+//    accumulator column, so dV^T += dO^T P and dK^T += Q^T dS take P / dS straight from the
+//    accumulator registers as their B operand; dK^T / dV^T for the wave's 32 keys stay in
+//    registers for the whole sweep over 32-query steps (one barrier per step).  Per-head
+//    partials are plain-stored in fp32 and summed over the H/G heads of each kv group by a
+//    tiny reduction (GQA without atomics; MHA writes bf16 directly).
+//  * dQ kernel — forward-shaped: one workgroup = 128 queries of one head, the query on the
+//    lane (S^T = K Q^T, dP^T = V dO^T), dQ^T += K^T dS^T accumulated in registers over the
+//    key tiles, written once.  Costs two extra MFMA products vs. a fused kernel but removes
+//    the ~300 MB/layer of fp32 dQ atomics that floored the fused version.
+// Softmax constants are lane-local: p = exp2(s*c - lse2), ds = p*(dp - delta)*scale;
+// delta = rowsum(dO * O) comes from a pre-pass (attn_naive.hip:attn_delta).  Q/dO (dK/dV
+// kernel) and K/V (dQ kernel) tiles arrive by global_load_lds DMA, double-buffered, stored as
+// 16-B-chunk XOR images for MFMA row reads and 64-B-chunk XOR images for hardware-transposed
+// reads (ds_read_b64_tr_b16).  Causal: only tiles at/below the diagonal; heaviest first.
 #include <float.h>
 #include "api.h"
 
@@ -87,9 +88,9 @@ constexpr int BWD_BQ = 32;    // queries per step
 constexpr float kLog2eB = 1.4426950408889634f;
 
 template <typename T, int HD>
-__global__ __launch_bounds__(256, 1) void attn_bwd_mfma_k(const T* __restrict__ qkv, const T* __restrict__ dout,
+__global__ __launch_bounds__(256, (HD == 64 ? 2 : 1)) void attn_bwd_mfma_k(const T* __restrict__ qkv, const T* __restrict__ dout,
                                                           const float* __restrict__ lse,
-                                                          const float* __restrict__ delta, float* __restrict__ dq_acc,
+                                                          const float* __restrict__ delta, T* __restrict__ dqkv,
                                                           float* __restrict__ dkv_part, int T_, int H, int G,
                                                           bool causal, uint32_t thr, float inv_keep, bool drop,
                                                           uint64_t seed, uint64_t doff) {
@@ -97,12 +98,9 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_mfma_k(const T* __restrict__ 
   constexpr int KK = HD / 16, DT = HD / 32, CH = HD / 8;
   constexpr int IMG = BWD_BQ * HD * 2;          // bytes of one [32][HD] image
   constexpr int PIECES = IMG / 1024;            // 1-KiB DMA pieces per image
-  constexpr int KIMG = BWD_BKV * HD * 2;
   constexpr int BUF = 4 * IMG + 256;            // QR, QT, OR, OT, lse+delta
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* kimg = smem;                            // K [128][HD], transposed-read image
-  char* bufs = smem + KIMG;                     // 2 x BUF
-  char* dsl = bufs + 2 * BUF;                   // dS [32][128] bf16
+  char* bufs = smem;                            // 2 x BUF
 
   const int kb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
   const int g = h / (H / G);
@@ -131,15 +129,6 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_mfma_k(const T* __restrict__ 
       vf[kk] = *reinterpret_cast<const v8*>(vb_ + (long)kr * rs + kk * 16 + hh * 8);
     }
   }
-  // ---- K image in LDS for the dQ product (rows = 128 keys)
-  for (int cidx = tid; cidx < BWD_BKV * CH; cidx += 256) {
-    const int r = cidx / CH, c16 = cidx % CH;
-    int key = k0 + r;
-    key = key < T_ ? key : T_ - 1;
-    *reinterpret_cast<uint4*>(kimg + t_off<HD>(r, c16 * 8)) =
-        *reinterpret_cast<const uint4*>(kb_ + (long)key * rs + c16 * 8);
-  }
-
   f32x16 dk[DT], dv[DT];
 #pragma unroll
   for (int i = 0; i < DT; ++i) { dk[i] = f32x16{}; dv[i] = f32x16{}; }
@@ -161,19 +150,20 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_mfma_k(const T* __restrict__ 
         c16 = c64 * 4 + (pc & 3);
       }
       const T* src = (img < 2) ? (qb_ + (long)qrow_g * rs + c16 * 8) : (ob_ + (long)qrow_g * ors + c16 * 8);
-      __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)(base + img * IMG + piece * 1024), 16, 0, 0);
+      glds16(src, base + img * IMG + piece * 1024);
     }
     if (w == 0) {
       int qq = q0 + (lane & 31);
       qq = qq < T_ ? qq : T_ - 1;
       const float* src = (lane < 32) ? (lse_ + qq) : (del_ + qq);
-      __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)(base + 4 * IMG), 4, 0, 0);
+      glds4(src, base + 4 * IMG);
     }
   };
 
   const int qstart = causal ? k0 : 0;
   int it = 0;
   if (qstart < T_) issue(qstart, 0);
+  wait_vm0();
   __syncthreads();
   for (int q0 = qstart; q0 < T_; q0 += BWD_BQ, ++it) {
     const int buf = it & 1;
@@ -238,44 +228,29 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_mfma_k(const T* __restrict__ 
           dk[dt] = MFb<T>::mma(aq, df, dk[dt]);
         }
       }
-      // dS (scaled) -> LDS [q][key] for the dQ product
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int ql = (r & 3) + 8 * (r >> 2) + 4 * hh;
-        *reinterpret_cast<T*>(dsl + ds_off(ql, 32 * w + l32)) = from_f<T>(dpacc[r]);
-      }
-    } else {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int ql = (r & 3) + 8 * (r >> 2) + 4 * hh;
-        *reinterpret_cast<T*>(dsl + ds_off(ql, 32 * w + l32)) = from_f<T>(0.f);
-      }
     }
-    __syncthreads();
-    // ---- dQ[q][d] += sum over the workgroup's 128 keys of dS[q][key] K[key][d]
-    //      (wave w owns d-tile w; HD = 64 uses waves 0,1)
-    if (w < DT) {
-      f32x16 dq = f32x16{};
-#pragma unroll
-      for (int ks = 0; ks < BWD_BKV / 16; ++ks) {
-        const v8 a = *reinterpret_cast<const v8*>(dsl + l32 * 256 + ((((2 * ks + hh)) ^ (l32 & 15)) << 4));
-        const int krow = ks * 16 + 8 * hh + qrow;
-        const int col = w * 32 + gl * 16 + pcol * 4;
-        const v8 bk = tr8<v8>(kimg, t_off<HD>(krow, col), t_off<HD>(krow + 4, col));
-        dq = MFb<T>::mma(a, bk, dq);
-      }
-      const int d = w * 32 + l32;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int q = q0 + (r & 3) + 8 * (r >> 2) + 4 * hh;
-        if (q < T_) atomicAdd(dq_acc + ((long)b * T_ + q) * ors + (long)h * HD + d, dq[r]);
-      }
-    }
+    wait_vm0();
     __syncthreads();
   }
 
-  // ---- per-head dK / dV partials (fp32): dkv_part[2][B*T][H][HD]
-  if (mykey < T_) {
+  // ---- MHA: write bf16 dK/dV straight into dqkv; GQA: per-head fp32 partials
+  if (mykey < T_ && H == G) {
+    T* pk = dqkv + ((long)b * T_ + mykey) * rs + (long)(H + g) * HD;
+    T* pv = dqkv + ((long)b * T_ + mykey) * rs + (long)(H + G + g) * HD;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int gq = 0; gq < 4; ++gq) {
+        const int d0 = dt * 32 + 8 * gq + 4 * hh;
+        uint2 a, bb;
+        a.x = pk2<T>(dk[dt][4 * gq], dk[dt][4 * gq + 1]);
+        a.y = pk2<T>(dk[dt][4 * gq + 2], dk[dt][4 * gq + 3]);
+        bb.x = pk2<T>(dv[dt][4 * gq], dv[dt][4 * gq + 1]);
+        bb.y = pk2<T>(dv[dt][4 * gq + 2], dv[dt][4 * gq + 3]);
+        *reinterpret_cast<uint2*>(pk + d0) = a;
+        *reinterpret_cast<uint2*>(pv + d0) = bb;
+      }
+  } else if (mykey < T_) {
     const long BT = (long)gridDim.z * T_;
     float* pk = dkv_part + ((long)b * T_ + mykey) * ors + (long)h * HD;
     float* pv = pk + BT * ors;
@@ -290,34 +265,165 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_mfma_k(const T* __restrict__ 
   }
 }
 
-// dqkv[:, q part] = bf16(dq_acc); dqkv[:, k/v part] = bf16(sum over the H/G heads of each group)
+// ---------------------------------------------------------------------------------------
+// dQ kernel (forward-shaped): 4 waves x 32 queries of head h; key tiles of 64 by DMA into
+// three images per buffer: K rows (S^T = K Q^T), K transposed (dQ^T += K^T dS^T), V rows
+// (dP^T = V dO^T).  The query is the lane column, so lse / delta are per-lane scalars.
+template <typename T, int HD>
+__global__ __launch_bounds__(256, 2) void attn_bwd_dq_k(const T* __restrict__ qkv, const T* __restrict__ dout,
+                                                        const float* __restrict__ lse,
+                                                        const float* __restrict__ delta, T* __restrict__ dqkv,
+                                                        int T_, int H, int G, bool causal, uint32_t thr,
+                                                        float inv_keep, bool drop, uint64_t seed, uint64_t doff) {
+  typedef typename MFb<T>::v8 v8;
+  constexpr int BQ = 128, BK = 64;
+  constexpr int KK = HD / 16, DT = HD / 32, CH = HD / 8;
+  constexpr int IMG = BK * HD * 2;              // bytes of one [64][HD] image
+  constexpr int LD = BK * CH / 256;             // 1-KiB pieces per wave per image
+  constexpr int BUF = 3 * IMG;                  // K rows, K transposed, V rows
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int nqb = (T_ + BQ - 1) / BQ;
+  const int qb = nqb - 1 - (int)blockIdx.x;
+  const int h = blockIdx.y, b = blockIdx.z;
+  const int g = h / (H / G);
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hh = lane >> 5, l32 = lane & 31;
+  const int gi = lane & 15, gl = (lane >> 4) & 1, qrow = gi >> 2, pcol = gi & 3;
+  const long rs = (long)(H + 2 * G) * HD;
+  const long ors = (long)H * HD;
+  const T* kb_ = qkv + (long)b * T_ * rs + (long)(H + g) * HD;
+  const T* vb_ = qkv + (long)b * T_ * rs + (long)(H + G + g) * HD;
+  const int q0 = qb * BQ;
+  const int qi = q0 + w * 32 + l32;
+  const int qc = qi < T_ ? qi : T_ - 1;
+  const float scale = rsqrtf((float)HD), c = scale * kLog2eB;
+
+  v8 qf[KK], of[KK];
+#pragma unroll
+  for (int kk = 0; kk < KK; ++kk) {
+    qf[kk] = *reinterpret_cast<const v8*>(qkv + ((long)b * T_ + qc) * rs + (long)h * HD + kk * 16 + hh * 8);
+    of[kk] = *reinterpret_cast<const v8*>(dout + ((long)b * T_ + qc) * ors + (long)h * HD + kk * 16 + hh * 8);
+  }
+  const float L = lse[((long)b * H + h) * T_ + qc];
+  const float D = delta[((long)b * H + h) * T_ + qc];
+  f32x16 dq[DT];
+#pragma unroll
+  for (int i = 0; i < DT; ++i) dq[i] = f32x16{};
+
+  auto issue = [&](int t, int buf) {
+    char* base = smem + buf * BUF;
+#pragma unroll
+    for (int i = 0; i < LD; ++i) {
+      const int piece = w * LD + i;
+      const int P = piece * 64 + lane;
+      const int r = P / CH, pc = P % CH;
+      int key = t * BK + r;
+      key = key < T_ ? key : T_ - 1;
+      int rc16;
+      if constexpr (HD == 128) rc16 = pc ^ (r & 15); else rc16 = pc ^ ((r >> 1) & 7);
+      const int c64 = (pc >> 2) ^ (HD == 128 ? (r & 3) : ((r >> 1) & 1));
+      const int tc16 = c64 * 4 + (pc & 3);
+      glds16(kb_ + (long)key * rs + rc16 * 8, base + piece * 1024);
+      glds16(kb_ + (long)key * rs + tc16 * 8, base + IMG + piece * 1024);
+      glds16(vb_ + (long)key * rs + rc16 * 8, base + 2 * IMG + piece * 1024);
+    }
+  };
+
+  const int kend = causal ? min(T_, q0 + BQ) : T_;
+  const int ntiles = (kend + BK - 1) / BK;
+  const int wq_lo = q0 + w * 32, wq_hi = wq_lo + 31;
+  issue(0, 0);
+  wait_vm0();
+  __syncthreads();
+  for (int t = 0; t < ntiles; ++t) {
+    const int buf = t & 1;
+    if (t + 1 < ntiles) issue(t + 1, buf ^ 1);
+    const int k0 = t * BK;
+    if ((!causal || k0 <= wq_hi) && wq_lo < T_) {
+      const char* KR = smem + buf * BUF;
+      const char* KT = KR + IMG;
+      const char* VR = KR + 2 * IMG;
+      f32x16 s[2], dp[2];
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt) {
+        s[kt] = f32x16{};
+        dp[kt] = f32x16{};
+#pragma unroll
+        for (int kk = 0; kk < KK; ++kk) {
+          const int off = r_off<HD>(kt * 32 + l32, kk * 2 + hh);
+          s[kt] = MFb<T>::mma(*reinterpret_cast<const v8*>(KR + off), qf[kk], s[kt]);
+          dp[kt] = MFb<T>::mma(*reinterpret_cast<const v8*>(VR + off), of[kk], dp[kt]);
+        }
+      }
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int key = k0 + kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+          float p = exp2f(s[kt][r] * c - L);
+          if ((causal && key > qi) || key >= T_ || qi >= T_) p = 0.f;
+          float d = dp[kt][r];
+          if (drop) d = (drop_hash(seed, doff + (((uint64_t)(b * H + h) * T_ + qi) * T_ + key)) >= thr) ? d * inv_keep : 0.f;
+          s[kt][r] = p * (d - D) * scale;
+        }
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          v8 df;
+          {
+            uint32_t u[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) u[j] = pk2<T>(s[kt][8 * s2 + 2 * j], s[kt][8 * s2 + 2 * j + 1]);
+            __builtin_memcpy(&df, u, 16);
+          }
+          const int base = kt * 32 + s2 * 16 + 4 * hh + qrow;
+#pragma unroll
+          for (int dt = 0; dt < DT; ++dt) {
+            const int col = dt * 32 + gl * 16 + pcol * 4;
+            const v8 a = tr8<v8>(KT, t_off<HD>(base, col), t_off<HD>(base + 8, col));
+            dq[dt] = MFb<T>::mma(a, df, dq[dt]);
+          }
+        }
+    }
+    wait_vm0();
+    __syncthreads();
+  }
+  if (qi < T_) {
+    T* row = dqkv + ((long)b * T_ + qi) * rs + (long)h * HD;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int gq = 0; gq < 4; ++gq) {
+        const int d0 = dt * 32 + 8 * gq + 4 * hh;
+        uint2 v;
+        v.x = pk2<T>(dq[dt][4 * gq], dq[dt][4 * gq + 1]);
+        v.y = pk2<T>(dq[dt][4 * gq + 2], dq[dt][4 * gq + 3]);
+        *reinterpret_cast<uint2*>(row + d0) = v;
+      }
+  }
+}
+
+// GQA: dqkv[:, k/v part] = bf16(sum over the H/G query heads of each kv group)
 template <typename T>
-__global__ __launch_bounds__(256) void attn_bwd_finalize_k(const float* __restrict__ dq_acc,
-                                                           const float* __restrict__ dkv_part, T* __restrict__ dqkv,
-                                                           long BT, int H, int G, int HD) {
+__global__ __launch_bounds__(256) void attn_bwd_kv_reduce_k(const float* __restrict__ dkv_part, T* __restrict__ dqkv,
+                                                            long BT, int H, int G, int HD) {
   const int rep = H / G;
   const long rs = (long)(H + 2 * G) * HD;
-  const long per_row = (long)(H + 2 * G) * HD / 4;  // 4-element groups per output row
+  const long per_row = 2L * G * HD / 4;
   const long total = BT * per_row;
   for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
     const long row = i / per_row;
-    const int col = (int)(i - row * per_row) * 4;
-    float v[4];
-    if (col < H * HD) {
-      const float4 x = *reinterpret_cast<const float4*>(dq_acc + row * H * HD + col);
-      v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
-    } else {
-      const int kvcol = col - H * HD;              // in [0, 2*G*HD)
-      const int which = kvcol / (G * HD);          // 0 = K, 1 = V
-      const int gg = (kvcol % (G * HD)) / HD, d = kvcol % HD;
-      const float* src = dkv_part + (long)which * BT * H * HD + row * H * HD;
-      v[0] = v[1] = v[2] = v[3] = 0.f;
-      for (int r = 0; r < rep; ++r) {
-        const float4 x = *reinterpret_cast<const float4*>(src + (long)(gg * rep + r) * HD + d);
-        v[0] += x.x; v[1] += x.y; v[2] += x.z; v[3] += x.w;
-      }
+    const int kvcol = (int)(i - row * per_row) * 4;  // in [0, 2*G*HD)
+    const int which = kvcol / (G * HD);
+    const int gg = (kvcol % (G * HD)) / HD, d = kvcol % HD;
+    const float* src = dkv_part + (long)which * BT * H * HD + row * H * HD;
+    float v[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int r = 0; r < rep; ++r) {
+      const float4 x = *reinterpret_cast<const float4*>(src + (long)(gg * rep + r) * HD + d);
+      v[0] += x.x; v[1] += x.y; v[2] += x.z; v[3] += x.w;
     }
-    T* dst = dqkv + row * rs + col;
+    T* dst = dqkv + row * rs + (long)H * HD + kvcol;
 #pragma unroll
     for (int j = 0; j < 4; ++j) dst[j] = from_f<T>(v[j]);
   }
@@ -326,26 +432,36 @@ __global__ __launch_bounds__(256) void attn_bwd_finalize_k(const float* __restri
 void attn_bwd_mfma(DType dt, const void* qkv, const void* o, const float* lse, const void* dout, void* dqkv,
                    float* delta, float* dq_acc, float* dkv_part, int B, int T_, int H, int G, int hd, bool causal,
                    float p, uint64_t seed, uint64_t offset, hipStream_t s) {
+  (void)dq_acc;
   const uint32_t thr = drop_threshold(p);
   const float ik = p > 0.f ? 1.f / (1.f - p) : 1.f;
   attn_delta(dt, o, dout, delta, B, T_, H, hd, s);
-  dim3 grid((T_ + BWD_BKV - 1) / BWD_BKV, H, B), block(256);
-  auto lds = [](int HD) { return BWD_BKV * HD * 2 + 2 * (4 * BWD_BQ * HD * 2 + 256) + BWD_BQ * BWD_BKV * 2; };
-#define LAUNCH(TT, HDD)                                                                                       \
-  hipLaunchKernelGGL((attn_bwd_mfma_k<TT, HDD>), grid, block, lds(HDD), s, (const TT*)qkv, (const TT*)dout,   \
-                     lse, delta, dq_acc, dkv_part, T_, H, G, causal, thr, ik, p > 0.f, seed, offset)
+  dim3 grid_kv((T_ + BWD_BKV - 1) / BWD_BKV, H, B), grid_q((T_ + 127) / 128, H, B), block(256);
+  auto lds_kv = [](int HD) { return 2 * (4 * BWD_BQ * HD * 2 + 256); };
+  auto lds_q = [](int HD) { return 2 * 3 * 64 * HD * 2; };
+#define LAUNCH(TT, HDD)                                                                                         \
+  do {                                                                                                          \
+    hipLaunchKernelGGL((attn_bwd_mfma_k<TT, HDD>), grid_kv, block, lds_kv(HDD), s, (const TT*)qkv,            \
+                       (const TT*)dout, lse, delta, (TT*)dqkv, dkv_part, T_, H, G, causal, thr, ik, p > 0.f,    \
+                       seed, offset);                                                                           \
+    hipLaunchKernelGGL((attn_bwd_dq_k<TT, HDD>), grid_q, block, lds_q(HDD), s, (const TT*)qkv,                 \
+                       (const TT*)dout, lse, delta, (TT*)dqkv, T_, H, G, causal, thr, ik, p > 0.f, seed,       \
+                       offset);                                                                                 \
+  } while (0)
   if (dt == DType::BF16) {
     if (hd == 128) LAUNCH(bf16_t, 128); else LAUNCH(bf16_t, 64);
   } else {
     if (hd == 128) LAUNCH(f16_t, 128); else LAUNCH(f16_t, 64);
   }
 #undef LAUNCH
-  const long BT = (long)B * T_;
-  const long groups = BT * (H + 2 * G) * hd / 4;
-  const int fg = (int)((groups + 255) / 256 < 4096 ? (groups + 255) / 256 : 4096);
-  BLLM_DISPATCH(dt, TT, {
-    hipLaunchKernelGGL(attn_bwd_finalize_k<TT>, dim3(fg), dim3(256), 0, s, dq_acc, dkv_part, (TT*)dqkv, BT, H, G, hd);
-  });
+  if (H != G) {
+    const long BT = (long)B * T_;
+    const long groups = BT * 2L * G * hd / 4;
+    const int fg = (int)((groups + 255) / 256 < 4096 ? (groups + 255) / 256 : 4096);
+    BLLM_DISPATCH(dt, TT, {
+      hipLaunchKernelGGL(attn_bwd_kv_reduce_k<TT>, dim3(fg), dim3(256), 0, s, dkv_part, (TT*)dqkv, BT, H, G, hd);
+    });
+  }
 }
 
 }  // namespace bllm

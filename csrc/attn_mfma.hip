@@ -70,10 +70,10 @@ template <typename T> __device__ __forceinline__ uint32_t pack2(float a, float b
   return (uint32_t)ux | ((uint32_t)uy << 16);
 }
 
-template <typename T, int HD>
+template <typename T, int HD, bool DROP>
 __global__ __launch_bounds__(256, 2) void attn_fwd_mfma_k(const T* __restrict__ qkv, T* __restrict__ out,
                                                           float* __restrict__ lse, int T_, int H, int G, bool causal,
-                                                          uint32_t thr, float inv_keep, bool drop, uint64_t seed,
+                                                          uint32_t thr, float inv_keep, uint64_t seed,
                                                           uint64_t doff) {
   typedef typename MF<T>::v8 v8;
   constexpr int KK = HD / 16;               // k-steps of the QK^T product
@@ -131,14 +131,13 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_mfma_k(const T* __restrict__ 
       if constexpr (HD == 128) kc16 = pc ^ (r & 15); else kc16 = pc ^ ((r >> 1) & 7);
       const int c64 = (pc >> 2) ^ (HD == 128 ? (r & 3) : ((r >> 1) & 1));
       const int vc16 = c64 * 4 + (pc & 3);
-      __builtin_amdgcn_global_load_lds((gbl_void*)(kbase + (long)key * rs + kc16 * 8),
-                                       (lds_void*)(kb + piece * 1024), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds((gbl_void*)(vbase + (long)key * rs + vc16 * 8),
-                                       (lds_void*)(vb + piece * 1024), 16, 0, 0);
+      glds16(kbase + (long)key * rs + kc16 * 8, kb + piece * 1024);
+      glds16(vbase + (long)key * rs + vc16 * 8, vb + piece * 1024);
     }
   };
 
   issue(0, 0);
+  wait_vm0();
   __syncthreads();
 
   const int wq_lo = q0 + w * 32, wq_hi = wq_lo + 31;  // this wave's query range
@@ -150,32 +149,46 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_mfma_k(const T* __restrict__ 
     if (active) {
       const char* kb = smem + buf * 2 * TILE_B;
       const char* vb = kb + TILE_B;
-      // ---- S^T = K Q^T for two 32-key sub-tiles
+      // ---- S^T = K Q^T for two 32-key sub-tiles: each sub-tile's K fragments are read
+      //      into distinct registers first (one lgkmcnt wait), then the MFMA chain
       f32x16 s[2];
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt) {
+        v8 ka[KK];
+#pragma unroll
+        for (int kk = 0; kk < KK; ++kk)
+          ka[kk] = *reinterpret_cast<const v8*>(kb + k_off<HD>(kt * 32 + l32, kk * 2 + hh));
+        __builtin_amdgcn_sched_barrier(0);
         s[kt] = f32x16{};
 #pragma unroll
-        for (int kk = 0; kk < KK; ++kk) {
-          const v8 a = *reinterpret_cast<const v8*>(kb + k_off<HD>(kt * 32 + l32, kk * 2 + hh));
-          s[kt] = MF<T>::mma(a, qf[kk], s[kt]);
-        }
+        for (int kk = 0; kk < KK; ++kk) s[kt] = MF<T>::mma(ka[kk], qf[kk], s[kt]);
       }
-      // ---- scale, mask, online softmax (per lane = per query; halves exchange once)
+      // ---- scale, mask (selects, no branches), online softmax (lane = query)
       const bool need_mask = (causal && k0 + FWD_BK - 1 > wq_lo) || (k0 + FWD_BK > T_);
       float mx = -INFINITY;
+      if (need_mask) {
 #pragma unroll
-      for (int kt = 0; kt < 2; ++kt)
+        for (int kt = 0; kt < 2; ++kt) {
+          const int kb0 = k0 + kt * 32 + 4 * hh;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          float v = s[kt][r] * c;
-          if (need_mask) {
-            const int key = k0 + kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
-            if ((causal && key > qi) || key >= T_) v = -INFINITY;
+          for (int r = 0; r < 16; ++r) {
+            const int key = kb0 + (r & 3) + 8 * (r >> 2);
+            const bool off = (causal & (key > qi)) | (key >= T_);
+            const float v = off ? -INFINITY : s[kt][r] * c;
+            s[kt][r] = v;
+            mx = fmaxf(mx, v);
           }
-          s[kt][r] = v;
-          mx = fmaxf(mx, v);
         }
+      } else {
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const float v = s[kt][r] * c;
+            s[kt][r] = v;
+            mx = fmaxf(mx, v);
+          }
+      }
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
       const float mn = fmaxf(m, mx);
       const float alpha = exp2f(m - mn);
@@ -187,13 +200,13 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_mfma_k(const T* __restrict__ 
         for (int r = 0; r < 16; ++r) {
           const float p = exp2f(s[kt][r] - mn);
           ls += p;
-          float pw = p;
-          if (drop) {
+          if constexpr (DROP) {
             const int key = k0 + kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
             const uint64_t e = (((uint64_t)(b * H + h) * T_ + qi) * T_ + key);
-            pw = (drop_hash(seed, doff + e) >= thr) ? p * inv_keep : 0.f;
+            s[kt][r] = (drop_hash(seed, doff + e) >= thr) ? p * inv_keep : 0.f;
+          } else {
+            s[kt][r] = p;
           }
-          s[kt][r] = pw;
         }
       l = l * alpha + ls;
 #pragma unroll
@@ -214,19 +227,22 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_mfma_k(const T* __restrict__ 
             __builtin_memcpy(&pf, u, 16);
           }
           const int base = kt * 32 + s2 * 16 + 4 * hh + qrow;
+          v8 va[DT];
 #pragma unroll
           for (int dt = 0; dt < DT; ++dt) {
             const int col = dt * 32 + gl * 16 + pcol * 4;
             const s16x4 r1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(vb + v_off<HD>(base, col)));
             const s16x4 r2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(vb + v_off<HD>(base + 8, col)));
             short tmp[8] = {r1[0], r1[1], r1[2], r1[3], r2[0], r2[1], r2[2], r2[3]};
-            v8 a;
-            __builtin_memcpy(&a, tmp, 16);
-            o[dt] = MF<T>::mma(a, pf, o[dt]);
+            __builtin_memcpy(&va[dt], tmp, 16);
           }
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int dt = 0; dt < DT; ++dt) o[dt] = MF<T>::mma(va[dt], pf, o[dt]);
         }
     }
-    __syncthreads();  // also retires the DMA of tile t+1 (vmcnt(0))
+    wait_vm0();       // the DMA of tile t+1 has landed (asm-issued, so drained by hand)
+    __syncthreads();
   }
 
   // ---- epilogue: combine the two halves' partial sums, normalise, store O and LSE
@@ -255,9 +271,15 @@ void attn_fwd_mfma(DType dt, const void* qkv, void* o, float* lse, int B, int T_
   const uint32_t thr = drop_threshold(p);
   const float ik = p > 0.f ? 1.f / (1.f - p) : 1.f;
   dim3 grid((T_ + FWD_BQ - 1) / FWD_BQ, H, B), block(256);
-#define LAUNCH(TT, HDD)                                                                                     \
-  hipLaunchKernelGGL((attn_fwd_mfma_k<TT, HDD>), grid, block, 2 * 2 * FWD_BK * HDD * 2, s, (const TT*)qkv,  \
-                     (TT*)o, lse, T_, H, G, causal, thr, ik, p > 0.f, seed, offset)
+#define LAUNCH(TT, HDD)                                                                                       \
+  do {                                                                                                        \
+    if (p > 0.f)                                                                                              \
+      hipLaunchKernelGGL((attn_fwd_mfma_k<TT, HDD, true>), grid, block, 2 * 2 * FWD_BK * HDD * 2, s,          \
+                         (const TT*)qkv, (TT*)o, lse, T_, H, G, causal, thr, ik, seed, offset);              \
+    else                                                                                                      \
+      hipLaunchKernelGGL((attn_fwd_mfma_k<TT, HDD, false>), grid, block, 2 * 2 * FWD_BK * HDD * 2, s,         \
+                         (const TT*)qkv, (TT*)o, lse, T_, H, G, causal, thr, ik, seed, offset);              \
+  } while (0)
   if (dt == DType::BF16) {
     if (hd == 128) LAUNCH(bf16_t, 128); else LAUNCH(bf16_t, 64);
   } else {

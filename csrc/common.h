@@ -109,6 +109,28 @@ inline uint32_t drop_threshold(float p) {
   return (uint32_t)t;
 }
 
+// LDS-DMA of 16 bytes per lane (global_load_lds_dwordx4) issued from inline asm so hipcc does
+// not track it: the compiler otherwise guards every later ds_read with s_waitcnt vmcnt(0)
+// (it cannot prove the in-flight DMA targets the other LDS buffer), which serialises the
+// prefetch with compute.  The caller drains it with an explicit vmcnt before the barrier that
+// precedes the reads (cdna_hip_programming.md §5.7).  ``lds_dst`` is the wave-uniform base;
+// lane i writes lds_dst + 16*i.
+__device__ __forceinline__ void glds16(const void* gsrc, const void* lds_dst) {
+  uint32_t lds = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)lds_dst;
+  lds = __builtin_amdgcn_readfirstlane(lds);
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(gsrc), "s"(lds) : "memory");
+}
+__device__ __forceinline__ void glds4(const void* gsrc, const void* lds_dst) {
+  uint32_t lds = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)lds_dst;
+  lds = __builtin_amdgcn_readfirstlane(lds);
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(gsrc), "s"(lds) : "memory");
+}
+__device__ __forceinline__ void wait_vm0() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
 inline int ceil_div(long a, long b) { return (int)((a + b - 1) / b); }
 
 }  // namespace bllm

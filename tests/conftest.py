@@ -11,6 +11,7 @@ if HERE not in sys.path:
     sys.path.insert(0, HERE)
 
 os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+os.environ.setdefault("GLOO_SOCKET_IFNAME", "lo")
 
 
 def pytest_configure(config):

@@ -16,6 +16,13 @@ from building_llm_from_scratch_amd.train.optim import FusedAdamW
 STEPS = 3
 
 
+def free_port() -> int:
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
 def _cfg(family):
     if family == "llama":
         return get_config("llama3_2", "1B").replace(context_length=16, emb_dim=64, n_heads=4, n_kv_groups=2,
@@ -89,7 +96,7 @@ def test_engine_matches_single_process(kind, family, lora):
     ref_sd, ref_losses = _reference(family, lora)
     with tempfile.TemporaryDirectory() as d:
         out = os.path.join(d, "r.pt")
-        port = 29600 + hash((kind, family, lora)) % 300
+        port = free_port()
         mp.start_processes(_worker, args=(2, kind, family, lora, "none", out, port), nprocs=2, join=True,
                            start_method="spawn")
         res = torch.load(out, weights_only=True)
@@ -107,7 +114,7 @@ def test_fsdp_full_ckpt_and_zero2_mode():
     ref_sd, _ = _reference("llama", False)
     with tempfile.TemporaryDirectory() as d:
         out = os.path.join(d, "r.pt")
-        mp.start_processes(_worker, args=(2, "fsdp", "llama", False, "full", out, 29950), nprocs=2, join=True,
+        mp.start_processes(_worker, args=(2, "fsdp", "llama", False, "full", out, free_port()), nprocs=2, join=True,
                            start_method="spawn")
         sd = torch.load(out, weights_only=True)["sd"]
     for k in ref_sd:

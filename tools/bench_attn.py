@@ -1,0 +1,51 @@
+#!/usr/bin/env python3
+"""Attention kernel micro-benchmark (GPU): fwd / bwd time and effective TFLOP/s at the
+Llama-3-8B (hd 128, GQA 32/8) and GPT-2 (hd 64) training shapes, causal.
+Usage: python tools/bench_attn.py [--iters 20]"""
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from building_llm_from_scratch_amd import ops  # noqa: E402
+
+
+def timeit(fn, iters):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iters", type=int, default=20)
+    a = ap.parse_args()
+    ops.load_ext(required=True)
+    shapes = [("llama3-8B", 4, 1024, 32, 8, 128, 0.0), ("gpt2-774M", 4, 1024, 20, 20, 64, 0.1),
+              ("gpt2-124M", 4, 1024, 12, 12, 64, 0.0)]
+    res = []
+    for name, B, T, H, G, hd, p in shapes:
+        qkv = torch.randn(B * T, (H + 2 * G) * hd, device="cuda", dtype=torch.bfloat16)
+        do = torch.randn(B * T, H * hd, device="cuda", dtype=torch.bfloat16)
+        o, lse = ops.flash_attn_fwd(qkv, B, T, H, G, hd, True, p, 1, 0)
+        tf = timeit(lambda: ops.flash_attn_fwd(qkv, B, T, H, G, hd, True, p, 1, 0), a.iters)
+        tb = timeit(lambda: ops.flash_attn_bwd(qkv, o, lse, do, B, T, H, G, hd, True, p, 1, 0), a.iters)
+        flop = 2 * 2 * B * H * T * T * hd / 2  # causal: two matmuls, half the square
+        res.append(dict(shape=name, fwd_ms=round(tf, 4), bwd_ms=round(tb, 4),
+                        fwd_tflops=round(flop / tf / 1e9, 1), bwd_tflops_5mm=round(2.5 * flop / tb / 1e9, 1)))
+    for r in res:
+        print(json.dumps(r))
+
+
+if __name__ == "__main__":
+    main()
