@@ -65,12 +65,14 @@ __device__ __forceinline__ int ds_off(int q, int key) {
   return q * 256 + ((((key >> 3) ^ (q & 15))) << 4) + ((key & 7) << 1);
 }
 
+// two floats -> packed pair (one v_cvt_pk_bf16_f32 for bf16)
 template <typename T> __device__ __forceinline__ uint32_t pk2(float a, float b) {
-  T x = from_f<T>(a), y = from_f<T>(b);
-  uint16_t ux, uy;
-  __builtin_memcpy(&ux, &x, 2);
-  __builtin_memcpy(&uy, &y, 2);
-  return (uint32_t)ux | ((uint32_t)uy << 16);
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  typedef T t2 __attribute__((ext_vector_type(2)));
+  const t2 v = __builtin_convertvector((f2{a, b}), t2);
+  uint32_t u;
+  __builtin_memcpy(&u, &v, 4);
+  return u;
 }
 
 template <typename v8> __device__ __forceinline__ v8 tr8(const char* base, int off_lo, int off_hi) {
@@ -85,26 +87,41 @@ template <typename v8> __device__ __forceinline__ v8 tr8(const char* base, int o
 
 constexpr int BWD_BKV = 128;  // keys per workgroup
 constexpr int BWD_BQ = 32;    // queries per step
+constexpr int BWD_NBUF = 3;   // LDS ring depth (prefetch distance 2)
 constexpr float kLog2eB = 1.4426950408889634f;
 
-template <typename T, int HD>
-__global__ __launch_bounds__(256, (HD == 64 ? 2 : 1)) void attn_bwd_mfma_k(const T* __restrict__ qkv, const T* __restrict__ dout,
+// LDS bytes of one ring slot of the dK/dV kernel: Q rows, Q^T image, dO rows, dO^T image,
+// and a per-wave copy of the step's lse/delta (so each wave's stats DMA is its own)
+template <int HD> constexpr int dkdv_buf_bytes() { return 4 * BWD_BQ * HD * 2 + 4 * 256; }
+
+// Instruction budget per 32-query step (per wave): 32 MFMAs, 16 b128 + 32 tr_b64 LDS reads at
+// loop-invariant per-lane offsets (+ a per-slot base), ~60 VALU of softmax math (the 1/sqrt(d)
+// of dS is folded into the final dK), 9 saddr LDS-DMA issues whose per-lane offsets are
+// precomputed.  Masking (causal diagonal, sequence tail) and dropout are compile-time variants
+// so the common interior step carries no per-element branches.
+template <typename T, int HD, bool DROP>
+__global__ __launch_bounds__(256, 1) void attn_bwd_mfma_k(const T* __restrict__ qkv, const T* __restrict__ dout,
                                                           const float* __restrict__ lse,
                                                           const float* __restrict__ delta, T* __restrict__ dqkv,
-                                                          float* __restrict__ dkv_part, int T_, int H, int G,
-                                                          bool causal, uint32_t thr, float inv_keep, bool drop,
+                                                          float* __restrict__ dkv_part, int T_, int H, int G, int B_,
+                                                          bool causal, uint32_t thr, float inv_keep,
                                                           uint64_t seed, uint64_t doff) {
   typedef typename MFb<T>::v8 v8;
-  constexpr int KK = HD / 16, DT = HD / 32, CH = HD / 8;
-  constexpr int IMG = BWD_BQ * HD * 2;          // bytes of one [32][HD] image
-  constexpr int PIECES = IMG / 1024;            // 1-KiB DMA pieces per image
-  constexpr int BUF = 4 * IMG + 256;            // QR, QT, OR, OT, lse+delta
+  constexpr int KK = HD / 16, DT = HD / 32, CH = HD / 8, ROWB = HD * 2;
+  constexpr int IMG = BWD_BQ * ROWB;            // bytes of one [32][HD] image
+  constexpr int PPW = IMG / 1024 / 4;           // 1-KiB DMA pieces per wave per image
+  constexpr int BUF = dkdv_buf_bytes<HD>();
+  constexpr int NPW = 4 * PPW + 1;              // DMA instructions per wave per step
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* bufs = smem;                            // 2 x BUF
 
-  const int kb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+  // heaviest (lowest) key block first across the whole grid; all key blocks of one (b, h)
+  // share lin % 8, i.e. one XCD and its L2 (Q / dO re-reads hit there)
+  const int lin = blockIdx.x, nbh = H * B_;
+  const int kb = lin / nbh, bh = lin - kb * nbh;
+  const int h = bh % H, b = bh / H;
   const int g = h / (H / G);
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hh = lane >> 5, l32 = lane & 31;
+  const int tid = threadIdx.x, lane = tid & 63, hh = lane >> 5, l32 = lane & 31;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (scalar branches)
   const int gi = lane & 15, gl = (lane >> 4) & 1, qrow = gi >> 2, pcol = gi & 3;
   const long rs = (long)(H + 2 * G) * HD;
   const long ors = (long)H * HD;
@@ -128,62 +145,121 @@ __global__ __launch_bounds__(256, (HD == 64 ? 2 : 1)) void attn_bwd_mfma_k(const
       kf[kk] = *reinterpret_cast<const v8*>(kb_ + (long)kr * rs + kk * 16 + hh * 8);
       vf[kk] = *reinterpret_cast<const v8*>(vb_ + (long)kr * rs + kk * 16 + hh * 8);
     }
+    // consume the fragments here: the compiler then retires these loads before the loop and
+    // inserts no vmcnt waits inside it (it cannot see the asm-issued DMA, whose counts the
+    // loop manages itself)
+#pragma unroll
+    for (int kk = 0; kk < KK; ++kk) asm volatile("" ::"v"(kf[kk]), "v"(vf[kk]));
   }
   f32x16 dk[DT], dv[DT];
 #pragma unroll
   for (int i = 0; i < DT; ++i) { dk[i] = f32x16{}; dv[i] = f32x16{}; }
 
-  // DMA of one query step (Q and dO, each into a row image and a transposed image) + stats
-  auto issue = [&](int q0, int buf) {
-    char* base = bufs + buf * BUF;
-    for (int pc_ = w; pc_ < 4 * PIECES; pc_ += 4) {
-      const int img = pc_ / PIECES, piece = pc_ % PIECES;
-      const int P = piece * 64 + lane;
-      const int r = P / CH, pc = P % CH;
-      int qrow_g = q0 + r;
-      qrow_g = qrow_g < T_ ? qrow_g : T_ - 1;
-      int c16;
-      if ((img & 1) == 0) {  // row image
-        if constexpr (HD == 128) c16 = pc ^ (r & 15); else c16 = pc ^ ((r >> 1) & 7);
-      } else {               // transposed image
-        const int c64 = (pc >> 2) ^ (HD == 128 ? (r & 3) : ((r >> 1) & 1));
-        c16 = c64 * 4 + (pc & 3);
+  // ---- loop-invariant per-lane offsets
+  int roff[KK];                                   // MFMA A rows (row image)
+#pragma unroll
+  for (int kk = 0; kk < KK; ++kk) roff[kk] = r_off<HD>(l32, kk * 2 + hh);
+  int troff[DT];                                  // transposed reads (rows +16*s2, +8 are immediates)
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) troff[dt] = t_off<HD>(4 * hh + qrow, dt * 32 + gl * 16 + pcol * 4);
+  uint32_t qoff[2][PPW], ooff[2][PPW];            // DMA source byte offsets from the step's row q0
+  int prow[PPW], pc16[2][PPW];
+#pragma unroll
+  for (int j = 0; j < PPW; ++j) {
+    const int P = (w + 4 * j) * 64 + lane;
+    const int r = P / CH, pc = P % CH;
+    int rc, tc;
+    if constexpr (HD == 128) rc = pc ^ (r & 15); else rc = pc ^ ((r >> 1) & 7);
+    {
+      const int c64 = (pc >> 2) ^ (HD == 128 ? (r & 3) : ((r >> 1) & 1));
+      tc = c64 * 4 + (pc & 3);
+    }
+    prow[j] = r;
+    pc16[0][j] = rc;
+    pc16[1][j] = tc;
+    qoff[0][j] = (uint32_t)(r * rs * 2 + rc * 16);
+    qoff[1][j] = (uint32_t)(r * rs * 2 + tc * 16);
+    ooff[0][j] = (uint32_t)(r * ors * 2 + rc * 16);
+    ooff[1][j] = (uint32_t)(r * ors * 2 + tc * 16);
+  }
+  const uint32_t smem_u = lds_u32(smem);
+  const float* stat_src = (lane < 32 ? lse_ : del_);
+
+  // DMA of one 32-query step into ring slot `slot`
+  auto issue = [&](int q0, int slot) {
+    const uint32_t base = smem_u + slot * BUF;
+    if (q0 + BWD_BQ <= T_) {
+      const void* qs = sgpr_ptr(qb_ + (long)q0 * rs);
+      const void* os = sgpr_ptr(ob_ + (long)q0 * ors);
+#pragma unroll
+      for (int j = 0; j < PPW; ++j) {
+        const uint32_t pd = (w + 4 * j) * 1024;
+        glds16s(qs, qoff[0][j], base + pd);
+        glds16s(qs, qoff[1][j], base + IMG + pd);
+        glds16s(os, ooff[0][j], base + 2 * IMG + pd);
+        glds16s(os, ooff[1][j], base + 3 * IMG + pd);
       }
-      const T* src = (img < 2) ? (qb_ + (long)qrow_g * rs + c16 * 8) : (ob_ + (long)qrow_g * ors + c16 * 8);
-      glds16(src, base + img * IMG + piece * 1024);
+    } else {  // sequence tail: clamp rows (rows >= T_ are masked in the step)
+#pragma unroll
+      for (int j = 0; j < PPW; ++j) {
+        const uint32_t pd = (w + 4 * j) * 1024;
+        const int r = min(q0 + prow[j], T_ - 1);
+        char* lb = smem + slot * BUF;
+        glds16(qb_ + (long)r * rs + pc16[0][j] * 8, lb + pd);
+        glds16(qb_ + (long)r * rs + pc16[1][j] * 8, lb + IMG + pd);
+        glds16(ob_ + (long)r * ors + pc16[0][j] * 8, lb + 2 * IMG + pd);
+        glds16(ob_ + (long)r * ors + pc16[1][j] * 8, lb + 3 * IMG + pd);
+      }
     }
-    if (w == 0) {
-      int qq = q0 + (lane & 31);
-      qq = qq < T_ ? qq : T_ - 1;
-      const float* src = (lane < 32) ? (lse_ + qq) : (del_ + qq);
-      glds4(src, base + 4 * IMG);
-    }
+    glds4(stat_src + min(q0 + l32, T_ - 1), smem + slot * BUF + 4 * IMG + w * 256);
   };
 
   const int qstart = causal ? k0 : 0;
-  int it = 0;
-  if (qstart < T_) issue(qstart, 0);
-  wait_vm0();
-  __syncthreads();
-  for (int q0 = qstart; q0 < T_; q0 += BWD_BQ, ++it) {
-    const int buf = it & 1;
-    if (q0 + BWD_BQ < T_) issue(q0 + BWD_BQ, buf ^ 1);
-    const char* QR = bufs + buf * BUF;
-    const char* QT = QR + IMG;
-    const char* OR = QR + 2 * IMG;
-    const char* OT = QR + 3 * IMG;
-    const float* LS = reinterpret_cast<const float*>(QR + 4 * IMG);   // lse[32], delta[32]
-    const bool active = (!causal || q0 + BWD_BQ - 1 >= kw0) && kw0 < T_;  // wave-uniform
-    if (active) {
+  const int nsteps = qstart < T_ ? (T_ - qstart + BWD_BQ - 1) / BWD_BQ : 0;
+  if (nsteps > 0) issue(qstart, 0);
+  if (nsteps > 1) {
+    issue(qstart + BWD_BQ, 1);
+    wait_vm<NPW>();
+  } else {
+    wait_vm0();
+  }
+  __builtin_amdgcn_s_barrier();
+  // Steps before this wave's first active one (causal: the wave's keys are above them) only
+  // keep the DMA ring and the barriers going; the compute loop after them runs the MFMAs on
+  // every step, so dK/dV stay in the same accumulator registers across iterations.
+  const int first = kw0 >= T_ ? nsteps : (causal ? min(w, nsteps) : 0);
+  int slot = 0, i = 0;
+  for (; i < first; ++i) {
+    const bool pre = i + 2 < nsteps;
+    if (pre) issue(qstart + (i + 2) * BWD_BQ, slot == 0 ? 2 : slot - 1);
+    if (pre) wait_vm<NPW>(); else wait_vm0();
+    __builtin_amdgcn_s_barrier();
+    slot = slot == 2 ? 0 : slot + 1;
+  }
+  for (; i < nsteps; ++i) {
+    const int q0 = qstart + i * BWD_BQ;
+    const bool pre = i + 2 < nsteps;
+    if (pre) issue(q0 + 2 * BWD_BQ, slot == 0 ? 2 : slot - 1);
+    const char* S = smem + slot * BUF;
+    // wave-uniform: the diagonal step or a sequence tail needs masking
+    const bool edge = (causal && i == first) || q0 + BWD_BQ > T_ || kw0 + 32 > T_;
+    {
       f32x16 sacc = f32x16{}, dpacc = f32x16{};
 #pragma unroll
       for (int kk = 0; kk < KK; ++kk) {
-        const v8 aq = *reinterpret_cast<const v8*>(QR + r_off<HD>(l32, kk * 2 + hh));
-        sacc = MFb<T>::mma(aq, kf[kk], sacc);
-        const v8 ao = *reinterpret_cast<const v8*>(OR + r_off<HD>(l32, kk * 2 + hh));
-        dpacc = MFb<T>::mma(ao, vf[kk], dpacc);
+        sacc = MFb<T>::mma(*reinterpret_cast<const v8*>(S + roff[kk]), kf[kk], sacc);
+        dpacc = MFb<T>::mma(*reinterpret_cast<const v8*>(S + 2 * IMG + roff[kk]), vf[kk], dpacc);
       }
       // rows of this lane's accumulator registers: q = q0 + (r&3) + 8(r>>2) + 4hh
+      if (edge) {  // uniform branch: -inf the masked scores (causal diagonal, sequence tail)
+        const int qb0 = q0 + 4 * hh;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int q = qb0 + (r & 3) + 8 * (r >> 2);
+          if ((causal && mykey > q) || q >= T_ || mykey >= T_) sacc[r] = -INFINITY;
+        }
+      }
+      const float* LS = reinterpret_cast<const float*>(S + 4 * IMG + w * 256);
 #pragma unroll
       for (int gq = 0; gq < 4; ++gq) {
         const f32x4 L4 = *reinterpret_cast<const f32x4*>(LS + 8 * gq + 4 * hh);
@@ -191,17 +267,16 @@ __global__ __launch_bounds__(256, (HD == 64 ? 2 : 1)) void attn_bwd_mfma_k(const
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int r = 4 * gq + j;
-          const int q = q0 + 8 * gq + 4 * hh + j;
-          float p = exp2f(sacc[r] * c - L4[j]);
-          if ((causal && mykey > q) || q >= T_ || mykey >= T_) p = 0.f;
+          const float p = __builtin_amdgcn_exp2f(fmaf(sacc[r], c, -L4[j]));
           float dp = dpacc[r], pd = p;
-          if (drop) {
+          if constexpr (DROP) {
+            const int q = q0 + 8 * gq + 4 * hh + j;
             const bool keep = drop_hash(seed, doff + (((uint64_t)(b * H + h) * T_ + q) * T_ + mykey)) >= thr;
             pd = keep ? p * inv_keep : 0.f;
             dp = keep ? dp * inv_keep : 0.f;
           }
           sacc[r] = pd;
-          dpacc[r] = p * (dp - D4[j]) * scale;
+          dpacc[r] = p * (dp - D4[j]);
         }
       }
       // dV^T += dO^T Pd ; dK^T += Q^T dS   (B operands straight from the accumulators)
@@ -218,19 +293,19 @@ __global__ __launch_bounds__(256, (HD == 64 ? 2 : 1)) void attn_bwd_mfma_k(const
           __builtin_memcpy(&pf, u, 16);
           __builtin_memcpy(&df, v, 16);
         }
-        const int base = s2 * 16 + 4 * hh + qrow;
 #pragma unroll
         for (int dt = 0; dt < DT; ++dt) {
-          const int col = dt * 32 + gl * 16 + pcol * 4;
-          const v8 ao = tr8<v8>(OT, t_off<HD>(base, col), t_off<HD>(base + 8, col));
+          const int o = troff[dt] + s2 * 16 * ROWB;
+          const v8 ao = tr8<v8>(S + 3 * IMG, o, o + 8 * ROWB);
           dv[dt] = MFb<T>::mma(ao, pf, dv[dt]);
-          const v8 aq = tr8<v8>(QT, t_off<HD>(base, col), t_off<HD>(base + 8, col));
+          const v8 aq = tr8<v8>(S + IMG, o, o + 8 * ROWB);
           dk[dt] = MFb<T>::mma(aq, df, dk[dt]);
         }
       }
     }
-    wait_vm0();
-    __syncthreads();
+    if (pre) wait_vm<NPW>(); else wait_vm0();
+    __builtin_amdgcn_s_barrier();
+    slot = slot == 2 ? 0 : slot + 1;
   }
 
   // ---- MHA: write bf16 dK/dV straight into dqkv; GQA: per-head fp32 partials
@@ -243,15 +318,15 @@ __global__ __launch_bounds__(256, (HD == 64 ? 2 : 1)) void attn_bwd_mfma_k(const
       for (int gq = 0; gq < 4; ++gq) {
         const int d0 = dt * 32 + 8 * gq + 4 * hh;
         uint2 a, bb;
-        a.x = pk2<T>(dk[dt][4 * gq], dk[dt][4 * gq + 1]);
-        a.y = pk2<T>(dk[dt][4 * gq + 2], dk[dt][4 * gq + 3]);
+        a.x = pk2<T>(dk[dt][4 * gq] * scale, dk[dt][4 * gq + 1] * scale);
+        a.y = pk2<T>(dk[dt][4 * gq + 2] * scale, dk[dt][4 * gq + 3] * scale);
         bb.x = pk2<T>(dv[dt][4 * gq], dv[dt][4 * gq + 1]);
         bb.y = pk2<T>(dv[dt][4 * gq + 2], dv[dt][4 * gq + 3]);
         *reinterpret_cast<uint2*>(pk + d0) = a;
         *reinterpret_cast<uint2*>(pv + d0) = bb;
       }
   } else if (mykey < T_) {
-    const long BT = (long)gridDim.z * T_;
+    const long BT = (long)B_ * T_;
     float* pk = dkv_part + ((long)b * T_ + mykey) * ors + (long)h * HD;
     float* pv = pk + BT * ors;
 #pragma unroll
@@ -259,42 +334,52 @@ __global__ __launch_bounds__(256, (HD == 64 ? 2 : 1)) void attn_bwd_mfma_k(const
 #pragma unroll
       for (int gq = 0; gq < 4; ++gq) {
         const int d0 = dt * 32 + 8 * gq + 4 * hh;
-        *reinterpret_cast<f32x4*>(pk + d0) = f32x4{dk[dt][4 * gq], dk[dt][4 * gq + 1], dk[dt][4 * gq + 2], dk[dt][4 * gq + 3]};
+        *reinterpret_cast<f32x4*>(pk + d0) = f32x4{dk[dt][4 * gq] * scale, dk[dt][4 * gq + 1] * scale,
+                                                   dk[dt][4 * gq + 2] * scale, dk[dt][4 * gq + 3] * scale};
         *reinterpret_cast<f32x4*>(pv + d0) = f32x4{dv[dt][4 * gq], dv[dt][4 * gq + 1], dv[dt][4 * gq + 2], dv[dt][4 * gq + 3]};
       }
   }
 }
 
 // ---------------------------------------------------------------------------------------
-// dQ kernel (forward-shaped): 4 waves x 32 queries of head h; key tiles of 64 by DMA into
-// three images per buffer: K rows (S^T = K Q^T), K transposed (dQ^T += K^T dS^T), V rows
-// (dP^T = V dO^T).  The query is the lane column, so lse / delta are per-lane scalars.
-template <typename T, int HD>
-__global__ __launch_bounds__(256, 2) void attn_bwd_dq_k(const T* __restrict__ qkv, const T* __restrict__ dout,
+// dQ kernel (forward-shaped): 4 waves x 32 queries of head h; key tiles of 64 by saddr DMA
+// (3-slot ring, prefetch distance 2) into three images per slot: K rows (S^T = K Q^T),
+// K transposed (dQ^T += K^T dS^T), V rows (dP^T = V dO^T).  The query is the lane column, so
+// lse / delta are per-lane scalars; 1/sqrt(d) is applied once to the final dQ.
+constexpr int DQ_BQ = 128, DQ_BK = 64, DQ_NBUF = 3;
+template <int HD> constexpr int dq_buf_bytes() { return 3 * DQ_BK * HD * 2; }
+
+template <typename T, int HD, bool DROP>
+__global__ __launch_bounds__(256, 1) void attn_bwd_dq_k(const T* __restrict__ qkv, const T* __restrict__ dout,
                                                         const float* __restrict__ lse,
                                                         const float* __restrict__ delta, T* __restrict__ dqkv,
-                                                        int T_, int H, int G, bool causal, uint32_t thr,
-                                                        float inv_keep, bool drop, uint64_t seed, uint64_t doff) {
+                                                        int T_, int H, int G, int B_, bool causal, uint32_t thr,
+                                                        float inv_keep, uint64_t seed, uint64_t doff) {
   typedef typename MFb<T>::v8 v8;
-  constexpr int BQ = 128, BK = 64;
-  constexpr int KK = HD / 16, DT = HD / 32, CH = HD / 8;
-  constexpr int IMG = BK * HD * 2;              // bytes of one [64][HD] image
-  constexpr int LD = BK * CH / 256;             // 1-KiB pieces per wave per image
-  constexpr int BUF = 3 * IMG;                  // K rows, K transposed, V rows
+  constexpr int KK = HD / 16, DT = HD / 32, CH = HD / 8, ROWB = HD * 2;
+  constexpr int IMG = DQ_BK * ROWB;             // bytes of one [64][HD] image
+  constexpr int LD = DQ_BK * CH / 256;          // 1-KiB pieces per wave per image
+  constexpr int BUF = dq_buf_bytes<HD>();
+  constexpr int NPW = 3 * LD;                   // DMA instructions per wave per step
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
-  const int nqb = (T_ + BQ - 1) / BQ;
-  const int qb = nqb - 1 - (int)blockIdx.x;
-  const int h = blockIdx.y, b = blockIdx.z;
+  // heaviest (last, for causal) query block first; one (b, h) per XCD residue
+  const int nqb = (T_ + DQ_BQ - 1) / DQ_BQ;
+  const int lin = blockIdx.x, nbh = H * B_;
+  const int qbi = lin / nbh, bh = lin - qbi * nbh;
+  const int qb = causal ? nqb - 1 - qbi : qbi;
+  const int h = bh % H, b = bh / H;
   const int g = h / (H / G);
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hh = lane >> 5, l32 = lane & 31;
+  const int tid = threadIdx.x, lane = tid & 63, hh = lane >> 5, l32 = lane & 31;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int gi = lane & 15, gl = (lane >> 4) & 1, qrow = gi >> 2, pcol = gi & 3;
   const long rs = (long)(H + 2 * G) * HD;
   const long ors = (long)H * HD;
   const T* kb_ = qkv + (long)b * T_ * rs + (long)(H + g) * HD;
   const T* vb_ = qkv + (long)b * T_ * rs + (long)(H + G + g) * HD;
-  const int q0 = qb * BQ;
-  const int qi = q0 + w * 32 + l32;
+  const int q0 = qb * DQ_BQ;
+  const int wq_lo = q0 + w * 32, wq_hi = wq_lo + 31;
+  const int qi = wq_lo + l32;
   const int qc = qi < T_ ? qi : T_ - 1;
   const float scale = rsqrtf((float)HD), c = scale * kLog2eB;
 
@@ -306,88 +391,147 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_k(const T* __restrict__ qk
   }
   const float L = lse[((long)b * H + h) * T_ + qc];
   const float D = delta[((long)b * H + h) * T_ + qc];
+  {
+    float lt = L, dt_ = D;
+#pragma unroll
+    for (int kk = 0; kk < KK; ++kk) asm volatile("" ::"v"(qf[kk]), "v"(of[kk]));
+    asm volatile("" ::"v"(lt), "v"(dt_));
+  }
   f32x16 dq[DT];
 #pragma unroll
   for (int i = 0; i < DT; ++i) dq[i] = f32x16{};
 
-  auto issue = [&](int t, int buf) {
-    char* base = smem + buf * BUF;
+  int roff[KK];
 #pragma unroll
-    for (int i = 0; i < LD; ++i) {
-      const int piece = w * LD + i;
-      const int P = piece * 64 + lane;
-      const int r = P / CH, pc = P % CH;
-      int key = t * BK + r;
-      key = key < T_ ? key : T_ - 1;
-      int rc16;
-      if constexpr (HD == 128) rc16 = pc ^ (r & 15); else rc16 = pc ^ ((r >> 1) & 7);
-      const int c64 = (pc >> 2) ^ (HD == 128 ? (r & 3) : ((r >> 1) & 1));
-      const int tc16 = c64 * 4 + (pc & 3);
-      glds16(kb_ + (long)key * rs + rc16 * 8, base + piece * 1024);
-      glds16(kb_ + (long)key * rs + tc16 * 8, base + IMG + piece * 1024);
-      glds16(vb_ + (long)key * rs + rc16 * 8, base + 2 * IMG + piece * 1024);
+  for (int kk = 0; kk < KK; ++kk) roff[kk] = r_off<HD>(l32, kk * 2 + hh);
+  int troff[DT];
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) troff[dt] = t_off<HD>(4 * hh + qrow, dt * 32 + gl * 16 + pcol * 4);
+  uint32_t roffg[LD], toffg[LD];
+  int prow[LD], prc[LD], ptc[LD];
+#pragma unroll
+  for (int i = 0; i < LD; ++i) {
+    const int P = (w * LD + i) * 64 + lane;
+    const int r = P / CH, pc = P % CH;
+    int rc;
+    if constexpr (HD == 128) rc = pc ^ (r & 15); else rc = pc ^ ((r >> 1) & 7);
+    const int c64 = (pc >> 2) ^ (HD == 128 ? (r & 3) : ((r >> 1) & 1));
+    const int tc = c64 * 4 + (pc & 3);
+    prow[i] = r; prc[i] = rc; ptc[i] = tc;
+    roffg[i] = (uint32_t)(r * rs * 2 + rc * 16);
+    toffg[i] = (uint32_t)(r * rs * 2 + tc * 16);
+  }
+  const uint32_t smem_u = lds_u32(smem);
+
+  auto issue = [&](int t, int slot) {
+    const int k0 = t * DQ_BK;
+    const uint32_t base = smem_u + slot * BUF;
+    if (k0 + DQ_BK <= T_) {
+      const void* ks = sgpr_ptr(kb_ + (long)k0 * rs);
+      const void* vs = sgpr_ptr(vb_ + (long)k0 * rs);
+#pragma unroll
+      for (int i = 0; i < LD; ++i) {
+        const uint32_t pd = (w * LD + i) * 1024;
+        glds16s(ks, roffg[i], base + pd);
+        glds16s(ks, toffg[i], base + IMG + pd);
+        glds16s(vs, roffg[i], base + 2 * IMG + pd);
+      }
+    } else {  // sequence tail: clamp rows (keys >= T_ are masked)
+      char* lb = smem + slot * BUF;
+#pragma unroll
+      for (int i = 0; i < LD; ++i) {
+        const int pd = (w * LD + i) * 1024;
+        const int key = min(k0 + prow[i], T_ - 1);
+        glds16(kb_ + (long)key * rs + prc[i] * 8, lb + pd);
+        glds16(kb_ + (long)key * rs + ptc[i] * 8, lb + IMG + pd);
+        glds16(vb_ + (long)key * rs + prc[i] * 8, lb + 2 * IMG + pd);
+      }
     }
   };
 
-  const int kend = causal ? min(T_, q0 + BQ) : T_;
-  const int ntiles = (kend + BK - 1) / BK;
-  const int wq_lo = q0 + w * 32, wq_hi = wq_lo + 31;
-  issue(0, 0);
-  wait_vm0();
-  __syncthreads();
-  for (int t = 0; t < ntiles; ++t) {
-    const int buf = t & 1;
-    if (t + 1 < ntiles) issue(t + 1, buf ^ 1);
-    const int k0 = t * BK;
-    if ((!causal || k0 <= wq_hi) && wq_lo < T_) {
-      const char* KR = smem + buf * BUF;
-      const char* KT = KR + IMG;
-      const char* VR = KR + 2 * IMG;
-      f32x16 s[2], dp[2];
+  const int kend = causal ? min(T_, q0 + DQ_BQ) : T_;
+  const int ntiles = (kend + DQ_BK - 1) / DQ_BK;
+  // tiles this wave computes: all up to the one holding its last query (causal)
+  const int nact = wq_lo >= T_ ? 0 : (causal ? min(ntiles, wq_hi / DQ_BK + 1) : ntiles);
+  if (ntiles > 0) issue(0, 0);
+  if (ntiles > 1) {
+    issue(1, 1);
+    wait_vm<NPW>();
+  } else {
+    wait_vm0();
+  }
+  __builtin_amdgcn_s_barrier();
+  int slot = 0, t = 0;
+  for (; t < nact; ++t) {
+    const bool pre = t + 2 < ntiles;
+    if (pre) issue(t + 2, slot == 0 ? 2 : slot - 1);
+    const int k0 = t * DQ_BK;
+    const char* KR = smem + slot * BUF;
+    const char* KT = KR + IMG;
+    const char* VR = KR + 2 * IMG;
+    f32x16 sc[2], dp[2];
 #pragma unroll
-      for (int kt = 0; kt < 2; ++kt) {
-        s[kt] = f32x16{};
-        dp[kt] = f32x16{};
+    for (int kt = 0; kt < 2; ++kt) {
+      sc[kt] = f32x16{};
+      dp[kt] = f32x16{};
 #pragma unroll
-        for (int kk = 0; kk < KK; ++kk) {
-          const int off = r_off<HD>(kt * 32 + l32, kk * 2 + hh);
-          s[kt] = MFb<T>::mma(*reinterpret_cast<const v8*>(KR + off), qf[kk], s[kt]);
-          dp[kt] = MFb<T>::mma(*reinterpret_cast<const v8*>(VR + off), of[kk], dp[kt]);
-        }
+      for (int kk = 0; kk < KK; ++kk) {
+        const int off = kt * 32 * ROWB + roff[kk];
+        sc[kt] = MFb<T>::mma(*reinterpret_cast<const v8*>(KR + off), qf[kk], sc[kt]);
+        dp[kt] = MFb<T>::mma(*reinterpret_cast<const v8*>(VR + off), of[kk], dp[kt]);
       }
+    }
+    // keys of this lane's accumulator rows: k0 + 32kt + (r&3) + 8(r>>2) + 4hh
+    const bool edge = (causal && k0 + DQ_BK - 1 > wq_lo) || k0 + DQ_BK > T_ || wq_hi >= T_;
+    if (edge) {
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int key = k0 + kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
-          float p = exp2f(s[kt][r] * c - L);
-          if ((causal && key > qi) || key >= T_ || qi >= T_) p = 0.f;
-          float d = dp[kt][r];
-          if (drop) d = (drop_hash(seed, doff + (((uint64_t)(b * H + h) * T_ + qi) * T_ + key)) >= thr) ? d * inv_keep : 0.f;
-          s[kt][r] = p * (d - D) * scale;
-        }
-#pragma unroll
-      for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) {
-          v8 df;
-          {
-            uint32_t u[4];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) u[j] = pk2<T>(s[kt][8 * s2 + 2 * j], s[kt][8 * s2 + 2 * j + 1]);
-            __builtin_memcpy(&df, u, 16);
-          }
-          const int base = kt * 32 + s2 * 16 + 4 * hh + qrow;
-#pragma unroll
-          for (int dt = 0; dt < DT; ++dt) {
-            const int col = dt * 32 + gl * 16 + pcol * 4;
-            const v8 a = tr8<v8>(KT, t_off<HD>(base, col), t_off<HD>(base + 8, col));
-            dq[dt] = MFb<T>::mma(a, df, dq[dt]);
-          }
+          if ((causal && key > qi) || key >= T_ || qi >= T_) sc[kt][r] = -INFINITY;
         }
     }
-    wait_vm0();
-    __syncthreads();
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float p = __builtin_amdgcn_exp2f(fmaf(sc[kt][r], c, -L));
+        float d = dp[kt][r];
+        if constexpr (DROP) {
+          const int key = k0 + kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+          d = (drop_hash(seed, doff + (((uint64_t)(b * H + h) * T_ + qi) * T_ + key)) >= thr) ? d * inv_keep : 0.f;
+        }
+        sc[kt][r] = p * (d - D);
+      }
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        v8 df;
+        {
+          uint32_t u[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) u[j] = pk2<T>(sc[kt][8 * s2 + 2 * j], sc[kt][8 * s2 + 2 * j + 1]);
+          __builtin_memcpy(&df, u, 16);
+        }
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) {
+          const int o = troff[dt] + (kt * 32 + s2 * 16) * ROWB;
+          const v8 a = tr8<v8>(KT, o, o + 8 * ROWB);
+          dq[dt] = MFb<T>::mma(a, df, dq[dt]);
+        }
+      }
+    if (pre) wait_vm<NPW>(); else wait_vm0();
+    __builtin_amdgcn_s_barrier();
+    slot = slot == 2 ? 0 : slot + 1;
+  }
+  for (; t < ntiles; ++t) {  // this wave is done; keep the ring and barriers going
+    const bool pre = t + 2 < ntiles;
+    if (pre) issue(t + 2, slot == 0 ? 2 : slot - 1);
+    if (pre) wait_vm<NPW>(); else wait_vm0();
+    __builtin_amdgcn_s_barrier();
+    slot = slot == 2 ? 0 : slot + 1;
   }
   if (qi < T_) {
     T* row = dqkv + ((long)b * T_ + qi) * rs + (long)h * HD;
@@ -397,8 +541,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_k(const T* __restrict__ qk
       for (int gq = 0; gq < 4; ++gq) {
         const int d0 = dt * 32 + 8 * gq + 4 * hh;
         uint2 v;
-        v.x = pk2<T>(dq[dt][4 * gq], dq[dt][4 * gq + 1]);
-        v.y = pk2<T>(dq[dt][4 * gq + 2], dq[dt][4 * gq + 3]);
+        v.x = pk2<T>(dq[dt][4 * gq] * scale, dq[dt][4 * gq + 1] * scale);
+        v.y = pk2<T>(dq[dt][4 * gq + 2] * scale, dq[dt][4 * gq + 3] * scale);
         *reinterpret_cast<uint2*>(row + d0) = v;
       }
   }
@@ -436,17 +580,27 @@ void attn_bwd_mfma(DType dt, const void* qkv, const void* o, const float* lse, c
   const uint32_t thr = drop_threshold(p);
   const float ik = p > 0.f ? 1.f / (1.f - p) : 1.f;
   attn_delta(dt, o, dout, delta, B, T_, H, hd, s);
-  dim3 grid_kv((T_ + BWD_BKV - 1) / BWD_BKV, H, B), grid_q((T_ + 127) / 128, H, B), block(256);
-  auto lds_kv = [](int HD) { return 2 * (4 * BWD_BQ * HD * 2 + 256); };
-  auto lds_q = [](int HD) { return 2 * 3 * 64 * HD * 2; };
+  const int nkb = (T_ + BWD_BKV - 1) / BWD_BKV;
+  dim3 grid_kv(nkb * H * B), grid_q(((T_ + DQ_BQ - 1) / DQ_BQ) * H * B), block(256);
+  const bool drop = p > 0.f;
 #define LAUNCH(TT, HDD)                                                                                         \
   do {                                                                                                          \
-    hipLaunchKernelGGL((attn_bwd_mfma_k<TT, HDD>), grid_kv, block, lds_kv(HDD), s, (const TT*)qkv,            \
-                       (const TT*)dout, lse, delta, (TT*)dqkv, dkv_part, T_, H, G, causal, thr, ik, p > 0.f,    \
-                       seed, offset);                                                                           \
-    hipLaunchKernelGGL((attn_bwd_dq_k<TT, HDD>), grid_q, block, lds_q(HDD), s, (const TT*)qkv,                 \
-                       (const TT*)dout, lse, delta, (TT*)dqkv, T_, H, G, causal, thr, ik, p > 0.f, seed,       \
-                       offset);                                                                                 \
+    const int lds_kv = BWD_NBUF * dkdv_buf_bytes<HDD>();                                                        \
+    if (drop)                                                                                                   \
+      hipLaunchKernelGGL((attn_bwd_mfma_k<TT, HDD, true>), grid_kv, block, lds_kv, s, (const TT*)qkv,          \
+                         (const TT*)dout, lse, delta, (TT*)dqkv, dkv_part, T_, H, G, B, causal, thr, ik, seed, \
+                         offset);                                                                               \
+    else                                                                                                        \
+      hipLaunchKernelGGL((attn_bwd_mfma_k<TT, HDD, false>), grid_kv, block, lds_kv, s, (const TT*)qkv,         \
+                         (const TT*)dout, lse, delta, (TT*)dqkv, dkv_part, T_, H, G, B, causal, thr, ik, seed, \
+                         offset);                                                                               \
+    const int lds_q = DQ_NBUF * dq_buf_bytes<HDD>();                                                           \
+    if (drop)                                                                                                   \
+      hipLaunchKernelGGL((attn_bwd_dq_k<TT, HDD, true>), grid_q, block, lds_q, s, (const TT*)qkv,               \
+                         (const TT*)dout, lse, delta, (TT*)dqkv, T_, H, G, B, causal, thr, ik, seed, offset);   \
+    else                                                                                                        \
+      hipLaunchKernelGGL((attn_bwd_dq_k<TT, HDD, false>), grid_q, block, lds_q, s, (const TT*)qkv,              \
+                         (const TT*)dout, lse, delta, (TT*)dqkv, T_, H, G, B, causal, thr, ik, seed, offset);   \
   } while (0)
   if (dt == DType::BF16) {
     if (hd == 128) LAUNCH(bf16_t, 128); else LAUNCH(bf16_t, 64);

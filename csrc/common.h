@@ -130,6 +130,27 @@ __device__ __forceinline__ void glds4(const void* gsrc, const void* lds_dst) {
                : "=&s"(keep) : "v"(gsrc), "s"(lds) : "memory");
 }
 __device__ __forceinline__ void wait_vm0() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+// wait until at most N vector-memory ops of this wave are outstanding (prefetch depth > 1)
+template <int N> __device__ __forceinline__ void wait_vm() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+
+// wave-uniform 64-bit pointer materialised in SGPRs (for the saddr form of LDS-DMA)
+__device__ __forceinline__ const void* sgpr_ptr(const void* p) {
+  const uint64_t v = (uint64_t)(uintptr_t)p;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return (const void*)(uintptr_t)(((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ uint32_t lds_u32(const void* p) {
+  return __builtin_amdgcn_readfirstlane(
+      (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p);
+}
+// LDS-DMA, saddr form: uniform SGPR base + per-lane 32-bit byte offset (loop-invariant, so a
+// tile step needs no per-lane address arithmetic); lds_dst is a wave-uniform LDS byte address.
+__device__ __forceinline__ void glds16s(const void* sbase, uint32_t voff, uint32_t lds_dst) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(voff), "s"(sbase), "s"(lds_dst) : "memory");
+}
 
 inline int ceil_div(long a, long b) { return (int)((a + b - 1) / b); }
 

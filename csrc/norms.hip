@@ -3,15 +3,15 @@
 // Replaces reference Models/Llama/common_components.py:54-70 (RMSNorm) and nn.LayerNorm
 // (Models/GPT2/GPT2.py:79-80).  Memory-bound: one wave64 per row, the row held in VGPRs
 // (16-B loads, NV vectors per lane), fp32 statistics, one pass over x in forward and one
-// over (x, dy[, dx_acc]) in backward.  Weight/bias gradients: per-lane register
-// accumulators -> LDS float atomics across the 4 waves of a workgroup -> one fp32 partial
-// row per workgroup -> a column-reduction kernel (deterministic, no global atomics).
+// over (x, dy[, dx_acc]) in backward (one workgroup per row there).  Weight/bias gradients:
+// per-thread register accumulators for the columns a thread owns -> one fp32 partial row per
+// workgroup -> a column-reduction kernel (deterministic, no global atomics).
 #include "common.h"
 
 namespace bllm {
 
 constexpr int ROWS_PER_WG = 4;  // 4 waves x 1 row
-constexpr int MAX_BWD_WG = 512;
+constexpr int MAX_BWD_WG = 1024;
 
 template <typename T, int NV, bool LN>
 __global__ __launch_bounds__(256) void norm_fwd_k(const T* __restrict__ x, const T* __restrict__ w,
@@ -77,6 +77,13 @@ __global__ __launch_bounds__(256) void norm_fwd_k(const T* __restrict__ x, const
 }
 
 // backward: dx = rs * (g - [LN: mean(g)] - xhat * mean(g * xhat)) (+ dx_acc), g = dy * w
+// One WORKGROUP per row (rows grid-strided): a row of d=4096 bf16 is 512 16-B vectors, i.e.
+// NV=2 per thread at 256 threads, so the per-thread state (raw x/dy vectors + the dW/dB
+// column accumulators, which each thread owns exclusively for its columns) stays far below
+// the VGPR budget and several workgroups share a CU to hide HBM latency.  The two row sums
+// cross the 4 waves through a parity-double-buffered LDS slot (one barrier per row).  Each
+// workgroup writes one fp32 partial row for dW (and dB); col_reduce_k sums them in a fixed
+// order (deterministic, no global atomics).
 template <typename T, int NV, bool LN>
 __global__ __launch_bounds__(256) void norm_bwd_k(const T* __restrict__ dy, const T* __restrict__ x,
                                                   const T* __restrict__ w, const float* __restrict__ mean,
@@ -84,64 +91,79 @@ __global__ __launch_bounds__(256) void norm_bwd_k(const T* __restrict__ dy, cons
                                                   T* __restrict__ dx, float* __restrict__ part_w,
                                                   float* __restrict__ part_b, int N, int d) {
   constexpr int VEC = 16 / sizeof(T);
-  extern __shared__ __attribute__((aligned(16))) float lds[];  // [d] (+[d] for LN bias)
-  const int lane = threadIdx.x & 63;
+  __shared__ float red[2][4][2];
+  const int tid = threadIdx.x, lane = tid & 63, wv_id = tid >> 6;
+  const int nwaves = blockDim.x >> 6;
   const int nvec = d / VEC;
-  for (int i = threadIdx.x; i < d * (LN ? 2 : 1); i += blockDim.x) lds[i] = 0.f;
-  float aw[NV][VEC], ab[NV][VEC];
+  float aw[NV][VEC], ab[LN ? NV : 1][VEC];
 #pragma unroll
   for (int i = 0; i < NV; ++i)
 #pragma unroll
-    for (int j = 0; j < VEC; ++j) { aw[i][j] = 0.f; ab[i][j] = 0.f; }
-  float wf[NV][VEC];
-#pragma unroll
-  for (int i = 0; i < NV; ++i) {
-    const int c = lane + 64 * i;
-    if (c < nvec) {
-      Vec16<T> wv = ld16(w + c * VEC);
-#pragma unroll
-      for (int j = 0; j < VEC; ++j) wf[i][j] = to_f(wv.v[j]);
+    for (int j = 0; j < VEC; ++j) {
+      aw[i][j] = 0.f;
+      if (LN) ab[LN ? i : 0][j] = 0.f;
     }
-  }
-  const int nw = gridDim.x * ROWS_PER_WG;
-  for (int row = blockIdx.x * ROWS_PER_WG + (threadIdx.x >> 6); row < N; row += nw) {
+  int par = 0;
+  for (int row = blockIdx.x; row < N; row += gridDim.x, par ^= 1) {
     const T* xr = x + (size_t)row * d;
     const T* dyr = dy + (size_t)row * d;
     const float rs = rstd[row];
     const float mu = LN ? mean[row] : 0.f;
-    float xh[NV][VEC], g[NV][VEC];
+    Vec16<T> xv[NV], dv[NV], wv[NV];
     float sg = 0.f, sgx = 0.f;
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
-      const int c = lane + 64 * i;
+      const int c = tid + (int)blockDim.x * i;
       if (c < nvec) {
-        Vec16<T> xv = ld16(xr + c * VEC), dv = ld16(dyr + c * VEC);
+        xv[i] = ld16(xr + c * VEC);
+        dv[i] = ld16(dyr + c * VEC);
+        wv[i] = ld16(w + c * VEC);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int c = tid + (int)blockDim.x * i;
+      if (c < nvec) {
 #pragma unroll
         for (int j = 0; j < VEC; ++j) {
-          const float dd = to_f(dv.v[j]);
-          xh[i][j] = (to_f(xv.v[j]) - mu) * rs;
-          g[i][j] = dd * wf[i][j];
-          aw[i][j] += dd * xh[i][j];
-          if (LN) ab[i][j] += dd;
-          sg += g[i][j];
-          sgx += g[i][j] * xh[i][j];
+          const float dd = to_f(dv[i].v[j]);
+          const float xh = (to_f(xv[i].v[j]) - mu) * rs;
+          const float gg = dd * to_f(wv[i].v[j]);
+          aw[i][j] += dd * xh;
+          if (LN) ab[LN ? i : 0][j] += dd;
+          sg += gg;
+          sgx += gg * xh;
         }
       }
     }
-    sgx = wave_sum(sgx) / d;
-    if (LN) sg = wave_sum(sg) / d;
+    sgx = wave_sum(sgx);
+    if (LN) sg = wave_sum(sg);
+    if (lane == 0) {
+      red[par][wv_id][0] = sgx;
+      red[par][wv_id][1] = sg;
+    }
+    __syncthreads();
+    sgx = 0.f;
+    sg = 0.f;
+    for (int k = 0; k < nwaves; ++k) {
+      sgx += red[par][k][0];
+      if (LN) sg += red[par][k][1];
+    }
+    sgx /= d;
+    sg /= d;
     T* dxr = dx + (size_t)row * d;
     const T* ar = dx_acc ? dx_acc + (size_t)row * d : nullptr;
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
-      const int c = lane + 64 * i;
+      const int c = tid + (int)blockDim.x * i;
       if (c < nvec) {
-        Vec16<T> o;
-        Vec16<T> av;
+        Vec16<T> o, av;
         if (ar) av = ld16(ar + c * VEC);
 #pragma unroll
         for (int j = 0; j < VEC; ++j) {
-          float r = rs * (g[i][j] - (LN ? sg : 0.f) - xh[i][j] * sgx);
+          const float xh = (to_f(xv[i].v[j]) - mu) * rs;
+          const float gg = to_f(dv[i].v[j]) * to_f(wv[i].v[j]);
+          float r = rs * (gg - (LN ? sg : 0.f) - xh * sgx);
           if (ar) r += to_f(av.v[j]);
           o.v[j] = from_f<T>(r);
         }
@@ -149,37 +171,43 @@ __global__ __launch_bounds__(256) void norm_bwd_k(const T* __restrict__ dy, cons
       }
     }
   }
-  __syncthreads();
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
-    const int c = lane + 64 * i;
+    const int c = tid + (int)blockDim.x * i;
     if (c < nvec) {
+      float* pw = part_w + (size_t)blockIdx.x * d + c * VEC;
 #pragma unroll
-      for (int j = 0; j < VEC; ++j) {
-        atomicAdd(&lds[c * VEC + j], aw[i][j]);
-        if (LN) atomicAdd(&lds[d + c * VEC + j], ab[i][j]);
+      for (int j = 0; j < VEC; j += 4)
+        *reinterpret_cast<float4*>(pw + j) = make_float4(aw[i][j], aw[i][j + 1], aw[i][j + 2], aw[i][j + 3]);
+      if (LN) {
+        float* pb = part_b + (size_t)blockIdx.x * d + c * VEC;
+#pragma unroll
+        for (int j = 0; j < VEC; j += 4)
+          *reinterpret_cast<float4*>(pb + j) = make_float4(ab[LN ? i : 0][j], ab[LN ? i : 0][j + 1],
+                                                           ab[LN ? i : 0][j + 2], ab[LN ? i : 0][j + 3]);
       }
     }
   }
-  __syncthreads();
-  for (int i = threadIdx.x; i < d; i += blockDim.x) {
-    part_w[(size_t)blockIdx.x * d + i] = lds[i];
-    if (LN) part_b[(size_t)blockIdx.x * d + i] = lds[d + i];
-  }
 }
 
-// out[c] = sum_p part[p][c]   (64 columns x 4 row-groups per workgroup, fixed order)
+// out[c] = sum_p part[p][c]   (16 columns x 16 row-groups per workgroup -> d/16 workgroups
+// so the partial matrix is streamed by many CUs; fixed summation order, deterministic)
 __global__ __launch_bounds__(256) void col_reduce_k(const float* __restrict__ part, float* __restrict__ out,
                                                     int P, int d) {
-  __shared__ float red[4][64];
-  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int g = threadIdx.x >> 6;
+  __shared__ float red[16][17];
+  const int cl = threadIdx.x & 15, g = threadIdx.x >> 4;
+  const int c = blockIdx.x * 16 + cl;
   float s = 0.f;
   if (c < d)
-    for (int p = g; p < P; p += 4) s += part[(size_t)p * d + c];
-  red[g][threadIdx.x & 63] = s;
+    for (int p = g; p < P; p += 16) s += part[(size_t)p * d + c];
+  red[g][cl] = s;
   __syncthreads();
-  if (g == 0 && c < d) out[c] = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+  if (threadIdx.x < 16 && c < d) {
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) t += red[k][cl];
+    out[c] = t;
+  }
 }
 
 // ----------------------------------------------------------------------------- launchers
@@ -202,19 +230,20 @@ static void bwd_dispatch(const void* dy, const void* x, const void* w, const flo
                          int N, int d, int nwg, hipStream_t s) {
   constexpr int VEC = 16 / sizeof(T);
   const int nvec = d / VEC;
-  const int nv = (nvec + 63) / 64;
-  dim3 grid(nwg), block(256);
-  size_t lds = sizeof(float) * d * (LN ? 2 : 1);
-#define L(NVV) hipLaunchKernelGGL((norm_bwd_k<T, NVV, LN>), grid, block, lds, s, (const T*)dy, (const T*)x, \
+  // threads per row: a multiple of 64 covering the row in <= 4 waves; NV vectors per thread
+  const int bt = nvec >= 256 ? 256 : ceil_div(nvec, 64) * 64;
+  const int nv = ceil_div(nvec, bt);
+  dim3 grid(nwg), block(bt);
+#define L(NVV) hipLaunchKernelGGL((norm_bwd_k<T, NVV, LN>), grid, block, 0, s, (const T*)dy, (const T*)x, \
                                   (const T*)w, mean, rstd, (const T*)dx_acc, (T*)dx, part_w, part_b, N, d)
-  if (nv <= 1) L(1); else if (nv <= 2) L(2); else if (nv <= 4) L(4); else if (nv <= 8) L(8); else L(16);
+  if (nv <= 1) L(1); else if (nv <= 2) L(2); else L(4);
 #undef L
-  hipLaunchKernelGGL(col_reduce_k, dim3(ceil_div(d, 64)), dim3(256), 0, s, part_w, dw, nwg, d);
-  if (LN) hipLaunchKernelGGL(col_reduce_k, dim3(ceil_div(d, 64)), dim3(256), 0, s, part_b, db, nwg, d);
+  hipLaunchKernelGGL(col_reduce_k, dim3(ceil_div(d, 16)), dim3(256), 0, s, part_w, dw, nwg, d);
+  if (LN) hipLaunchKernelGGL(col_reduce_k, dim3(ceil_div(d, 16)), dim3(256), 0, s, part_b, db, nwg, d);
 }
 
 int norm_bwd_num_wg(int N) {
-  int n = ceil_div(N, ROWS_PER_WG);
+  int n = N;
   return n < MAX_BWD_WG ? n : MAX_BWD_WG;
 }
 

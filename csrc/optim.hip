@@ -10,7 +10,42 @@
 
 namespace bllm {
 
-template <typename P, typename G, int VEC>
+// UNROLL independent VEC-groups per thread per iteration keep more loads in flight (the
+// kernel streams 28 B/param once: every access is a non-temporal load/store so the stream
+// does not evict L2/MALL-resident data of the overlapped forward).
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+
+template <typename T, int N>
+__device__ __forceinline__ VecN<T, N> ldnt(const T* p) {
+  VecN<T, N> r;
+  if constexpr (sizeof(r) == 16) {
+    const u32x4 u = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+    __builtin_memcpy(&r, &u, 16);
+  } else if constexpr (sizeof(r) == 8) {
+    const u32x2 u = __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(p));
+    __builtin_memcpy(&r, &u, 8);
+  } else {
+    r = ldv<T, N>(p);
+  }
+  return r;
+}
+template <typename T, int N>
+__device__ __forceinline__ void stnt(T* p, const VecN<T, N>& r) {
+  if constexpr (sizeof(r) == 16) {
+    u32x4 u;
+    __builtin_memcpy(&u, &r, 16);
+    __builtin_nontemporal_store(u, reinterpret_cast<u32x4*>(p));
+  } else if constexpr (sizeof(r) == 8) {
+    u32x2 u;
+    __builtin_memcpy(&u, &r, 8);
+    __builtin_nontemporal_store(u, reinterpret_cast<u32x2*>(p));
+  } else {
+    stv<T, N>(p, r);
+  }
+}
+
+template <typename P, typename G, int VEC, int UNROLL>
 __global__ __launch_bounds__(256) void adamw_k(P* __restrict__ param, float* __restrict__ master,
                                                const G* __restrict__ grad, float* __restrict__ m,
                                                float* __restrict__ v, long nvec, float lr, float b1, float b2,
@@ -19,31 +54,48 @@ __global__ __launch_bounds__(256) void adamw_k(P* __restrict__ param, float* __r
   const float gs = gscale ? gscale[0] : 1.f;
   const float decay = 1.f - lr * wd;
   const float step = lr / bc1;
-  for (long i = blockIdx.x * 256L + threadIdx.x; i < nvec; i += (long)gridDim.x * 256) {
-    const long o = i * VEC;
-    VecN<G, VEC> gv = ldv<G, VEC>(grad + o);
-    VecN<float, VEC> mv = ldv<float, VEC>(m + o), vv = ldv<float, VEC>(v + o), pv;
-    if (master) pv = ldv<float, VEC>(master + o);
-    else {
-      VecN<P, VEC> pp = ldv<P, VEC>(param + o);
+  const long stride = (long)gridDim.x * 256 * UNROLL;
+  for (long i0 = blockIdx.x * 256L * UNROLL + threadIdx.x; i0 < nvec; i0 += stride) {
+    VecN<G, VEC> gv[UNROLL];
+    VecN<float, VEC> mv[UNROLL], vv[UNROLL], pv[UNROLL];
 #pragma unroll
-      for (int j = 0; j < VEC; ++j) pv.v[j] = to_f(pp.v[j]);
-    }
-    VecN<P, VEC> po;
+    for (int u = 0; u < UNROLL; ++u) {
+      const long i = i0 + u * 256L;
+      if (i < nvec) {
+        const long o = i * VEC;
+        gv[u] = ldnt<G, VEC>(grad + o);
+        mv[u] = ldnt<float, VEC>(m + o);
+        vv[u] = ldnt<float, VEC>(v + o);
+        if (master) pv[u] = ldnt<float, VEC>(master + o);
+        else {
+          VecN<P, VEC> pp = ldv<P, VEC>(param + o);
 #pragma unroll
-    for (int j = 0; j < VEC; ++j) {
-      const float g = to_f(gv.v[j]) * gs;
-      mv.v[j] = b1 * mv.v[j] + (1.f - b1) * g;
-      vv.v[j] = b2 * vv.v[j] + (1.f - b2) * g * g;
-      float p = pv.v[j] * decay;
-      p -= step * mv.v[j] / (sqrtf(vv.v[j]) / bc2_sqrt + eps);
-      pv.v[j] = p;
-      po.v[j] = from_f<P>(p);
+          for (int j = 0; j < VEC; ++j) pv[u].v[j] = to_f(pp.v[j]);
+        }
+      }
     }
-    stv<float, VEC>(m + o, mv);
-    stv<float, VEC>(v + o, vv);
-    if (master) stv<float, VEC>(master + o, pv);
-    stv<P, VEC>(param + o, po);
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+      const long i = i0 + u * 256L;
+      if (i < nvec) {
+        const long o = i * VEC;
+        VecN<P, VEC> po;
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) {
+          const float g = to_f(gv[u].v[j]) * gs;
+          mv[u].v[j] = b1 * mv[u].v[j] + (1.f - b1) * g;
+          vv[u].v[j] = b2 * vv[u].v[j] + (1.f - b2) * g * g;
+          float p = pv[u].v[j] * decay;
+          p -= step * mv[u].v[j] / (sqrtf(vv[u].v[j]) / bc2_sqrt + eps);
+          pv[u].v[j] = p;
+          po.v[j] = from_f<P>(p);
+        }
+        stnt<float, VEC>(m + o, mv[u]);
+        stnt<float, VEC>(v + o, vv[u]);
+        if (master) stnt<float, VEC>(master + o, pv[u]);
+        stnt<P, VEC>(param + o, po);
+      }
+    }
   }
 }
 
@@ -74,12 +126,12 @@ static void adamw_launch(void* param, float* master, const void* grad, float* m,
                          hipStream_t s) {
   if (n % 4 == 0) {
     long nv = n / 4;
-    int g = (int)((nv + 255) / 256 < 4096 ? (nv + 255) / 256 : 4096);
-    hipLaunchKernelGGL((adamw_k<P, G, 4>), dim3(g > 0 ? g : 1), dim3(256), 0, s, (P*)param, master,
+    int g = (int)((nv + 511) / 512 < 2048 ? (nv + 511) / 512 : 2048);
+    hipLaunchKernelGGL((adamw_k<P, G, 4, 2>), dim3(g > 0 ? g : 1), dim3(256), 0, s, (P*)param, master,
                        (const G*)grad, m, v, nv, lr, b1, b2, eps, wd, bc1, bc2s, gscale);
   } else {
     int g = (int)((n + 255) / 256 < 4096 ? (n + 255) / 256 : 4096);
-    hipLaunchKernelGGL((adamw_k<P, G, 1>), dim3(g > 0 ? g : 1), dim3(256), 0, s, (P*)param, master,
+    hipLaunchKernelGGL((adamw_k<P, G, 1, 1>), dim3(g > 0 ? g : 1), dim3(256), 0, s, (P*)param, master,
                        (const G*)grad, m, v, n, lr, b1, b2, eps, wd, bc1, bc2s, gscale);
   }
 }

@@ -166,15 +166,18 @@ def test_adamw_and_norm(pdt):
 
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("B,T,H,G,hd", [(2, 64, 4, 4, 64), (1, 200, 8, 2, 128), (2, 33, 4, 2, 64),
-                                         (1, 10, 16, 8, 2), (2, 256, 4, 1, 128)])
+                                         (1, 10, 16, 8, 2), (2, 256, 4, 1, 128), (1, 512, 8, 2, 128),
+                                         (1, 300, 2, 2, 128), (1, 96, 3, 3, 64)])
 @pytest.mark.parametrize("p", [0.0, 0.1])
-def test_flash_attention(dt, B, T, H, G, hd, p):
+@pytest.mark.parametrize("causal", [True, False])
+def test_flash_attention(dt, B, T, H, G, hd, p, causal):
     qkv = torch.randn(B * T, (H + 2 * G) * hd, device=DEV).to(dt)
     do = torch.randn(B * T, H * hd, device=DEV).to(dt)
-    o, lse = ops.flash_attn_fwd(qkv, B, T, H, G, hd, True, p, 99, 12345)
-    o0, lse0 = ref.flash_attn_fwd(qkv.cpu().float(), B, T, H, G, hd, True, p, 99, 12345)
+    o, lse = ops.flash_attn_fwd(qkv, B, T, H, G, hd, causal, p, 99, 12345)
+    o0, lse0 = ref.flash_attn_fwd(qkv.cpu().float(), B, T, H, G, hd, causal, p, 99, 12345)
     _close(o, o0, dt, 2, name="o")
     _close(lse, lse0, torch.float32, 1000, name="lse")
-    dqkv = ops.flash_attn_bwd(qkv, o, lse, do, B, T, H, G, hd, True, p, 99, 12345)
-    dqkv0 = ref.flash_attn_bwd(qkv.cpu().float(), o0, lse0, do.cpu().float(), B, T, H, G, hd, True, p, 99, 12345)
+    dqkv = ops.flash_attn_bwd(qkv, o, lse, do, B, T, H, G, hd, causal, p, 99, 12345)
+    dqkv0 = ref.flash_attn_bwd(qkv.cpu().float(), o0, lse0, do.cpu().float(), B, T, H, G, hd, causal, p, 99,
+                               12345)
     _close(dqkv, dqkv0, dt, 4, name="dqkv")

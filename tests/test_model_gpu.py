@@ -66,3 +66,25 @@ def test_gpu_lora_and_training_decreases_loss():
         opt.step()
         losses.append(loss.item())
     assert losses[-1] < losses[0] - 0.5, losses
+
+
+def test_overlapped_optimizer_matches_serial():
+    """The side-stream (overlapped) AdamW must produce exactly the serial result."""
+    ops.load_ext(required=True)
+    cfg = _cfgs()["llama_hd64"]
+    idx = torch.randint(0, cfg.vocab_size, (3, 4, 129), device="cuda")
+    finals = []
+    for overlap in (False, True):
+        torch.manual_seed(0)
+        m = build_model(cfg, device="cuda")
+        m.flatten()
+        opt = FusedAdamW(m, lr=1e-3, weight_decay=0.1, overlap=overlap)
+        assert opt.overlap == overlap
+        for i in range(3):
+            loss = m(idx[i, :, :-1], idx[i, :, 1:])
+            loss.backward()
+            opt.clip_grad_norm_(1.0)
+            opt.step()
+        finals.append({k: v.float().cpu() for k, v in m.state_dict().items()})
+    for k in finals[0]:
+        assert torch.equal(finals[0][k], finals[1][k]), k
