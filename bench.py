@@ -40,6 +40,8 @@ def parse():
     ap.add_argument("--reshard_after_forward", type=int, default=1)
     ap.add_argument("--layers", type=int, default=None, help="(debug only) override n_layers; invalidates the metric")
     ap.add_argument("--profile", action="store_true", help="print a per-phase timing breakdown")
+    ap.add_argument("--overlap_optimizer", action="store_true",
+                    help="run AdamW on a side HIP stream under the next forward")
     return ap.parse_args()
 
 
@@ -73,7 +75,7 @@ def main():
     model = build_model(cfg, use_actv_ckpt=a.actv_ckpt, device=dev)
     engine = setup_engine(model, a.parallel if distributed else "local", device=dev,
                           reshard_after_forward=bool(a.reshard_after_forward))
-    opt = FusedAdamW(model, lr=3e-4, weight_decay=0.1, engine=engine)
+    opt = FusedAdamW(model, lr=3e-4, weight_decay=0.1, engine=engine, overlap=a.overlap_optimizer)
     B, T = a.batch_size, a.seq_len
     g = torch.Generator(device=dev)
     g.manual_seed(1000 + rank)

@@ -38,7 +38,7 @@ def local_slots(model) -> List[OptSlot]:
 class FusedAdamW(torch.optim.Optimizer):
     def __init__(self, model=None, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8,
                  weight_decay: float = 0.01, slots: Optional[List[OptSlot]] = None, engine=None,
-                 overlap: bool = True):
+                 overlap: bool = False):
         if slots is None:
             eng = engine or (model.rctx.engine if model is not None else None)
             slots = eng.optimizer_slots(model) if eng is not None and hasattr(eng, "optimizer_slots") \
@@ -59,9 +59,12 @@ class FusedAdamW(torch.optim.Optimizer):
         # data-parallel engines reduce with SUM; the 1/world average is folded in here
         self.grad_prescale = float(getattr(self.engine, "grad_prescale", 1.0))
         self._prescale_t: Optional[torch.Tensor] = None
-        # Overlapped update: the (HBM-bound) AdamW of unit i runs on a side HIP stream and the
-        # next forward of unit i waits on its event only, so the update streams under the
-        # (MFMA-bound) forward GEMMs of the preceding units.
+        # Overlapped update (opt-in): the (HBM-bound) AdamW of unit i runs on a side HIP stream
+        # and the next forward of unit i waits on its event only.  Measured on MI355X
+        # (profiles/r1_llama3_8b_1gpu_v2.md): the forward GEMMs hold every CU's full register
+        # file, so the update only runs in the gaps and slows the memory-bound forward kernels
+        # that it does overlap (norm/rope/swiglu 15-60 us -> ~1 ms) -- no net gain, hence off by
+        # default.  It pays when compute leaves CUs idle (small models, sharded updates).
         self.rctx = model.rctx if model is not None else None
         dev = slots[0].param.device if slots else torch.device("cpu")
         self.overlap = bool(overlap and dev.type == "cuda" and self.rctx is not None

@@ -62,38 +62,53 @@ template <int HD> __device__ __forceinline__ int v_off(int r, int col) {
   else return r * 128 + ((c64 ^ ((r >> 1) & 1)) << 6) + w;
 }
 
+// two floats -> packed pair (one v_cvt_pk_bf16_f32 for bf16)
 template <typename T> __device__ __forceinline__ uint32_t pack2(float a, float b) {
-  T x = from_f<T>(a), y = from_f<T>(b);
-  uint16_t ux, uy;
-  __builtin_memcpy(&ux, &x, 2);
-  __builtin_memcpy(&uy, &y, 2);
-  return (uint32_t)ux | ((uint32_t)uy << 16);
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  typedef T t2 __attribute__((ext_vector_type(2)));
+  const t2 v = __builtin_convertvector((f2{a, b}), t2);
+  uint32_t u;
+  __builtin_memcpy(&u, &v, 4);
+  return u;
 }
 
+// Per 64-key tile and wave: 32 MFMAs, 16 b128 + 32 tr_b64 LDS reads at loop-invariant
+// per-lane offsets, 2x(LD) saddr DMA issues with precomputed per-lane source offsets, and
+// ~130 VALU of online softmax (scale folded into the exp2 FMA; the O rescale is skipped when
+// no lane's running max moved, which is the common case after the first tiles).
 template <typename T, int HD, bool DROP>
 __global__ __launch_bounds__(256, 2) void attn_fwd_mfma_k(const T* __restrict__ qkv, T* __restrict__ out,
-                                                          float* __restrict__ lse, int T_, int H, int G, bool causal,
-                                                          uint32_t thr, float inv_keep, uint64_t seed,
+                                                          float* __restrict__ lse, int T_, int H, int G, int B_,
+                                                          bool causal, uint32_t thr, float inv_keep, uint64_t seed,
                                                           uint64_t doff) {
   typedef typename MF<T>::v8 v8;
   constexpr int KK = HD / 16;               // k-steps of the QK^T product
   constexpr int DT = HD / 32;               // 32-row tiles of O^T
   constexpr int CH = HD / 8;                // 16-B chunks per K/V row
-  constexpr int TILE_B = FWD_BK * HD * 2;   // bytes per K (or V) tile
-  constexpr int LD = FWD_BK * CH / 256;     // 16-B chunks per thread per tile (K and V each)
+  constexpr int ROWB = HD * 2;
+  constexpr int TILE_B = FWD_BK * ROWB;     // bytes per K (or V) tile
+  constexpr int LD = FWD_BK * CH / 256;     // 1-KiB pieces per wave per tile (K and V each)
+  constexpr int NPW = 2 * LD;
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
+  // heaviest (latest, for causal) q-blocks first over the whole grid; the q-blocks of one
+  // (b, h) share lin % 8 (one XCD / L2 for their common K/V stream)
   const int nqb = (T_ + FWD_BQ - 1) / FWD_BQ;
-  const int qb = nqb - 1 - (int)blockIdx.x;  // heaviest (latest) q-blocks first
-  const int h = blockIdx.y, b = blockIdx.z;
+  const int lin = blockIdx.x, nbh = H * B_;
+  const int qbi = lin / nbh, bh = lin - qbi * nbh;
+  const int qb = causal ? nqb - 1 - qbi : qbi;
+  const int h = bh % H, b = bh / H;
   const int g = h / (H / G);
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hh = lane >> 5, l32 = lane & 31;
+  const int tid = threadIdx.x, lane = tid & 63, hh = lane >> 5, l32 = lane & 31;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int gi = lane & 15, gl = (lane >> 4) & 1, qrow = gi >> 2, pcol = gi & 3;
   const long rs = (long)(H + 2 * G) * HD;
   const T* qbase = qkv + (long)b * T_ * rs + (long)h * HD;
   const T* kbase = qkv + (long)b * T_ * rs + (long)(H + g) * HD;
   const T* vbase = qkv + (long)b * T_ * rs + (long)(H + G + g) * HD;
   const int q0 = qb * FWD_BQ;
-  const int qi = q0 + w * 32 + l32;  // this lane's query
+  const int wq_lo = q0 + w * 32, wq_hi = wq_lo + 31;  // this wave's query range
+  const int qi = wq_lo + l32;                          // this lane's query
   const float c = rsqrtf((float)HD) * kLog2e;
 
   // ---- Q fragments (B operand): Q[qi][16kk + 8hh + 0..7]
@@ -103,146 +118,162 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_mfma_k(const T* __restrict__ 
     if (qi < T_) qf[kk] = *reinterpret_cast<const v8*>(qbase + (long)qi * rs + kk * 16 + hh * 8);
     else qf[kk] = v8{};
   }
+#pragma unroll
+  for (int kk = 0; kk < KK; ++kk) asm volatile("" ::"v"(qf[kk]));  // retire before the loop
 
   f32x16 o[DT];
 #pragma unroll
   for (int i = 0; i < DT; ++i) o[i] = f32x16{};
   float m = -1e30f, l = 0.f;
 
+  // ---- loop-invariant per-lane offsets
+  int koff[KK];
+#pragma unroll
+  for (int kk = 0; kk < KK; ++kk) koff[kk] = k_off<HD>(l32, kk * 2 + hh);
+  int voff[DT];
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) voff[dt] = v_off<HD>(4 * hh + qrow, dt * 32 + gl * 16 + pcol * 4);
+  uint32_t kgo[LD], vgo[LD];
+  int prow[LD], pkc[LD], pvc[LD];
+#pragma unroll
+  for (int i = 0; i < LD; ++i) {
+    const int P = (w * LD + i) * 64 + lane;
+    const int r = P / CH, pc = P % CH;
+    int kc16;
+    if constexpr (HD == 128) kc16 = pc ^ (r & 15); else kc16 = pc ^ ((r >> 1) & 7);
+    const int c64 = (pc >> 2) ^ (HD == 128 ? (r & 3) : ((r >> 1) & 1));
+    const int vc16 = c64 * 4 + (pc & 3);
+    prow[i] = r; pkc[i] = kc16; pvc[i] = vc16;
+    kgo[i] = (uint32_t)(r * rs * 2 + kc16 * 16);
+    vgo[i] = (uint32_t)(r * rs * 2 + vc16 * 16);
+  }
+  const uint32_t smem_u = lds_u32(smem);
+
   const int kend = causal ? min(T_, q0 + FWD_BQ) : T_;
   const int ntiles = (kend + FWD_BK - 1) / FWD_BK;
+  const int nact = wq_lo >= T_ ? 0 : (causal ? min(ntiles, wq_hi / FWD_BK + 1) : ntiles);
 
-  // K/V tiles land in LDS by direct DMA (global_load_lds_dwordx4: 1 KiB per wave
-  // instruction, lane-linear destination); the XOR swizzle is applied to the per-lane SOURCE
-  // address, so the linear DMA image IS the swizzled layout.  No staging VGPRs.
-  typedef __attribute__((address_space(3))) void lds_void;
-  typedef const __attribute__((address_space(1))) void gbl_void;
+  // K/V tiles land in LDS by direct DMA (1 KiB per wave instruction, lane-linear destination);
+  // the XOR swizzle is applied to the per-lane SOURCE offset, so the linear DMA image IS the
+  // swizzled layout.
   auto issue = [&](int t, int buf) {
-    char* kb = smem + buf * 2 * TILE_B;
-    char* vb = kb + TILE_B;
+    const int k0 = t * FWD_BK;
+    const uint32_t base = smem_u + buf * 2 * TILE_B;
+    if (k0 + FWD_BK <= T_) {
+      const void* ks = sgpr_ptr(kbase + (long)k0 * rs);
+      const void* vs = sgpr_ptr(vbase + (long)k0 * rs);
 #pragma unroll
-    for (int i = 0; i < LD; ++i) {
-      const int piece = w * LD + i;             // 1 KiB piece of the 16 KiB tile
-      const int P = piece * 64 + lane;          // 16-B chunk position in the image
-      const int r = P / CH, pc = P % CH;
-      int key = t * FWD_BK + r;
-      key = key < T_ ? key : T_ - 1;            // clamp: masked / multiplied by P = 0 later
-      int kc16;
-      if constexpr (HD == 128) kc16 = pc ^ (r & 15); else kc16 = pc ^ ((r >> 1) & 7);
-      const int c64 = (pc >> 2) ^ (HD == 128 ? (r & 3) : ((r >> 1) & 1));
-      const int vc16 = c64 * 4 + (pc & 3);
-      glds16(kbase + (long)key * rs + kc16 * 8, kb + piece * 1024);
-      glds16(vbase + (long)key * rs + vc16 * 8, vb + piece * 1024);
+      for (int i = 0; i < LD; ++i) {
+        const uint32_t pd = (w * LD + i) * 1024;
+        glds16s(ks, kgo[i], base + pd);
+        glds16s(vs, vgo[i], base + TILE_B + pd);
+      }
+    } else {  // sequence tail: clamp rows (masked / multiplied by P = 0 later)
+      char* kb = smem + buf * 2 * TILE_B;
+#pragma unroll
+      for (int i = 0; i < LD; ++i) {
+        const int pd = (w * LD + i) * 1024;
+        const int key = min(k0 + prow[i], T_ - 1);
+        glds16(kbase + (long)key * rs + pkc[i] * 8, kb + pd);
+        glds16(vbase + (long)key * rs + pvc[i] * 8, kb + TILE_B + pd);
+      }
     }
   };
 
-  issue(0, 0);
+  if (ntiles > 0) issue(0, 0);
   wait_vm0();
-  __syncthreads();
-
-  const int wq_lo = q0 + w * 32, wq_hi = wq_lo + 31;  // this wave's query range
-  for (int t = 0; t < ntiles; ++t) {
+  __builtin_amdgcn_s_barrier();
+  int t = 0;
+  for (; t < nact; ++t) {
     const int buf = t & 1;
-    if (t + 1 < ntiles) issue(t + 1, buf ^ 1);
+    const bool pre = t + 1 < ntiles;
+    if (pre) issue(t + 1, buf ^ 1);
     const int k0 = t * FWD_BK;
-    const bool active = !causal || k0 <= wq_hi;  // wave-uniform
-    if (active) {
-      const char* kb = smem + buf * 2 * TILE_B;
-      const char* vb = kb + TILE_B;
-      // ---- S^T = K Q^T for two 32-key sub-tiles: each sub-tile's K fragments are read
-      //      into distinct registers first (one lgkmcnt wait), then the MFMA chain
-      f32x16 s[2];
+    const char* kb = smem + buf * 2 * TILE_B;
+    const char* vb = kb + TILE_B;
+    // ---- S^T = K Q^T for two 32-key sub-tiles
+    f32x16 s[2];
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
+      s[kt] = f32x16{};
+#pragma unroll
+      for (int kk = 0; kk < KK; ++kk)
+        s[kt] = MF<T>::mma(*reinterpret_cast<const v8*>(kb + kt * 32 * ROWB + koff[kk]), qf[kk], s[kt]);
+    }
+    // ---- mask (uniform branch: causal diagonal / tail tiles only), online softmax
+    const bool edge = (causal && k0 + FWD_BK - 1 > wq_lo) || k0 + FWD_BK > T_ || wq_hi >= T_;
+    if (edge) {
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt) {
-        v8 ka[KK];
-#pragma unroll
-        for (int kk = 0; kk < KK; ++kk)
-          ka[kk] = *reinterpret_cast<const v8*>(kb + k_off<HD>(kt * 32 + l32, kk * 2 + hh));
-        __builtin_amdgcn_sched_barrier(0);
-        s[kt] = f32x16{};
-#pragma unroll
-        for (int kk = 0; kk < KK; ++kk) s[kt] = MF<T>::mma(ka[kk], qf[kk], s[kt]);
-      }
-      // ---- scale, mask (selects, no branches), online softmax (lane = query)
-      const bool need_mask = (causal && k0 + FWD_BK - 1 > wq_lo) || (k0 + FWD_BK > T_);
-      float mx = -INFINITY;
-      if (need_mask) {
-#pragma unroll
-        for (int kt = 0; kt < 2; ++kt) {
-          const int kb0 = k0 + kt * 32 + 4 * hh;
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int key = kb0 + (r & 3) + 8 * (r >> 2);
-            const bool off = (causal & (key > qi)) | (key >= T_);
-            const float v = off ? -INFINITY : s[kt][r] * c;
-            s[kt][r] = v;
-            mx = fmaxf(mx, v);
-          }
-        }
-      } else {
-#pragma unroll
-        for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const float v = s[kt][r] * c;
-            s[kt][r] = v;
-            mx = fmaxf(mx, v);
-          }
-      }
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float mn = fmaxf(m, mx);
-      const float alpha = exp2f(m - mn);
-      m = mn;
-      float ls = 0.f;
-#pragma unroll
-      for (int kt = 0; kt < 2; ++kt)
+        const int kb0 = k0 + kt * 32 + 4 * hh;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const float p = exp2f(s[kt][r] - mn);
-          ls += p;
-          if constexpr (DROP) {
-            const int key = k0 + kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
-            const uint64_t e = (((uint64_t)(b * H + h) * T_ + qi) * T_ + key);
-            s[kt][r] = (drop_hash(seed, doff + e) >= thr) ? p * inv_keep : 0.f;
-          } else {
-            s[kt][r] = p;
-          }
+          const int key = kb0 + (r & 3) + 8 * (r >> 2);
+          if ((causal && key > qi) || key >= T_) s[kt][r] = -INFINITY;
         }
-      l = l * alpha + ls;
+      }
+    }
+    float mx = -INFINITY;
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s[kt][r]);
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64)) * c;
+    const float mn = fmaxf(m, mx);
+    // lazy rescale: only when some lane's running max moved
+    if (__builtin_amdgcn_ballot_w64(mn > m)) {
+      const float alpha = __builtin_amdgcn_exp2f(m - mn);
+      l *= alpha;
 #pragma unroll
       for (int i = 0; i < DT; ++i) o[i] *= alpha;
-      // ---- O^T += V^T P^T: P fragments converted just in time from the accumulators,
-      //      V^T fragments by hardware-transposed LDS reads
-      const int gi = lane & 15, gl = (lane >> 4) & 1;
-      const int qrow = gi >> 2, pcol = gi & 3;
-#pragma unroll
-      for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) {
-          v8 pf;
-          {
-            uint32_t u[4];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) u[j] = pack2<T>(s[kt][8 * s2 + 2 * j], s[kt][8 * s2 + 2 * j + 1]);
-            __builtin_memcpy(&pf, u, 16);
-          }
-          const int base = kt * 32 + s2 * 16 + 4 * hh + qrow;
-          v8 va[DT];
-#pragma unroll
-          for (int dt = 0; dt < DT; ++dt) {
-            const int col = dt * 32 + gl * 16 + pcol * 4;
-            const s16x4 r1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(vb + v_off<HD>(base, col)));
-            const s16x4 r2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(vb + v_off<HD>(base + 8, col)));
-            short tmp[8] = {r1[0], r1[1], r1[2], r1[3], r2[0], r2[1], r2[2], r2[3]};
-            __builtin_memcpy(&va[dt], tmp, 16);
-          }
-          __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-          for (int dt = 0; dt < DT; ++dt) o[dt] = MF<T>::mma(va[dt], pf, o[dt]);
-        }
+      m = mn;
     }
-    wait_vm0();       // the DMA of tile t+1 has landed (asm-issued, so drained by hand)
-    __syncthreads();
+    float ls = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float p = __builtin_amdgcn_exp2f(fmaf(s[kt][r], c, -m));
+        ls += p;
+        if constexpr (DROP) {
+          const int key = k0 + kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+          const uint64_t e = (((uint64_t)(b * H + h) * T_ + qi) * T_ + key);
+          s[kt][r] = (drop_hash(seed, doff + e) >= thr) ? p * inv_keep : 0.f;
+        } else {
+          s[kt][r] = p;
+        }
+      }
+    l += ls;
+    // ---- O^T += V^T P^T: P fragments packed from the accumulators, V^T by transposed reads
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        v8 pf;
+        {
+          uint32_t u[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) u[j] = pack2<T>(s[kt][8 * s2 + 2 * j], s[kt][8 * s2 + 2 * j + 1]);
+          __builtin_memcpy(&pf, u, 16);
+        }
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) {
+          const int off = voff[dt] + (kt * 32 + s2 * 16) * ROWB;
+          const s16x4 r1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(vb + off));
+          const s16x4 r2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(vb + off + 8 * ROWB));
+          short tmp[8] = {r1[0], r1[1], r1[2], r1[3], r2[0], r2[1], r2[2], r2[3]};
+          v8 va;
+          __builtin_memcpy(&va, tmp, 16);
+          o[dt] = MF<T>::mma(va, pf, o[dt]);
+        }
+      }
+    wait_vm0();  // the DMA of tile t+1 has landed (asm-issued, so drained by hand)
+    __builtin_amdgcn_s_barrier();
+  }
+  for (; t < ntiles; ++t) {  // wave done (causal): keep the DMA ring and barriers going
+    if (t + 1 < ntiles) issue(t + 1, (t & 1) ^ 1);
+    wait_vm0();
+    __builtin_amdgcn_s_barrier();
   }
 
   // ---- epilogue: combine the two halves' partial sums, normalise, store O and LSE
@@ -270,15 +301,15 @@ void attn_fwd_mfma(DType dt, const void* qkv, void* o, float* lse, int B, int T_
                    float p, uint64_t seed, uint64_t offset, hipStream_t s) {
   const uint32_t thr = drop_threshold(p);
   const float ik = p > 0.f ? 1.f / (1.f - p) : 1.f;
-  dim3 grid((T_ + FWD_BQ - 1) / FWD_BQ, H, B), block(256);
+  dim3 grid(((T_ + FWD_BQ - 1) / FWD_BQ) * H * B), block(256);
 #define LAUNCH(TT, HDD)                                                                                       \
   do {                                                                                                        \
     if (p > 0.f)                                                                                              \
       hipLaunchKernelGGL((attn_fwd_mfma_k<TT, HDD, true>), grid, block, 2 * 2 * FWD_BK * HDD * 2, s,          \
-                         (const TT*)qkv, (TT*)o, lse, T_, H, G, causal, thr, ik, seed, offset);              \
+                         (const TT*)qkv, (TT*)o, lse, T_, H, G, B, causal, thr, ik, seed, offset);              \
     else                                                                                                      \
       hipLaunchKernelGGL((attn_fwd_mfma_k<TT, HDD, false>), grid, block, 2 * 2 * FWD_BK * HDD * 2, s,         \
-                         (const TT*)qkv, (TT*)o, lse, T_, H, G, causal, thr, ik, seed, offset);              \
+                         (const TT*)qkv, (TT*)o, lse, T_, H, G, B, causal, thr, ik, seed, offset);              \
   } while (0)
   if (dt == DType::BF16) {
     if (hd == 128) LAUNCH(bf16_t, 128); else LAUNCH(bf16_t, 64);
