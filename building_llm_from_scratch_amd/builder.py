@@ -19,15 +19,23 @@ from .models import build_model as _build_model
 from .models.lora import replace_linear_with_lora
 from .models.weights import load_pretrained
 from .parallel import setup_engine
+from .parallel.mixed_precision import get_policy
 from .train.optim import FusedAdamW
 from .utils import misc
 
 logger = setup_logger("build_components")
 
 
+def precision_policy(args):
+    """``--mixed_precision`` policy (parallel/mixed_precision.py) or None."""
+    mp = getattr(args, "mixed_precision", None)
+    return get_policy(mp) if mp else None
+
+
 def compute_dtype(args) -> torch.dtype:
-    if getattr(args, "mixed_precision", None):
-        return datatype_mapping[args.mixed_precision]
+    pol = precision_policy(args)
+    if pol is not None:
+        return pol.param_dtype
     return datatype_mapping[args.data_type]
 
 
@@ -69,9 +77,10 @@ def build_model(config, rank, device, args):
         if rank == 0:
             n = sum(p.numel() for p in model.parameters() if p.requires_grad)
             logger.info(f"Total trainable LoRA parameters: {n:,}")
-    reduce = None
-    if getattr(args, "mixed_precision", None):
-        reduce = datatype_mapping[args.mixed_precision]
+    pol = precision_policy(args)
+    reduce = pol.reduce_dtype if pol is not None else None
+    if pol is not None and rank == 0:
+        logger.info(f"Mixed precision: {pol}")
     engine = setup_engine(model, engine_kind(args), device=device, reduce_dtype=reduce,
                           reshard_after_forward=not getattr(args, "no_reshard_after_forward", False),
                           bucket_mb=getattr(args, "bucket_mb", 256.0))

@@ -68,7 +68,7 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--use_zero_opt", action="store_true")
     p.add_argument("--use_actv_ckpt", action="store_true")
     p.add_argument("--data_type", type=str, default="fp32", choices=["fp32", "fp16", "bf16"])
-    p.add_argument("--mixed_precision", type=str, choices=["fp16", "bf16"])
+    p.add_argument("--mixed_precision", type=str, choices=["fp16", "bf16", "bf16_hybrid", "fp32"])
     p.add_argument("--finetune", action="store_true")
     p.add_argument("--dataset", type=str, default="gutenberg", choices=["gutenberg", "alpaca"])
     p.add_argument("--use_lora", action="store_true")

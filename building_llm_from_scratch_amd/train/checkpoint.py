@@ -46,7 +46,7 @@ def save_resume_state(path, optimizer, trainer_state: dict, rank: int = 0, world
         "optim": [{k: (v.detach().cpu() if torch.is_tensor(v) else v) for k, v in optimizer.state[s.param].items()}
                   for s in optimizer.slots],
         "lr": optimizer.param_groups[0]["lr"],
-        "rng": {"torch": torch.get_rng_state(), "numpy": np.random.get_state(), "python": random.getstate()},
+        "rng": _rng_state(),
         "world": world,
     }
     p = Path(path)
@@ -59,7 +59,7 @@ def load_resume_state(path, optimizer, rank: int = 0, world: int = 1) -> dict:
     p = Path(path)
     if world > 1:
         p = p.with_name(p.stem + f".rank{rank}" + p.suffix)
-    st = torch.load(p, map_location="cpu", weights_only=False)  # file written by this framework
+    st = torch.load(p, map_location="cpu", weights_only=True)
     assert st["world"] == world, "resume requires the same world size"
     for s, saved in zip(optimizer.slots, st["optim"]):
         cur = optimizer.state[s.param]
@@ -70,7 +70,22 @@ def load_resume_state(path, optimizer, rank: int = 0, world: int = 1) -> dict:
                 cur[k] = v
         if "master" in cur:
             s.param.reshape(-1).copy_(cur["master"].to(s.param.dtype))
-    torch.set_rng_state(st["rng"]["torch"])
-    np.random.set_state(st["rng"]["numpy"])
-    random.setstate(st["rng"]["python"])
+    _set_rng_state(st["rng"])
     return st["trainer"]
+
+
+# RNG states as tensors / ints only, so resume files load with ``weights_only=True``
+def _rng_state() -> dict:
+    name, keys, pos, has_gauss, gauss = np.random.get_state()
+    version, pstate, pgauss = random.getstate()
+    return {"torch": torch.get_rng_state(), "np_name": name, "np_keys": torch.from_numpy(keys.astype(np.int64)),
+            "np_pos": int(pos), "np_has_gauss": int(has_gauss), "np_gauss": float(gauss),
+            "py_version": version, "py_state": torch.tensor(pstate, dtype=torch.int64),
+            "py_gauss": pgauss}
+
+
+def _set_rng_state(r: dict):
+    torch.set_rng_state(r["torch"])
+    np.random.set_state((r["np_name"], r["np_keys"].numpy().astype(np.uint32), r["np_pos"], r["np_has_gauss"],
+                         r["np_gauss"]))
+    random.setstate((r["py_version"], tuple(int(x) for x in r["py_state"].tolist()), r["py_gauss"]))
