@@ -71,9 +71,9 @@ def _reference(family, lora):
     return {k: v.clone() for k, v in m.state_dict().items()}, losses
 
 
-def _worker(rank, world, kind, family, lora, ckpt, out, port):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+def _worker(rank, world, kind, family, lora, ckpt, out, store):
+    # file-based rendezvous: no TCP-store port to race for between consecutive tests
+    dist.init_process_group("gloo", init_method=f"file://{store}", rank=rank, world_size=world)
     try:
         cfg, m = _build(family, lora, ckpt)
         eng = setup_engine(m, kind, device="cpu", bucket_mb=0.05)
@@ -86,6 +86,7 @@ def _worker(rank, world, kind, family, lora, ckpt, out, port):
             {k: v.detach().clone() for k, v in m.state_dict().items()}
         if rank == 0:
             torch.save({"sd": sd, "losses": (t / world).tolist()}, out)
+        dist.barrier()  # no rank tears the group down while a peer still has traffic in flight
     finally:
         dist.destroy_process_group()
 
@@ -96,9 +97,8 @@ def test_engine_matches_single_process(kind, family, lora):
     ref_sd, ref_losses = _reference(family, lora)
     with tempfile.TemporaryDirectory() as d:
         out = os.path.join(d, "r.pt")
-        port = free_port()
-        mp.start_processes(_worker, args=(2, kind, family, lora, "none", out, port), nprocs=2, join=True,
-                           start_method="spawn")
+        mp.start_processes(_worker, args=(2, kind, family, lora, "none", out, os.path.join(d, "store")), nprocs=2,
+                           join=True, start_method="spawn")
         res = torch.load(out, weights_only=True)
     for a, b in zip(res["losses"], ref_losses):
         assert abs(a - b) < 1e-4, (res["losses"], ref_losses)
@@ -114,8 +114,8 @@ def test_fsdp_full_ckpt_and_zero2_mode():
     ref_sd, _ = _reference("llama", False)
     with tempfile.TemporaryDirectory() as d:
         out = os.path.join(d, "r.pt")
-        mp.start_processes(_worker, args=(2, "fsdp", "llama", False, "full", out, free_port()), nprocs=2, join=True,
-                           start_method="spawn")
+        mp.start_processes(_worker, args=(2, "fsdp", "llama", False, "full", out, os.path.join(d, "store")), nprocs=2,
+                           join=True, start_method="spawn")
         sd = torch.load(out, weights_only=True)["sd"]
     for k in ref_sd:
         assert torch.allclose(sd[k].float(), ref_sd[k].float(), atol=1e-4, rtol=1e-4), k
