@@ -8,8 +8,9 @@ hand (models/gpt2.py, models/llama.py) on top of the HIP kernels and hipBLASLt G
 gives exact control over:
 
   * what each block saves for backward (``actv_ckpt``: ``none`` | ``selective`` — recompute
-    norms/activations only | ``full`` — save the block input only, the reference's
-    ``checkpoint_sequential(segments=n_layers)`` semantics);
+    only the norm outputs, the cheapest memory-bound ops; everything a GEMM or the attention
+    kernel produced is kept, which 288 GB of HBM affords | ``full`` — save the block input
+    only, the reference's ``checkpoint_sequential(segments=n_layers)`` semantics);
   * where distributed hooks fire (``engine.pre_forward/post_forward/pre_backward/
     post_backward`` per unit — FSDP gathers and reduce-scatters, DDP bucket all-reduce);
   * fused head + cross-entropy: ``model(idx, targets)`` returns the mean loss without

@@ -147,10 +147,10 @@ class GPTBlockCompute(UnitCompute):
             # full-recompute mode: _BlockFn keeps ``offs`` as the replay token so the
             # recomputed forward regenerates identical dropout masks
             return x3.view(B, T, d), offs
-        saved = dict(x=x2d, m1=m1, r1=r1, qkv=qkv, o=o, lse=lse, x2=x2, m2=m2, r2=r2, f=f,
+        saved = dict(x=x2d, m1=m1, r1=r1, qkv=qkv, o=o, lse=lse, x2=x2, m2=m2, r2=r2, f=f, g=g,
                      p=p, offs=offs, xa=(xa_qkv, xa_o, xa_fc, xa_pr))
         if rc.actv_ckpt == "none":
-            saved.update(h1=h1, h2=h2, g=g)
+            saved.update(h1=h1, h2=h2)
         return x3.view(B, T, d), saved
 
     def backward(self, dy, s):

@@ -160,10 +160,10 @@ class LlamaBlockCompute(UnitCompute):
         x3, xa_dn = self.down.forward(act, residual=x2)
         saved = None
         if save:
-            saved = dict(x=x2d, r1=r1, qkv=qkv, o=o, lse=lse, x2=x2, r2=r2, gu=gu,
+            saved = dict(x=x2d, r1=r1, qkv=qkv, o=o, lse=lse, x2=x2, r2=r2, gu=gu, act=act,
                          xa=(xa_qkv, xa_o, xa_gu, xa_dn))
             if rc.actv_ckpt == "none":
-                saved.update(h1=h1, h2=h2, act=act)
+                saved.update(h1=h1, h2=h2)
         return x3.view(B, T, d), saved
 
     def backward(self, dy, s):

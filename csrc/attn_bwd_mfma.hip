@@ -16,11 +16,13 @@
 //    key tiles, written once.  Costs two extra MFMA products vs. a fused kernel but removes
 //    the ~300 MB/layer of fp32 dQ atomics that floored the fused version.
 // Softmax constants are lane-local: p = exp2(s*c - lse2), ds = p*(dp - delta)*scale;
-// delta = rowsum(dO * O) comes from a pre-pass (attn_naive.hip:attn_delta).  Q/dO (dK/dV
+// delta = rowsum(dO * O) is computed by the dQ kernel (which holds dO in registers anyway
+// and runs first) and handed to the dK/dV kernel through a [B,H,T] fp32 buffer.  Q/dO (dK/dV
 // kernel) and K/V (dQ kernel) tiles arrive by global_load_lds DMA, double-buffered, stored as
 // 16-B-chunk XOR images for MFMA row reads and 64-B-chunk XOR images for hardware-transposed
 // reads (ds_read_b64_tr_b16).  Causal: only tiles at/below the diagonal; heaviest first.
 #include <float.h>
+#include <stdlib.h>
 #include "api.h"
 
 namespace bllm {
@@ -87,7 +89,6 @@ template <typename v8> __device__ __forceinline__ v8 tr8(const char* base, int o
 
 constexpr int BWD_BKV = 128;  // keys per workgroup
 constexpr int BWD_BQ = 32;    // queries per step
-constexpr int BWD_NBUF = 3;   // LDS ring depth (prefetch distance 2)
 constexpr float kLog2eB = 1.4426950408889634f;
 
 // LDS bytes of one ring slot of the dK/dV kernel: Q rows, Q^T image, dO rows, dO^T image,
@@ -99,19 +100,21 @@ template <int HD> constexpr int dkdv_buf_bytes() { return 4 * BWD_BQ * HD * 2 + 
 // of dS is folded into the final dK), 9 saddr LDS-DMA issues whose per-lane offsets are
 // precomputed.  Masking (causal diagonal, sequence tail) and dropout are compile-time variants
 // so the common interior step carries no per-element branches.
-template <typename T, int HD, bool DROP>
-__global__ __launch_bounds__(256, 1) void attn_bwd_mfma_k(const T* __restrict__ qkv, const T* __restrict__ dout,
-                                                          const float* __restrict__ lse,
-                                                          const float* __restrict__ delta, T* __restrict__ dqkv,
-                                                          float* __restrict__ dkv_part, int T_, int H, int G, int B_,
-                                                          bool causal, uint32_t thr, float inv_keep,
-                                                          uint64_t seed, uint64_t doff) {
+template <typename T, int HD, bool DROP, int NBUF, int OCC>
+__global__ __launch_bounds__(256, OCC) void attn_bwd_mfma_k(const T* __restrict__ qkv, const T* __restrict__ dout,
+                                                            const float* __restrict__ lse,
+                                                            const float* __restrict__ delta, T* __restrict__ dqkv,
+                                                            float* __restrict__ dkv_part, int T_, int H, int G, int B_,
+                                                            bool causal, uint32_t thr, float inv_keep,
+                                                            uint64_t seed, uint64_t doff) {
   typedef typename MFb<T>::v8 v8;
   constexpr int KK = HD / 16, DT = HD / 32, CH = HD / 8, ROWB = HD * 2;
   constexpr int IMG = BWD_BQ * ROWB;            // bytes of one [32][HD] image
   constexpr int PPW = IMG / 1024 / 4;           // 1-KiB DMA pieces per wave per image
+  constexpr int PROWS = 256 / CH;               // rows between a wave's consecutive pieces
   constexpr int BUF = dkdv_buf_bytes<HD>();
   constexpr int NPW = 4 * PPW + 1;              // DMA instructions per wave per step
+  static_assert(NBUF == 2 || NBUF == 3, "ring depth");
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   // heaviest (lowest) key block first across the whole grid; all key blocks of one (b, h)
@@ -122,7 +125,6 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_mfma_k(const T* __restrict__ 
   const int g = h / (H / G);
   const int tid = threadIdx.x, lane = tid & 63, hh = lane >> 5, l32 = lane & 31;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (scalar branches)
-  const int gi = lane & 15, gl = (lane >> 4) & 1, qrow = gi >> 2, pcol = gi & 3;
   const long rs = (long)(H + 2 * G) * HD;
   const long ors = (long)H * HD;
   const T* qb_ = qkv + (long)b * T_ * rs + (long)h * HD;
@@ -155,32 +157,20 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_mfma_k(const T* __restrict__ 
 #pragma unroll
   for (int i = 0; i < DT; ++i) { dk[i] = f32x16{}; dv[i] = f32x16{}; }
 
-  // ---- loop-invariant per-lane offsets
-  int roff[KK];                                   // MFMA A rows (row image)
-#pragma unroll
-  for (int kk = 0; kk < KK; ++kk) roff[kk] = r_off<HD>(l32, kk * 2 + hh);
-  int troff[DT];                                  // transposed reads (rows +16*s2, +8 are immediates)
-#pragma unroll
-  for (int dt = 0; dt < DT; ++dt) troff[dt] = t_off<HD>(4 * hh + qrow, dt * 32 + gl * 16 + pcol * 4);
-  uint32_t qoff[2][PPW], ooff[2][PPW];            // DMA source byte offsets from the step's row q0
-  int prow[PPW], pc16[2][PPW];
-#pragma unroll
-  for (int j = 0; j < PPW; ++j) {
-    const int P = (w + 4 * j) * 64 + lane;
+  // DMA source offsets of this lane's piece (j = 0; piece j adds j*PROWS rows, folded into the
+  // uniform SGPR base), one for the row image and one for the transposed image
+  uint32_t q_r, q_t, o_r, o_t;
+  {
+    const int P = w * 64 + lane;
     const int r = P / CH, pc = P % CH;
-    int rc, tc;
+    int rc;
     if constexpr (HD == 128) rc = pc ^ (r & 15); else rc = pc ^ ((r >> 1) & 7);
-    {
-      const int c64 = (pc >> 2) ^ (HD == 128 ? (r & 3) : ((r >> 1) & 1));
-      tc = c64 * 4 + (pc & 3);
-    }
-    prow[j] = r;
-    pc16[0][j] = rc;
-    pc16[1][j] = tc;
-    qoff[0][j] = (uint32_t)(r * rs * 2 + rc * 16);
-    qoff[1][j] = (uint32_t)(r * rs * 2 + tc * 16);
-    ooff[0][j] = (uint32_t)(r * ors * 2 + rc * 16);
-    ooff[1][j] = (uint32_t)(r * ors * 2 + tc * 16);
+    const int c64 = (pc >> 2) ^ (HD == 128 ? (r & 3) : ((r >> 1) & 1));
+    const int tc = c64 * 4 + (pc & 3);
+    q_r = (uint32_t)(r * rs * 2 + rc * 16);
+    q_t = (uint32_t)(r * rs * 2 + tc * 16);
+    o_r = (uint32_t)(r * ors * 2 + rc * 16);
+    o_t = (uint32_t)(r * ors * 2 + tc * 16);
   }
   const uint32_t smem_u = lds_u32(smem);
   const float* stat_src = (lane < 32 ? lse_ : del_);
@@ -189,37 +179,53 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_mfma_k(const T* __restrict__ 
   auto issue = [&](int q0, int slot) {
     const uint32_t base = smem_u + slot * BUF;
     if (q0 + BWD_BQ <= T_) {
-      const void* qs = sgpr_ptr(qb_ + (long)q0 * rs);
-      const void* os = sgpr_ptr(ob_ + (long)q0 * ors);
 #pragma unroll
       for (int j = 0; j < PPW; ++j) {
+        const void* qs = sgpr_ptr(qb_ + (long)(q0 + j * PROWS) * rs);
+        const void* os = sgpr_ptr(ob_ + (long)(q0 + j * PROWS) * ors);
         const uint32_t pd = (w + 4 * j) * 1024;
-        glds16s(qs, qoff[0][j], base + pd);
-        glds16s(qs, qoff[1][j], base + IMG + pd);
-        glds16s(os, ooff[0][j], base + 2 * IMG + pd);
-        glds16s(os, ooff[1][j], base + 3 * IMG + pd);
+        glds16s(qs, q_r, base + pd);
+        glds16s(qs, q_t, base + IMG + pd);
+        glds16s(os, o_r, base + 2 * IMG + pd);
+        glds16s(os, o_t, base + 3 * IMG + pd);
       }
     } else {  // sequence tail: clamp rows (rows >= T_ are masked in the step)
+      char* lb = smem + slot * BUF;
 #pragma unroll
       for (int j = 0; j < PPW; ++j) {
+        const int P = (w + 4 * j) * 64 + lane;
+        const int r = P / CH, pc = P % CH;
+        int rc;
+        if constexpr (HD == 128) rc = pc ^ (r & 15); else rc = pc ^ ((r >> 1) & 7);
+        const int c64 = (pc >> 2) ^ (HD == 128 ? (r & 3) : ((r >> 1) & 1));
+        const int tc = c64 * 4 + (pc & 3);
         const uint32_t pd = (w + 4 * j) * 1024;
-        const int r = min(q0 + prow[j], T_ - 1);
-        char* lb = smem + slot * BUF;
-        glds16(qb_ + (long)r * rs + pc16[0][j] * 8, lb + pd);
-        glds16(qb_ + (long)r * rs + pc16[1][j] * 8, lb + IMG + pd);
-        glds16(ob_ + (long)r * ors + pc16[0][j] * 8, lb + 2 * IMG + pd);
-        glds16(ob_ + (long)r * ors + pc16[1][j] * 8, lb + 3 * IMG + pd);
+        const int rr = min(q0 + r, T_ - 1);
+        glds16(qb_ + (long)rr * rs + rc * 8, lb + pd);
+        glds16(qb_ + (long)rr * rs + tc * 8, lb + IMG + pd);
+        glds16(ob_ + (long)rr * ors + rc * 8, lb + 2 * IMG + pd);
+        glds16(ob_ + (long)rr * ors + tc * 8, lb + 3 * IMG + pd);
       }
     }
     glds4(stat_src + min(q0 + l32, T_ - 1), smem + slot * BUF + 4 * IMG + w * 256);
   };
+  // after step i: wait for step i+1's DMA (NBUF = 3 may leave step i+2's in flight)
+  auto ring_wait = [&](int i, int nsteps) {
+    if constexpr (NBUF == 3) {
+      if (i + 2 < nsteps) wait_vm<NPW>(); else wait_vm0();
+    } else {
+      wait_vm0();
+    }
+    __builtin_amdgcn_s_barrier();
+  };
 
   const int qstart = causal ? k0 : 0;
   const int nsteps = qstart < T_ ? (T_ - qstart + BWD_BQ - 1) / BWD_BQ : 0;
-  if (nsteps > 0) issue(qstart, 0);
-  if (nsteps > 1) {
-    issue(qstart + BWD_BQ, 1);
-    wait_vm<NPW>();
+#pragma unroll
+  for (int j = 0; j < NBUF - 1; ++j)
+    if (j < nsteps) issue(qstart + j * BWD_BQ, j);
+  if constexpr (NBUF == 3) {
+    if (nsteps > 1) wait_vm<NPW>(); else wait_vm0();
   } else {
     wait_vm0();
   }
@@ -230,25 +236,31 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_mfma_k(const T* __restrict__ 
   const int first = kw0 >= T_ ? nsteps : (causal ? min(w, nsteps) : 0);
   int slot = 0, i = 0;
   for (; i < first; ++i) {
-    const bool pre = i + 2 < nsteps;
-    if (pre) issue(qstart + (i + 2) * BWD_BQ, slot == 0 ? 2 : slot - 1);
-    if (pre) wait_vm<NPW>(); else wait_vm0();
-    __builtin_amdgcn_s_barrier();
-    slot = slot == 2 ? 0 : slot + 1;
+    if (i + NBUF - 1 < nsteps) issue(qstart + (i + NBUF - 1) * BWD_BQ, slot == 0 ? NBUF - 1 : slot - 1);
+    ring_wait(i, nsteps);
+    slot = slot == NBUF - 1 ? 0 : slot + 1;
   }
   for (; i < nsteps; ++i) {
     const int q0 = qstart + i * BWD_BQ;
-    const bool pre = i + 2 < nsteps;
-    if (pre) issue(q0 + 2 * BWD_BQ, slot == 0 ? 2 : slot - 1);
+    if (i + NBUF - 1 < nsteps) issue(q0 + (NBUF - 1) * BWD_BQ, slot == 0 ? NBUF - 1 : slot - 1);
     const char* S = smem + slot * BUF;
+    // per-lane LDS offsets, recomputed each step from an opaque copy of the lane id (a few
+    // VALU) instead of being held in VGPRs across the loop
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+    const int hh_ = ln >> 5, l32_ = ln & 31, gi = ln & 15;
+    const int gl = (gi >> 4) & 1;  // always 0 for gi < 16; kept for the transposed-read form
+    (void)gl;
+    const int qrow = gi >> 2, pcol = gi & 3, glb = (ln >> 4) & 1;
     // wave-uniform: the diagonal step or a sequence tail needs masking
     const bool edge = (causal && i == first) || q0 + BWD_BQ > T_ || kw0 + 32 > T_;
     {
       f32x16 sacc = f32x16{}, dpacc = f32x16{};
 #pragma unroll
       for (int kk = 0; kk < KK; ++kk) {
-        sacc = MFb<T>::mma(*reinterpret_cast<const v8*>(S + roff[kk]), kf[kk], sacc);
-        dpacc = MFb<T>::mma(*reinterpret_cast<const v8*>(S + 2 * IMG + roff[kk]), vf[kk], dpacc);
+        const int ro = r_off<HD>(l32_, kk * 2 + hh_);
+        sacc = MFb<T>::mma(*reinterpret_cast<const v8*>(S + ro), kf[kk], sacc);
+        dpacc = MFb<T>::mma(*reinterpret_cast<const v8*>(S + 2 * IMG + ro), vf[kk], dpacc);
       }
       // rows of this lane's accumulator registers: q = q0 + (r&3) + 8(r>>2) + 4hh
       if (edge) {  // uniform branch: -inf the masked scores (causal diagonal, sequence tail)
@@ -262,8 +274,8 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_mfma_k(const T* __restrict__ 
       const float* LS = reinterpret_cast<const float*>(S + 4 * IMG + w * 256);
 #pragma unroll
       for (int gq = 0; gq < 4; ++gq) {
-        const f32x4 L4 = *reinterpret_cast<const f32x4*>(LS + 8 * gq + 4 * hh);
-        const f32x4 D4 = *reinterpret_cast<const f32x4*>(LS + 32 + 8 * gq + 4 * hh);
+        const f32x4 L4 = *reinterpret_cast<const f32x4*>(LS + 8 * gq + 4 * hh_);
+        const f32x4 D4 = *reinterpret_cast<const f32x4*>(LS + 32 + 8 * gq + 4 * hh_);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int r = 4 * gq + j;
@@ -295,7 +307,7 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_mfma_k(const T* __restrict__ 
         }
 #pragma unroll
         for (int dt = 0; dt < DT; ++dt) {
-          const int o = troff[dt] + s2 * 16 * ROWB;
+          const int o = t_off<HD>(4 * hh_ + qrow, dt * 32 + glb * 16 + pcol * 4) + s2 * 16 * ROWB;
           const v8 ao = tr8<v8>(S + 3 * IMG, o, o + 8 * ROWB);
           dv[dt] = MFb<T>::mma(ao, pf, dv[dt]);
           const v8 aq = tr8<v8>(S + IMG, o, o + 8 * ROWB);
@@ -303,9 +315,8 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_mfma_k(const T* __restrict__ 
         }
       }
     }
-    if (pre) wait_vm<NPW>(); else wait_vm0();
-    __builtin_amdgcn_s_barrier();
-    slot = slot == 2 ? 0 : slot + 1;
+    ring_wait(i, nsteps);
+    slot = slot == NBUF - 1 ? 0 : slot + 1;
   }
 
   // ---- MHA: write bf16 dK/dV straight into dqkv; GQA: per-head fp32 partials
@@ -346,20 +357,23 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_mfma_k(const T* __restrict__ 
 // (3-slot ring, prefetch distance 2) into three images per slot: K rows (S^T = K Q^T),
 // K transposed (dQ^T += K^T dS^T), V rows (dP^T = V dO^T).  The query is the lane column, so
 // lse / delta are per-lane scalars; 1/sqrt(d) is applied once to the final dQ.
-constexpr int DQ_BQ = 128, DQ_BK = 64, DQ_NBUF = 3;
-template <int HD> constexpr int dq_buf_bytes() { return 3 * DQ_BK * HD * 2; }
+constexpr int DQ_BQ = 128;
+template <int HD, int BK> constexpr int dq_buf_bytes() { return 3 * BK * HD * 2; }
 
-template <typename T, int HD, bool DROP>
-__global__ __launch_bounds__(256, 1) void attn_bwd_dq_k(const T* __restrict__ qkv, const T* __restrict__ dout,
+template <typename T, int HD, bool DROP, int DQ_BK, int NBUF, int OCC>
+__global__ __launch_bounds__(256, OCC) void attn_bwd_dq_k(const T* __restrict__ qkv, const T* __restrict__ out,
+                                                        const T* __restrict__ dout,
                                                         const float* __restrict__ lse,
-                                                        const float* __restrict__ delta, T* __restrict__ dqkv,
+                                                        float* __restrict__ delta, T* __restrict__ dqkv,
                                                         int T_, int H, int G, int B_, bool causal, uint32_t thr,
                                                         float inv_keep, uint64_t seed, uint64_t doff) {
   typedef typename MFb<T>::v8 v8;
   constexpr int KK = HD / 16, DT = HD / 32, CH = HD / 8, ROWB = HD * 2;
-  constexpr int IMG = DQ_BK * ROWB;             // bytes of one [64][HD] image
+  constexpr int IMG = DQ_BK * ROWB;             // bytes of one [BK][HD] image
   constexpr int LD = DQ_BK * CH / 256;          // 1-KiB pieces per wave per image
-  constexpr int BUF = dq_buf_bytes<HD>();
+  constexpr int NKT = DQ_BK / 32;               // 32-key MFMA tiles per step
+  constexpr int BUF = dq_buf_bytes<HD, DQ_BK>();
+  static_assert(NBUF == 2 || NBUF == 3, "ring depth");
   constexpr int NPW = 3 * LD;                   // DMA instructions per wave per step
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
@@ -390,7 +404,19 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dq_k(const T* __restrict__ qk
     of[kk] = *reinterpret_cast<const v8*>(dout + ((long)b * T_ + qc) * ors + (long)h * HD + kk * 16 + hh * 8);
   }
   const float L = lse[((long)b * H + h) * T_ + qc];
-  const float D = delta[((long)b * H + h) * T_ + qc];
+  // delta = rowsum(dO * O): this lane holds half of the row (elements 16kk + 8hh + 0..7)
+  float D;
+  {
+    float part = 0.f;
+#pragma unroll
+    for (int kk = 0; kk < KK; ++kk) {
+      const v8 ov = *reinterpret_cast<const v8*>(out + ((long)b * T_ + qc) * ors + (long)h * HD + kk * 16 + hh * 8);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) part += (float)ov[j] * (float)of[kk][j];
+    }
+    D = part + __shfl_xor(part, 32, 64);
+    if (hh == 0 && qi < T_) delta[((long)b * H + h) * T_ + qi] = D;
+  }
   {
     float lt = L, dt_ = D;
 #pragma unroll
@@ -453,25 +479,33 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dq_k(const T* __restrict__ qk
   const int ntiles = (kend + DQ_BK - 1) / DQ_BK;
   // tiles this wave computes: all up to the one holding its last query (causal)
   const int nact = wq_lo >= T_ ? 0 : (causal ? min(ntiles, wq_hi / DQ_BK + 1) : ntiles);
-  if (ntiles > 0) issue(0, 0);
-  if (ntiles > 1) {
-    issue(1, 1);
-    wait_vm<NPW>();
+  auto ring_wait = [&](int t) {
+    if constexpr (NBUF == 3) {
+      if (t + 2 < ntiles) wait_vm<NPW>(); else wait_vm0();
+    } else {
+      wait_vm0();
+    }
+    __builtin_amdgcn_s_barrier();
+  };
+#pragma unroll
+  for (int j = 0; j < NBUF - 1; ++j)
+    if (j < ntiles) issue(j, j);
+  if constexpr (NBUF == 3) {
+    if (ntiles > 1) wait_vm<NPW>(); else wait_vm0();
   } else {
     wait_vm0();
   }
   __builtin_amdgcn_s_barrier();
   int slot = 0, t = 0;
   for (; t < nact; ++t) {
-    const bool pre = t + 2 < ntiles;
-    if (pre) issue(t + 2, slot == 0 ? 2 : slot - 1);
+    if (t + NBUF - 1 < ntiles) issue(t + NBUF - 1, slot == 0 ? NBUF - 1 : slot - 1);
     const int k0 = t * DQ_BK;
     const char* KR = smem + slot * BUF;
     const char* KT = KR + IMG;
     const char* VR = KR + 2 * IMG;
-    f32x16 sc[2], dp[2];
+    f32x16 sc[NKT], dp[NKT];
 #pragma unroll
-    for (int kt = 0; kt < 2; ++kt) {
+    for (int kt = 0; kt < NKT; ++kt) {
       sc[kt] = f32x16{};
       dp[kt] = f32x16{};
 #pragma unroll
@@ -485,7 +519,7 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dq_k(const T* __restrict__ qk
     const bool edge = (causal && k0 + DQ_BK - 1 > wq_lo) || k0 + DQ_BK > T_ || wq_hi >= T_;
     if (edge) {
 #pragma unroll
-      for (int kt = 0; kt < 2; ++kt)
+      for (int kt = 0; kt < NKT; ++kt)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int key = k0 + kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
@@ -493,7 +527,7 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dq_k(const T* __restrict__ qk
         }
     }
 #pragma unroll
-    for (int kt = 0; kt < 2; ++kt)
+    for (int kt = 0; kt < NKT; ++kt)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const float p = __builtin_amdgcn_exp2f(fmaf(sc[kt][r], c, -L));
@@ -505,7 +539,7 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dq_k(const T* __restrict__ qk
         sc[kt][r] = p * (d - D);
       }
 #pragma unroll
-    for (int kt = 0; kt < 2; ++kt)
+    for (int kt = 0; kt < NKT; ++kt)
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) {
         v8 df;
@@ -522,16 +556,13 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dq_k(const T* __restrict__ qk
           dq[dt] = MFb<T>::mma(a, df, dq[dt]);
         }
       }
-    if (pre) wait_vm<NPW>(); else wait_vm0();
-    __builtin_amdgcn_s_barrier();
-    slot = slot == 2 ? 0 : slot + 1;
+    ring_wait(t);
+    slot = slot == NBUF - 1 ? 0 : slot + 1;
   }
   for (; t < ntiles; ++t) {  // this wave is done; keep the ring and barriers going
-    const bool pre = t + 2 < ntiles;
-    if (pre) issue(t + 2, slot == 0 ? 2 : slot - 1);
-    if (pre) wait_vm<NPW>(); else wait_vm0();
-    __builtin_amdgcn_s_barrier();
-    slot = slot == 2 ? 0 : slot + 1;
+    if (t + NBUF - 1 < ntiles) issue(t + NBUF - 1, slot == 0 ? NBUF - 1 : slot - 1);
+    ring_wait(t);
+    slot = slot == NBUF - 1 ? 0 : slot + 1;
   }
   if (qi < T_) {
     T* row = dqkv + ((long)b * T_ + qi) * rs + (long)h * HD;
@@ -573,34 +604,74 @@ __global__ __launch_bounds__(256) void attn_bwd_kv_reduce_k(const float* __restr
   }
 }
 
+// dK/dV variant: 0 = 2-slot ring at 2 workgroups per CU (one wave's waits hide under the other
+// wave's MFMAs), 1 = 3-slot ring (prefetch distance 2) at 1 workgroup per CU.
+// BLLM_ATTN_KV_VARIANT selects one for A/B measurement.
+static int kv_variant_from_env() {
+  const char* e = getenv("BLLM_ATTN_KV_VARIANT");
+  return e ? atoi(e) : 0;
+}
+// dQ variant: 0 = 32-key tiles, 3-slot ring, 2 workgroups per CU; 1 = 64-key tiles, 1 per CU
+static int q_variant_from_env() {
+  const char* e = getenv("BLLM_ATTN_Q_VARIANT");
+  return e ? atoi(e) : 0;
+}
+
 void attn_bwd_mfma(DType dt, const void* qkv, const void* o, const float* lse, const void* dout, void* dqkv,
                    float* delta, float* dq_acc, float* dkv_part, int B, int T_, int H, int G, int hd, bool causal,
                    float p, uint64_t seed, uint64_t offset, hipStream_t s) {
   (void)dq_acc;
   const uint32_t thr = drop_threshold(p);
   const float ik = p > 0.f ? 1.f / (1.f - p) : 1.f;
-  attn_delta(dt, o, dout, delta, B, T_, H, hd, s);
+  static const int kv_variant = kv_variant_from_env();
+  static const int q_variant = q_variant_from_env();
   const int nkb = (T_ + BWD_BKV - 1) / BWD_BKV;
   dim3 grid_kv(nkb * H * B), grid_q(((T_ + DQ_BQ - 1) / DQ_BQ) * H * B), block(256);
   const bool drop = p > 0.f;
 #define LAUNCH(TT, HDD)                                                                                         \
   do {                                                                                                          \
-    const int lds_kv = BWD_NBUF * dkdv_buf_bytes<HDD>();                                                        \
-    if (drop)                                                                                                   \
-      hipLaunchKernelGGL((attn_bwd_mfma_k<TT, HDD, true>), grid_kv, block, lds_kv, s, (const TT*)qkv,          \
-                         (const TT*)dout, lse, delta, (TT*)dqkv, dkv_part, T_, H, G, B, causal, thr, ik, seed, \
-                         offset);                                                                               \
-    else                                                                                                        \
-      hipLaunchKernelGGL((attn_bwd_mfma_k<TT, HDD, false>), grid_kv, block, lds_kv, s, (const TT*)qkv,         \
-                         (const TT*)dout, lse, delta, (TT*)dqkv, dkv_part, T_, H, G, B, causal, thr, ik, seed, \
-                         offset);                                                                               \
-    const int lds_q = DQ_NBUF * dq_buf_bytes<HDD>();                                                           \
-    if (drop)                                                                                                   \
-      hipLaunchKernelGGL((attn_bwd_dq_k<TT, HDD, true>), grid_q, block, lds_q, s, (const TT*)qkv,               \
-                         (const TT*)dout, lse, delta, (TT*)dqkv, T_, H, G, B, causal, thr, ik, seed, offset);   \
-    else                                                                                                        \
-      hipLaunchKernelGGL((attn_bwd_dq_k<TT, HDD, false>), grid_q, block, lds_q, s, (const TT*)qkv,              \
-                         (const TT*)dout, lse, delta, (TT*)dqkv, T_, H, G, B, causal, thr, ik, seed, offset);   \
+    if (q_variant == 0) {                                                                                       \
+      const int lds_q = 3 * dq_buf_bytes<HDD, 32>();                                                            \
+      if (drop)                                                                                                 \
+        hipLaunchKernelGGL((attn_bwd_dq_k<TT, HDD, true, 32, 3, 2>), grid_q, block, lds_q, s, (const TT*)qkv,  \
+                           (const TT*)o, (const TT*)dout, lse, delta, (TT*)dqkv, T_, H, G, B, causal, thr, ik, \
+                           seed, offset);                                                                       \
+      else                                                                                                      \
+        hipLaunchKernelGGL((attn_bwd_dq_k<TT, HDD, false, 32, 3, 2>), grid_q, block, lds_q, s, (const TT*)qkv, \
+                           (const TT*)o, (const TT*)dout, lse, delta, (TT*)dqkv, T_, H, G, B, causal, thr, ik, \
+                           seed, offset);                                                                       \
+    } else {                                                                                                    \
+      const int lds_q = 3 * dq_buf_bytes<HDD, 64>();                                                            \
+      if (drop)                                                                                                 \
+        hipLaunchKernelGGL((attn_bwd_dq_k<TT, HDD, true, 64, 3, 1>), grid_q, block, lds_q, s, (const TT*)qkv,  \
+                           (const TT*)o, (const TT*)dout, lse, delta, (TT*)dqkv, T_, H, G, B, causal, thr, ik, \
+                           seed, offset);                                                                       \
+      else                                                                                                      \
+        hipLaunchKernelGGL((attn_bwd_dq_k<TT, HDD, false, 64, 3, 1>), grid_q, block, lds_q, s, (const TT*)qkv, \
+                           (const TT*)o, (const TT*)dout, lse, delta, (TT*)dqkv, T_, H, G, B, causal, thr, ik, \
+                           seed, offset);                                                                       \
+    }                                                                                                           \
+    if (kv_variant == 0) {                                                                                      \
+      const int lds_kv = 2 * dkdv_buf_bytes<HDD>();                                                             \
+      if (drop)                                                                                                 \
+        hipLaunchKernelGGL((attn_bwd_mfma_k<TT, HDD, true, 2, 2>), grid_kv, block, lds_kv, s, (const TT*)qkv,  \
+                           (const TT*)dout, lse, delta, (TT*)dqkv, dkv_part, T_, H, G, B, causal, thr, ik,     \
+                           seed, offset);                                                                       \
+      else                                                                                                      \
+        hipLaunchKernelGGL((attn_bwd_mfma_k<TT, HDD, false, 2, 2>), grid_kv, block, lds_kv, s, (const TT*)qkv, \
+                           (const TT*)dout, lse, delta, (TT*)dqkv, dkv_part, T_, H, G, B, causal, thr, ik,     \
+                           seed, offset);                                                                       \
+    } else {                                                                                                    \
+      const int lds_kv = 3 * dkdv_buf_bytes<HDD>();                                                             \
+      if (drop)                                                                                                 \
+        hipLaunchKernelGGL((attn_bwd_mfma_k<TT, HDD, true, 3, 1>), grid_kv, block, lds_kv, s, (const TT*)qkv,  \
+                           (const TT*)dout, lse, delta, (TT*)dqkv, dkv_part, T_, H, G, B, causal, thr, ik,     \
+                           seed, offset);                                                                       \
+      else                                                                                                      \
+        hipLaunchKernelGGL((attn_bwd_mfma_k<TT, HDD, false, 3, 1>), grid_kv, block, lds_kv, s, (const TT*)qkv, \
+                           (const TT*)dout, lse, delta, (TT*)dqkv, dkv_part, T_, H, G, B, causal, thr, ik,     \
+                           seed, offset);                                                                       \
+    }                                                                                                           \
   } while (0)
   if (dt == DType::BF16) {
     if (hd == 128) LAUNCH(bf16_t, 128); else LAUNCH(bf16_t, 64);
