@@ -21,6 +21,7 @@
 // ds_read_b128 row reads), V in 64-B chunks (conflict-free transposed reads).
 // Attention-probability dropout (GPT-2) uses the stateless counter hash of common.h.
 #include <float.h>
+#include <stdlib.h>
 #include "api.h"
 
 namespace bllm {
@@ -47,7 +48,7 @@ template <> struct MF<f16_t> {
 
 constexpr float kLog2e = 1.4426950408889634f;
 constexpr int FWD_BQ = 128;  // queries per workgroup
-constexpr int FWD_BK = 64;   // keys per tile
+// keys per tile (FWD_BK), LDS ring depth and workgroups per CU are template parameters
 
 // ---- swizzled LDS images (byte offsets) -------------------------------------------------
 // K: [64 keys][HD] bf16, 16-B chunk c16 of row r stored at chunk c16 ^ swz
@@ -76,8 +77,8 @@ template <typename T> __device__ __forceinline__ uint32_t pack2(float a, float b
 // per-lane offsets, 2x(LD) saddr DMA issues with precomputed per-lane source offsets, and
 // ~130 VALU of online softmax (scale folded into the exp2 FMA; the O rescale is skipped when
 // no lane's running max moved, which is the common case after the first tiles).
-template <typename T, int HD, bool DROP>
-__global__ __launch_bounds__(256, 2) void attn_fwd_mfma_k(const T* __restrict__ qkv, T* __restrict__ out,
+template <typename T, int HD, bool DROP, int FWD_BK, int NBUF, int OCC>
+__global__ __launch_bounds__(256, OCC) void attn_fwd_mfma_k(const T* __restrict__ qkv, T* __restrict__ out,
                                                           float* __restrict__ lse, int T_, int H, int G, int B_,
                                                           bool causal, uint32_t thr, float inv_keep, uint64_t seed,
                                                           uint64_t doff) {
@@ -89,6 +90,8 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_mfma_k(const T* __restrict__ 
   constexpr int TILE_B = FWD_BK * ROWB;     // bytes per K (or V) tile
   constexpr int LD = FWD_BK * CH / 256;     // 1-KiB pieces per wave per tile (K and V each)
   constexpr int NPW = 2 * LD;
+  constexpr int NKT = FWD_BK / 32;          // 32-key MFMA tiles per step
+  static_assert(NBUF == 2 || NBUF == 3, "ring depth");
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   // heaviest (latest, for causal) q-blocks first over the whole grid; the q-blocks of one
@@ -180,21 +183,33 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_mfma_k(const T* __restrict__ 
     }
   };
 
-  if (ntiles > 0) issue(0, 0);
-  wait_vm0();
+  auto ring_wait = [&](int t) {
+    if constexpr (NBUF == 3) {
+      if (t + 2 < ntiles) wait_vm<NPW>(); else wait_vm0();
+    } else {
+      wait_vm0();
+    }
+    __builtin_amdgcn_s_barrier();
+  };
+#pragma unroll
+  for (int j = 0; j < NBUF - 1; ++j)
+    if (j < ntiles) issue(j, j);
+  if constexpr (NBUF == 3) {
+    if (ntiles > 1) wait_vm<NPW>(); else wait_vm0();
+  } else {
+    wait_vm0();
+  }
   __builtin_amdgcn_s_barrier();
-  int t = 0;
+  int t = 0, buf = 0;
   for (; t < nact; ++t) {
-    const int buf = t & 1;
-    const bool pre = t + 1 < ntiles;
-    if (pre) issue(t + 1, buf ^ 1);
+    if (t + NBUF - 1 < ntiles) issue(t + NBUF - 1, buf == 0 ? NBUF - 1 : buf - 1);
     const int k0 = t * FWD_BK;
     const char* kb = smem + buf * 2 * TILE_B;
     const char* vb = kb + TILE_B;
-    // ---- S^T = K Q^T for two 32-key sub-tiles
-    f32x16 s[2];
+    // ---- S^T = K Q^T for the 32-key sub-tiles
+    f32x16 s[NKT];
 #pragma unroll
-    for (int kt = 0; kt < 2; ++kt) {
+    for (int kt = 0; kt < NKT; ++kt) {
       s[kt] = f32x16{};
 #pragma unroll
       for (int kk = 0; kk < KK; ++kk)
@@ -204,7 +219,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_mfma_k(const T* __restrict__ 
     const bool edge = (causal && k0 + FWD_BK - 1 > wq_lo) || k0 + FWD_BK > T_ || wq_hi >= T_;
     if (edge) {
 #pragma unroll
-      for (int kt = 0; kt < 2; ++kt) {
+      for (int kt = 0; kt < NKT; ++kt) {
         const int kb0 = k0 + kt * 32 + 4 * hh;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
@@ -215,7 +230,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_mfma_k(const T* __restrict__ 
     }
     float mx = -INFINITY;
 #pragma unroll
-    for (int kt = 0; kt < 2; ++kt)
+    for (int kt = 0; kt < NKT; ++kt)
 #pragma unroll
       for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s[kt][r]);
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64)) * c;
@@ -230,7 +245,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_mfma_k(const T* __restrict__ 
     }
     float ls = 0.f;
 #pragma unroll
-    for (int kt = 0; kt < 2; ++kt)
+    for (int kt = 0; kt < NKT; ++kt)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const float p = __builtin_amdgcn_exp2f(fmaf(s[kt][r], c, -m));
@@ -246,7 +261,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_mfma_k(const T* __restrict__ 
     l += ls;
     // ---- O^T += V^T P^T: P fragments packed from the accumulators, V^T by transposed reads
 #pragma unroll
-    for (int kt = 0; kt < 2; ++kt)
+    for (int kt = 0; kt < NKT; ++kt)
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) {
         v8 pf;
@@ -267,13 +282,13 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_mfma_k(const T* __restrict__ 
           o[dt] = MF<T>::mma(va, pf, o[dt]);
         }
       }
-    wait_vm0();  // the DMA of tile t+1 has landed (asm-issued, so drained by hand)
-    __builtin_amdgcn_s_barrier();
+    ring_wait(t);  // the DMA of tile t+1 has landed (asm-issued, so drained by hand)
+    buf = buf == NBUF - 1 ? 0 : buf + 1;
   }
   for (; t < ntiles; ++t) {  // wave done (causal): keep the DMA ring and barriers going
-    if (t + 1 < ntiles) issue(t + 1, (t & 1) ^ 1);
-    wait_vm0();
-    __builtin_amdgcn_s_barrier();
+    if (t + NBUF - 1 < ntiles) issue(t + NBUF - 1, buf == 0 ? NBUF - 1 : buf - 1);
+    ring_wait(t);
+    buf = buf == NBUF - 1 ? 0 : buf + 1;
   }
 
   // ---- epilogue: combine the two halves' partial sums, normalise, store O and LSE
@@ -297,19 +312,35 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_mfma_k(const T* __restrict__ 
 
 bool attn_mfma_head_dim(int hd) { return hd == 64 || hd == 128; }
 
+// forward variant (BLLM_ATTN_FWD_VARIANT, for A/B measurement): 0 = 64-key tiles, 2-slot ring,
+// 2 WGs/CU (measured best: equal at hd 128, +7% at hd 64); 1 = 32-key tiles, 3-slot ring;
+// 2 = 32-key tiles, 2-slot ring (up to 3 WGs/CU)
+static int fwd_variant_from_env() {
+  const char* e = getenv("BLLM_ATTN_FWD_VARIANT");
+  return e ? atoi(e) : 0;
+}
+
 void attn_fwd_mfma(DType dt, const void* qkv, void* o, float* lse, int B, int T_, int H, int G, int hd, bool causal,
                    float p, uint64_t seed, uint64_t offset, hipStream_t s) {
   const uint32_t thr = drop_threshold(p);
   const float ik = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  static const int fwd_variant = fwd_variant_from_env();
   dim3 grid(((T_ + FWD_BQ - 1) / FWD_BQ) * H * B), block(256);
+#define LAUNCH_V(TT, HDD, BK, NB, OC)                                                                         \
+  do {                                                                                                        \
+    const int lds = NB * 2 * BK * HDD * 2;                                                                    \
+    if (p > 0.f)                                                                                              \
+      hipLaunchKernelGGL((attn_fwd_mfma_k<TT, HDD, true, BK, NB, OC>), grid, block, lds, s, (const TT*)qkv,   \
+                         (TT*)o, lse, T_, H, G, B, causal, thr, ik, seed, offset);                            \
+    else                                                                                                      \
+      hipLaunchKernelGGL((attn_fwd_mfma_k<TT, HDD, false, BK, NB, OC>), grid, block, lds, s, (const TT*)qkv,  \
+                         (TT*)o, lse, T_, H, G, B, causal, thr, ik, seed, offset);                            \
+  } while (0)
 #define LAUNCH(TT, HDD)                                                                                       \
   do {                                                                                                        \
-    if (p > 0.f)                                                                                              \
-      hipLaunchKernelGGL((attn_fwd_mfma_k<TT, HDD, true>), grid, block, 2 * 2 * FWD_BK * HDD * 2, s,          \
-                         (const TT*)qkv, (TT*)o, lse, T_, H, G, B, causal, thr, ik, seed, offset);              \
-    else                                                                                                      \
-      hipLaunchKernelGGL((attn_fwd_mfma_k<TT, HDD, false>), grid, block, 2 * 2 * FWD_BK * HDD * 2, s,         \
-                         (const TT*)qkv, (TT*)o, lse, T_, H, G, B, causal, thr, ik, seed, offset);              \
+    if (fwd_variant == 1) LAUNCH_V(TT, HDD, 32, 3, 2);                                                        \
+    else if (fwd_variant == 2) LAUNCH_V(TT, HDD, 32, 2, 3);                                                   \
+    else LAUNCH_V(TT, HDD, 64, 2, 2);                                                                         \
   } while (0)
   if (dt == DType::BF16) {
     if (hd == 128) LAUNCH(bf16_t, 128); else LAUNCH(bf16_t, 64);
@@ -317,6 +348,7 @@ void attn_fwd_mfma(DType dt, const void* qkv, void* o, float* lse, int B, int T_
     if (hd == 128) LAUNCH(f16_t, 128); else LAUNCH(f16_t, 64);
   }
 #undef LAUNCH
+#undef LAUNCH_V
 }
 
 }  // namespace bllm
