@@ -112,31 +112,35 @@ template <typename T>
 __global__ __launch_bounds__(256) void rope_k(T* __restrict__ qkv, const float* __restrict__ cosT,
                                               const float* __restrict__ sinT, long N, int T_, int nh_rot,
                                               int row_stride, int hd, int pos_offset, float sgn) {
+  // one thread = 8 rotation pairs (two 16-B vectors of the head, 8 fp32 cos/sin each);
+  // 32-bit index math (N * heads * chunks < 2^31 for every supported shape)
+  static_assert(sizeof(T) == 2, "16-bit element types (fp32 uses rope_scalar_k)");
   const int half = hd / 2;
   const int cpb = half / 8;  // chunks of 8 pairs per head
-  const long total = N * nh_rot * cpb;
-  for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
-    const int ch = (int)(i % cpb);
-    const long t = i / cpb;
-    const int h = (int)(t % nh_rot);
-    const long r = t / nh_rot;
-    const int pos = (int)(r % T_) + pos_offset;
-    T* base = qkv + r * row_stride + (long)h * hd + ch * 8;
+  const int per_row = nh_rot * cpb;
+  const int total = (int)(N * per_row);
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
+    const int r = i / per_row;
+    const int rem = i - r * per_row;
+    const int h = rem / cpb, ch = rem - h * cpb;
+    const int pos = r % T_ + pos_offset;
+    T* base = qkv + (long)r * row_stride + h * hd + ch * 8;
     const float* cp = cosT + (long)pos * half + ch * 8;
     const float* sp = sinT + (long)pos * half + ch * 8;
-    float x1[8], x2[8], c[8], s[8];
+    const Vec16<T> a = ld16(base), b = ld16(base + half);
+    const float4 c0 = *reinterpret_cast<const float4*>(cp), c1 = *reinterpret_cast<const float4*>(cp + 4);
+    const float4 s0 = *reinterpret_cast<const float4*>(sp), s1 = *reinterpret_cast<const float4*>(sp + 4);
+    const float c[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+    const float sn[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+    Vec16<T> oa, ob;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      x1[j] = to_f(base[j]);
-      x2[j] = to_f(base[half + j]);
-      c[j] = cp[j];
-      s[j] = sgn * sp[j];
+      const float x1 = to_f(a.v[j]), x2 = to_f(b.v[j]), sj = sgn * sn[j];
+      oa.v[j] = from_f<T>(x1 * c[j] - x2 * sj);
+      ob.v[j] = from_f<T>(x2 * c[j] + x1 * sj);
     }
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      base[j] = from_f<T>(x1[j] * c[j] - x2[j] * s[j]);
-      base[half + j] = from_f<T>(x2[j] * c[j] + x1[j] * s[j]);
-    }
+    st16(base, oa);
+    st16(base + half, ob);
   }
 }
 
@@ -215,11 +219,15 @@ void rope(DType dt, void* qkv, const float* cosT, const float* sinT, long N, int
   const int nh = H + G, stride = (H + 2 * G) * hd;
   const float sgn = inverse ? -1.f : 1.f;
   BLLM_DISPATCH(dt, T, {
-    if ((hd / 2) % 8 == 0) {
-      long tot = N * nh * (hd / 16);
-      hipLaunchKernelGGL(rope_k<T>, dim3(ew_grid(tot)), dim3(256), 0, s, (T*)qkv, cosT, sinT, N, T_, nh, stride,
-                         hd, pos_offset, sgn);
-    } else {
+    if constexpr (sizeof(T) == 2) {
+      if ((hd / 2) % 8 == 0) {
+        long tot = N * nh * (hd / 16);
+        hipLaunchKernelGGL(rope_k<T>, dim3(ew_grid(tot)), dim3(256), 0, s, (T*)qkv, cosT, sinT, N, T_, nh, stride,
+                           hd, pos_offset, sgn);
+        return;
+      }
+    }
+    {
       long tot = N * nh * (hd / 2);
       hipLaunchKernelGGL(rope_scalar_k<T>, dim3(ew_grid(tot)), dim3(256), 0, s, (T*)qkv, cosT, sinT, N, T_, nh,
                          stride, hd, pos_offset, sgn);

@@ -11,7 +11,7 @@
 namespace bllm {
 
 constexpr int ROWS_PER_WG = 4;  // 4 waves x 1 row
-constexpr int MAX_BWD_WG = 1024;
+constexpr int MAX_BWD_WG = 512;
 
 template <typename T, int NV, bool LN>
 __global__ __launch_bounds__(256) void norm_fwd_k(const T* __restrict__ x, const T* __restrict__ w,
@@ -197,10 +197,17 @@ __global__ __launch_bounds__(256) void col_reduce_k(const float* __restrict__ pa
   __shared__ float red[16][17];
   const int cl = threadIdx.x & 15, g = threadIdx.x >> 4;
   const int c = blockIdx.x * 16 + cl;
-  float s = 0.f;
-  if (c < d)
-    for (int p = g; p < P; p += 16) s += part[(size_t)p * d + c];
-  red[g][cl] = s;
+  float s = 0.f, s2 = 0.f;
+  if (c < d) {
+    int p = g;
+#pragma unroll 4
+    for (; p + 16 < P; p += 32) {  // two independent chains keep more loads in flight
+      s += part[(size_t)p * d + c];
+      s2 += part[(size_t)(p + 16) * d + c];
+    }
+    if (p < P) s += part[(size_t)p * d + c];
+  }
+  red[g][cl] = s + s2;
   __syncthreads();
   if (threadIdx.x < 16 && c < d) {
     float t = 0.f;
