@@ -162,20 +162,24 @@ class FSDPEngine(LocalEngine):
         fb = unit.train
         if fb is not None:
             w = dist.reduce_scatter_tensor(fb.grad_shard, fb.grad, group=self.pg, async_op=True)
-            if self.is_cuda:
-                # RCCL records fb.grad on its stream: releasing the storage now is stream-safe
-                self._rs_works.append((w, None))
-                _free(fb.grad)
-            else:
-                self._rs_works.append((w, fb))
+            # the full gradient is released only after the reduce-scatter completed: freeing it
+            # now would hand the block back to the compute stream's allocator pool while RCCL
+            # may still be reading it (288 GB leaves room to hold them until the end of backward)
+            self._rs_works.append((w, fb))
+            self._retire_rs(keep=2)
         self._reshard(unit)
 
-    def finish_backward(self):
-        for w, fb in self._rs_works:
+    def _retire_rs(self, keep: int):
+        """Wait for and free all but the ``keep`` most recent reduce-scatters (bounded memory
+        without stalling the stream on the one just issued)."""
+        while len(self._rs_works) > keep:
+            w, fb = self._rs_works.pop(0)
             w.wait()
             if fb is not None:
                 _free(fb.grad)
-        self._rs_works = []
+
+    def finish_backward(self):
+        self._retire_rs(keep=0)
         self._in_backward = False
 
     # ------------------------------------------------------------------ optimizer
