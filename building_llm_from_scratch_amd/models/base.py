@@ -18,6 +18,7 @@ gives exact control over:
 """
 from __future__ import annotations
 
+from contextlib import contextmanager
 from typing import List, Optional
 
 import torch
@@ -46,6 +47,12 @@ class LocalEngine:
 
     def finish_backward(self):
         pass
+
+    @contextmanager
+    def params_resident(self):
+        """Inference over many forwards (KV-cache decode): every unit's full parameters stay
+        available for the duration (FSDP gathers them once instead of per forward)."""
+        yield
 
 
 class RunCtx:
@@ -106,6 +113,37 @@ class UnitCompute:
 
     def backward(self, dy, saved):
         raise NotImplementedError
+
+    def infer(self, *args):
+        """KV-cache inference step (see BaseLM.forward_cached)."""
+        raise NotImplementedError
+
+
+def cached_attention(qkv, B: int, t: int, pos: int, H: int, G: int, hd: int, kv, causal: bool = True):
+    """Attention of ``t`` new tokens at positions ``pos..pos+t-1`` (packed qkv rows, RoPE
+    already applied) against a per-block KV cache ``kv = (k, v)`` of [B, G, Tmax, hd]; the new
+    keys/values are appended to the cache first.  Prefill from position 0 runs the flash kernel
+    on the packed rows; single-token decode runs the HIP decode kernel over the cache."""
+    from .. import ops
+    kc, vc = kv
+    rows = qkv.view(B, t, H + 2 * G, hd)
+    kc[:, :, pos:pos + t].copy_(rows[:, :, H:H + G].transpose(1, 2))
+    vc[:, :, pos:pos + t].copy_(rows[:, :, H + G:].transpose(1, 2))
+    if pos == 0:
+        return ops.flash_attn_fwd(qkv, B, t, H, G, hd, causal)[0]
+    if t == 1:
+        return ops.attn_decode(rows[:, 0, :H], kc, vc, pos + 1)
+    # chunked continuation (t > 1 after a prefix): explicit masked attention over the cache
+    L = pos + t
+    q = rows[:, :, :H].transpose(1, 2).float()                                   # [B,H,t,hd]
+    k = kc[:, :, :L].float().repeat_interleave(H // G, dim=1)                    # [B,H,L,hd]
+    v = vc[:, :, :L].float().repeat_interleave(H // G, dim=1)
+    sc = (q @ k.transpose(-1, -2)) / (hd ** 0.5)
+    qpos = torch.arange(pos, L, device=qkv.device)[:, None]
+    kpos = torch.arange(L, device=qkv.device)[None, :]
+    sc = sc.masked_fill(kpos > qpos, float("-inf"))
+    o = torch.softmax(sc, dim=-1) @ v                                            # [B,H,t,hd]
+    return o.transpose(1, 2).reshape(B * t, H * hd).to(qkv.dtype)
 
 
 # ---------------------------------------------------------------------------
@@ -337,6 +375,33 @@ class BaseLM(nn.Module):
             logits, _ = head.forward_logits(x, save=False)
             eng.post_forward(head.unit)
             return logits.view(B, T, -1)
+
+    # -- KV-cache inference -------------------------------------------------------------
+    def new_kv_cache(self, B: int, max_len: int):
+        """Per-block (K, V) caches [B, G, max_len, hd] in the parameter dtype."""
+        self._ensure_flat()
+        cfg = self.cfg
+        G = cfg.n_kv_groups if cfg.is_llama else cfg.n_heads
+        p = self._comps[1].unit
+        dev, dt = self._anchor.device, (p.train.dtype if p.train is not None else p.frozen.dtype)
+        return [(torch.empty(B, G, max_len, cfg.head_dim, device=dev, dtype=dt),
+                 torch.empty(B, G, max_len, cfg.head_dim, device=dev, dtype=dt))
+                for _ in range(len(self._comps) - 2)]
+
+    @torch.no_grad()
+    def forward_cached(self, idx: torch.Tensor, cache, pos: int) -> torch.Tensor:
+        """Run ``idx`` [B, t] (positions ``pos..pos+t-1``) through the model, appending to
+        ``cache``; returns the last position's logits [B, V].  Call inside
+        ``engine.params_resident()`` (FSDP) — see train/generate.py:generate_cached."""
+        self._ensure_flat()
+        comps, rc = self._comps, self._rctx
+        rc.sync_all_params()
+        B, t = idx.shape
+        idx = idx.to(self._anchor.device)
+        x = comps[0].infer(idx, pos)
+        for c, kv in zip(comps[1:-1], cache):
+            x = c.infer(x, B, t, pos, kv)
+        return comps[-1].infer(x, B, t)
 
     def sync_params(self):
         """Make the current stream wait for every in-flight (overlapped) optimizer update."""

@@ -20,7 +20,7 @@ import torch
 import torch.nn as nn
 
 from .. import ops
-from .base import BaseLM, UnitCompute
+from .base import BaseLM, UnitCompute, cached_attention
 from .linear import FusedLinear
 from .llama import HeadComputeMixin, _write_vec_grad
 
@@ -80,6 +80,12 @@ class GPTEmbedCompute(UnitCompute):
                               self.unit.data(self.m.pos_emb.weight), rc.T, p, rc.seed, off)
         return x.view(rc.B, rc.T, -1), ((idx.reshape(-1), p, off) if save else None)
 
+    def infer(self, idx, pos):
+        B, t = idx.shape
+        wte = self.unit.data(self.m.tok_emb.weight)
+        wpe = self.unit.data(self.m.pos_emb.weight)
+        return (wte[idx.reshape(-1)].view(B, t, -1) + wpe[pos:pos + t]).reshape(B * t, -1)
+
     def backward(self, dx, saved):
         idx, p, off = saved
         rc = self.rctx
@@ -118,6 +124,17 @@ class GPTBlockCompute(UnitCompute):
     def _ln(self, x, norm):
         u = self.unit
         return ops.layernorm_fwd(x, u.data(norm.weight), u.data(norm.bias), 1e-5)
+
+    def infer(self, x2d, B, t, pos, kv):
+        cfg, b = self.rctx.cfg, self.block
+        H, hd = cfg.n_heads, cfg.head_dim
+        h1 = self._ln(x2d, b.norm1)[0]
+        qkv, _ = self.qkv.forward(h1)
+        a, _ = self.o.forward(cached_attention(qkv, B, t, pos, H, H, hd, kv))
+        x2 = x2d + a
+        f, _ = self.fc.forward(self._ln(x2, b.norm2)[0])
+        m, _ = self.proj.forward(ops.gelu_fwd(f))
+        return x2 + m
 
     def forward(self, x, save, replay=None):
         rc, cfg, b = self.rctx, self.rctx.cfg, self.block

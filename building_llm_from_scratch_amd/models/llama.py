@@ -21,7 +21,7 @@ import torch
 import torch.nn as nn
 
 from .. import ops
-from .base import BaseLM, UnitCompute
+from .base import BaseLM, UnitCompute, cached_attention
 from .linear import FusedLinear
 
 
@@ -119,6 +119,10 @@ class LlamaEmbedCompute(UnitCompute):
             ops.embedding_bwd(saved, dx.view(-1, dx.shape[-1]), g, None, self.rctx.T, self.rctx.accumulate)
         return None
 
+    def infer(self, idx, pos):
+        W = self.unit.data(self.m.tok_emb.weight)
+        return ops.embedding_fwd(idx.reshape(-1).contiguous(), W, None, idx.shape[1])
+
 
 class LlamaBlockCompute(UnitCompute):
     def __init__(self, rctx, block: TransformerBlock, i: int):
@@ -166,6 +170,20 @@ class LlamaBlockCompute(UnitCompute):
                 saved.update(h1=h1, h2=h2)
         return x3.view(B, T, d), saved
 
+    def infer(self, x2d, B, t, pos, kv):
+        cfg, u, b = self.rctx.cfg, self.unit, self.block
+        H, G, hd, eps = cfg.n_heads, cfg.n_kv_groups, cfg.head_dim, cfg.norm_eps
+        cos, sin = self.rctx.rope
+        h1, _ = ops.rmsnorm_fwd(x2d, u.data(b.norm1.weight), eps)
+        qkv, _ = self.qkv.forward(h1)
+        ops.rope_(qkv, cos, sin, t, H, G, hd, pos_offset=pos)
+        o = cached_attention(qkv, B, t, pos, H, G, hd, kv)
+        x2, _ = self.o.forward(o, residual=x2d)
+        h2, _ = ops.rmsnorm_fwd(x2, u.data(b.norm2.weight), eps)
+        gu, _ = self.gu.forward(h2)
+        x3, _ = self.down.forward(ops.swiglu_fwd(gu), residual=x2)
+        return x3
+
     def backward(self, dy, s):
         rc, cfg, u, b = self.rctx, self.rctx.cfg, self.unit, self.block
         B, T = rc.B, rc.T
@@ -211,6 +229,11 @@ class HeadComputeMixin:
 
     def _norm_bwd(self, dh, ns, dx_acc=None):
         raise NotImplementedError
+
+    def infer(self, x2d, B, t):
+        last = x2d.view(B, t, -1)[:, -1, :].contiguous()
+        logits, _ = self.forward_logits(last, save=False)
+        return logits
 
     def forward_logits(self, x, save):
         x2d = x.reshape(-1, x.shape[-1])

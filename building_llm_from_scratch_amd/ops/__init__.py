@@ -19,7 +19,7 @@ __all__ = [
     "rmsnorm_fwd", "rmsnorm_bwd", "layernorm_fwd", "layernorm_bwd", "dropout_add", "dropout_bwd",
     "rope_", "rope_tables", "flash_attn_fwd", "flash_attn_bwd", "swiglu_fwd", "swiglu_bwd",
     "gelu_fwd", "gelu_bwd", "ce_fwd", "ce_bwd_", "embedding_fwd", "embedding_bwd",
-    "sq_norm_multi", "adamw_step_", "ext_available", "load_ext", "attention_backend",
+    "sq_norm_multi", "adamw_step_", "attn_decode", "ext_available", "load_ext", "attention_backend",
 ]
 
 rope_tables = ref.rope_tables
@@ -94,6 +94,15 @@ def flash_attn_fwd(qkv, B, T, H, G, hd, causal=True, dropout_p=0.0, seed=0, offs
         load_ext(required=True)
         return _k().flash_attn_fwd(qkv, B, T, H, G, hd, causal, float(dropout_p), int(seed), int(offset))
     return ref.flash_attn_fwd(qkv, B, T, H, G, hd, causal, dropout_p, seed, offset)
+
+
+def attn_decode(q, kcache, vcache, L: int):
+    """One new query per sequence against the first ``L`` cached positions.
+    q [B, H, hd]; kcache / vcache [B, G, Tmax, hd] -> [B, H*hd]."""
+    if q.device.type == "cuda" and q.dtype in (torch.bfloat16, torch.float16):
+        load_ext(required=True)
+        return _k().attn_decode(q.contiguous(), kcache, vcache, int(L))
+    return ref.attn_decode(q, kcache, vcache, L)
 
 
 def flash_attn_bwd(qkv, o, lse, do, B, T, H, G, hd, causal=True, dropout_p=0.0, seed=0, offset=0):

@@ -344,3 +344,14 @@ def adamw_step_(param: torch.Tensor, master: Optional[torch.Tensor], grad: torch
     p32.addcdiv_(exp_avg, denom, value=-lr / bc1)
     if master is not None:
         param.copy_(master.to(param.dtype))
+
+
+def attn_decode(q, kcache, vcache, L: int):
+    """Reference for the KV-cache decode kernel: q [B,H,hd], cache [B,G,Tmax,hd] -> [B,H*hd]."""
+    B, H, hd = q.shape
+    G = kcache.shape[1]
+    k = kcache[:, :, :L].float().repeat_interleave(H // G, dim=1)   # [B,H,L,hd]
+    v = vcache[:, :, :L].float().repeat_interleave(H // G, dim=1)
+    s = torch.einsum("bhd,bhld->bhl", q.float(), k) / math.sqrt(hd)
+    p = torch.softmax(s, dim=-1)
+    return torch.einsum("bhl,bhld->bhd", p, v).reshape(B, H * hd).to(q.dtype)

@@ -22,6 +22,7 @@ gradients are reduced in that dtype (reference bf16 policy), master weights stay
 """
 from __future__ import annotations
 
+from contextlib import contextmanager
 from typing import Dict, List, Optional
 
 import torch
@@ -202,6 +203,21 @@ class FSDPEngine(LocalEngine):
         for ui in slot.units:
             if ui < self.prefetch_after_step:
                 self._issue_gather(self.units[ui], async_op=True)
+
+    # ------------------------------------------------------------------ inference
+    @contextmanager
+    def params_resident(self):
+        """Gather every unit once for a multi-forward inference (KV-cache sampling) instead of
+        re-gathering the whole model per generated token (reference X11: 200 full gathers per
+        sample print)."""
+        self.model.rctx.sync_all_params()
+        for u in self.units:
+            self._wait_gather(u)
+        try:
+            yield
+        finally:
+            for u in self.units:
+                self._reshard(u)
 
     # ------------------------------------------------------------------ checkpoint
     def full_state_dict(self) -> Optional[Dict[str, torch.Tensor]]:

@@ -11,6 +11,7 @@ all-gather per bucket rebuilds the full bf16 parameters in place.
 """
 from __future__ import annotations
 
+from contextlib import contextmanager
 from typing import Optional
 
 import torch
@@ -101,6 +102,12 @@ class ZeroEngine(LocalEngine):
         for w in self._ag_works.values():
             w.wait()
         self._ag_works = {}
+
+    @contextmanager
+    def params_resident(self):
+        self.model.rctx.sync_all_params()
+        self.sync()
+        yield
 
     def full_state_dict(self):
         self.model.rctx.sync_all_params()

@@ -27,7 +27,7 @@ import torch.distributed as dist
 from ..logger import MetricsWriter, setup_logger
 from ..utils.misc import read_json_file, read_text_file, text_to_token_ids, token_ids_to_text
 from .checkpoint import save_model, save_resume_state
-from .generate import generate
+from .generate import generate_cached
 
 logger = setup_logger("train")
 
@@ -237,7 +237,7 @@ class Trainer:
                                   max_new_tokens=None):
         self.model.eval()
         encoded = text_to_token_ids(start_context, self.loaderObj.tokenizer, self.config).to(self.device)
-        token_ids = generate(self.model, encoded, max_new_tokens or self.sample_tokens,
+        token_ids = generate_cached(self.model, encoded, max_new_tokens or self.sample_tokens,
                              self.config["context_length"], temperature=temperature, top_k=top_k,
                              eos_id=self.config["eos_id"])
         decoded = token_ids_to_text(token_ids.cpu(), self.loaderObj.tokenizer)

@@ -46,6 +46,11 @@ void attn_bwd_naive(DType dt, const void* qkv, const void* o, const float* lse, 
 void attn_delta(DType dt, const void* o, const void* dout, float* delta, int B, int T, int H, int hd,
                 hipStream_t s);
 
+// attn_decode.hip — single-query attention over a [B, G, Tmax, hd] KV cache
+int attn_decode_max_len();
+void attn_decode(DType dt, const void* q, const void* kc, const void* vc, void* out, int B, int H, int G, int hd,
+                 int Tmax, int L, hipStream_t s);
+
 // loss.hip
 void ce_fwd(DType dt, const void* logits, const int64_t* tgt, float* loss, float* lse, long N, long V,
             long ignore_index, hipStream_t s);

@@ -187,6 +187,23 @@ void rope_(Tensor& qkv, const Tensor& cos, const Tensor& sin, int64_t T, int64_t
 }
 
 // ------------------------------------------------------------------ attention
+// q [B, H, hd]; kc / vc [B, G, Tmax, hd] with the first L positions valid -> out [B, H*hd]
+Tensor attn_decode(const Tensor& q, const Tensor& kc, const Tensor& vc, int64_t L) {
+  check_gpu(q, "q"); check_gpu(kc, "kcache"); check_gpu(vc, "vcache");
+  c10::DeviceGuard g(q.device());
+  TORCH_CHECK(q.scalar_type() == at::kBFloat16 || q.scalar_type() == at::kHalf, "attn_decode: bf16/fp16 only");
+  TORCH_CHECK(kc.scalar_type() == q.scalar_type() && vc.scalar_type() == q.scalar_type());
+  TORCH_CHECK(q.dim() == 3 && kc.dim() == 4 && vc.sizes() == kc.sizes(), "attn_decode: shapes");
+  const int64_t B = q.size(0), H = q.size(1), hd = q.size(2), G = kc.size(1), Tmax = kc.size(2);
+  TORCH_CHECK(kc.size(0) == B && kc.size(3) == hd && H % G == 0, "attn_decode: cache/q mismatch");
+  TORCH_CHECK(hd == 64 || hd == 128, "attn_decode: head_dim 64 or 128");
+  TORCH_CHECK(L >= 1 && L <= Tmax && L <= bllm::attn_decode_max_len(), "attn_decode: bad length ", L);
+  auto out = at::empty({B, H * hd}, q.options());
+  bllm::attn_decode(dt_of(q), q.data_ptr(), kc.data_ptr(), vc.data_ptr(), out.data_ptr(), (int)B, (int)H, (int)G,
+                    (int)hd, (int)Tmax, (int)L, stream());
+  return out;
+}
+
 std::tuple<Tensor, Tensor> flash_attn_fwd(const Tensor& qkv, int64_t B, int64_t T, int64_t H, int64_t G,
                                           int64_t hd, bool causal, double p, int64_t seed, int64_t offset) {
   check_gpu(qkv, "qkv");
@@ -352,6 +369,7 @@ TORCH_LIBRARY(bllm, m) {
   m.def("gelu_fwd(Tensor f) -> Tensor");
   m.def("gelu_bwd(Tensor f, Tensor dg) -> Tensor");
   m.def("rope_(Tensor(a!) qkv, Tensor cos, Tensor sin, int T, int H, int G, int hd, bool inverse, int pos_offset) -> ()");
+  m.def("attn_decode(Tensor q, Tensor kcache, Tensor vcache, int L) -> Tensor");
   m.def("flash_attn_fwd(Tensor qkv, int B, int T, int H, int G, int hd, bool causal, float p, int seed, int offset) -> (Tensor, Tensor)");
   m.def("flash_attn_bwd(Tensor qkv, Tensor o, Tensor lse, Tensor dout, int B, int T, int H, int G, int hd, bool causal, float p, int seed, int offset) -> Tensor");
   m.def("ce_fwd(Tensor logits, Tensor targets, int ignore_index) -> (Tensor, Tensor)");
@@ -375,6 +393,7 @@ TORCH_LIBRARY_IMPL(bllm, CUDA, m) {
   m.impl("gelu_bwd", &gelu_bwd);
   m.impl("rope_", &rope_);
   m.impl("flash_attn_fwd", &flash_attn_fwd);
+  m.impl("attn_decode", &attn_decode);
   m.impl("flash_attn_bwd", &flash_attn_bwd);
   m.impl("ce_fwd", &ce_fwd);
   m.impl("ce_bwd_", &ce_bwd_);

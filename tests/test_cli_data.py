@@ -294,3 +294,20 @@ def test_generate_greedy_matches_manual_loop():
             logits = m(cur[:, -cfg.context_length:])[:, -1, :]
             cur = torch.cat([cur, logits.argmax(-1, keepdim=True)], 1)
     assert torch.equal(out, cur)
+
+
+@pytest.mark.parametrize("model,size,G", [("llama3_2", "1B", 2), ("GPT2", "124M", 4), ("llama2", "7B", 4)])
+def test_generate_cached_matches_recompute(model, size, G):
+    """KV-cache decode (incl. the sliding-window re-prefill) == the reference's full recompute."""
+    from building_llm_from_scratch_amd.train.generate import generate_cached
+    cfg = get_config(model, size).replace(context_length=24, emb_dim=64, n_heads=4, n_kv_groups=G, hidden_dim=96,
+                                          n_layers=2, vocab_size=101, dtype=torch.float32, drop_rate=0.0)
+    torch.manual_seed(0)
+    m = build_model(cfg)
+    m.flatten()
+    idx = torch.randint(0, 101, (2, 5))
+    assert torch.equal(generate(m, idx, 30, 24), generate_cached(m, idx, 30, 24))
+    g1, g2 = torch.Generator().manual_seed(3), torch.Generator().manual_seed(3)
+    a = generate(m, idx, 12, 24, temperature=1.0, top_k=5, generator=g1)
+    b = generate_cached(m, idx, 12, 24, temperature=1.0, top_k=5, generator=g2)
+    assert torch.equal(a, b)

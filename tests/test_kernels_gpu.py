@@ -181,3 +181,14 @@ def test_flash_attention(dt, B, T, H, G, hd, p, causal):
     dqkv0 = ref.flash_attn_bwd(qkv.cpu().float(), o0, lse0, do.cpu().float(), B, T, H, G, hd, causal, p, 99,
                                12345)
     _close(dqkv, dqkv0, dt, 4, name="dqkv")
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("B,H,G,hd,L,Tmax", [(2, 8, 2, 128, 37, 64), (1, 4, 4, 64, 1, 16), (3, 32, 8, 128, 1000, 1024)])
+def test_attn_decode(dt, B, H, G, hd, L, Tmax):
+    q = torch.randn(B, H, hd, device=DEV).to(dt)
+    kc = torch.randn(B, G, Tmax, hd, device=DEV).to(dt)
+    vc = torch.randn(B, G, Tmax, hd, device=DEV).to(dt)
+    o = ops.attn_decode(q, kc, vc, L)
+    o0 = ref.attn_decode(q.cpu().float(), kc.cpu().float(), vc.cpu().float(), L)
+    _close(o, o0, dt, 2, name="decode")

@@ -88,3 +88,24 @@ def test_overlapped_optimizer_matches_serial():
         finals.append({k: v.float().cpu() for k, v in m.state_dict().items()})
     for k in finals[0]:
         assert torch.equal(finals[0][k], finals[1][k]), k
+
+
+@pytest.mark.parametrize("name", ["llama_hd64", "llama_hd128", "gpt2"])
+def test_kv_cache_decode_matches_full_forward(name):
+    """Prefill (flash kernel) + token-by-token decode (HIP decode kernel over the KV cache)
+    must reproduce the full-sequence forward's logits at every decoded position."""
+    ops.load_ext(required=True)
+    cfg = _cfgs()[name]
+    torch.manual_seed(0)
+    m = build_model(cfg, device="cuda")
+    m.flatten()
+    m.eval()
+    idx = torch.randint(0, cfg.vocab_size, (2, 40), device="cuda")
+    with torch.no_grad():
+        full = m(idx).float()
+        cache = m.new_kv_cache(2, cfg.context_length)
+        lg = m.forward_cached(idx[:, :24], cache, 0)
+        assert _rel(lg, full[:, 23]) < 2e-2
+        for p in range(24, 40):
+            lg = m.forward_cached(idx[:, p:p + 1], cache, p)
+            assert _rel(lg, full[:, p]) < 2e-2, p
