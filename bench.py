@@ -40,6 +40,8 @@ def parse():
     ap.add_argument("--reshard_after_forward", type=int, default=1)
     ap.add_argument("--layers", type=int, default=None, help="(debug only) override n_layers; invalidates the metric")
     ap.add_argument("--profile", action="store_true", help="print a per-phase timing breakdown")
+    ap.add_argument("--lora_rank", type=int, default=0, help="LoRA finetune benchmark (freeze base, rank r)")
+    ap.add_argument("--lora_alpha", type=int, default=32)
     ap.add_argument("--overlap_optimizer", action="store_true",
                     help="run AdamW on a side HIP stream under the next forward")
     return ap.parse_args()
@@ -68,11 +70,16 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
     ops.load_ext(required=True)
 
-    cfg = get_config(a.model, a.num_params, context_length=a.seq_len)
+    cfg = get_config(a.model, a.num_params, context_length=a.seq_len).replace(dtype=torch.bfloat16)
     if a.layers:
         cfg = cfg.replace(n_layers=a.layers)
     torch.manual_seed(123)
     model = build_model(cfg, use_actv_ckpt=a.actv_ckpt, device=dev)
+    if a.lora_rank:
+        from building_llm_from_scratch_amd.models import replace_linear_with_lora
+        for p in model.parameters():
+            p.requires_grad = False
+        replace_linear_with_lora(model, rank=a.lora_rank, alpha=a.lora_alpha)
     engine = setup_engine(model, a.parallel if distributed else "local", device=dev,
                           reshard_after_forward=bool(a.reshard_after_forward))
     opt = FusedAdamW(model, lr=3e-4, weight_decay=0.1, engine=engine, overlap=a.overlap_optimizer)
@@ -120,7 +127,9 @@ def main():
         print(json.dumps({"profile_ms": prof}), file=sys.stderr)
     if rank == 0:
         out = {
-            "metric": "tokens/sec (whole node) Llama-3-8B bf16 FSDP",
+            "metric": ("tokens/sec (whole node) Llama-3-8B bf16 FSDP" if (a.model, a.num_params) == ("llama3", "8B")
+                       else f"tokens/sec (whole node) {cfg.name}-{cfg.size} bf16 {a.parallel}"
+                       + (f" LoRA r={a.lora_rank}" if a.lora_rank else "")),
             "value": round(tps, 1),
             "unit": "tokens/s",
             "n_gpus": world,

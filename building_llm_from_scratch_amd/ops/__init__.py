@@ -19,7 +19,7 @@ __all__ = [
     "rmsnorm_fwd", "rmsnorm_bwd", "layernorm_fwd", "layernorm_bwd", "dropout_add", "dropout_bwd",
     "rope_", "rope_tables", "flash_attn_fwd", "flash_attn_bwd", "swiglu_fwd", "swiglu_bwd",
     "gelu_fwd", "gelu_bwd", "ce_fwd", "ce_bwd_", "embedding_fwd", "embedding_bwd",
-    "sq_norm_multi", "adamw_step_", "attn_decode", "ext_available", "load_ext", "attention_backend",
+    "sq_norm_multi", "adamw_step_", "attn_decode", "bias_grad_", "ext_available", "load_ext", "attention_backend",
 ]
 
 rope_tables = ref.rope_tables
@@ -94,6 +94,19 @@ def flash_attn_fwd(qkv, B, T, H, G, hd, causal=True, dropout_p=0.0, seed=0, offs
         load_ext(required=True)
         return _k().flash_attn_fwd(qkv, B, T, H, G, hd, causal, float(dropout_p), int(seed), int(offset))
     return ref.flash_attn_fwd(qkv, B, T, H, G, hd, causal, dropout_p, seed, offset)
+
+
+def bias_grad_(dy, db, accumulate: bool = False):
+    """db (+)= dy.sum(0) (fp32 accumulation, deterministic)."""
+    if _hip(dy) and dy.shape[1] * dy.element_size() % 16 == 0:
+        _k().bias_grad_(dy.contiguous(), db, bool(accumulate))
+        return db
+    s = dy.sum(0, dtype=torch.float32)
+    if accumulate:
+        db.add_(s.to(db.dtype))
+    else:
+        db.copy_(s)
+    return db
 
 
 def attn_decode(q, kcache, vcache, L: int):

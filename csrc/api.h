@@ -46,6 +46,11 @@ void attn_bwd_naive(DType dt, const void* qkv, const void* o, const float* lse, 
 void attn_delta(DType dt, const void* o, const void* dout, float* delta, int B, int T, int H, int hd,
                 hipStream_t s);
 
+// elementwise.hip — bias gradient (column sums), part must hold colsum_bands(N) * F floats
+int colsum_bands(int N);
+void bias_grad(DType dt, DType odt, const void* dy, float* part, void* out, int N, int F, bool accumulate,
+               hipStream_t s);
+
 // attn_decode.hip — single-query attention over a [B, G, Tmax, hd] KV cache
 int attn_decode_max_len();
 void attn_decode(DType dt, const void* q, const void* kc, const void* vc, void* out, int B, int H, int G, int hd,

@@ -187,6 +187,18 @@ void rope_(Tensor& qkv, const Tensor& cos, const Tensor& sin, int64_t T, int64_t
 }
 
 // ------------------------------------------------------------------ attention
+// db (+)= dy.sum(0): dy [N, F] bf16/fp16/fp32, db [F] any float dtype (written in place)
+void bias_grad_(const Tensor& dy, Tensor& db, bool accumulate) {
+  check_gpu(dy, "dy"); check_gpu(db, "db");
+  c10::DeviceGuard g(dy.device());
+  TORCH_CHECK(dy.dim() == 2 && db.dim() == 1 && db.size(0) == dy.size(1), "bias_grad: shapes");
+  const int N = (int)dy.size(0), F = (int)dy.size(1);
+  TORCH_CHECK(F % (16 / (int)dy.element_size()) == 0, "bias_grad: F must be a multiple of 16 bytes");
+  auto part = at::empty({bllm::colsum_bands(N), F}, dy.options().dtype(at::kFloat));
+  bllm::bias_grad(dt_of(dy), dt_of(db), dy.data_ptr(), part.data_ptr<float>(), db.data_ptr(), N, F, accumulate,
+                  stream());
+}
+
 // q [B, H, hd]; kc / vc [B, G, Tmax, hd] with the first L positions valid -> out [B, H*hd]
 Tensor attn_decode(const Tensor& q, const Tensor& kc, const Tensor& vc, int64_t L) {
   check_gpu(q, "q"); check_gpu(kc, "kcache"); check_gpu(vc, "vcache");
@@ -369,6 +381,7 @@ TORCH_LIBRARY(bllm, m) {
   m.def("gelu_fwd(Tensor f) -> Tensor");
   m.def("gelu_bwd(Tensor f, Tensor dg) -> Tensor");
   m.def("rope_(Tensor(a!) qkv, Tensor cos, Tensor sin, int T, int H, int G, int hd, bool inverse, int pos_offset) -> ()");
+  m.def("bias_grad_(Tensor dy, Tensor(a!) db, bool accumulate) -> ()");
   m.def("attn_decode(Tensor q, Tensor kcache, Tensor vcache, int L) -> Tensor");
   m.def("flash_attn_fwd(Tensor qkv, int B, int T, int H, int G, int hd, bool causal, float p, int seed, int offset) -> (Tensor, Tensor)");
   m.def("flash_attn_bwd(Tensor qkv, Tensor o, Tensor lse, Tensor dout, int B, int T, int H, int G, int hd, bool causal, float p, int seed, int offset) -> Tensor");
@@ -394,6 +407,7 @@ TORCH_LIBRARY_IMPL(bllm, CUDA, m) {
   m.impl("rope_", &rope_);
   m.impl("flash_attn_fwd", &flash_attn_fwd);
   m.impl("attn_decode", &attn_decode);
+  m.impl("bias_grad_", &bias_grad_);
   m.impl("flash_attn_bwd", &flash_attn_bwd);
   m.impl("ce_fwd", &ce_fwd);
   m.impl("ce_bwd_", &ce_bwd_);

@@ -165,6 +165,58 @@ __global__ __launch_bounds__(256) void rope_scalar_k(T* __restrict__ qkv, const 
   }
 }
 
+// Bias gradient db[f] (+)= sum_n dy[n, f]: replaces the eager column reduction of the GPT-2
+// bias grads (reference nn.Linear bias).  Pass 1: workgroup (x = 256 threads x 8-column
+// vectors, y = a row band) writes fp32 partial sums; pass 2 sums the bands in a fixed order and
+// writes / accumulates the gradient in its dtype (deterministic, no atomics).
+template <typename T>
+__global__ __launch_bounds__(256) void colsum_partial_k(const T* __restrict__ dy, float* __restrict__ part, int N,
+                                                        int F, int rows_per) {
+  constexpr int VEC = 16 / sizeof(T);
+  const int cv = blockIdx.x * 256 + threadIdx.x;   // column vector index
+  if (cv * VEC >= F) return;
+  const int r0 = blockIdx.y * rows_per, r1 = min(N, r0 + rows_per);
+  float acc[VEC];
+#pragma unroll
+  for (int j = 0; j < VEC; ++j) acc[j] = 0.f;
+  for (int r = r0; r < r1; ++r) {
+    const Vec16<T> v = ld16(dy + (long)r * F + cv * VEC);
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) acc[j] += to_f(v.v[j]);
+  }
+  float* o = part + (long)blockIdx.y * F + cv * VEC;
+#pragma unroll
+  for (int j = 0; j < VEC; ++j) o[j] = acc[j];
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void colsum_final_k(const float* __restrict__ part, int P, int F,
+                                                      T* __restrict__ out, bool accumulate) {
+  const int f = blockIdx.x * 256 + threadIdx.x;
+  if (f >= F) return;
+  float s = 0.f;
+  for (int p = 0; p < P; ++p) s += part[(long)p * F + f];
+  if (accumulate) s += to_f(out[f]);
+  out[f] = from_f<T>(s);
+}
+
+int colsum_bands(int N) { return N >= 64 * 64 ? 64 : (N + 63) / 64; }
+
+// dy [N, F] (F % (16/sizeof(T)) == 0), out [F] in dtype OT (fp32 or T)
+void bias_grad(DType dt, DType odt, const void* dy, float* part, void* out, int N, int F, bool accumulate,
+               hipStream_t s) {
+  const int P = colsum_bands(N);
+  const int rows_per = (N + P - 1) / P;
+  BLLM_DISPATCH(dt, T, {
+    constexpr int VEC = 16 / sizeof(T);
+    dim3 grid((F / VEC + 255) / 256, P);
+    hipLaunchKernelGGL(colsum_partial_k<T>, grid, dim3(256), 0, s, (const T*)dy, part, N, F, rows_per);
+  });
+  BLLM_DISPATCH(odt, OT, {
+    hipLaunchKernelGGL(colsum_final_k<OT>, dim3((F + 255) / 256), dim3(256), 0, s, part, P, F, (OT*)out, accumulate);
+  });
+}
+
 // ----------------------------------------------------------------------------- launchers
 // VEC = 16 bytes per lane when the sizes allow it, else 1 (tiny debug shapes)
 #define EW_VEC(T, cond, ...)                          \

@@ -192,3 +192,14 @@ def test_attn_decode(dt, B, H, G, hd, L, Tmax):
     o = ops.attn_decode(q, kc, vc, L)
     o0 = ref.attn_decode(q.cpu().float(), kc.cpu().float(), vc.cpu().float(), L)
     _close(o, o0, dt, 2, name="decode")
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+@pytest.mark.parametrize("N,F", [(4096, 3840), (7, 64), (300, 5120)])
+@pytest.mark.parametrize("acc", [False, True])
+def test_bias_grad(dt, N, F, acc):
+    dy = torch.randn(N, F, device=DEV).to(dt)
+    db = torch.randn(F, device=DEV).to(dt)
+    ref0 = dy.float().sum(0) + (db.float() if acc else 0)
+    ops.bias_grad_(dy, db, acc)
+    _close(db, ref0.cpu(), dt, 4, name="bias_grad")

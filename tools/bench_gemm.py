@@ -29,7 +29,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--tokens", type=int, default=4096)
+    ap.add_argument("--backend", choices=["default", "hipblaslt", "rocblas"], default="default")
     a = ap.parse_args()
+    if a.backend != "default":
+        torch.backends.cuda.preferred_blas_library("cublaslt" if a.backend == "hipblaslt" else "cublas")
     N = a.tokens
     shapes = {"qkv": (4096, 6144), "o": (4096, 4096), "gate_up": (4096, 28672), "down": (14336, 4096),
               "head": (4096, 128256)}
@@ -49,8 +52,11 @@ def main():
         r["dx_dyW"] = timeit(lambda: torch.mm(dy, w, out=dx), a.iters)
         r["dx_dyWt_T"] = timeit(lambda: torch.mm(dy, wt.t(), out=dx), a.iters)
         r["dw_dyTx"] = timeit(lambda: torch.mm(dy.t(), x, out=dw), a.iters)
+        r["dw_xTdy_outT"] = timeit(lambda: torch.mm(x.t(), dy, out=dw.t()), a.iters)
+        dwt = torch.empty(k_in, n_out, device="cuda", dtype=dt)
+        r["dwT_xTdy"] = timeit(lambda: torch.mm(x.t(), dy, out=dwt), a.iters)
         r["transpose_w"] = timeit(lambda: wt.copy_(w.t()), a.iters)
-        for k in ("fwd_xWt", "dx_dyW", "dx_dyWt_T", "dw_dyTx"):
+        for k in ("fwd_xWt", "dx_dyW", "dx_dyWt_T", "dw_dyTx", "dw_xTdy_outT", "dwT_xTdy"):
             r[k + "_tflops"] = round(fl / r[k] / 1e9, 1)
         for k in list(r):
             if isinstance(r[k], float) and not k.endswith("tflops"):
