@@ -97,6 +97,8 @@ def build_parser() -> argparse.ArgumentParser:
     x.add_argument("--no_reshard_after_forward", action="store_true",
                    help="FSDP: keep gathered params from forward to backward (ZeRO-2 style)")
     x.add_argument("--no_plot", action="store_true")
+    x.add_argument("--profile_steps", type=str, default=None,
+                   help="torch.profiler window 'first:last' (global steps) -> chrome trace in --output_dir")
     return p
 
 
@@ -188,7 +190,7 @@ def main(rank: int, args):
                       engine=engine, metrics_file=args.metrics_file,
                       loss_scaler=DynamicLossScaler() if config.dtype == torch.float16 else None,
                       max_steps=args.max_steps, sample_tokens=args.sample_tokens,
-                      save_resume=args.save_resume_state, world_size=world)
+                      save_resume=args.save_resume_state, world_size=world, profile_steps=args.profile_steps)
     if args.resume:
         st_path = Path(args.resume).with_name("trainer_state_" + Path(args.resume).stem.split("_")[-1] + ".pt")
         if st_path.exists() or Path(str(st_path).replace(".pt", f".rank{rank}.pt")).exists():

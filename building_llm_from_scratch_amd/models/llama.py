@@ -253,7 +253,9 @@ class HeadComputeMixin:
         h, ns = self._norm_fwd(x2d)
         logits, xa = self.head.forward(h)
         rows, lse = ops.ce_fwd(logits, targets, self.ignore_index)
-        nvalid = (targets != self.ignore_index).sum().to(torch.float32)
+        # a batch whose targets are all ignore_index (e.g. prompts longer than the context in
+        # instruction finetuning) gives loss 0 and zero gradients (torch's mean CE gives NaN)
+        nvalid = (targets != self.ignore_index).sum().to(torch.float32).clamp_(min=1.0)
         loss = rows.sum() / nvalid
         if not save:
             return loss, None

@@ -59,7 +59,8 @@ class Trainer:
                  initial_lr=1e-5, min_lr=1e-6, device="cpu", rank=0, eval_freq=1, save_ckpt_freq=1,
                  print_sample_iter=1, eval_iter=1, engine=None, max_grad_norm=1.0, metrics_file=None,
                  loss_scaler: Optional[DynamicLossScaler] = None, max_steps: Optional[int] = None,
-                 sample_tokens: int = 200, save_resume: bool = False, world_size: int = 1):
+                 sample_tokens: int = 200, save_resume: bool = False, world_size: int = 1,
+                 profile_steps: Optional[str] = None):
         self.config = config
         self.model = model
         self.optimizer = optimizer
@@ -92,6 +93,12 @@ class Trainer:
         self.total_training_steps = 1
         self.lr_increment = 0.0
         self.stop = False
+        # torch.profiler window "first:last" (global steps, inclusive) -> chrome trace per rank
+        self.profile_steps = None
+        if profile_steps:
+            a, b = (int(v) for v in str(profile_steps).split(":"))
+            self.profile_steps = (a, b)
+        self._prof = None
 
     # ------------------------------------------------------------------ helpers
     def _dist(self) -> bool:
@@ -117,9 +124,32 @@ class Trainer:
         target_batch = target_batch.to(self.device, non_blocking=True)
         return self.model(input_batch, target_batch)
 
+    def _profiler_tick(self):
+        """Start / stop torch.profiler around the requested step window (HIP kernels appear as
+        device events; rocprofv3 gives the kernel-level view, see profiles/)."""
+        if self.profile_steps is None:
+            return
+        a, b = self.profile_steps
+        if self.global_step == a and self._prof is None:
+            acts = [torch.profiler.ProfilerActivity.CPU]
+            if torch.cuda.is_available():
+                acts.append(torch.profiler.ProfilerActivity.CUDA)
+            self._prof = torch.profiler.profile(activities=acts, record_shapes=False)
+            self._prof.__enter__()
+        elif self.global_step == b + 1 and self._prof is not None:
+            if torch.cuda.is_available():
+                torch.cuda.synchronize()
+            self._prof.__exit__(None, None, None)
+            path = self.save_dir / f"trace_steps{a}-{b}_rank{self.rank}.json"
+            self._prof.export_chrome_trace(str(path))
+            if self.rank == 0:
+                logger.info(f"profiler trace written: {path}")
+            self._prof = None
+
     def train_batch(self, input_batch, target_batch):
         self.optimizer.zero_grad()
         self.global_step += 1
+        self._profiler_tick()
         lr = self.lr_at(self.global_step)
         for g in self.optimizer.param_groups:
             g["lr"] = lr
