@@ -8,7 +8,9 @@ module provides:
 * :class:`BPETokenizer` — a byte-level BPE that reads local vocab files in either format
   (tiktoken ``*.tiktoken`` / Llama-3 ``tokenizer.model`` base64-rank files, or GPT-2
   ``encoder.json`` + ``vocab.bpe``) with the GPT-2 / Llama-3 pre-tokenisation regexes and
-  tiktoken's ``allowed_special`` semantics;
+  tiktoken's ``allowed_special`` semantics.  Encoding runs in the native C++ core
+  (csrc/host/bpe.cpp -> ``_bpe``: pre-tokeniser + rank merging, like tiktoken's Rust core);
+  the pure-Python path is kept as its oracle and fallback;
 * :class:`Llama2Tokenizer` — SentencePiece wrapper whose ``encode`` accepts the
   ``allowed_special`` kwarg the reference passes (fixes SURVEY §2.8 defect 1);
 * :class:`ByteTokenizer` — deterministic fallback (one id per UTF-8 byte, special tokens
@@ -60,6 +62,23 @@ def _bytes_to_unicode() -> Dict[int, str]:
     return dict(zip(bs, (chr(c) for c in cs)))
 
 
+_CLASS_TABLE: Optional[bytes] = None
+
+
+def _class_table(limit: int = 0x30000) -> bytes:
+    """Per-code-point class for the native pre-tokeniser (0 other, 1 \\p{L}, 2 \\p{N}, 3 \\s),
+    derived from the same ``regex`` classes the patterns use, so both paths agree."""
+    global _CLASS_TABLE
+    if _CLASS_TABLE is None:
+        arr = bytearray(limit)
+        chars = "".join(chr(c) if not 0xD800 <= c <= 0xDFFF else "\x00" for c in range(limit))
+        for cid, pat in ((1, r"\p{L}+"), (2, r"\p{N}+"), (3, r"\s+")):
+            for m in re.finditer(pat, chars):
+                arr[m.start():m.end()] = bytes([cid]) * (m.end() - m.start())
+        _CLASS_TABLE = bytes(arr)
+    return _CLASS_TABLE
+
+
 def _special_split(text: str, specials: Iterable[str]):
     """Yield (is_special, piece) splitting ``text`` at any of the ``specials``."""
     specials = sorted(set(specials), key=len, reverse=True)
@@ -90,6 +109,17 @@ class BPETokenizer:
         self.pat = re.compile(pat_str)
         self.n_vocab = max(list(self.decoder) + list(self.special_decoder) + [0]) + 1
         self._cache: Dict[bytes, List[int]] = {}
+        self._native_kind = {GPT2_PAT: "gpt2", LLAMA3_PAT: "llama3"}.get(pat_str)
+        self._native = None
+
+    def _native_core(self):
+        if self._native is None and self._native_kind and os.environ.get("BLLM_NATIVE_BPE", "1") != "0":
+            try:
+                from .. import _bpe
+                self._native = _bpe.BPECore(self.ranks, self._native_kind, _class_table())
+            except ImportError:
+                self._native_kind = None
+        return self._native
 
     # ------------------------------------------------------------------ loaders
     @classmethod
@@ -141,6 +171,12 @@ class BPETokenizer:
         return out
 
     def encode_ordinary(self, text: str) -> List[int]:
+        core = self._native_core()
+        if core is not None:
+            return core.encode_ordinary(text)
+        return self._encode_ordinary_py(text)
+
+    def _encode_ordinary_py(self, text: str) -> List[int]:
         ids: List[int] = []
         for m in self.pat.finditer(text):
             ids.extend(self._bpe(m.group(0).encode("utf-8")))

@@ -109,7 +109,31 @@ def build(jobs: int = 8, clean: bool = False, debug: bool = False, verbose: bool
             raise RuntimeError(f"link failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
         if verbose:
             print(f"[build] linked {OUT}")
+    build_host(verbose=verbose)
     return OUT
+
+
+def build_host(verbose: bool = False):
+    """Host-side native modules (csrc/host/*.cpp, pybind11, g++ -O3): the BPE tokenizer core."""
+    import pybind11
+    suffix = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
+    hdir = os.path.join(CSRC, "host")
+    outs = []
+    for f in sorted(os.listdir(hdir)) if os.path.isdir(hdir) else []:
+        if not f.endswith(".cpp"):
+            continue
+        src = os.path.join(hdir, f)
+        out = os.path.join(ROOT, "building_llm_from_scratch_amd", "_" + f[:-4] + suffix)
+        cmd = [os.environ.get("CXX", "g++"), "-O3", "-std=c++17", "-shared", "-fPIC", "-fvisibility=hidden",
+               f"-I{pybind11.get_include()}", f"-I{sysconfig.get_paths()['include']}", src, "-o", out]
+        if not os.path.exists(out) or os.path.getmtime(src) > os.path.getmtime(out):
+            r = subprocess.run(cmd, capture_output=True, text=True)
+            if r.returncode != 0:
+                raise RuntimeError(f"host build failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+            if verbose:
+                print(f"[build] host {os.path.basename(out)}")
+        outs.append(out)
+    return outs
 
 
 if __name__ == "__main__":
