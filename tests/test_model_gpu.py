@@ -109,3 +109,28 @@ def test_kv_cache_decode_matches_full_forward(name):
         for p in range(24, 40):
             lg = m.forward_cached(idx[:, p:p + 1], cache, p)
             assert _rel(lg, full[:, p]) < 2e-2, p
+
+
+@pytest.mark.parametrize("name", ["llama_hd128", "gpt2"])
+def test_training_is_bitwise_deterministic(name):
+    """Two identical runs (same seed, same data) must give bit-identical parameters: every
+    HIP kernel reduces in a fixed order (no float atomics), dropout masks are counter-based."""
+    ops.load_ext(required=True)
+    cfg = _cfgs()[name]
+    if name == "gpt2":
+        cfg = cfg.replace(drop_rate=0.1)
+    idx = torch.randint(0, cfg.vocab_size, (3, 4, 129), device="cuda")
+    finals = []
+    for _ in range(2):
+        torch.manual_seed(0)
+        m = build_model(cfg, device="cuda")
+        m.flatten()
+        opt = FusedAdamW(m, lr=1e-3, weight_decay=0.1)
+        for i in range(3):
+            loss = m(idx[i, :, :-1], idx[i, :, 1:])
+            loss.backward()
+            opt.clip_grad_norm_(1.0)
+            opt.step()
+        finals.append({k: v.float().cpu() for k, v in m.state_dict().items()})
+    for k in finals[0]:
+        assert torch.equal(finals[0][k], finals[1][k]), k
