@@ -22,7 +22,7 @@ import torch.nn as nn
 from .. import ops
 from .base import BaseLM, UnitCompute, cached_attention
 from .linear import FusedLinear
-from .llama import HeadComputeMixin, _write_vec_grad
+from .llama import HeadComputeMixin
 
 
 class MultiHeadAttention(nn.Module):
@@ -95,9 +95,11 @@ class GPTEmbedCompute(UnitCompute):
         return None
 
 
-def _ln_grads(unit, norm, dw, db, acc):
-    _write_vec_grad(unit, norm.weight, dw, acc)
-    _write_vec_grad(unit, norm.bias, db, acc)
+def _ln_bwd(unit, norm, dy, x, mean, rstd, dx_acc, acc):
+    """LayerNorm backward whose dW / dB land straight in the unit's flat gradient."""
+    dx, _, _ = ops.layernorm_bwd(dy, x, unit.data(norm.weight), mean, rstd, dx_acc, unit.grad(norm.weight),
+                                 unit.grad(norm.bias), acc)
+    return dx
 
 
 class GPTBlockCompute(UnitCompute):
@@ -188,8 +190,7 @@ class GPTBlockCompute(UnitCompute):
         h2 = s["h2"] if "h2" in s else self._ln(s["x2"], b.norm2)[0]
         dh2 = self.fc.backward(df, h2, xa_fc, accumulate=acc)
         del df, h2
-        dx2, dw2, db2 = ops.layernorm_bwd(dh2, s["x2"], u.data(b.norm2.weight), s["m2"], s["r2"], dy2)
-        _ln_grads(u, b.norm2, dw2, db2, acc)
+        dx2 = _ln_bwd(u, b.norm2, dh2, s["x2"], s["m2"], s["r2"], dy2, acc)
         # ---- attention branch: x2 = x + drop(out_proj(attn(ln1(x))))
         da = ops.dropout_bwd(dx2, p, rc.seed, offs[1])
         d_o = self.o.backward(da, s["o"], xa_o, accumulate=acc)
@@ -199,8 +200,7 @@ class GPTBlockCompute(UnitCompute):
         h1 = s["h1"] if "h1" in s else self._ln(s["x"], b.norm1)[0]
         dh1 = self.qkv.backward(dqkv, h1, xa_qkv, accumulate=acc)
         del dqkv, h1
-        dx, dw1, db1 = ops.layernorm_bwd(dh1, s["x"], u.data(b.norm1.weight), s["m1"], s["r1"], dx2)
-        _ln_grads(u, b.norm1, dw1, db1, acc)
+        dx = _ln_bwd(u, b.norm1, dh1, s["x"], s["m1"], s["r1"], dx2, acc)
         return dx.view(B, T, d)
 
 
@@ -227,8 +227,7 @@ class GPTHeadCompute(HeadComputeMixin, UnitCompute):
     def _norm_bwd(self, dh, ns):
         x2d, mean, rstd = ns
         u, n = self.unit, self.m.norm
-        dx, dw, db = ops.layernorm_bwd(dh, x2d, u.data(n.weight), mean, rstd, None)
-        _ln_grads(u, n, dw, db, self.rctx.accumulate)
+        dx = _ln_bwd(u, n, dh, x2d, mean, rstd, None, self.rctx.accumulate)
         return dx
 
 

@@ -87,16 +87,6 @@ class TransformerBlock(nn.Module):
 # ---------------------------------------------------------------------------
 # unit computes
 # ---------------------------------------------------------------------------
-def _write_vec_grad(unit, p, g32, accumulate):
-    gv = unit.grad(p)
-    if gv is None:
-        return
-    if accumulate:
-        gv.add_(g32.to(gv.dtype))
-    else:
-        gv.copy_(g32)
-
-
 class LlamaEmbedCompute(UnitCompute):
     name = "tok_emb"
 
@@ -203,8 +193,7 @@ class LlamaBlockCompute(UnitCompute):
         h2 = s["h2"] if "h2" in s else ops.rmsnorm_fwd(s["x2"], w2, eps)[0]
         dh2 = self.gu.backward(d_gu, h2, xa_gu, accumulate=acc)
         del d_gu, h2
-        dx2, dw2 = ops.rmsnorm_bwd(dh2, s["x2"], w2, s["r2"], dy2)
-        _write_vec_grad(u, b.norm2.weight, dw2, acc)
+        dx2, _ = ops.rmsnorm_bwd(dh2, s["x2"], w2, s["r2"], dy2, u.grad(b.norm2.weight), acc)
         del dh2
         # ---- attention
         d_o = self.o.backward(dx2, s["o"], xa_o, accumulate=acc)
@@ -214,8 +203,7 @@ class LlamaBlockCompute(UnitCompute):
         h1 = s["h1"] if "h1" in s else ops.rmsnorm_fwd(s["x"], w1, eps)[0]
         dh1 = self.qkv.backward(dqkv, h1, xa_qkv, accumulate=acc)
         del dqkv, h1
-        dx, dw1 = ops.rmsnorm_bwd(dh1, s["x"], w1, s["r1"], dx2)
-        _write_vec_grad(u, b.norm1.weight, dw1, acc)
+        dx, _ = ops.rmsnorm_bwd(dh1, s["x"], w1, s["r1"], dx2, u.grad(b.norm1.weight), acc)
         return dx.view(B, T, d)
 
 
@@ -293,8 +281,7 @@ class LlamaHeadCompute(HeadComputeMixin, UnitCompute):
     def _norm_bwd(self, dh, ns):
         x2d, r = ns
         w = self.m.final_norm.weight
-        dx, dw = ops.rmsnorm_bwd(dh, x2d, self.unit.data(w), r, None)
-        _write_vec_grad(self.unit, w, dw, self.rctx.accumulate)
+        dx, _ = ops.rmsnorm_bwd(dh, x2d, self.unit.data(w), r, None, self.unit.grad(w), self.rctx.accumulate)
         return dx
 
 

@@ -43,10 +43,24 @@ def rmsnorm_fwd(x, w, eps: float):
     return ref.rmsnorm_fwd(x, w, eps)
 
 
-def rmsnorm_bwd(dy, x, w, rstd, dx_acc: Optional[torch.Tensor] = None):
+def _vec_into(out, g32, accumulate):
+    if out is None:
+        return g32
+    if accumulate:
+        out.add_(g32.to(out.dtype))
+    else:
+        out.copy_(g32)
+    return out
+
+
+def rmsnorm_bwd(dy, x, w, rstd, dx_acc: Optional[torch.Tensor] = None, dw_out: Optional[torch.Tensor] = None,
+                accumulate: bool = False):
+    """-> (dx [+ dx_acc], dW).  With ``dw_out`` the weight gradient is written (or added, when
+    ``accumulate``) straight into it by the reduction kernel, in its dtype."""
     if _hip(x):
-        return _k().rmsnorm_bwd(dy, x, w, rstd, dx_acc)
-    return ref.rmsnorm_bwd(dy, x, w, rstd, dx_acc)
+        return _k().rmsnorm_bwd(dy, x, w, rstd, dx_acc, dw_out, bool(accumulate))
+    dx, dw = ref.rmsnorm_bwd(dy, x, w, rstd, dx_acc)
+    return dx, _vec_into(dw_out, dw, accumulate)
 
 
 def layernorm_fwd(x, w, b, eps: float):
@@ -55,10 +69,16 @@ def layernorm_fwd(x, w, b, eps: float):
     return ref.layernorm_fwd(x, w, b, eps)
 
 
-def layernorm_bwd(dy, x, w, mean, rstd, dx_acc: Optional[torch.Tensor] = None):
-    if _hip(x):
-        return _k().layernorm_bwd(dy, x, w, mean, rstd, dx_acc)
-    return ref.layernorm_bwd(dy, x, w, mean, rstd, dx_acc)
+def layernorm_bwd(dy, x, w, mean, rstd, dx_acc: Optional[torch.Tensor] = None,
+                  dw_out: Optional[torch.Tensor] = None, db_out: Optional[torch.Tensor] = None,
+                  accumulate: bool = False):
+    if _hip(x) and (dw_out is None) == (db_out is None):
+        return _k().layernorm_bwd(dy, x, w, mean, rstd, dx_acc, dw_out, db_out, bool(accumulate))
+    if _hip(x):  # only one of the two outputs requested (e.g. a frozen bias)
+        dx, dw, db = _k().layernorm_bwd(dy, x, w, mean, rstd, dx_acc, None, None, False)
+    else:
+        dx, dw, db = ref.layernorm_bwd(dy, x, w, mean, rstd, dx_acc)
+    return dx, _vec_into(dw_out, dw, accumulate), _vec_into(db_out, db, accumulate)
 
 
 def dropout_add(x, a, p: float, seed: int, offset: int):

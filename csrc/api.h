@@ -13,11 +13,13 @@ int norm_max_dim(DType dt);
 void rmsnorm_fwd(DType dt, const void* x, const void* w, void* y, float* rstd, int N, int d, float eps, hipStream_t s);
 void layernorm_fwd(DType dt, const void* x, const void* w, const void* b, void* y, float* mean, float* rstd, int N,
                    int d, float eps, hipStream_t s);
+// dW / dB land in `dw` / `db` of dtype `odt` (written, or added when `accumulate`)
 void rmsnorm_bwd(DType dt, const void* dy, const void* x, const void* w, const float* rstd, const void* dx_acc,
-                 void* dx, float* part, float* dw, int N, int d, int nwg, hipStream_t s);
+                 void* dx, float* part, DType odt, void* dw, bool accumulate, int N, int d, int nwg, hipStream_t s);
 void layernorm_bwd(DType dt, const void* dy, const void* x, const void* w, const float* mean, const float* rstd,
-                   const void* dx_acc, void* dx, float* part_w, float* part_b, float* dw, float* db, int N, int d,
-                   int nwg, hipStream_t s);
+                   const void* dx_acc, void* dx, float* part_w, float* part_b, DType odt, void* dw, void* db,
+                   bool accumulate, int N, int d, int nwg, hipStream_t s);
+void col_reduce(const float* part, DType odt, void* out, int P, int d, bool accumulate, hipStream_t s);
 
 // elementwise.hip
 void swiglu_fwd(DType dt, const void* gu, void* act, long N, int F, hipStream_t s);

@@ -54,8 +54,19 @@ std::tuple<Tensor, Tensor> rmsnorm_fwd(const Tensor& x, const Tensor& w, double 
   return {y, rstd};
 }
 
+// dW goes to `dw_out` (any float dtype, written or accumulated) when given, else a new fp32 [d]
+static Tensor vec_out(const optional<Tensor>& o, const Tensor& x, int64_t d, const char* name) {
+  if (o.has_value()) {
+    check_gpu(*o, name);
+    TORCH_CHECK(o->numel() == d, "bllm: ", name, " must have ", d, " elements");
+    return *o;
+  }
+  return at::empty({d}, x.options().dtype(at::kFloat));
+}
+
 std::tuple<Tensor, Tensor> rmsnorm_bwd(const Tensor& dy, const Tensor& x, const Tensor& w, const Tensor& rstd,
-                                       const optional<Tensor>& dx_acc) {
+                                       const optional<Tensor>& dx_acc, const optional<Tensor>& dw_out,
+                                       bool accumulate) {
   check_gpu(dy, "dy"); check_gpu(x, "x"); check_gpu(w, "w"); check_gpu(rstd, "rstd");
   c10::DeviceGuard g(x.device());
   check_rows(x, 16 / x.element_size());
@@ -71,9 +82,10 @@ std::tuple<Tensor, Tensor> rmsnorm_bwd(const Tensor& dy, const Tensor& x, const 
   auto dx = at::empty_like(x);
   const int nwg = bllm::norm_bwd_num_wg(N);
   auto part = at::empty({nwg, d}, x.options().dtype(at::kFloat));
-  auto dw = at::empty({d}, x.options().dtype(at::kFloat));
+  Tensor dw = vec_out(dw_out, x, d, "dw_out");
   bllm::rmsnorm_bwd(dt_of(x), dy.data_ptr(), x.data_ptr(), w.data_ptr(), rstd.data_ptr<float>(), acc, dx.data_ptr(),
-                    part.data_ptr<float>(), dw.data_ptr<float>(), N, d, nwg, stream());
+                    part.data_ptr<float>(), dt_of(dw), dw.data_ptr(), accumulate && dw_out.has_value(), N, d, nwg,
+                    stream());
   return {dx, dw};
 }
 
@@ -93,7 +105,8 @@ std::tuple<Tensor, Tensor, Tensor> layernorm_fwd(const Tensor& x, const Tensor& 
 
 std::tuple<Tensor, Tensor, Tensor> layernorm_bwd(const Tensor& dy, const Tensor& x, const Tensor& w,
                                                  const Tensor& mean, const Tensor& rstd,
-                                                 const optional<Tensor>& dx_acc) {
+                                                 const optional<Tensor>& dx_acc, const optional<Tensor>& dw_out,
+                                                 const optional<Tensor>& db_out, bool accumulate) {
   check_gpu(dy, "dy"); check_gpu(x, "x"); check_gpu(w, "w");
   c10::DeviceGuard g(x.device());
   check_rows(x, 16 / x.element_size());
@@ -110,11 +123,14 @@ std::tuple<Tensor, Tensor, Tensor> layernorm_bwd(const Tensor& dy, const Tensor&
   const int nwg = bllm::norm_bwd_num_wg(N);
   auto pw = at::empty({nwg, d}, x.options().dtype(at::kFloat));
   auto pb = at::empty({nwg, d}, x.options().dtype(at::kFloat));
-  auto dw = at::empty({d}, x.options().dtype(at::kFloat));
-  auto db = at::empty({d}, x.options().dtype(at::kFloat));
+  TORCH_CHECK(dw_out.has_value() == db_out.has_value(), "layernorm_bwd: give both dw_out and db_out or neither");
+  Tensor dw = vec_out(dw_out, x, d, "dw_out");
+  Tensor db = vec_out(db_out, x, d, "db_out");
+  TORCH_CHECK(dw.scalar_type() == db.scalar_type(), "layernorm_bwd: dw_out / db_out dtypes differ");
   bllm::layernorm_bwd(dt_of(x), dy.data_ptr(), x.data_ptr(), w.data_ptr(), mean.data_ptr<float>(),
                       rstd.data_ptr<float>(), acc, dx.data_ptr(), pw.data_ptr<float>(), pb.data_ptr<float>(),
-                      dw.data_ptr<float>(), db.data_ptr<float>(), N, d, nwg, stream());
+                      dt_of(dw), dw.data_ptr(), db.data_ptr(), accumulate && dw_out.has_value(), N, d, nwg,
+                      stream());
   return {dx, dw, db};
 }
 
@@ -371,9 +387,9 @@ void adamw_step_(Tensor& param, const optional<Tensor>& master, const Tensor& gr
 
 TORCH_LIBRARY(bllm, m) {
   m.def("rmsnorm_fwd(Tensor x, Tensor w, float eps) -> (Tensor, Tensor)");
-  m.def("rmsnorm_bwd(Tensor dy, Tensor x, Tensor w, Tensor rstd, Tensor? dx_acc) -> (Tensor, Tensor)");
+  m.def("rmsnorm_bwd(Tensor dy, Tensor x, Tensor w, Tensor rstd, Tensor? dx_acc, Tensor(a!)? dw_out, bool accumulate) -> (Tensor, Tensor)");
   m.def("layernorm_fwd(Tensor x, Tensor w, Tensor b, float eps) -> (Tensor, Tensor, Tensor)");
-  m.def("layernorm_bwd(Tensor dy, Tensor x, Tensor w, Tensor mean, Tensor rstd, Tensor? dx_acc) -> (Tensor, Tensor, Tensor)");
+  m.def("layernorm_bwd(Tensor dy, Tensor x, Tensor w, Tensor mean, Tensor rstd, Tensor? dx_acc, Tensor(a!)? dw_out, Tensor(b!)? db_out, bool accumulate) -> (Tensor, Tensor, Tensor)");
   m.def("dropout_add(Tensor x, Tensor a, float p, int seed, int offset) -> Tensor");
   m.def("dropout_bwd(Tensor dy, float p, int seed, int offset) -> Tensor");
   m.def("swiglu_fwd(Tensor gu) -> Tensor");

@@ -3,7 +3,7 @@
 // Replaces reference common_components.py:6-35 (RoPE), :78-124 (SiLU/SwiGLU),
 // GPT2.py:58-62 (nn.GELU, exact erf), and nn.Dropout.  All are HBM-bound: 16-byte
 // accesses per lane, grid-stride loops capped at 256 CUs x 8 workgroups.
-#include "common.h"
+#include "api.h"
 
 namespace bllm {
 
@@ -189,20 +189,9 @@ __global__ __launch_bounds__(256) void colsum_partial_k(const T* __restrict__ dy
   for (int j = 0; j < VEC; ++j) o[j] = acc[j];
 }
 
-template <typename T>
-__global__ __launch_bounds__(256) void colsum_final_k(const float* __restrict__ part, int P, int F,
-                                                      T* __restrict__ out, bool accumulate) {
-  const int f = blockIdx.x * 256 + threadIdx.x;
-  if (f >= F) return;
-  float s = 0.f;
-  for (int p = 0; p < P; ++p) s += part[(long)p * F + f];
-  if (accumulate) s += to_f(out[f]);
-  out[f] = from_f<T>(s);
-}
+int colsum_bands(int N) { return N >= 16 * 256 ? 256 : (N + 15) / 16; }
 
-int colsum_bands(int N) { return N >= 64 * 64 ? 64 : (N + 63) / 64; }
-
-// dy [N, F] (F % (16/sizeof(T)) == 0), out [F] in dtype OT (fp32 or T)
+// dy [N, F] (F % (16/sizeof(T)) == 0), out [F] in dtype odt (written, or added when accumulate)
 void bias_grad(DType dt, DType odt, const void* dy, float* part, void* out, int N, int F, bool accumulate,
                hipStream_t s) {
   const int P = colsum_bands(N);
@@ -212,9 +201,7 @@ void bias_grad(DType dt, DType odt, const void* dy, float* part, void* out, int 
     dim3 grid((F / VEC + 255) / 256, P);
     hipLaunchKernelGGL(colsum_partial_k<T>, grid, dim3(256), 0, s, (const T*)dy, part, N, F, rows_per);
   });
-  BLLM_DISPATCH(odt, OT, {
-    hipLaunchKernelGGL(colsum_final_k<OT>, dim3((F + 255) / 256), dim3(256), 0, s, part, P, F, (OT*)out, accumulate);
-  });
+  col_reduce(part, odt, out, P, F, accumulate, s);
 }
 
 // ----------------------------------------------------------------------------- launchers

@@ -192,8 +192,9 @@ __global__ __launch_bounds__(256) void norm_bwd_k(const T* __restrict__ dy, cons
 
 // out[c] = sum_p part[p][c]   (16 columns x 16 row-groups per workgroup -> d/16 workgroups
 // so the partial matrix is streamed by many CUs; fixed summation order, deterministic)
-__global__ __launch_bounds__(256) void col_reduce_k(const float* __restrict__ part, float* __restrict__ out,
-                                                    int P, int d) {
+template <typename OT>
+__global__ __launch_bounds__(256) void col_reduce_k(const float* __restrict__ part, OT* __restrict__ out, int P,
+                                                    int d, bool accumulate) {
   __shared__ float red[16][17];
   const int cl = threadIdx.x & 15, g = threadIdx.x >> 4;
   const int c = blockIdx.x * 16 + cl;
@@ -213,8 +214,16 @@ __global__ __launch_bounds__(256) void col_reduce_k(const float* __restrict__ pa
     float t = 0.f;
 #pragma unroll
     for (int k = 0; k < 16; ++k) t += red[k][cl];
-    out[c] = t;
+    if (accumulate) t += to_f(out[c]);
+    out[c] = from_f<OT>(t);
   }
+}
+
+// sum P fp32 partial rows into out[d] (dtype odt; written or accumulated) in a fixed order
+void col_reduce(const float* part, DType odt, void* out, int P, int d, bool accumulate, hipStream_t s) {
+  BLLM_DISPATCH(odt, OT, {
+    hipLaunchKernelGGL(col_reduce_k<OT>, dim3(ceil_div(d, 16)), dim3(256), 0, s, part, (OT*)out, P, d, accumulate);
+  });
 }
 
 // ----------------------------------------------------------------------------- launchers
@@ -233,8 +242,8 @@ static void fwd_dispatch(const void* x, const void* w, const void* b, void* y, f
 
 template <typename T, bool LN>
 static void bwd_dispatch(const void* dy, const void* x, const void* w, const float* mean, const float* rstd,
-                         const void* dx_acc, void* dx, float* part_w, float* part_b, float* dw, float* db,
-                         int N, int d, int nwg, hipStream_t s) {
+                         const void* dx_acc, void* dx, float* part_w, float* part_b, DType odt, void* dw, void* db,
+                         bool accumulate, int N, int d, int nwg, hipStream_t s) {
   constexpr int VEC = 16 / sizeof(T);
   const int nvec = d / VEC;
   // threads per row: a multiple of 64 covering the row in <= 4 waves; NV vectors per thread
@@ -245,8 +254,8 @@ static void bwd_dispatch(const void* dy, const void* x, const void* w, const flo
                                   (const T*)w, mean, rstd, (const T*)dx_acc, (T*)dx, part_w, part_b, N, d)
   if (nv <= 1) L(1); else if (nv <= 2) L(2); else L(4);
 #undef L
-  hipLaunchKernelGGL(col_reduce_k, dim3(ceil_div(d, 16)), dim3(256), 0, s, part_w, dw, nwg, d);
-  if (LN) hipLaunchKernelGGL(col_reduce_k, dim3(ceil_div(d, 16)), dim3(256), 0, s, part_b, db, nwg, d);
+  col_reduce(part_w, odt, dw, nwg, d, accumulate, s);
+  if (LN) col_reduce(part_b, odt, db, nwg, d, accumulate, s);
 }
 
 int norm_bwd_num_wg(int N) {
@@ -266,15 +275,15 @@ void layernorm_fwd(DType dt, const void* x, const void* w, const void* b, void* 
   BLLM_DISPATCH(dt, T, (fwd_dispatch<T, true>(x, w, b, y, mean, rstd, N, d, eps, s)));
 }
 void rmsnorm_bwd(DType dt, const void* dy, const void* x, const void* w, const float* rstd, const void* dx_acc,
-                 void* dx, float* part, float* dw, int N, int d, int nwg, hipStream_t s) {
-  BLLM_DISPATCH(dt, T, (bwd_dispatch<T, false>(dy, x, w, nullptr, rstd, dx_acc, dx, part, nullptr, dw,
-                                               nullptr, N, d, nwg, s)));
+                 void* dx, float* part, DType odt, void* dw, bool accumulate, int N, int d, int nwg, hipStream_t s) {
+  BLLM_DISPATCH(dt, T, (bwd_dispatch<T, false>(dy, x, w, nullptr, rstd, dx_acc, dx, part, nullptr, odt, dw,
+                                               nullptr, accumulate, N, d, nwg, s)));
 }
 void layernorm_bwd(DType dt, const void* dy, const void* x, const void* w, const float* mean, const float* rstd,
-                   const void* dx_acc, void* dx, float* part_w, float* part_b, float* dw, float* db, int N, int d,
-                   int nwg, hipStream_t s) {
-  BLLM_DISPATCH(dt, T, (bwd_dispatch<T, true>(dy, x, w, mean, rstd, dx_acc, dx, part_w, part_b, dw, db, N,
-                                              d, nwg, s)));
+                   const void* dx_acc, void* dx, float* part_w, float* part_b, DType odt, void* dw, void* db,
+                   bool accumulate, int N, int d, int nwg, hipStream_t s) {
+  BLLM_DISPATCH(dt, T, (bwd_dispatch<T, true>(dy, x, w, mean, rstd, dx_acc, dx, part_w, part_b, odt, dw, db,
+                                              accumulate, N, d, nwg, s)));
 }
 
 }  // namespace bllm

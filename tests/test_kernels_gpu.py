@@ -42,6 +42,12 @@ def test_rmsnorm(dt, d):
     dx0, dw0 = ref.rmsnorm_bwd(dy.cpu().float(), x.cpu().float(), w.cpu().float(), r0, acc.cpu().float())
     _close(dx, dx0, dt, 2, name="dx")
     _close(dw, dw0, dt, 2, name="dw")
+    # weight gradient written / accumulated straight into a parameter-dtype buffer
+    for accumulate in (False, True):
+        out = torch.randn(d, device=DEV).to(dt)
+        expect = dw0 + (out.cpu().float() if accumulate else 0)
+        ops.rmsnorm_bwd(dy, x, w, r, acc, out, accumulate)
+        _close(out, expect, dt, 4, name=f"dw_out acc={accumulate}")
 
 
 @pytest.mark.parametrize("dt", DTYPES)
@@ -60,6 +66,13 @@ def test_layernorm(dt, d):
     _close(dx, dx0, dt, 2, name="dx")
     _close(dw, dw0, dt, 2, name="dw")
     _close(db, db0, dt, 2, name="db")
+    for accumulate in (False, True):
+        ow, ob = torch.randn(d, device=DEV).to(dt), torch.randn(d, device=DEV).to(dt)
+        ew = dw0 + (ow.cpu().float() if accumulate else 0)
+        eb = db0 + (ob.cpu().float() if accumulate else 0)
+        ops.layernorm_bwd(dy, x, w, m, r, None, ow, ob, accumulate)
+        _close(ow, ew, dt, 4, name="dw_out")
+        _close(ob, eb, dt, 4, name="db_out")
 
 
 @pytest.mark.parametrize("dt", DTYPES)
