@@ -23,7 +23,8 @@ from typing import Optional, Tuple
 import torch
 
 # ---------------------------------------------------------------------------
-# counter-based dropout RNG (identical bit-for-bit to csrc/common.h::drop_hash)
+# counter-based dropout RNG (identical bit-for-bit to csrc/common.h::drop_bits16):
+# one 32-bit hash per PAIR of element indices, 16 bits per element, 16-bit threshold
 # ---------------------------------------------------------------------------
 _M32 = 0xFFFFFFFF
 
@@ -39,15 +40,24 @@ def _mix32(x: torch.Tensor) -> torch.Tensor:
     return x
 
 
+def drop_threshold16(p: float) -> int:
+    return min(int(p * 65536.0), 65536)
+
+
+def drop_inv_keep(p: float) -> float:
+    """Scale of kept elements: 1 / P(keep) for the quantised 16-bit threshold."""
+    t = drop_threshold16(p)
+    return 0.0 if t >= 65536 else 65536.0 / (65536.0 - t)
+
+
 def drop_keep_mask(seed: int, offset: int, numel: int, p: float, device=None) -> torch.Tensor:
-    """keep[i] = hash(seed, offset + i) >= p * 2^32."""
+    """keep[i] = bits16(seed, offset + i) >= p * 2^16."""
     idx = torch.arange(numel, dtype=torch.int64, device=device) + offset
-    lo = idx & _M32
-    hi = idx >> 32
-    s = _mix32(torch.full_like(lo, seed & _M32) + (hi * 0x9E3779B9 & _M32))
-    h = _mix32(lo ^ s)
-    thr = min(int(p * 4294967296.0), 4294967295)
-    return h >= thr
+    pair = idx >> 1
+    s = _mix32(torch.full_like(pair, seed & _M32) + ((pair >> 32) * 0x9E3779B9 & _M32))
+    h = _mix32((pair & _M32) ^ s)
+    bits = torch.where((idx & 1) == 1, h >> 16, h & 0xFFFF)
+    return bits >= drop_threshold16(p)
 
 
 # ---------------------------------------------------------------------------
@@ -99,14 +109,14 @@ def dropout_add(x, a, p: float, seed: int, offset: int):
     if p <= 0.0:
         return (x.float() + a.float()).to(x.dtype)
     keep = drop_keep_mask(seed, offset, a.numel(), p, a.device).view_as(a)
-    return (x.float() + a.float() * keep / (1.0 - p)).to(x.dtype)
+    return (x.float() + a.float() * keep * drop_inv_keep(p)).to(x.dtype)
 
 
 def dropout_bwd(dy, p: float, seed: int, offset: int):
     if p <= 0.0:
         return dy
     keep = drop_keep_mask(seed, offset, dy.numel(), p, dy.device).view_as(dy)
-    return (dy.float() * keep / (1.0 - p)).to(dy.dtype)
+    return (dy.float() * keep * drop_inv_keep(p)).to(dy.dtype)
 
 
 # ---------------------------------------------------------------------------
@@ -183,7 +193,7 @@ def flash_attn_fwd(qkv, B: int, T: int, H: int, G: int, hd: int, causal: bool = 
     p = torch.exp(s - lse[..., None])
     if dropout_p > 0.0:
         keep = _attn_dropout_keep(B, H, T, dropout_p, seed, offset, qkv.device)
-        p = p * keep / (1.0 - dropout_p)
+        p = p * keep * drop_inv_keep(dropout_p)
     o = (p @ v).permute(0, 2, 1, 3).reshape(B * T, H * hd).to(qkv.dtype)
     return o, lse * (1.0 / math.log(2.0))
 
@@ -205,13 +215,13 @@ def flash_attn_bwd(qkv, o, lse2, do, B: int, T: int, H: int, G: int, hd: int, ca
     O = o.view(B, T, H, hd).permute(0, 2, 1, 3).float()
     if dropout_p > 0.0:
         keep = _attn_dropout_keep(B, H, T, dropout_p, seed, offset, qkv.device)
-        pd = p * keep / (1.0 - dropout_p)
+        pd = p * keep * drop_inv_keep(dropout_p)
     else:
         keep = None
         pd = p
     dv = pd.transpose(-1, -2) @ dO
     dpd = dO @ vx.transpose(-1, -2)
-    dp = dpd * keep / (1.0 - dropout_p) if keep is not None else dpd
+    dp = dpd * keep * drop_inv_keep(dropout_p) if keep is not None else dpd
     delta = (dO * O).sum(-1, keepdim=True)          # = rowsum(P * dP) incl. dropout
     ds = p * (dp - delta) * scale
     dq = ds @ kx
@@ -295,7 +305,7 @@ def embedding_fwd(idx: torch.Tensor, wte: torch.Tensor, wpe: Optional[torch.Tens
         x = (x.float() + wpe.index_select(0, pos).float()).to(wte.dtype)
     if dropout_p > 0.0:
         keep = drop_keep_mask(seed, offset, x.numel(), dropout_p, x.device).view_as(x)
-        x = (x.float() * keep / (1 - dropout_p)).to(x.dtype)
+        x = (x.float() * keep * drop_inv_keep(dropout_p)).to(x.dtype)
     return x
 
 

@@ -137,6 +137,12 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_mfma_k(const T* __restrict_
   const int kw0 = k0 + 32 * w;
   const int mykey = kw0 + l32;
   const float scale = rsqrtf((float)HD), c = scale * kLog2eB;
+  DropSlab ds;
+  uint64_t dslab = 0;
+  if constexpr (DROP) {
+    dslab = doff + (uint64_t)(b * H + h) * T_ * T_;
+    ds.init(seed, dslab);
+  }
 
   // ---- K / V fragments of this wave's 32 keys (B operands, key = lane column)
   v8 kf[KK], vf[KK];
@@ -283,7 +289,7 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_mfma_k(const T* __restrict_
           float dp = dpacc[r], pd = p;
           if constexpr (DROP) {
             const int q = q0 + 8 * gq + 4 * hh + j;
-            const bool keep = drop_hash(seed, doff + (((uint64_t)(b * H + h) * T_ + q) * T_ + mykey)) >= thr;
+            const bool keep = ds.bits16(dslab + (uint64_t)q * T_ + mykey) >= thr;
             pd = keep ? p * inv_keep : 0.f;
             dp = keep ? dp * inv_keep : 0.f;
           }
@@ -396,6 +402,13 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_dq_k(const T* __restrict__ 
   const int qi = wq_lo + l32;
   const int qc = qi < T_ ? qi : T_ - 1;
   const float scale = rsqrtf((float)HD), c = scale * kLog2eB;
+  DropSlab ds;
+  uint64_t dslab = 0;
+  if constexpr (DROP) {
+    dslab = doff + (uint64_t)(b * H + h) * T_ * T_;
+    ds.init(seed, dslab);
+  }
+  const bool dpair = ((doff | (uint64_t)T_) & 1) == 0;
 
   v8 qf[KK], of[KK];
 #pragma unroll
@@ -526,17 +539,34 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_dq_k(const T* __restrict__ 
           if ((causal && key > qi) || key >= T_ || qi >= T_) sc[kt][r] = -INFINITY;
         }
     }
+    if constexpr (DROP) {
+      const uint64_t rowbase = dslab + (uint64_t)qi * T_;
+      if (dpair) {
+#pragma unroll
+        for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+          for (int r = 0; r < 16; r += 2) {
+            const int key = k0 + kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+            const uint32_t hv = ds.pair_hash((rowbase + key) >> 1);
+            dp[kt][r] = (hv & 0xFFFFu) >= thr ? dp[kt][r] * inv_keep : 0.f;
+            dp[kt][r + 1] = (hv >> 16) >= thr ? dp[kt][r + 1] * inv_keep : 0.f;
+          }
+      } else {
+#pragma unroll
+        for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int key = k0 + kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+            dp[kt][r] = ds.bits16(rowbase + key) >= thr ? dp[kt][r] * inv_keep : 0.f;
+          }
+      }
+    }
 #pragma unroll
     for (int kt = 0; kt < NKT; ++kt)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const float p = __builtin_amdgcn_exp2f(fmaf(sc[kt][r], c, -L));
-        float d = dp[kt][r];
-        if constexpr (DROP) {
-          const int key = k0 + kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
-          d = (drop_hash(seed, doff + (((uint64_t)(b * H + h) * T_ + qi) * T_ + key)) >= thr) ? d * inv_keep : 0.f;
-        }
-        sc[kt][r] = p * (d - D);
+        sc[kt][r] = p * (dp[kt][r] - D);
       }
 #pragma unroll
     for (int kt = 0; kt < NKT; ++kt)
@@ -621,8 +651,8 @@ void attn_bwd_mfma(DType dt, const void* qkv, const void* o, const float* lse, c
                    float* delta, float* dq_acc, float* dkv_part, int B, int T_, int H, int G, int hd, bool causal,
                    float p, uint64_t seed, uint64_t offset, hipStream_t s) {
   (void)dq_acc;
-  const uint32_t thr = drop_threshold(p);
-  const float ik = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  const uint32_t thr = drop_threshold16(p);
+  const float ik = drop_inv_keep(p);
   static const int kv_variant = kv_variant_from_env();
   static const int q_variant = q_variant_from_env();
   const int nkb = (T_ + BWD_BKV - 1) / BWD_BKV;

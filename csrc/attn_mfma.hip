@@ -113,6 +113,14 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd_mfma_k(const T* __restrict_
   const int wq_lo = q0 + w * 32, wq_hi = wq_lo + 31;  // this wave's query range
   const int qi = wq_lo + l32;                          // this lane's query
   const float c = rsqrtf((float)HD) * kLog2e;
+  DropSlab ds;
+  uint64_t dslab = 0;
+  bool dpair = false;
+  if constexpr (DROP) {
+    dslab = doff + (uint64_t)(b * H + h) * T_ * T_;
+    ds.init(seed, dslab);
+    dpair = ((doff | (uint64_t)T_) & 1) == 0;
+  }
 
   // ---- Q fragments (B operand): Q[qi][16kk + 8hh + 0..7]
   v8 qf[KK];
@@ -250,15 +258,32 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd_mfma_k(const T* __restrict_
       for (int r = 0; r < 16; ++r) {
         const float p = __builtin_amdgcn_exp2f(fmaf(s[kt][r], c, -m));
         ls += p;
-        if constexpr (DROP) {
-          const int key = k0 + kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
-          const uint64_t e = (((uint64_t)(b * H + h) * T_ + qi) * T_ + key);
-          s[kt][r] = (drop_hash(seed, doff + e) >= thr) ? p * inv_keep : 0.f;
-        } else {
-          s[kt][r] = p;
-        }
+        s[kt][r] = p;
       }
     l += ls;
+    if constexpr (DROP) {
+      // keys (r, r+1) with r even are adjacent: one hash serves both when the row base is even
+      const uint64_t rowbase = dslab + (uint64_t)qi * T_;
+      if (dpair) {
+#pragma unroll
+        for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+          for (int r = 0; r < 16; r += 2) {
+            const int key = k0 + kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+            const uint32_t hv = ds.pair_hash((rowbase + key) >> 1);
+            s[kt][r] = (hv & 0xFFFFu) >= thr ? s[kt][r] * inv_keep : 0.f;
+            s[kt][r + 1] = (hv >> 16) >= thr ? s[kt][r + 1] * inv_keep : 0.f;
+          }
+      } else {
+#pragma unroll
+        for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int key = k0 + kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+            s[kt][r] = ds.bits16(rowbase + key) >= thr ? s[kt][r] * inv_keep : 0.f;
+          }
+      }
+    }
     // ---- O^T += V^T P^T: P fragments packed from the accumulators, V^T by transposed reads
 #pragma unroll
     for (int kt = 0; kt < NKT; ++kt)
@@ -322,8 +347,8 @@ static int fwd_variant_from_env() {
 
 void attn_fwd_mfma(DType dt, const void* qkv, void* o, float* lse, int B, int T_, int H, int G, int hd, bool causal,
                    float p, uint64_t seed, uint64_t offset, hipStream_t s) {
-  const uint32_t thr = drop_threshold(p);
-  const float ik = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  const uint32_t thr = drop_threshold16(p);
+  const float ik = drop_inv_keep(p);
   static const int fwd_variant = fwd_variant_from_env();
   dim3 grid(((T_ + FWD_BQ - 1) / FWD_BQ) * H * B), block(256);
 #define LAUNCH_V(TT, HDD, BK, NB, OC)                                                                         \

@@ -42,7 +42,7 @@ __global__ __launch_bounds__(64) void attn_fwd_naive_k(const T* __restrict__ qkv
     const float pr = exp2f(s - mn);
     l = l * alpha + pr;
     float pw = pr;
-    if (drop) pw = (drop_hash(seed, offset + (((uint64_t)(b * H + h) * T_ + q) * T_ + k)) >= thr) ? pr * inv_keep : 0.f;
+    if (drop) pw = (drop_bits16(seed, offset + (((uint64_t)(b * H + h) * T_ + q) * T_ + k)) >= thr) ? pr * inv_keep : 0.f;
     for (int i = 0; i < hd; ++i) acc[i] = acc[i] * alpha + pw * to_f(vp[i]);
     m = mn;
   }
@@ -96,7 +96,7 @@ __global__ __launch_bounds__(64) void attn_bwd_dq_naive_k(const T* __restrict__ 
     float s = 0.f, dp = 0.f;
     for (int i = 0; i < hd; ++i) { s += qv[i] * to_f(kp[i]); dp += dov[i] * to_f(vp[i]); }
     const float pr = exp2f(s * c - L);
-    if (drop) dp = (drop_hash(seed, offset + (((uint64_t)(b * H + h) * T_ + q) * T_ + k)) >= thr) ? dp * inv_keep : 0.f;
+    if (drop) dp = (drop_bits16(seed, offset + (((uint64_t)(b * H + h) * T_ + q) * T_ + k)) >= thr) ? dp * inv_keep : 0.f;
     const float ds = pr * (dp - D) * scale;
     for (int i = 0; i < hd; ++i) dq[i] += ds * to_f(kp[i]);
   }
@@ -133,7 +133,7 @@ __global__ __launch_bounds__(64) void attn_bwd_dkv_naive_k(const T* __restrict__
       const float pr = exp2f(s * c - L);
       float pd = pr;
       if (drop) {
-        const bool keep = drop_hash(seed, offset + (((uint64_t)(b * H + h) * T_ + q) * T_ + k)) >= thr;
+        const bool keep = drop_bits16(seed, offset + (((uint64_t)(b * H + h) * T_ + q) * T_ + k)) >= thr;
         pd = keep ? pr * inv_keep : 0.f;
         dp = keep ? dp * inv_keep : 0.f;
       }
@@ -157,8 +157,8 @@ __global__ __launch_bounds__(64) void attn_bwd_dkv_naive_k(const T* __restrict__
 
 void attn_fwd_naive(DType dt, const void* qkv, void* o, float* lse, int B, int T_, int H, int G, int hd, bool causal,
                     float p, uint64_t seed, uint64_t offset, hipStream_t s) {
-  const uint32_t thr = drop_threshold(p);
-  const float ik = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  const uint32_t thr = drop_threshold16(p);
+  const float ik = drop_inv_keep(p);
   const long n = (long)B * H * T_;
   BLLM_DISPATCH(dt, T, NAIVE_HD(hd, {
     hipLaunchKernelGGL((attn_fwd_naive_k<T, MAXD>), dim3(ceil_div(n, 64)), dim3(64), 0, s, (const T*)qkv, (T*)o,
@@ -177,8 +177,8 @@ void attn_delta(DType dt, const void* o, const void* dout, float* delta, int B, 
 void attn_bwd_naive(DType dt, const void* qkv, const void* o, const float* lse, const void* dout, void* dqkv,
                     float* delta, int B, int T_, int H, int G, int hd, bool causal, float p, uint64_t seed,
                     uint64_t offset, hipStream_t s) {
-  const uint32_t thr = drop_threshold(p);
-  const float ik = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  const uint32_t thr = drop_threshold16(p);
+  const float ik = drop_inv_keep(p);
   attn_delta(dt, o, dout, delta, B, T_, H, hd, s);
   BLLM_DISPATCH(dt, T, NAIVE_HD(hd, {
     hipLaunchKernelGGL((attn_bwd_dq_naive_k<T, MAXD>), dim3(ceil_div((long)B * H * T_, 64)), dim3(64), 0, s,

@@ -97,16 +97,60 @@ __device__ __forceinline__ uint32_t mix32(uint32_t x) {
   x ^= x >> 16;
   return x;
 }
-// keep iff hash(seed, idx) >= thr,   thr = floor(p * 2^32)
-__device__ __forceinline__ uint32_t drop_hash(uint64_t seed, uint64_t idx) {
-  uint32_t lo = (uint32_t)idx, hi = (uint32_t)(idx >> 32);
-  uint32_t s = mix32((uint32_t)seed + hi * 0x9E3779B9u);
-  return mix32(lo ^ s);
+// Counter-based dropout: ONE 32-bit hash per PAIR of consecutive element indices, 16 bits per
+// element; keep iff bits >= thr16 = floor(p * 2^16) (p resolution 1.5e-5).  Every kernel and the
+// CPU oracle (ops/reference.py:drop_keep_mask) use exactly this function of (seed, index).
+__device__ __forceinline__ uint32_t drop_seed_mix(uint64_t seed, uint32_t pair_hi) {
+  return mix32((uint32_t)seed + pair_hi * 0x9E3779B9u);
 }
-inline uint32_t drop_threshold(float p) {
-  double t = (double)p * 4294967296.0;
-  if (t >= 4294967295.0) return 4294967295u;
-  return (uint32_t)t;
+__device__ __forceinline__ uint32_t drop_pair(uint64_t seed, uint64_t pair) {
+  return mix32((uint32_t)pair ^ drop_seed_mix(seed, (uint32_t)(pair >> 32)));
+}
+__device__ __forceinline__ uint32_t drop_bits16(uint64_t seed, uint64_t idx) {
+  const uint32_t h = drop_pair(seed, idx >> 1);
+  return (idx & 1) ? (h >> 16) : (h & 0xFFFFu);
+}
+// Dropout bits inside one attention (batch, head) slab [base, base + T*T) (T <= 65536, so the
+// slab spans at most two 2^32-pair windows): the seed mix of both windows is computed once and
+// each pair then costs a single mix32.
+struct DropSlab {
+  uint32_t sm0, sm1, hi0;
+  __device__ __forceinline__ void init(uint64_t seed, uint64_t base) {
+    hi0 = (uint32_t)(base >> 33);
+    sm0 = drop_seed_mix(seed, hi0);
+    sm1 = drop_seed_mix(seed, hi0 + 1);
+  }
+  __device__ __forceinline__ uint32_t pair_hash(uint64_t pair) const {
+    return mix32((uint32_t)pair ^ ((uint32_t)(pair >> 32) == hi0 ? sm0 : sm1));
+  }
+  __device__ __forceinline__ uint32_t bits16(uint64_t idx) const {
+    const uint32_t h = pair_hash(idx >> 1);
+    return (idx & 1) ? (h >> 16) : (h & 0xFFFFu);
+  }
+};
+// bits of VEC consecutive indices from e0; pairs share one hash when e0 is even
+template <int VEC>
+__device__ __forceinline__ void drop_bits_run(uint64_t seed, uint64_t e0, uint32_t (&bits)[VEC]) {
+  if ((e0 & 1) == 0) {
+#pragma unroll
+    for (int j = 0; j < VEC; j += 2) {
+      const uint32_t h = drop_pair(seed, (e0 + j) >> 1);
+      bits[j] = h & 0xFFFFu;
+      if (j + 1 < VEC) bits[j + 1] = h >> 16;
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) bits[j] = drop_bits16(seed, e0 + j);
+  }
+}
+inline uint32_t drop_threshold16(float p) {
+  const double t = (double)p * 65536.0;
+  return t >= 65536.0 ? 65536u : (uint32_t)t;
+}
+// exact inverse of the realised keep probability (1 - thr16 / 2^16)
+inline float drop_inv_keep(float p) {
+  const uint32_t t = drop_threshold16(p);
+  return t >= 65536u ? 0.f : (float)(65536.0 / (65536.0 - (double)t));
 }
 
 // LDS-DMA of 16 bytes per lane (global_load_lds_dwordx4) issued from inline asm so hipcc does

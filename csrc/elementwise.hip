@@ -93,10 +93,11 @@ __global__ __launch_bounds__(256) void dropout_add_k(const T* __restrict__ x, co
     VecN<T, VEC> av = ldv<T, VEC>(a + i * VEC), o;
     VecN<T, VEC> xv;
     if (x) xv = ldv<T, VEC>(x + i * VEC);
+    uint32_t bits[VEC];
+    drop_bits_run<VEC>(seed, offset + (uint64_t)(i * VEC), bits);
 #pragma unroll
     for (int j = 0; j < VEC; ++j) {
-      const uint64_t e = (uint64_t)(i * VEC + j);
-      const bool keep = drop_hash(seed, offset + e) >= thr;
+      const bool keep = bits[j] >= thr;
       float r = keep ? to_f(av.v[j]) * inv_keep : 0.f;
       if (x) r += to_f(xv.v[j]);
       o.v[j] = from_f<T>(r);
@@ -244,8 +245,8 @@ void gelu_bwd(DType dt, const void* f, const void* dg, void* df, long n, hipStre
 }
 void dropout_add(DType dt, const void* x, const void* a, void* out, long n, float p, uint64_t seed,
                  uint64_t offset, hipStream_t s) {
-  const uint32_t thr = drop_threshold(p);
-  const float inv_keep = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  const uint32_t thr = drop_threshold16(p);
+  const float inv_keep = drop_inv_keep(p);
   BLLM_DISPATCH(dt, T, {
     EW_VEC(T, n % (16 / sizeof(T)) == 0, {
       hipLaunchKernelGGL((dropout_add_k<T, VEC>), dim3(ew_grid(n / VEC)), dim3(256), 0, s, (const T*)x,

@@ -24,11 +24,13 @@ __global__ __launch_bounds__(256) void emb_fwd_k(const int64_t* __restrict__ idx
     VecN<T, VEC> a = ldv<T, VEC>(wte + idx[r] * d + c), o;
     VecN<T, VEC> b;
     if (wpe) b = ldv<T, VEC>(wpe + (long)(r % T_) * d + c);
+    uint32_t bits[VEC];
+    if (drop) drop_bits_run<VEC>(seed, offset + (uint64_t)(r * d + c), bits);
 #pragma unroll
     for (int j = 0; j < VEC; ++j) {
       float x = to_f(a.v[j]);
       if (wpe) x += to_f(b.v[j]);
-      if (drop) x = (drop_hash(seed, offset + (uint64_t)(r * d + c + j)) >= thr) ? x * inv_keep : 0.f;
+      if (drop) x = (bits[j] >= thr) ? x * inv_keep : 0.f;
       o.v[j] = from_f<T>(x);
     }
     stv<T, VEC>(out + r * d + c, o);
@@ -107,8 +109,8 @@ static inline int grid_of(long n) {
 
 void embedding_fwd(DType dt, const int64_t* idx, const void* wte, const void* wpe, void* out, long N, int d,
                    int T_, float p, uint64_t seed, uint64_t offset, hipStream_t s) {
-  const uint32_t thr = drop_threshold(p);
-  const float inv_keep = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  const uint32_t thr = drop_threshold16(p);
+  const float inv_keep = drop_inv_keep(p);
   BLLM_DISPATCH(dt, T, {
     EMB_VEC(T, d, {
       hipLaunchKernelGGL((emb_fwd_k<T, VEC>), dim3(grid_of(N * d / VEC)), dim3(256), 0, s, idx, (const T*)wte,

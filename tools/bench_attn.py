@@ -32,6 +32,7 @@ def main():
     a = ap.parse_args()
     ops.load_ext(required=True)
     shapes = [("llama3-8B", 4, 1024, 32, 8, 128, 0.0), ("gpt2-774M", 4, 1024, 20, 20, 64, 0.1),
+              ("gpt2-774M-nodrop", 4, 1024, 20, 20, 64, 0.0),
               ("gpt2-124M", 4, 1024, 12, 12, 64, 0.0)]
     res = []
     for name, B, T, H, G, hd, p in shapes:
