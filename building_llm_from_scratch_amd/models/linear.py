@@ -7,6 +7,14 @@ members add ``scaling * (x @ A) @ B`` into their column slice of ``y`` in place.
 
 Backward writes ``dW`` / ``db`` / ``dA`` / ``dB`` directly into the unit's flat gradient
 buffer (``out=`` GEMMs; ``addmm_`` when accumulating micro-batches).
+
+LoRA on the GPU runs on the fused kernels of csrc/lora.hip (reference lora.py:24-26,45-46),
+a fixed number of launches per group however many members it has:
+  fwd  P = [A_1^T; A_2^T; ...] (pack), t = x P^T (lora_down), y[:, cols_m] += s t_m B_m (lora_up)
+  bwd  u_m = dy[:, cols_m] B_m^T (lora_down), dB_m = s t_m^T dy[:, cols_m] and
+       dA_m = s x^T u_m (lora_wgrad, into the flat gradient), dx += s u P (lora_up)
+Groups the kernels cannot take (fp32, ranks not a multiple of 16, odd widths, token counts not
+a multiple of 64 such as single-token decode) use per-member hipBLASLt GEMMs.
 """
 from __future__ import annotations
 
@@ -75,6 +83,10 @@ def _weight_grad(dy: torch.Tensor, x: torch.Tensor, gW: torch.Tensor, accumulate
         _mm_out(dy.t(), x, gW, accumulate)
 
 
+# tests set this to drive the grouped LoRA path through the CPU oracles of ops.reference
+FORCE_GROUPED_LORA = False
+
+
 class FusedLinear:
     def __init__(self, modules: Sequence[nn.Module]):
         self.modules = list(modules)
@@ -100,6 +112,22 @@ class FusedLinear:
             c += s.out_features
         self.out_total = c
         self.has_lora = any(s.lora_A is not None for s in self.specs)
+        lm = [(c, s) for c, s in zip(self.cols, self.specs) if s.lora_A is not None]
+        self.lora_c0 = [c0 for (c0, _), _ in lm]
+        self.lora_len = [c1 - c0 for (c0, c1), _ in lm]
+        self.lora_r = [s.lora_A.shape[1] for _, s in lm]
+        self.lora_off = [sum(self.lora_r[:i]) for i in range(len(lm))]
+        self.lora_R = sum(self.lora_r)
+        self.lora_specs = [s for _, s in lm]
+        scales = {float(s.scaling) for s in self.lora_specs}
+        self.lora_scale = scales.pop() if len(scales) == 1 else None
+
+    def _grouped_lora(self, x: torch.Tensor) -> bool:
+        if self.lora_scale is None or len(self.lora_specs) != len(self.specs):
+            return False
+        if FORCE_GROUPED_LORA:
+            return True
+        return ops.lora_kernel_ok(x, self.lora_r, [x.shape[1]] + self.lora_len + self.lora_c0)
 
     # views are re-fetched every call: FSDP may have re-materialised the storage
     def W(self):
@@ -114,6 +142,18 @@ class FusedLinear:
         b = self.b()
         if residual is not None:
             assert b is None
+        if self.has_lora and self._grouped_lora(x):
+            # y = (residual | bias) + s t B, written by lora_up, then the base GEMM accumulates
+            # onto it (beta = 1): the rank-r update costs no read-modify-write pass of y
+            u = self.unit
+            P = ops.lora_pack_t([u.data(s.lora_A) for s in self.lora_specs])          # [R, K]
+            t = ops.lora_down(x, [P], [0], [x.shape[1]], [0], self.lora_R)            # x A_cat
+            y = torch.empty(x.shape[0], self.out_total, dtype=x.dtype, device=x.device)
+            ops.lora_up_(y, t, [u.data(s.lora_B) for s in self.lora_specs], self.lora_c0,
+                         self.lora_off, self.lora_scale, base=residual, bias=b)
+            y.addmm_(x, W.t())
+            return y, ("grouped", t, P)
+        if residual is not None:
             y = torch.addmm(residual, x, W.t())
         elif b is not None:
             y = torch.addmm(b, x, W.t())
@@ -145,6 +185,8 @@ class FusedLinear:
             gb = u.fused_grad(self.b_params)
             if gb is not None:
                 ops.bias_grad_(dy, gb, accumulate)
+        if self.has_lora and isinstance(xa, tuple) and xa[0] == "grouped":
+            return self._grouped_lora_backward(dy, x, xa[1], xa[2], need_dx, dx_acc, accumulate)
         dx = None
         if need_dx:
             W = self.W()
@@ -165,15 +207,35 @@ class FusedLinear:
                     if accumulate:
                         gB.addmm_(t.t(), dys, alpha=s.scaling)
                     else:
-                        torch.mm(t.t(), dys, out=gB)
-                        gB.mul_(s.scaling)
+                        torch.addmm(gB, t.t(), dys, beta=0, alpha=s.scaling, out=gB)
                 gA = u.grad(s.lora_A)
                 if gA is not None:
                     if accumulate:
                         gA.addmm_(x.t(), dyB, alpha=s.scaling)
                     else:
-                        torch.mm(x.t(), dyB, out=gA)
-                        gA.mul_(s.scaling)
+                        torch.addmm(gA, x.t(), dyB, beta=0, alpha=s.scaling, out=gA)
                 if need_dx:
                     dx.addmm_(dyB, A.t(), alpha=s.scaling)
+        return dx
+
+    def _grouped_lora_backward(self, dy, x, t, P, need_dx, dx_acc, accumulate):
+        u_ = self.unit
+        sc = self.lora_scale
+        Bs = [u_.data(s.lora_B) for s in self.lora_specs]
+        u = ops.lora_down(dy, Bs, self.lora_c0, self.lora_len, self.lora_off, self.lora_R)   # dy B^T
+        gB = [(u_.grad(s.lora_B), c0, off) for s, c0, off in zip(self.lora_specs, self.lora_c0, self.lora_off)]
+        gB = [g for g in gB if g[0] is not None]
+        if gB:
+            ops.lora_wgrad(t, dy, [g for g, _, _ in gB], [o for _, _, o in gB], [c for _, c, _ in gB], sc,
+                           accumulate)
+        gA = [(u_.grad(s.lora_A), off) for s, off in zip(self.lora_specs, self.lora_off)]
+        gA = [g for g in gA if g[0] is not None]
+        if gA:
+            ops.lora_wgrad(u, x, [g.t() for g, _ in gA], [o for _, o in gA], [0] * len(gA), sc, accumulate)
+        if not need_dx:
+            return None
+        # dx = dx_acc + s u A_cat^T (lora_up, write-only) then += dy W (beta = 1 GEMM)
+        dx = torch.empty(x.shape, dtype=x.dtype, device=x.device)
+        ops.lora_up_(dx, u, [P], [0], [0], sc, base=dx_acc)
+        dx.addmm_(dy, self.W())
         return dx

@@ -20,6 +20,7 @@ __all__ = [
     "rope_", "rope_tables", "flash_attn_fwd", "flash_attn_bwd", "swiglu_fwd", "swiglu_bwd",
     "gelu_fwd", "gelu_bwd", "ce_fwd", "ce_bwd_", "embedding_fwd", "embedding_bwd",
     "sq_norm_multi", "adamw_step_", "attn_decode", "bias_grad_", "ext_available", "load_ext", "attention_backend",
+    "lora_down", "lora_up_", "lora_wgrad", "lora_pack_t", "lora_kernel_ok",
 ]
 
 rope_tables = ref.rope_tables
@@ -197,6 +198,49 @@ def embedding_bwd(idx, dx, grad_wte, grad_wpe, T: int, accumulate: bool = False)
         _k().embedding_bwd(idx, dx, grad_wte, grad_wpe, T, accumulate)
         return
     ref.embedding_bwd(idx, dx, grad_wte, grad_wpe, T, accumulate)
+
+
+# --------------------------------------------------------------------------- LoRA
+def lora_kernel_ok(x: torch.Tensor, ranks, widths) -> bool:
+    """Whether the fused LoRA kernels (csrc/lora.hip) take a group: bf16/fp16 on the GPU,
+    N % 64 == 0 tokens, every rank a multiple of 16 (<= 64) and every column width (input and
+    member outputs) a multiple of 32.  Otherwise the caller uses the hipBLASLt GEMM path."""
+    if x.device.type != "cuda" or x.dtype not in (torch.bfloat16, torch.float16):
+        return False
+    if x.dim() != 2 or x.shape[0] % 64 or x.shape[1] % 32:
+        return False
+    return all(r % 16 == 0 and 0 < r <= 64 for r in ranks) and all(w % 32 == 0 for w in widths)
+
+
+def lora_down(x, ws, c0, lens, ocol, R: int, scale: float = 1.0):
+    """out[:, ocol_i : +r_i] = scale * x[:, c0_i : +len_i] @ w_i^T  -> [N, R]"""
+    if _hip(x):
+        return _k().lora_down(x, list(ws), list(c0), list(lens), list(ocol), int(R), float(scale))
+    return ref.lora_down(x, ws, c0, lens, ocol, R, scale)
+
+
+def lora_up_(y, t, us, c0, toff, scale: float, base=None, bias=None):
+    """y[:, c0_i : +len_i] = base + bias + scale * t[:, toff_i : +r_i] @ u_i  (u_i [r_i, len_i], any
+    strides; ``base`` [N, M] and ``bias`` [M] optional, ``base`` may be ``y`` itself)."""
+    if _hip(y):
+        _k().lora_up_(y, t, list(us), list(c0), list(toff), float(scale), base, bias)
+        return y
+    return ref.lora_up_(y, t, us, c0, toff, scale, base, bias)
+
+
+def lora_wgrad(p, q, gs, pa, qb, scale: float, accumulate: bool = False):
+    """g_i[a][b] (+)= scale * sum_n p[n][pa_i + a] q[n][qb_i + b], written into g_i in its dtype."""
+    if _hip(p):
+        _k().lora_wgrad(p, q, list(gs), list(pa), list(qb), float(scale), bool(accumulate))
+        return
+    ref.lora_wgrad(p, q, gs, pa, qb, scale, accumulate)
+
+
+def lora_pack_t(As):
+    """[sum r_i, K] = concat_i A_i^T (A_i [K, r_i])"""
+    if _hip(As[0]):
+        return _k().lora_pack_t(list(As))
+    return ref.lora_pack_t(As)
 
 
 # --------------------------------------------------------------------------- optimizer

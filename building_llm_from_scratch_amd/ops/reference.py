@@ -365,3 +365,41 @@ def attn_decode(q, kcache, vcache, L: int):
     s = torch.einsum("bhd,bhld->bhl", q.float(), k) / math.sqrt(hd)
     p = torch.softmax(s, dim=-1)
     return torch.einsum("bhl,bhld->bhd", p, v).reshape(B, H * hd).to(q.dtype)
+
+
+# ------------------------------------------------------------------ LoRA (csrc/lora.hip oracle)
+def lora_down(x, ws, c0, lens, ocol, R: int, scale: float = 1.0):
+    """out[:, ocol_i : ocol_i + r_i] = scale * x[:, c0_i : c0_i + len_i] @ w_i[:, :len_i]^T"""
+    out = torch.zeros(x.shape[0], R, dtype=torch.float32, device=x.device)
+    for w, c, n, o in zip(ws, c0, lens, ocol):
+        out[:, o:o + w.shape[0]] = x[:, c:c + n].float() @ w[:, :n].float().t()
+    return (out * scale).to(x.dtype)
+
+
+def lora_up_(y, t, us, c0, toff, scale: float, base=None, bias=None):
+    """y[:, c0_i : c0_i + len_i] = base + bias + scale * t[:, toff_i : toff_i + r_i] @ u_i
+    (u_i [r_i, len_i]; base / bias optional)"""
+    for u, c, o in zip(us, c0, toff):
+        r, n = u.shape
+        v = scale * (t[:, o:o + r].float() @ u.float())
+        if base is not None:
+            v = v + base[:, c:c + n].float()
+        if bias is not None:
+            v = v + bias[c:c + n].float()
+        y[:, c:c + n] = v.to(y.dtype)
+    return y
+
+
+def lora_wgrad(p, q, gs, pa, qb, scale: float, accumulate: bool):
+    """g_i[a][b] (+)= scale * sum_n p[n][pa_i + a] q[n][qb_i + b]  (g_i [r_i, len_i], may be a view)"""
+    for g, a0, b0 in zip(gs, pa, qb):
+        r, n = g.shape
+        v = scale * (p[:, a0:a0 + r].float().t() @ q[:, b0:b0 + n].float())
+        if accumulate:
+            v = v + g.float()
+        g.copy_(v.to(g.dtype))
+
+
+def lora_pack_t(As):
+    """[sum r_i, K] = concat_i A_i^T"""
+    return torch.cat([a.t() for a in As], 0).contiguous()

@@ -71,6 +71,49 @@ void embedding_bwd_tok(DType dt, const int64_t* sorted, const int64_t* perm, con
                        bool accumulate, hipStream_t s);
 void embedding_bwd_pos(DType dt, const void* dx, void* grad, int B, int T, int d, bool accumulate, hipStream_t s);
 
+// lora.hip — see the file header for the operand conventions
+constexpr int LORA_MAX = 8;
+struct LoraDownArgs {  // chunk c: out[:, ocol_c : +16*nt_c] = x[:, c0_c : +len_c] . W_c^T
+  const void* x; long ldx;
+  void* out; long ldo;
+  float scale;
+  int n;
+  int c0[LORA_MAX], len[LORA_MAX], ocol[LORA_MAX], nt[LORA_MAX];
+  const void* w[LORA_MAX]; long ldw[LORA_MAX];
+};
+struct LoraUpArgs {  // member m: y[:, c0_m : +len_m] = base + bias + scale . t[:, toff_m : +r_m] . U_m
+  void* y; long ldy;
+  const void* base; long ldb;  // optional (may alias y)
+  const void* bias;            // optional, indexed by absolute column
+  const void* t; long ldt;
+  float scale;
+  int n;
+  int c0[LORA_MAX], len[LORA_MAX], toff[LORA_MAX], r[LORA_MAX];
+  const void* u[LORA_MAX]; long su_j[LORA_MAX], su_c[LORA_MAX];
+};
+struct LoraWgradArgs {  // member m: G_m[a*sa + b*sb] (+)= scale . sum_n p[n][pa_m + a] q[n][qb_m + b]
+  const void* p; long ldp;
+  const void* q; long ldq;
+  float scale;
+  bool accumulate;
+  int n;
+  int pa[LORA_MAX], qb[LORA_MAX], r[LORA_MAX], len[LORA_MAX], nblk[LORA_MAX];
+  long sa[LORA_MAX], sb[LORA_MAX];
+  void* g[LORA_MAX];
+  float* part; long part_ld; long part_off[LORA_MAX];  // S > 1: part[s][part_off_m + e], row length part_ld
+};
+struct LoraPackArgs {  // out[off_m + j][k] = a_m[k][j]
+  void* out;
+  int n;
+  int off[LORA_MAX], r[LORA_MAX];
+  const void* a[LORA_MAX];
+};
+void lora_down(DType dt, const LoraDownArgs& a, int N, hipStream_t s);
+void lora_up(DType dt, const LoraUpArgs& a, int N, int max_len, hipStream_t s);
+int lora_wgrad_splits(int blocks, int N);
+void lora_wgrad(DType dt, DType odt, const LoraWgradArgs& a, int N, int S, hipStream_t s);
+void lora_pack_t(DType dt, const LoraPackArgs& a, int K, int max_r, hipStream_t s);
+
 // optim.hip
 void adamw_step(DType pdt, DType gdt, void* param, float* master, const void* grad, float* m, float* v, long n,
                 float lr, float b1, float b2, float eps, float wd, int step, const float* gscale, hipStream_t s);

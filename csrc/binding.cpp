@@ -335,6 +335,144 @@ void embedding_bwd(const Tensor& idx, const Tensor& dx, const optional<Tensor>& 
   }
 }
 
+// ------------------------------------------------------------------ LoRA (csrc/lora.hip)
+static void check_lora_mat(const Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda() && t.dim() == 2, "bllm lora: ", name, " must be a 2-D GPU tensor");
+  TORCH_CHECK(t.stride(1) == 1 && t.stride(0) % 8 == 0 && (uintptr_t)t.data_ptr() % 16 == 0,
+              "bllm lora: ", name, " rows must be 16-byte aligned and unit-stride");
+}
+
+// out[:, ocol_i : ocol_i + r_i] = scale * x[:, c0_i : c0_i + len_i] . w_i^T ;  w_i [r_i, >= len_i]
+Tensor lora_down(const Tensor& x, at::TensorList ws, at::IntArrayRef c0, at::IntArrayRef lens,
+                 at::IntArrayRef ocol, int64_t R, double scale) {
+  check_lora_mat(x, "x");
+  c10::DeviceGuard g(x.device());
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kHalf, "lora_down: bf16/fp16 only");
+  const int64_t N = x.size(0);
+  TORCH_CHECK(N % 16 == 0 && R % 16 == 0 && R > 0, "lora_down: N and R must be multiples of 16");
+  TORCH_CHECK(ws.size() == c0.size() && ws.size() == lens.size() && ws.size() == ocol.size());
+  auto out = at::empty({N, R}, x.options());
+  bllm::LoraDownArgs a{};
+  a.x = x.data_ptr(); a.ldx = x.stride(0); a.out = out.data_ptr(); a.ldo = R; a.scale = (float)scale;
+  for (size_t i = 0; i < ws.size(); ++i) {
+    const Tensor& w = ws[i];
+    check_lora_mat(w, "w");
+    TORCH_CHECK(w.scalar_type() == x.scalar_type(), "lora_down: dtype mismatch");
+    const int64_t r = w.size(0);
+    TORCH_CHECK(r % 16 == 0 && lens[i] % 32 == 0 && c0[i] % 8 == 0 && w.size(1) >= lens[i],
+                "lora_down: rank % 16, len % 32, c0 % 8 required");
+    TORCH_CHECK(c0[i] + lens[i] <= x.size(1) && ocol[i] + r <= R && ocol[i] % 8 == 0, "lora_down: window out of range");
+    for (int64_t off = 0; off < r; off += 64) {
+      TORCH_CHECK(a.n < bllm::LORA_MAX, "lora_down: too many rank chunks");
+      a.c0[a.n] = (int)c0[i]; a.len[a.n] = (int)lens[i]; a.ocol[a.n] = (int)(ocol[i] + off);
+      a.nt[a.n] = (int)(std::min<int64_t>(64, r - off) / 16);
+      a.w[a.n] = (const char*)w.data_ptr() + off * w.stride(0) * w.element_size();
+      a.ldw[a.n] = w.stride(0);
+      ++a.n;
+    }
+  }
+  bllm::lora_down(dt_of(x), a, (int)N, stream());
+  return out;
+}
+
+// y[:, c0_i : c0_i + len_i] = base + bias + scale * t[:, toff_i : toff_i + r_i] . u_i ;  u_i [r_i, len_i], any
+// strides; base (same shape as y, may be y itself) and bias ([y.size(1)]) are optional
+void lora_up_(Tensor& y, const Tensor& t, at::TensorList us, at::IntArrayRef c0, at::IntArrayRef toff, double scale,
+              const optional<Tensor>& base, const optional<Tensor>& bias) {
+  check_lora_mat(y, "y"); check_lora_mat(t, "t");
+  c10::DeviceGuard g(y.device());
+  TORCH_CHECK(y.scalar_type() == t.scalar_type() && (y.scalar_type() == at::kBFloat16 || y.scalar_type() == at::kHalf));
+  const int64_t N = y.size(0);
+  TORCH_CHECK(t.size(0) == N && N % 64 == 0, "lora_up: N must be a multiple of 64");
+  TORCH_CHECK(us.size() == c0.size() && us.size() == toff.size() && (int)us.size() <= bllm::LORA_MAX);
+  bllm::LoraUpArgs a{};
+  a.y = y.data_ptr(); a.ldy = y.stride(0); a.t = t.data_ptr(); a.ldt = t.stride(0); a.scale = (float)scale;
+  if (base.has_value()) {
+    check_lora_mat(*base, "base");
+    TORCH_CHECK(base->sizes() == y.sizes() && base->scalar_type() == y.scalar_type(), "lora_up: base shape");
+    a.base = base->data_ptr(); a.ldb = base->stride(0);
+  }
+  if (bias.has_value()) {
+    check_gpu(*bias, "bias");
+    TORCH_CHECK(bias->numel() == y.size(1) && bias->scalar_type() == y.scalar_type() &&
+                (uintptr_t)bias->data_ptr() % 16 == 0, "lora_up: bias");
+    a.bias = bias->data_ptr();
+  }
+  int max_len = 0;
+  for (size_t i = 0; i < us.size(); ++i) {
+    const Tensor& u = us[i];
+    TORCH_CHECK(u.is_cuda() && u.dim() == 2 && u.scalar_type() == y.scalar_type(), "lora_up: u must be 2-D");
+    const int64_t r = u.size(0), len = u.size(1);
+    TORCH_CHECK(r % 16 == 0 && r <= 256 && toff[i] % 8 == 0 && toff[i] + r <= t.size(1), "lora_up: rank window");
+    TORCH_CHECK(c0[i] % 8 == 0 && len % 8 == 0 && c0[i] + len <= y.size(1), "lora_up: output window");
+    a.c0[a.n] = (int)c0[i]; a.len[a.n] = (int)len; a.toff[a.n] = (int)toff[i]; a.r[a.n] = (int)r;
+    a.u[a.n] = u.data_ptr(); a.su_j[a.n] = u.stride(0); a.su_c[a.n] = u.stride(1);
+    max_len = std::max<int>(max_len, (int)len);
+    ++a.n;
+  }
+  bllm::lora_up(dt_of(y), a, (int)N, max_len, stream());
+}
+
+// g_i[a][b] (+)= scale * sum_n p[n][pa_i + a] * q[n][qb_i + b] ;  g_i [r_i, len_i] view of a contiguous block
+void lora_wgrad(const Tensor& p, const Tensor& q, at::TensorList gs, at::IntArrayRef pa, at::IntArrayRef qb,
+                double scale, bool accumulate) {
+  check_lora_mat(p, "p"); check_lora_mat(q, "q");
+  c10::DeviceGuard g(p.device());
+  TORCH_CHECK(p.scalar_type() == q.scalar_type() && (p.scalar_type() == at::kBFloat16 || p.scalar_type() == at::kHalf));
+  const int64_t N = p.size(0);
+  TORCH_CHECK(q.size(0) == N && N % 64 == 0, "lora_wgrad: N must be a multiple of 64");
+  TORCH_CHECK(gs.size() == pa.size() && gs.size() == qb.size() && (int)gs.size() <= bllm::LORA_MAX && !gs.empty());
+  bllm::LoraWgradArgs a{};
+  a.p = p.data_ptr(); a.ldp = p.stride(0); a.q = q.data_ptr(); a.ldq = q.stride(0);
+  a.scale = (float)scale; a.accumulate = accumulate;
+  const DType odt = dt_of(gs[0]);
+  int blocks = 0;
+  for (size_t i = 0; i < gs.size(); ++i) {
+    const Tensor& gm = gs[i];
+    TORCH_CHECK(gm.is_cuda() && gm.dim() == 2 && dt_of(gm) == odt, "lora_wgrad: grads must share a dtype");
+    TORCH_CHECK(gm.is_contiguous() || gm.t().is_contiguous(), "lora_wgrad: grad must be a (transposed) contiguous block");
+    const int64_t r = gm.size(0), len = gm.size(1);
+    TORCH_CHECK(r % 16 == 0 && r <= 64 && len % 8 == 0 && pa[i] % 8 == 0 && qb[i] % 8 == 0, "lora_wgrad: alignment");
+    TORCH_CHECK(pa[i] + r <= p.size(1) && qb[i] + len <= q.size(1), "lora_wgrad: window out of range");
+    a.pa[a.n] = (int)pa[i]; a.qb[a.n] = (int)qb[i]; a.r[a.n] = (int)r; a.len[a.n] = (int)len;
+    a.nblk[a.n] = bllm::ceil_div(len, 64); a.sa[a.n] = gm.stride(0); a.sb[a.n] = gm.stride(1);
+    a.g[a.n] = gm.data_ptr();
+    blocks += a.nblk[a.n];
+    ++a.n;
+  }
+  const int S = bllm::lora_wgrad_splits(blocks, (int)N);
+  Tensor part;
+  if (S > 1) {
+    int64_t total = 0;
+    for (int i = 0; i < a.n; ++i) { a.part_off[i] = total; total += (int64_t)a.len[i] * a.r[i]; }
+    part = at::empty({S, total}, p.options().dtype(at::kFloat));
+    a.part = part.data_ptr<float>(); a.part_ld = total;
+  }
+  bllm::lora_wgrad(dt_of(p), odt, a, (int)N, S, stream());
+}
+
+// [R, K] = concat_i a_i^T  (a_i [K, r_i] contiguous)
+Tensor lora_pack_t(at::TensorList as) {
+  TORCH_CHECK(!as.empty() && (int)as.size() <= bllm::LORA_MAX);
+  c10::DeviceGuard g(as[0].device());
+  const int64_t K = as[0].size(0);
+  bllm::LoraPackArgs a{};
+  int64_t R = 0;
+  int max_r = 0;
+  for (auto& t : as) {
+    check_gpu(t, "lora A");
+    TORCH_CHECK(t.dim() == 2 && t.size(0) == K && t.scalar_type() == as[0].scalar_type());
+    a.off[a.n] = (int)R; a.r[a.n] = (int)t.size(1); a.a[a.n] = t.data_ptr();
+    R += t.size(1);
+    max_r = std::max<int>(max_r, (int)t.size(1));
+    ++a.n;
+  }
+  auto out = at::empty({R, K}, as[0].options());
+  a.out = out.data_ptr();
+  bllm::lora_pack_t(dt_of(as[0]), a, (int)K, max_r, stream());
+  return out;
+}
+
 // ------------------------------------------------------------------ optimizer
 Tensor sq_norm_multi(at::TensorList ts) {
   TORCH_CHECK(!ts.empty());
@@ -405,6 +543,10 @@ TORCH_LIBRARY(bllm, m) {
   m.def("ce_bwd_(Tensor(a!) logits, Tensor targets, Tensor lse, Tensor scale, int ignore_index) -> ()");
   m.def("embedding_fwd(Tensor idx, Tensor wte, Tensor? wpe, int T, float p, int seed, int offset) -> Tensor");
   m.def("embedding_bwd(Tensor idx, Tensor dx, Tensor(a!)? grad_wte, Tensor(b!)? grad_wpe, int T, bool accumulate) -> ()");
+  m.def("lora_down(Tensor x, Tensor[] ws, int[] c0, int[] lens, int[] ocol, int R, float scale) -> Tensor");
+  m.def("lora_up_(Tensor(a!) y, Tensor t, Tensor[] us, int[] c0, int[] toff, float scale, Tensor? base, Tensor? bias) -> ()");
+  m.def("lora_wgrad(Tensor p, Tensor q, Tensor(a!)[] gs, int[] pa, int[] qb, float scale, bool accumulate) -> ()");
+  m.def("lora_pack_t(Tensor[] a) -> Tensor");
   m.def("sq_norm_multi(Tensor[] ts) -> Tensor");
   m.def("adamw_step_(Tensor(a!) param, Tensor(b!)? master, Tensor grad, Tensor(c!) exp_avg, Tensor(d!) exp_avg_sq, float lr, float beta1, float beta2, float eps, float wd, int step, Tensor? grad_scale) -> ()");
 }
@@ -429,6 +571,10 @@ TORCH_LIBRARY_IMPL(bllm, CUDA, m) {
   m.impl("ce_bwd_", &ce_bwd_);
   m.impl("embedding_fwd", &embedding_fwd);
   m.impl("embedding_bwd", &embedding_bwd);
+  m.impl("lora_down", &lora_down);
+  m.impl("lora_up_", &lora_up_);
+  m.impl("lora_wgrad", &lora_wgrad);
+  m.impl("lora_pack_t", &lora_pack_t);
   m.impl("sq_norm_multi", &sq_norm_multi);
   m.impl("adamw_step_", &adamw_step_);
 }

@@ -1,0 +1,377 @@
+// LoRA low-rank path on CDNA4 matrix cores (v_mfma_f32_16x16x32_{bf16,f16}).
+//
+// Replaces reference lora.py:24-26,45-46 (``x @ A @ B * scaling`` added to every nn.Linear,
+// LinearWithLoRA) and its autograd.  A fused linear group (Q/K/V, gate/up, or a single
+// projection) has up to LORA_MAX_MEMBERS LoRA members m with A_m [in, r_m], B_m [r_m, out_m];
+// member m owns the column window [c0_m, c0_m + out_m) of the group's output.  Three kernels
+// cover forward and backward (s = alpha / r):
+//
+//   lora_down   T[:, off_m : off_m + r_m] = X[:, c0_m : c0_m + len_m] . W_m^T
+//               fwd: t = x . A  (W = packed A^T, all members read the whole x)
+//               bwd: u = dy . B^T (W = B itself, member m reads its dy window)
+//   lora_up     Y[:, c0_m : c0_m + len_m] += s . T[:, off_m : off_m + r_m] . U_m
+//               fwd: y += s t B  (U = B);  bwd: dx += s u A^T (U = A^T)
+//   lora_wgrad  G_m = s . P[:, a-window]^T . Q[:, b-window]   (reduction over the N tokens)
+//               dB = s t^T dy,  dA = s x^T u — written (or accumulated) straight into the
+//               unit's flat gradient in its dtype; deterministic (fixed-order split-N partials)
+//
+// All three are HBM-bound (the rank is 8-64): x / dy / y are streamed exactly once per kernel
+// with 16-byte lane accesses; the small operands (A, B, t, u) stay L2-resident.
+#include "api.h"
+
+namespace bllm {
+namespace {
+
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+
+template <typename T> struct MF16;
+template <> struct MF16<bf16_t> {
+  static __device__ __forceinline__ f32x4 mma(s16x8 a, s16x8 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c,
+                                                   0, 0, 0);
+  }
+};
+template <> struct MF16<f16_t> {
+  static __device__ __forceinline__ f32x4 mma(s16x8 a, s16x8 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c,
+                                                  0, 0, 0);
+  }
+};
+
+__device__ __forceinline__ s16x8 ld8(const void* p) { return *reinterpret_cast<const s16x8*>(p); }
+
+template <typename T> __device__ __forceinline__ short bits_of(float v) {
+  const T h = from_f<T>(v);
+  return __builtin_bit_cast(short, h);
+}
+template <typename T> __device__ __forceinline__ float from_bits(short b) {
+  return to_f(__builtin_bit_cast(T, b));
+}
+
+// --------------------------------------------------------------------------- lora_down
+// Block = 8 waves on 16 rows; the K loop is split over the waves (wave w takes k-steps
+// w, w+8, ...; four per trip so four 16-B x loads are in flight per lane) and the eight
+// partial 16 x (16*NT) tiles are summed through LDS.
+// MFMA: A = X rows (lane: X[row l&15][k 8(l>>4)..+8], one 16-B load), B[k][col] = W[col][k]
+// (W rows are k-contiguous -> one 16-B load per column tile).
+template <typename T>
+__global__ __launch_bounds__(512) void lora_down_k(LoraDownArgs a) {
+  constexpr int NW = 8;
+  __shared__ float red[NW][16][4 * 16 + 1];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int ch = blockIdx.y;
+  const int nt = a.nt[ch];
+  const long row0 = (long)blockIdx.x * 16;
+  const T* x = (const T*)a.x + (row0 + (lane & 15)) * a.ldx + a.c0[ch] + 8 * (lane >> 4);
+  const T* w = (const T*)a.w[ch] + (long)(lane & 15) * a.ldw[ch] + 8 * (lane >> 4);
+  const long wstep = 16 * a.ldw[ch];
+  f32x4 acc[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int nks = a.len[ch] >> 5;
+  int ks = wave;
+  for (; ks + 3 * NW < nks; ks += 4 * NW) {
+    s16x8 xa[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) xa[u] = ld8(x + (ks + u * NW) * 32);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      if (t < nt) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) acc[t] = MF16<T>::mma(xa[u], ld8(w + t * wstep + (ks + u * NW) * 32), acc[t]);
+      }
+    }
+  }
+  for (; ks < nks; ks += NW) {
+    const s16x8 xa0 = ld8(x + ks * 32);
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+      if (t < nt) acc[t] = MF16<T>::mma(xa0, ld8(w + t * wstep + ks * 32), acc[t]);
+  }
+  // C layout: lane holds C[row 4(l>>4)+i][col l&15]
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+    if (t < nt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) red[wave][4 * (lane >> 4) + i][t * 16 + (lane & 15)] = acc[t][i];
+  __syncthreads();
+  const int cols = nt * 16;
+  T* out = (T*)a.out + row0 * a.ldo + a.ocol[ch];
+  for (int e = threadIdx.x; e < 16 * cols; e += NW * 64) {
+    const int r = e / cols, c = e - r * cols;
+    float v = 0.f;
+#pragma unroll
+    for (int q = 0; q < NW; ++q) v += red[q][r][c];
+    out[(long)r * a.ldo + c] = from_f<T>(v * a.scale);
+  }
+}
+
+// --------------------------------------------------------------------------- lora_up
+// out[:, c0 + c] = base[:, c0 + c] + bias[c0 + c] + s . (t[:, toff : toff + r] . U)[:, c]
+// (base / bias optional; base may alias out).  Used write-only ahead of a beta=1 GEMM, so the
+// low-rank update rides on the GEMM's C read instead of a separate read-modify-write pass.
+// Block = `rows` (64-256) rows x 128 columns of one member window; each of the 4 waves walks its rows in
+// 16-row tiles reusing U's [r x 128] slice, staged once per block in LDS as [col][r] (one 16-B
+// read per A fragment).  The product is formed transposed, Y^T tile [16 cols x 16 rows] =
+// U^T . T^T (B fragment = a 16-B global read of a t row); the fp32 tile is re-laid through a
+// per-wave LDS buffer so every lane stores 16 contiguous bytes.
+template <typename T>
+__global__ __launch_bounds__(256) void lora_up_k(LoraUpArgs a, int rows) {
+  constexpr int BN = 128, RP = 64 + 8, EP = BN + 4;
+  __shared__ __attribute__((aligned(16))) short us[BN * RP];
+  __shared__ __attribute__((aligned(16))) float eps_[4 * 16 * EP];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int m = blockIdx.z;
+  const int r = a.r[m], len = a.len[m];
+  const int cb = blockIdx.y * BN;
+  if (cb >= len) return;
+  const T* U = (const T*)a.u[m];
+  const long su_j = a.su_j[m], su_c = a.su_c[m];
+  float* ep = eps_ + wave * 16 * EP;
+  const int c8 = (lane & 15) * 8;
+  const bool col_ok = cb + c8 + 8 <= len;
+  const T* bias = (const T*)a.bias;
+  VecN<T, 8> bb;
+  if (bias && col_ok) bb = ldv<T, 8>(bias + a.c0[m] + cb + c8);
+  const s16x8 zero = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int j0 = 0; j0 < r; j0 += 64) {  // ranks > 64 in 64-wide LDS passes (rare: r <= 64 is one)
+    const int rc = r - j0 < 64 ? r - j0 : 64;
+    if (j0) __syncthreads();
+    if (su_c == 1 && (len & 7) == 0) {  // 16-B loads of 8 columns of one U row
+      for (int e = threadIdx.x; e < (BN / 8) * rc; e += 256) {
+        const int j = e / (BN / 8), c = (e - j * (BN / 8)) * 8;
+        s16x8 v = zero;
+        if (cb + c < len) v = ld8(U + (long)(j0 + j) * su_j + cb + c);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) us[(c + i) * RP + j] = v[i];
+      }
+    } else {
+      for (int e = threadIdx.x; e < BN * rc; e += 256) {
+        const int c = e / rc, j = e - c * rc;  // r-fastest: coalesced when su_j == 1 (U = A^T)
+        short v = 0;
+        if (cb + c < len) v = __builtin_bit_cast(short, U[(long)(j0 + j) * su_j + (long)(cb + c) * su_c]);
+        us[c * RP + j] = v;
+      }
+    }
+    __syncthreads();
+    for (int rt = 0; rt < rows / 64; ++rt) {
+      const long row0 = (long)blockIdx.x * rows + rt * 64 + wave * 16;
+      const T* t = (const T*)a.t + (row0 + (lane & 15)) * a.ldt + a.toff[m] + j0;
+      f32x4 acc[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int k0 = 0; k0 < rc; k0 += 32) {
+        const int kk = k0 + 8 * (lane >> 4);
+        const bool live = kk < rc;  // r % 16 == 0: the upper half of the last step may be padding
+        const s16x8 tb = live ? ld8(t + kk) : zero;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const s16x8 ua = live ? *reinterpret_cast<const s16x8*>(&us[(q * 16 + (lane & 15)) * RP + kk]) : zero;
+          acc[q] = MF16<T>::mma(ua, tb, acc[q]);
+        }
+      }
+      // lane holds Y^T[col q*16 + 4(l>>4) + i][row l&15] -> per-wave [16 rows][128 cols] fp32 tile
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+        *reinterpret_cast<f32x4*>(&ep[(lane & 15) * EP + q * 16 + 4 * (lane >> 4)]) = acc[q];
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's tile writes have landed
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        const int row = (lane >> 4) + 4 * p;
+        if (!col_ok) continue;
+        const long g = (row0 + row) * a.ldy + a.c0[m] + cb + c8;
+        const f32x4 v0 = *reinterpret_cast<const f32x4*>(&ep[row * EP + c8]);
+        const f32x4 v1 = *reinterpret_cast<const f32x4*>(&ep[row * EP + c8 + 4]);
+        const float v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+        VecN<T, 8> bs, o;
+        if (a.base) bs = ldv<T, 8>((const T*)a.base + (row0 + row) * a.ldb + a.c0[m] + cb + c8);
+        if (j0) {  // later rank pass: accumulate onto what the first pass wrote
+          bs = ldv<T, 8>((const T*)a.y + g);
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          float z = a.scale * v[i];
+          if (a.base || j0) z += to_f(bs.v[i]);
+          if (bias && !j0) z += to_f(bb.v[i]);
+          o.v[i] = from_f<T>(z);
+        }
+        stv<T, 8>((T*)a.y + g, o);
+      }
+      __builtin_amdgcn_wave_barrier();  // tile reads done before the next tile's writes
+    }
+  }
+}
+
+// --------------------------------------------------------------------------- lora_wgrad
+// G[b][a] = s . sum_n Q[n][qb + b] . P[n][pa + a]  for b < len (64 per block), a < r.
+// The token dimension is the MFMA K.  64-token chunks of Q [64 n x 64 b] and P [64 n x r] are
+// stored row-major into LDS with 16-B writes and consumed column-major through the hardware
+// transpose read (ds_read_b64_tr_b16: a 16-lane group gets 4 rows x 16 columns delivered
+// column-major), two reads per 8-token fragment.  The next chunk's global loads are issued
+// before the current chunk's MFMAs.  Split-N over gridDim.y; with S > 1 each split writes an
+// fp32 partial G that lora_reduce sums in a fixed order (deterministic, no atomics).
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+__device__ __forceinline__ s16x8 tr_frag(const short* base, int stride) {
+  // rows 0..3 and 4..7 of an 8-row column block -> the 8 k-elements of a 16x16x32 fragment
+  const s16x4 r1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base));
+  const s16x4 r2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + 4 * stride));
+  return s16x8{r1[0], r1[1], r1[2], r1[3], r2[0], r2[1], r2[2], r2[3]};
+}
+
+template <typename T, typename OT>
+__global__ __launch_bounds__(256) void lora_wgrad_k(LoraWgradArgs a, int N) {
+  constexpr int NP = 64 + 8;  // padded row (144 B) of the [n][col] images
+  __shared__ __attribute__((aligned(16))) short qs[64 * NP];
+  __shared__ __attribute__((aligned(16))) short ps[64 * NP];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  int m = 0, bx = blockIdx.x;
+  while (m + 1 < a.n && bx >= a.nblk[m]) { bx -= a.nblk[m]; ++m; }
+  const int r = a.r[m], len = a.len[m];
+  const int b0 = bx * 64;
+  const int S = gridDim.y, split = blockIdx.y;
+  const int nchunks = N / 64;
+  const int c_lo = (int)((long)nchunks * split / S), c_hi = (int)((long)nchunks * (split + 1) / S);
+  const T* Q = (const T*)a.q + a.qb[m];
+  const T* P = (const T*)a.p + a.pa[m];
+  const int nt = r >> 4;
+  f32x4 acc[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int sn = threadIdx.x >> 3, sc = (threadIdx.x & 7) * 8;  // staging: token sn (+32), 8 columns
+  const bool q_ok = b0 + sc + 8 <= len, p_ok = sc < r;
+  const s16x8 zero = {0, 0, 0, 0, 0, 0, 0, 0};
+  s16x8 qv[2], pv[2];
+  auto load = [&](int ck) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const long n = (long)ck * 64 + sn + 32 * h;
+      qv[h] = q_ok ? ld8(Q + n * a.ldq + b0 + sc) : zero;
+      pv[h] = p_ok ? ld8(P + n * a.ldp + sc) : zero;
+    }
+  };
+  // tr-read addresses: lane 4q+p of each 16-lane group -> row q, columns 4p..4p+3 of the block
+  const int tq = (lane & 15) >> 2, tp = lane & 3, tg = lane >> 4;
+  if (c_lo < c_hi) load(c_lo);
+  for (int ck = c_lo; ck < c_hi; ++ck) {
+    __syncthreads();  // previous chunk's fragment reads are done
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      *reinterpret_cast<s16x8*>(&qs[(sn + 32 * h) * NP + sc]) = qv[h];
+      *reinterpret_cast<s16x8*>(&ps[(sn + 32 * h) * NP + sc]) = pv[h];
+    }
+    if (ck + 1 < c_hi) load(ck + 1);
+    __syncthreads();
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int n = ks * 32 + 8 * tg + tq;
+      const s16x8 qa = tr_frag(&qs[n * NP + wave * 16 + 4 * tp], NP);
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+        if (t < nt) acc[t] = MF16<T>::mma(qa, tr_frag(&ps[n * NP + t * 16 + 4 * tp], NP), acc[t]);
+    }
+  }
+  // lane holds G[b = b0 + 16*wave + 4(l>>4) + i][a = 16t + (l&15)]
+  const long sa = a.sa[m], sb = a.sb[m];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    if (t >= nt) continue;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int b = b0 + wave * 16 + 4 * (lane >> 4) + i, aa = t * 16 + (lane & 15);
+      if (b >= len) continue;
+      const long o = (long)aa * sa + (long)b * sb;
+      const float v = acc[t][i] * a.scale;
+      if (S > 1) {
+        a.part[(long)split * a.part_ld + a.part_off[m] + o] = v;
+      } else {
+        OT* g = (OT*)a.g[m];
+        g[o] = from_f<OT>(a.accumulate ? to_f(g[o]) + v : v);
+      }
+    }
+  }
+}
+
+// g_m[e] (+)= sum_s part[s][off_m + e] for every member, one launch, fixed summation order
+template <typename OT>
+__global__ __launch_bounds__(256) void lora_reduce_k(LoraWgradArgs a, int S, long total) {
+  for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < total; e += (long)gridDim.x * 256) {
+    int m = 0;
+    while (m + 1 < a.n && e >= a.part_off[m + 1]) ++m;
+    const long o = e - a.part_off[m];
+    float v = 0.f;
+    for (int s = 0; s < S; ++s) v += a.part[(long)s * a.part_ld + e];
+    OT* g = (OT*)a.g[m];
+    g[o] = from_f<OT>(a.accumulate ? to_f(g[o]) + v : v);
+  }
+}
+
+// P[off_m + j][k] = A_m[k][j]: pack the members' A [K, r_m] into one k-contiguous [R, K] operand
+template <typename T>
+__global__ __launch_bounds__(256) void lora_pack_t_k(LoraPackArgs a, int K) {
+  const int m = blockIdx.y;
+  const int r = a.r[m];
+  const T* A = (const T*)a.a[m];
+  T* P = (T*)a.out + (long)a.off[m] * K;
+  for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < (long)K * r; e += (long)gridDim.x * 256) {
+    const long k = e / r;
+    const int j = (int)(e - k * r);
+    P[(long)j * K + k] = A[e];
+  }
+}
+
+}  // namespace
+
+// ----------------------------------------------------------------------------- launchers
+void lora_down(DType dt, const LoraDownArgs& a, int N, hipStream_t s) {
+  dim3 grid(N / 16, a.n);
+  if (dt == DType::BF16) hipLaunchKernelGGL(lora_down_k<bf16_t>, grid, dim3(512), 0, s, a);
+  else hipLaunchKernelGGL(lora_down_k<f16_t>, grid, dim3(512), 0, s, a);
+}
+
+void lora_up(DType dt, const LoraUpArgs& a, int N, int max_len, hipStream_t s) {
+  // tall blocks amortise the U staging; shrink them until the grid fills the chip (>= 4 per CU)
+  int col_blocks = 0;
+  for (int m = 0; m < a.n; ++m) col_blocks += ceil_div(a.len[m], 128);
+  int rows = 256;
+  while (rows > 64 && ((long)N / rows * col_blocks < 1024 || N % rows)) rows /= 2;
+  dim3 grid(N / rows, ceil_div(max_len, 128), a.n);
+  if (dt == DType::BF16) hipLaunchKernelGGL(lora_up_k<bf16_t>, grid, dim3(256), 0, s, a, rows);
+  else hipLaunchKernelGGL(lora_up_k<f16_t>, grid, dim3(256), 0, s, a, rows);
+}
+
+int lora_wgrad_splits(int blocks, int N) {
+  // aim for >= 2 blocks per CU; every split keeps at least 4 chunks of 64 tokens
+  int S = ceil_div(512, blocks > 0 ? blocks : 1);
+  const int max_s = (N / 64) / 4;
+  if (S > max_s) S = max_s;
+  return S < 1 ? 1 : S;
+}
+
+void lora_wgrad(DType dt, DType odt, const LoraWgradArgs& a, int N, int S, hipStream_t s) {
+  int blocks = 0;
+  for (int m = 0; m < a.n; ++m) blocks += a.nblk[m];
+  dim3 grid(blocks, S);
+  BLLM_DISPATCH(odt, OT, {
+    if (dt == DType::BF16) hipLaunchKernelGGL((lora_wgrad_k<bf16_t, OT>), grid, dim3(256), 0, s, a, N);
+    else hipLaunchKernelGGL((lora_wgrad_k<f16_t, OT>), grid, dim3(256), 0, s, a, N);
+    if (S > 1) {
+      const long total = a.part_ld;
+      const int g = (int)((total + 255) / 256 < 2048 ? (total + 255) / 256 : 2048);
+      hipLaunchKernelGGL(lora_reduce_k<OT>, dim3(g), dim3(256), 0, s, a, S, total);
+    }
+  });
+}
+
+void lora_pack_t(DType dt, const LoraPackArgs& a, int K, int max_r, hipStream_t s) {
+  dim3 grid(ceil_div((long)K * max_r, 256) < 256 ? ceil_div((long)K * max_r, 256) : 256, a.n);
+  if (dt == DType::BF16) hipLaunchKernelGGL(lora_pack_t_k<bf16_t>, grid, dim3(256), 0, s, a, K);
+  else hipLaunchKernelGGL(lora_pack_t_k<f16_t>, grid, dim3(256), 0, s, a, K);
+}
+
+}  // namespace bllm

@@ -101,3 +101,12 @@ def test_logits_path_matches_loss_path():
     with torch.no_grad():
         last = m(idx, last_only=True)
     assert torch.allclose(last[:, 0], logits[:, -1].detach(), atol=1e-5)
+
+
+@pytest.mark.parametrize("family", ["llama", "gpt2"])
+def test_grouped_lora_path_grads(family, monkeypatch):
+    """The grouped LoRA plumbing (pack / down / up / wgrad, as the HIP kernels run it) driven
+    through the CPU oracles gives the eager-autograd gradients."""
+    from building_llm_from_scratch_amd.models import linear
+    monkeypatch.setattr(linear, "FORCE_GROUPED_LORA", True)
+    test_lora_grads(family)
