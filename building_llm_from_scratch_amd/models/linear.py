@@ -73,14 +73,35 @@ def _mm_out(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, accumulate: boo
         torch.mm(a, b, out=out)
 
 
+def weight_grad_splits(n_tokens: int, out_f: int, in_f: int) -> int:
+    """Split-K factor for dW = dy^T x (K = tokens).  With 16k tokens and small projections
+    (GPT-2 d=1280: 25-100 output tiles of 256x256 for 256 CUs) one GEMM leaves most of the chip
+    idle for a 16k-deep K loop; splitting the tokens into S batched GEMMs and summing the
+    partials measured 1.5-1.6x faster on MI355X (tools/bench_dw.py), and slower once the output
+    alone fills the chip (Llama-3-8B, Llama-3.2-1B gate/up and down)."""
+    tiles = -(-out_f // 256) * -(-in_f // 256)
+    S = 8 if tiles <= 32 else 4 if tiles <= 128 else 1
+    while S > 1 and (n_tokens % S or n_tokens // S < 1024):
+        S //= 2
+    return S
+
+
 def _weight_grad(dy: torch.Tensor, x: torch.Tensor, gW: torch.Tensor, accumulate: bool):
-    """gW[out, in] (+)= dy^T x, issued as gW^T = x^T dy into the transposed view: the same
-    memory, but hipBLASLt then picks a kernel family that measured 3-6 % faster for the Llama
-    projections on MI355X (tools/bench_gemm.py: dw_dyTx vs dw_xTdy_outT)."""
-    if gW.is_cuda:
-        _mm_out(x.t(), dy, gW.t(), accumulate)
-    else:
+    """gW[out, in] (+)= dy^T x.  Single GEMM: issued as gW^T = x^T dy into the transposed view
+    (same memory; hipBLASLt then picks a kernel family that measured 3-6 % faster for the Llama
+    projections, tools/bench_gemm.py).  Few output tiles: split-K over token chunks (batched
+    GEMM into [S, out, in] partials + one deterministic fixed-order sum kernel)."""
+    if not gW.is_cuda:
         _mm_out(dy.t(), x, gW, accumulate)
+        return
+    N = x.shape[0]
+    S = weight_grad_splits(N, gW.shape[0], gW.shape[1]) \
+        if gW.is_contiguous() and dy.is_contiguous() and x.is_contiguous() else 1
+    if S == 1:
+        _mm_out(x.t(), dy, gW.t(), accumulate)
+        return
+    part = torch.bmm(dy.view(S, N // S, -1).transpose(1, 2), x.view(S, N // S, -1))   # [S, out, in]
+    ops.sum_partials_(part, gW, accumulate)
 
 
 # tests set this to drive the grouped LoRA path through the CPU oracles of ops.reference

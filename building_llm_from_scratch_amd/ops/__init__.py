@@ -20,7 +20,7 @@ __all__ = [
     "rope_", "rope_tables", "flash_attn_fwd", "flash_attn_bwd", "swiglu_fwd", "swiglu_bwd",
     "gelu_fwd", "gelu_bwd", "ce_fwd", "ce_bwd_", "embedding_fwd", "embedding_bwd",
     "sq_norm_multi", "adamw_step_", "attn_decode", "bias_grad_", "ext_available", "load_ext", "attention_backend",
-    "lora_down", "lora_up_", "lora_wgrad", "lora_pack_t", "lora_kernel_ok",
+    "lora_down", "lora_up_", "lora_wgrad", "lora_pack_t", "lora_kernel_ok", "sum_partials_",
 ]
 
 rope_tables = ref.rope_tables
@@ -128,6 +128,18 @@ def bias_grad_(dy, db, accumulate: bool = False):
     else:
         db.copy_(s)
     return db
+
+
+def sum_partials_(part, out, accumulate: bool = False):
+    """out (+)= part.sum(0) in fp32, fixed order (split-K reduction); ``out`` contiguous."""
+    if _hip(part) and out.numel() % 8 == 0:
+        _k().sum_partials_(part, out, bool(accumulate))
+        return out
+    s = part.float().sum(0).view(out.shape)
+    if accumulate:
+        s = s + out.float()
+    out.copy_(s)
+    return out
 
 
 def attn_decode(q, kcache, vcache, L: int):

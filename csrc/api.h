@@ -53,6 +53,10 @@ int colsum_bands(int N);
 void bias_grad(DType dt, DType odt, const void* dy, float* part, void* out, int N, int F, bool accumulate,
                hipStream_t s);
 
+// elementwise.hip — out[e] (+)= sum_s part[s][e] (n % 8 == 0)
+void sum_partials_into(DType pdt, DType odt, const void* part, void* out, long n, int S, bool accumulate,
+                       hipStream_t s);
+
 // attn_decode.hip — single-query attention over a [B, G, Tmax, hd] KV cache
 int attn_decode_max_len();
 void attn_decode(DType dt, const void* q, const void* kc, const void* vc, void* out, int B, int H, int G, int hd,

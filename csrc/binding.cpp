@@ -215,6 +215,15 @@ void bias_grad_(const Tensor& dy, Tensor& db, bool accumulate) {
                   stream());
 }
 
+// out (+)= part.sum(0): part [S, ...] any float dtype, out contiguous with part[0]'s numel
+void sum_partials_(const Tensor& part, Tensor& out, bool accumulate) {
+  check_gpu(part, "part"); check_gpu(out, "out");
+  c10::DeviceGuard g(part.device());
+  const int64_t S = part.size(0), n = out.numel();
+  TORCH_CHECK(part.numel() == S * n && n % 8 == 0, "sum_partials: shapes");
+  bllm::sum_partials_into(dt_of(part), dt_of(out), part.data_ptr(), out.data_ptr(), n, (int)S, accumulate, stream());
+}
+
 // q [B, H, hd]; kc / vc [B, G, Tmax, hd] with the first L positions valid -> out [B, H*hd]
 Tensor attn_decode(const Tensor& q, const Tensor& kc, const Tensor& vc, int64_t L) {
   check_gpu(q, "q"); check_gpu(kc, "kcache"); check_gpu(vc, "vcache");
@@ -536,6 +545,7 @@ TORCH_LIBRARY(bllm, m) {
   m.def("gelu_bwd(Tensor f, Tensor dg) -> Tensor");
   m.def("rope_(Tensor(a!) qkv, Tensor cos, Tensor sin, int T, int H, int G, int hd, bool inverse, int pos_offset) -> ()");
   m.def("bias_grad_(Tensor dy, Tensor(a!) db, bool accumulate) -> ()");
+  m.def("sum_partials_(Tensor part, Tensor(a!) out, bool accumulate) -> ()");
   m.def("attn_decode(Tensor q, Tensor kcache, Tensor vcache, int L) -> Tensor");
   m.def("flash_attn_fwd(Tensor qkv, int B, int T, int H, int G, int hd, bool causal, float p, int seed, int offset) -> (Tensor, Tensor)");
   m.def("flash_attn_bwd(Tensor qkv, Tensor o, Tensor lse, Tensor dout, int B, int T, int H, int G, int hd, bool causal, float p, int seed, int offset) -> Tensor");
@@ -565,6 +575,7 @@ TORCH_LIBRARY_IMPL(bllm, CUDA, m) {
   m.impl("rope_", &rope_);
   m.impl("flash_attn_fwd", &flash_attn_fwd);
   m.impl("attn_decode", &attn_decode);
+  m.impl("sum_partials_", &sum_partials_);
   m.impl("bias_grad_", &bias_grad_);
   m.impl("flash_attn_bwd", &flash_attn_bwd);
   m.impl("ce_fwd", &ce_fwd);

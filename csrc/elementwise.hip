@@ -275,4 +275,44 @@ void rope(DType dt, void* qkv, const float* cosT, const float* sinT, long N, int
   });
 }
 
+// ---------------------------------------------------------------- split-K partial sum
+// out[e] (+)= sum_{s < S} part[s][e] in fp32, fixed order (deterministic); the reduction step
+// of the split-K weight-gradient GEMMs (models/linear.py:_weight_grad).  8 elements per lane.
+template <typename PT, typename OT>
+__global__ __launch_bounds__(256) void sum_partials_k(const PT* __restrict__ part, OT* __restrict__ out, long n8,
+                                                      int S, bool accumulate) {
+  const long n = n8 * 8;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n8; i += (long)gridDim.x * 256) {
+    float acc[8];
+    if (accumulate) {
+      const VecN<OT, 8> o = ldv<OT, 8>(out + i * 8);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] = to_f(o.v[j]);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+    }
+    for (int q = 0; q < S; ++q) {
+      const VecN<PT, 8> p = ldv<PT, 8>(part + q * n + i * 8);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += to_f(p.v[j]);
+    }
+    VecN<OT, 8> r;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r.v[j] = from_f<OT>(acc[j]);
+    stv<OT, 8>(out + i * 8, r);
+  }
+}
+
+void sum_partials_into(DType pdt, DType odt, const void* part, void* out, long n, int S, bool accumulate,
+                       hipStream_t s) {
+  const long n8 = n / 8;
+  BLLM_DISPATCH(pdt, PT, {
+    BLLM_DISPATCH(odt, OT, {
+      hipLaunchKernelGGL((sum_partials_k<PT, OT>), dim3(ew_grid(n8)), dim3(256), 0, s, (const PT*)part, (OT*)out,
+                         n8, S, accumulate);
+    });
+  });
+}
+
 }  // namespace bllm

@@ -313,3 +313,18 @@ def test_lora_model_uses_kernels_and_matches_gemm_path(monkeypatch):
     for k in ga:
         err = (ga[k] - gb[k]).abs().max().item()
         assert err <= 3e-2 * max(gb[k].abs().max().item(), 1e-3), (k, err)
+
+
+@pytest.mark.parametrize("gdt", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("accumulate", [False, True])
+def test_split_k_weight_grad(gdt, accumulate):
+    """Split-K dW (batched GEMM partials + sum_partials_ kernel) vs an fp32 matmul."""
+    from building_llm_from_scratch_amd.models.linear import _weight_grad, weight_grad_splits
+    N, out_f, in_f = 8192, 1280, 768
+    assert weight_grad_splits(N, out_f, in_f) > 1
+    dy = torch.randn(N, out_f, device=DEV).to(torch.bfloat16)
+    x = torch.randn(N, in_f, device=DEV).to(torch.bfloat16)
+    gW = torch.randn(out_f, in_f, device=DEV).to(gdt)
+    expect = dy.float().t() @ x.float() + (gW.float() if accumulate else 0)
+    _weight_grad(dy, x, gW, accumulate)
+    _close(gW, expect, torch.bfloat16, 2, name="split-K dW")
