@@ -94,6 +94,11 @@ def _weight_grad(dy: torch.Tensor, x: torch.Tensor, gW: torch.Tensor, accumulate
     if not gW.is_cuda:
         _mm_out(dy.t(), x, gW, accumulate)
         return
+    if ops.wgrad_gemm_enabled() and ops.wgrad_gemm_ok(dy, x, gW):
+        # token-major MFMA kernel (csrc/gemm_wgrad.hip): both operands consumed as stored,
+        # transposed by the LDS read; split-K chosen by ops.wgrad_splits
+        ops.wgrad_gemm_(dy, x, gW, accumulate)
+        return
     N = x.shape[0]
     S = weight_grad_splits(N, gW.shape[0], gW.shape[1]) \
         if gW.is_contiguous() and dy.is_contiguous() and x.is_contiguous() else 1

@@ -8,6 +8,7 @@ the reference attention math, which ``ops.attention_backend(dtype)`` reports.
 """
 from __future__ import annotations
 
+import os
 from typing import List, Optional
 
 import torch
@@ -21,6 +22,7 @@ __all__ = [
     "gelu_fwd", "gelu_bwd", "ce_fwd", "ce_bwd_", "embedding_fwd", "embedding_bwd",
     "sq_norm_multi", "adamw_step_", "attn_decode", "bias_grad_", "ext_available", "load_ext", "attention_backend",
     "lora_down", "lora_up_", "lora_wgrad", "lora_pack_t", "lora_kernel_ok", "sum_partials_",
+    "wgrad_gemm_", "wgrad_gemm_ok", "wgrad_gemm_enabled", "wgrad_gemm_preferred", "wgrad_splits",
 ]
 
 rope_tables = ref.rope_tables
@@ -128,6 +130,59 @@ def bias_grad_(dy, db, accumulate: bool = False):
     else:
         db.copy_(s)
     return db
+
+
+WGRAD_TILE, WGRAD_KGRAN = 256, 128
+
+
+def wgrad_gemm_enabled() -> bool:
+    """``BLLM_WGRAD_GEMM=0`` routes weight gradients back to hipBLASLt (A/B measurements)."""
+    return os.environ.get("BLLM_WGRAD_GEMM", "1") != "0"
+
+
+def wgrad_gemm_ok(a: torch.Tensor, b: torch.Tensor, c: torch.Tensor) -> bool:
+    """Shapes/layouts the token-major MFMA dW kernel (csrc/gemm_wgrad.hip) takes: a [K, M],
+    b [K, N], c [M, N] with M, N multiples of 256, K of 128, 16-B aligned unit-stride rows."""
+    if not (a.is_cuda and a.dtype in (torch.bfloat16, torch.float16) and b.dtype == a.dtype):
+        return False
+    K, M = a.shape
+    N = b.shape[1]
+    return (M % WGRAD_TILE == 0 and N % WGRAD_TILE == 0 and K % WGRAD_KGRAN == 0 and K >= WGRAD_KGRAN
+            and a.stride(1) == 1 and b.stride(1) == 1 and c.stride(1) == 1
+            and a.stride(0) % 8 == 0 and b.stride(0) % 8 == 0
+            and a.data_ptr() % 16 == 0 and b.data_ptr() % 16 == 0)
+
+
+def wgrad_splits(M: int, N: int, K: int, n_cu: int = 256) -> int:
+    """Split-K factor for the dW kernel: one 256x256 tile per CU at a time, so a GEMM with few
+    tiles (GPT-2: 25-100) or a ragged last wave leaves CUs idle.  Pick S minimising
+    compute / wave-utilisation + the fp32 partial round trip (S * M * N * 8 B through HBM)."""
+    tiles = (M // WGRAD_TILE) * (N // WGRAD_TILE)
+    best, best_t = 1, None
+    for S in range(1, 9):
+        if S > K // WGRAD_KGRAN or (S > 1 and K // S < 1024):
+            break
+        work = tiles * S
+        util = work / (n_cu * -(-work // n_cu))
+        t = 2.0 * M * N * K / (1.3e15 * util)
+        if S > 1:
+            t += (S * M * N * 8 + M * N * 4) / 4.5e12 + 6e-6
+        if best_t is None or t < best_t * 0.97:
+            best, best_t = S, t
+    return best
+
+
+def wgrad_gemm_(a, b, c, accumulate: bool = False, splits: Optional[int] = None):
+    """c (+)= a^T b with a [K, M], b [K, N] token-major (dW = dY^T X), fp32 accumulation."""
+    if _hip(a):
+        S = wgrad_splits(a.shape[1], b.shape[1], a.shape[0]) if splits is None else int(splits)
+        _k().wgrad_gemm_(a, b, c, bool(accumulate), S)
+        return c
+    r = a.float().t() @ b.float()
+    if accumulate:
+        r += c.float()
+    c.copy_(r)
+    return c
 
 
 def sum_partials_(part, out, accumulate: bool = False):

@@ -118,6 +118,12 @@ int lora_wgrad_splits(int blocks, int N);
 void lora_wgrad(DType dt, DType odt, const LoraWgradArgs& a, int N, int S, hipStream_t s);
 void lora_pack_t(DType dt, const LoraPackArgs& a, int K, int max_r, hipStream_t s);
 
+// gemm_wgrad.hip — C[M, N] (+)= A^T B with A [K, M], B [K, N] row-major (dW = dY^T X).
+// S > 1: split s writes fp32 partial C + s * c_split (accumulate must be false).
+bool wgrad_gemm_supported(int M, int N, int K, int S);
+void wgrad_gemm(DType dt, DType odt, const void* a, long lda, const void* b, long ldb, void* c, long ldc,
+                long c_split, int M, int N, int K, int S, bool accumulate, hipStream_t s);
+
 // optim.hip
 void adamw_step(DType pdt, DType gdt, void* param, float* master, const void* grad, float* m, float* v, long n,
                 float lr, float b1, float b2, float eps, float wd, int step, const float* gscale, hipStream_t s);

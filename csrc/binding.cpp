@@ -224,6 +224,37 @@ void sum_partials_(const Tensor& part, Tensor& out, bool accumulate) {
   bllm::sum_partials_into(dt_of(part), dt_of(out), part.data_ptr(), out.data_ptr(), n, (int)S, accumulate, stream());
 }
 
+// c (+)= a^T b on the token-major MFMA kernel: a [K, M], b [K, N], c [M, N], unit column
+// strides, 16-B aligned rows; splits > 1 reduce K ranges into fp32 partials summed in order
+void wgrad_gemm_(const Tensor& a, const Tensor& b, Tensor& c, bool accumulate, int64_t splits) {
+  TORCH_CHECK(a.is_cuda() && b.is_cuda() && c.is_cuda(), "wgrad_gemm: GPU tensors");
+  c10::DeviceGuard g(a.device());
+  TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && c.dim() == 2, "wgrad_gemm: 2-D operands");
+  const int64_t K = a.size(0), M = a.size(1), N = b.size(1);
+  TORCH_CHECK(b.size(0) == K && c.size(0) == M && c.size(1) == N, "wgrad_gemm: shapes");
+  TORCH_CHECK(a.scalar_type() == b.scalar_type() &&
+                  (a.scalar_type() == at::kBFloat16 || a.scalar_type() == at::kHalf), "wgrad_gemm: bf16/fp16 operands");
+  TORCH_CHECK(a.stride(1) == 1 && b.stride(1) == 1 && c.stride(1) == 1, "wgrad_gemm: unit column strides");
+  TORCH_CHECK(a.stride(0) % 8 == 0 && b.stride(0) % 8 == 0, "wgrad_gemm: rows must be 16-B aligned");
+  TORCH_CHECK((reinterpret_cast<uintptr_t>(a.data_ptr()) | reinterpret_cast<uintptr_t>(b.data_ptr())) % 16 == 0,
+              "wgrad_gemm: operands must be 16-B aligned");
+  TORCH_CHECK(a.stride(0) < (int64_t(1) << 26) && b.stride(0) < (int64_t(1) << 26), "wgrad_gemm: row stride too large");
+  TORCH_CHECK(K < (int64_t(1) << 31) && M < (int64_t(1) << 31) && N < (int64_t(1) << 31));
+  TORCH_CHECK(bllm::wgrad_gemm_supported((int)M, (int)N, (int)K, (int)splits), "wgrad_gemm: unsupported shape ",
+              K, "x", M, "x", N, " splits ", splits);
+  if (splits == 1) {
+    bllm::wgrad_gemm(dt_of(a), dt_of(c), a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0), c.data_ptr(),
+                     c.stride(0), 0, (int)M, (int)N, (int)K, 1, accumulate, stream());
+    return;
+  }
+  TORCH_CHECK(c.is_contiguous(), "wgrad_gemm: split-K output must be contiguous");
+  auto part = at::empty({splits, M, N}, a.options().dtype(at::kFloat));
+  bllm::wgrad_gemm(dt_of(a), DType::F32, a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0), part.data_ptr(), N,
+                   M * N, (int)M, (int)N, (int)K, (int)splits, false, stream());
+  bllm::sum_partials_into(DType::F32, dt_of(c), part.data_ptr(), c.data_ptr(), M * N, (int)splits, accumulate,
+                          stream());
+}
+
 // q [B, H, hd]; kc / vc [B, G, Tmax, hd] with the first L positions valid -> out [B, H*hd]
 Tensor attn_decode(const Tensor& q, const Tensor& kc, const Tensor& vc, int64_t L) {
   check_gpu(q, "q"); check_gpu(kc, "kcache"); check_gpu(vc, "vcache");
@@ -546,6 +577,7 @@ TORCH_LIBRARY(bllm, m) {
   m.def("rope_(Tensor(a!) qkv, Tensor cos, Tensor sin, int T, int H, int G, int hd, bool inverse, int pos_offset) -> ()");
   m.def("bias_grad_(Tensor dy, Tensor(a!) db, bool accumulate) -> ()");
   m.def("sum_partials_(Tensor part, Tensor(a!) out, bool accumulate) -> ()");
+  m.def("wgrad_gemm_(Tensor a, Tensor b, Tensor(a!) c, bool accumulate, int splits) -> ()");
   m.def("attn_decode(Tensor q, Tensor kcache, Tensor vcache, int L) -> Tensor");
   m.def("flash_attn_fwd(Tensor qkv, int B, int T, int H, int G, int hd, bool causal, float p, int seed, int offset) -> (Tensor, Tensor)");
   m.def("flash_attn_bwd(Tensor qkv, Tensor o, Tensor lse, Tensor dout, int B, int T, int H, int G, int hd, bool causal, float p, int seed, int offset) -> Tensor");
@@ -576,6 +608,7 @@ TORCH_LIBRARY_IMPL(bllm, CUDA, m) {
   m.impl("flash_attn_fwd", &flash_attn_fwd);
   m.impl("attn_decode", &attn_decode);
   m.impl("sum_partials_", &sum_partials_);
+  m.impl("wgrad_gemm_", &wgrad_gemm_);
   m.impl("bias_grad_", &bias_grad_);
   m.impl("flash_attn_bwd", &flash_attn_bwd);
   m.impl("ce_fwd", &ce_fwd);

@@ -328,3 +328,33 @@ def test_split_k_weight_grad(gdt, accumulate):
     expect = dy.float().t() @ x.float() + (gW.float() if accumulate else 0)
     _weight_grad(dy, x, gW, accumulate)
     _close(gW, expect, torch.bfloat16, 2, name="split-K dW")
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("odt", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("K,M,N,S", [(128, 256, 256, 1), (384, 512, 768, 1), (2048, 768, 512, 3), (1024, 256, 1024, 2)])
+@pytest.mark.parametrize("accumulate", [False, True])
+def test_wgrad_gemm(dt, odt, K, M, N, S, accumulate):
+    """Token-major MFMA dW kernel c (+)= a^T b (strided a, split-K) vs an fp32 matmul."""
+    a_full = torch.randn(K, M + 64, device=DEV).to(dt)
+    a = a_full[:, 32:32 + M]                      # lda = M + 64, 64-B offset
+    b = torch.randn(K, N, device=DEV).to(dt)
+    c = torch.randn(M, N, device=DEV).to(odt)
+    assert ops.wgrad_gemm_ok(a, b, c)
+    expect = a.float().t() @ b.float() + (c.float() if accumulate else 0)
+    ops.wgrad_gemm_(a, b, c, accumulate, S)
+    err = (c.float() - expect).abs().max().item()
+    mag = expect.abs().max().item()
+    assert err <= (8e-3 if odt == torch.bfloat16 else 1e-4) * mag, (err, mag)
+
+
+def test_wgrad_gemm_in_weight_grad_path():
+    """_weight_grad routes eligible dW through the MFMA kernel; result == hipBLASLt path."""
+    from building_llm_from_scratch_amd.models.linear import _weight_grad
+    N, out_f, in_f = 4096, 1536, 1024
+    dy = torch.randn(N, out_f, device=DEV).to(torch.bfloat16)
+    x = torch.randn(N, in_f, device=DEV).to(torch.bfloat16)
+    g1 = torch.empty(out_f, in_f, device=DEV, dtype=torch.bfloat16)
+    _weight_grad(dy, x, g1, False)
+    g0 = (x.float().t() @ dy.float()).t()
+    _close(g1, g0, torch.bfloat16, 1, name="dW")
