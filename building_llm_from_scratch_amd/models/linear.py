@@ -94,7 +94,8 @@ def _weight_grad(dy: torch.Tensor, x: torch.Tensor, gW: torch.Tensor, accumulate
     if not gW.is_cuda:
         _mm_out(dy.t(), x, gW, accumulate)
         return
-    if ops.wgrad_gemm_enabled() and ops.wgrad_gemm_ok(dy, x, gW):
+    if ops.wgrad_gemm_enabled() and ops.wgrad_gemm_ok(dy, x, gW) \
+            and ops.wgrad_gemm_preferred(gW.shape[0], gW.shape[1]):
         # token-major MFMA kernel (csrc/gemm_wgrad.hip): both operands consumed as stored,
         # transposed by the LDS read; split-K chosen by ops.wgrad_splits
         ops.wgrad_gemm_(dy, x, gW, accumulate)

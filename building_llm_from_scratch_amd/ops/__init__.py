@@ -153,6 +153,19 @@ def wgrad_gemm_ok(a: torch.Tensor, b: torch.Tensor, c: torch.Tensor) -> bool:
             and a.data_ptr() % 16 == 0 and b.data_ptr() % 16 == 0)
 
 
+WGRAD_MAX_TILES = 4096
+
+
+def wgrad_gemm_preferred(M: int, N: int) -> bool:
+    """Whether the MFMA dW kernel beats hipBLASLt for an [M, N] weight gradient.  Measured on
+    MI355X at 16k tokens, interleaved in one process (tools/bench_wgrad.py,
+    profiles/r1_wgrad_kernel.md): 1.28-1.40 PF on the Llama-3-8B projections (1.09-1.30x
+    hipBLASLt), 1.05-1.40 PF on Llama-3.2-1B (1.07-1.32x) and 0.82-1.12 PF with split-K on GPT-2
+    (1.9-2.2x); hipBLASLt stays 2 % ahead only on the 128k-vocab LM head (8016 output tiles),
+    which therefore stays on it."""
+    return (M // WGRAD_TILE) * (N // WGRAD_TILE) <= WGRAD_MAX_TILES
+
+
 def wgrad_splits(M: int, N: int, K: int, n_cu: int = 256) -> int:
     """Split-K factor for the dW kernel: one 256x256 tile per CU at a time, so a GEMM with few
     tiles (GPT-2: 25-100) or a ragged last wave leaves CUs idle.  Pick S minimising

@@ -10,11 +10,11 @@
 // staged exactly as they sit in memory and the transpose is done by the LDS read instead of a
 // copy:
 //
-//  * tile 256 x 256 per workgroup (8 waves = 2 (M) x 4 (N), 128 x 64 outputs per wave,
-//    acc[8][4] of 16x16 fp32 fragments), one 32-deep k-step per LDS ring slot;
+//  * tile 256 x 256 per workgroup, 8 waves = 2 (M) x 4 (N), 128 x 64 outputs per wave
+//    (acc[8][4]), two waves per SIMD; one 32-deep k-step per LDS ring slot;
 //  * a ring of 4 slots (A [32 k][256 m] + B [32 k][256 n] images, 16 KiB each, 128 KiB total)
-//    filled by LDS-DMA (global_load_lds_dwordx4, 4 per lane per slot) 3 slots ahead of the
-//    MFMAs; one raw s_barrier per slot, counted vmcnt (never drained to 0 inside the loop);
+//    filled by LDS-DMA (global_load_lds_dwordx4) 3 slots ahead of the MFMAs; one raw s_barrier
+//    per slot, counted vmcnt (never drained to 0 inside the loop);
 //  * fragments are read with ds_read_b64_tr_b16 (a 16-lane group gets 4 k-rows x 16 columns
 //    delivered column-major = 4 k-values of one m/n column per lane); two reads give the 8
 //    k-values of a 16x16x32 A or B fragment;
@@ -24,11 +24,22 @@
 //    lane-linearly, so the permutation is applied to the per-lane GLOBAL source address (a
 //    permutation of 16-B chunks inside one 512-B row: the loads stay fully coalesced);
 //  * blockIdx.x -> tile: XCD-aware (each XCD gets a contiguous range of tiles, bijective for
-//    any count), grouped 8 tile-rows deep so the 32 tiles an XCD runs at once share 8 A and 4 B
+//    any count), grouped 8 tile-rows deep so the tiles an XCD runs at once share A and B
 //    panels in its L2;
 //  * blockIdx.y = split-K index (few-tile GEMMs): split s reduces its own 128-aligned token
 //    range into fp32 partial s of C (c_split elements apart), summed afterwards in a fixed
 //    order — deterministic either way (each output element has one owner per split).
+//
+//  * epilogue staged through LDS: the 256 x 256 fp32 tile is written into the (then idle) LDS
+//    ring in two 128-row passes and leaves as 16-B row-contiguous global stores (and 16-B loads
+//    when accumulating) instead of 128 scattered 2-/4-byte stores per lane.
+//
+// Variants (BLLM_WGRAD_VARIANT, read per launch so one process can A/B them):
+//   0  fragments read after each barrier
+//   1  next slot's fragments read under the current slot's MFMAs (default)
+// Measured and dropped (tools/bench_wgrad.py, profiles/r1_wgrad_kernel.md): 4 waves of 128 x 128
+// (one wave per SIMD) -25 %; LDS-DMA pieces interleaved between MFMA groups instead of one burst
+// after the barrier -5 %.
 #include <stdlib.h>
 
 #include <type_traits>
@@ -66,8 +77,18 @@ constexpr int ROWB = 512;                   // bytes of one k-row of a 256-wide 
 constexpr int SLOTB = BK * ROWB;            // 16 KiB
 constexpr int B_BASE = NSLOT * SLOTB;       // A slots [0, 64 KiB), B slots [64, 128 KiB)
 constexpr int LDS_BYTES = 2 * NSLOT * SLOTB;
-constexpr int THREADS = 512;
 constexpr int GROUP_M = 8;
+
+// wave layout / schedule per variant
+template <int VAR> struct Geo {
+  static constexpr int NW = 8;                         // waves per workgroup
+  static constexpr int THREADS = NW * 64;
+  static constexpr int WAVES_N = 4;                    // waves along N (2 along M)
+  static constexpr int FN = BN / WAVES_N / 16;         // 16-wide n fragments per wave
+  static constexpr int DJ = (SLOTB / 1024) / NW;       // LDS-DMA pieces per operand per slot per wave
+  static constexpr int PER_STAGE = 2 * DJ;             // vmcnt units one staged slot adds
+  static constexpr bool PREFETCH = VAR >= 1;           // next slot's fragments under this slot's MFMAs
+};
 
 __device__ __forceinline__ int swz(int r) { return 2 * ((r & 3) | (((r >> 3) & 1) << 2)); }
 
@@ -80,9 +101,12 @@ __device__ __forceinline__ s16x8 frag(const char* p) {
 template <int N> __device__ __forceinline__ void vm_wait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
 
 template <typename T, typename OT, int VAR>
-__global__ __launch_bounds__(THREADS) void wgrad_gemm_k(const T* __restrict__ A, long lda, const T* __restrict__ B,
-                                                        long ldb, OT* __restrict__ C, long ldc, long c_split, int M,
-                                                        int N, int K, int accumulate) {
+__global__ __launch_bounds__(Geo<VAR>::THREADS) void wgrad_gemm_k(const T* __restrict__ A, long lda,
+                                                                  const T* __restrict__ B, long ldb,
+                                                                  OT* __restrict__ C, long ldc, long c_split,
+                                                                  int M, int N, int K, int accumulate, int wide) {
+  using G = Geo<VAR>;
+  constexpr int FN = G::FN, DJ = G::DJ, PS = G::PER_STAGE;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
 
@@ -103,60 +127,64 @@ __global__ __launch_bounds__(THREADS) void wgrad_gemm_k(const T* __restrict__ A,
   const int c_lo = (int)((long)nch * sp / S), c_hi = (int)((long)nch * (sp + 1) / S);
   const int nk = (c_hi - c_lo) * NSLOT;  // >= NSLOT (host: S <= K / KCH)
 
-  // ---- staging: lane-linear LDS rows, XOR-permuted global chunks (loop-invariant offsets)
-  uint32_t voffA[2], voffB[2];
+  // ---- staging: lane-linear LDS rows, XOR-permuted global chunks (loop-invariant offsets);
+  //      one piece (wave-instruction) moves 2 k-rows (1 KiB) of one operand
+  uint32_t voffA[DJ], voffB[DJ];
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int r = (wave * 2 + j) * 2 + (lane >> 5), c = (lane & 31) ^ swz(r);
+  for (int j = 0; j < DJ; ++j) {
+    const int r = (wave * DJ + j) * 2 + (lane >> 5), c = (lane & 31) ^ swz(r);
     voffA[j] = (uint32_t)((r * lda + 8 * c) * (long)sizeof(T));
     voffB[j] = (uint32_t)((r * ldb + 8 * c) * (long)sizeof(T));
   }
   const uint32_t lds0 = lds_u32(smem);
   const T* Abase = A + (long)c_lo * KCH * lda + m0;
   const T* Bbase = B + (long)c_lo * KCH * ldb + n0;
+  // piece q of a stage: q even = A piece q/2, q odd = B piece q/2 (issue order A0 B0 A1 B1 ..)
+  auto piece = [&](const void* a, const void* b, int q, int slot) {
+    const int j = q >> 1;
+    if (q & 1) glds16s(b, voffB[j], lds0 + B_BASE + slot * SLOTB + (wave * DJ + j) * 1024);
+    else glds16s(a, voffA[j], lds0 + slot * SLOTB + (wave * DJ + j) * 1024);
+  };
   auto stage = [&](int kt, int slot) {
     const void* a = sgpr_ptr(Abase + (long)kt * BK * lda);
     const void* b = sgpr_ptr(Bbase + (long)kt * BK * ldb);
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      glds16s(a, voffA[j], lds0 + slot * SLOTB + (wave * 2 + j) * 1024);
-      glds16s(b, voffB[j], lds0 + B_BASE + slot * SLOTB + (wave * 2 + j) * 1024);
-    }
+    for (int q = 0; q < PS; ++q) piece(a, b, q, slot);
   };
 
   // ---- fragment read offsets: lane (g, q, p) reads k-row 8g + q (+4), columns 4p..4p+3
   const int g = lane >> 4, qq = (lane & 15) >> 2, p = lane & 3;
   const int f = 2 * (qq | ((g & 1) << 2));  // == swz(8g + qq + 4h) for h = 0, 1
-  const int wm = wave >> 2, wn = wave & 3;
+  const int wm = wave / G::WAVES_N, wn = wave % G::WAVES_N;
   const int rowb = (8 * g + qq) * ROWB + (p & 1) * 8 + (p >> 1) * 16;
-  int aoff[8], boff[4];
+  int aoff[8], boff[FN];
 #pragma unroll
   for (int i = 0; i < 8; ++i) aoff[i] = rowb + (wm * 16 + ((2 * i) ^ f)) * 16;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) boff[j] = B_BASE + rowb + ((wn * 8 + 2 * j) ^ f) * 16;
+  for (int j = 0; j < FN; ++j) boff[j] = B_BASE + rowb + ((wn * 2 * FN + 2 * j) ^ f) * 16;
 
-  f32x4 acc[8][4];
+  f32x4 acc[8][FN];
 #pragma unroll
   for (int i = 0; i < 8; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  if constexpr (VAR == 1) {
+  if constexpr (G::PREFETCH) {
     // Fragments of slot kt+1 are read into the second register set WHILE slot kt's MFMAs
     // run, so no wave waits on LDS latency after a barrier: the MFMA pipe stays fed across it.
     // Ring: DMA of k-slot kt+4 refills LDS slot kt as soon as every wave holds slot kt in VGPRs.
-    struct Frags { s16x8 a[8], b[4]; };
+    struct Frags { s16x8 a[8], b[FN]; };
     auto load = [&](Frags& F, int slot) {
       const char* base = smem + slot * SLOTB;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) F.b[j] = frag(base + boff[j]);
+      for (int j = 0; j < FN; ++j) F.b[j] = frag(base + boff[j]);
 #pragma unroll
       for (int i = 0; i < 8; ++i) F.a[i] = frag(base + aoff[i]);
     };
     // G.b first, then G.a[i] just before F.a[i]'s MFMAs: F.a[i] dies as G.a[i] arrives, so the
-    // two sets cost 8 B-fragments + 9 A-fragments of VGPRs, not 2 x 12.  The loop body is
-    // branch-free (the final trip is peeled) so hipcc's lgkmcnt counting stays exact.
-    auto it = [&](auto wait_n, auto do_stage, auto last, int kt, Frags& F, Frags& G) {
+    // two sets cost 2 x FN B-fragments + 9 A-fragments of VGPRs, not 2 x (8 + FN).  The loop
+    // body is branch-free (the final trip is peeled) so hipcc's lgkmcnt counting stays exact.
+    auto it = [&](auto wait_n, auto do_stage, auto last, int kt, Frags& F, Frags& Gn) {
       constexpr int WAITN = decltype(wait_n)::value;
       constexpr bool STAGE = decltype(do_stage)::value, LAST = decltype(last)::value;
       const char* nxt = smem + ((kt + 1) & (NSLOT - 1)) * SLOTB;
@@ -167,19 +195,19 @@ __global__ __launch_bounds__(THREADS) void wgrad_gemm_k(const T* __restrict__ A,
         asm volatile("" ::: "memory");
         if constexpr (STAGE) stage(kt + 4, kt & (NSLOT - 1));
 #pragma unroll
-        for (int j = 0; j < 4; ++j) G.b[j] = frag(nxt + boff[j]);
+        for (int j = 0; j < FN; ++j) Gn.b[j] = frag(nxt + boff[j]);
       }
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
-        if constexpr (!LAST) G.a[i] = frag(nxt + aoff[i]);
+        if constexpr (!LAST) Gn.a[i] = frag(nxt + aoff[i]);
         __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = Mfma<T>::run(F.a[i], F.b[j], acc[i][j]);
+        for (int j = 0; j < FN; ++j) acc[i][j] = Mfma<T>::run(F.a[i], F.b[j], acc[i][j]);
         __builtin_amdgcn_s_setprio(0);
       }
     };
-    using W8 = std::integral_constant<int, 8>;
-    using W4 = std::integral_constant<int, 4>;
+    using W2 = std::integral_constant<int, 2 * PS>;  // 2 slots still in flight behind kt+1
+    using W1 = std::integral_constant<int, PS>;
     using W0 = std::integral_constant<int, 0>;
     using Y = std::true_type;
     using Nn = std::false_type;
@@ -187,20 +215,20 @@ __global__ __launch_bounds__(THREADS) void wgrad_gemm_k(const T* __restrict__ A,
     stage(1, 1);
     stage(2, 2);
     stage(3, 3);
-    vm_wait<12>();
+    vm_wait<3 * PS>();
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     Frags F0, F1;
     load(F0, 0);
     int kt = 0;
     for (; kt < nk - NSLOT; kt += NSLOT) {
-      it(W8{}, Y{}, Nn{}, kt + 0, F0, F1);
-      it(W8{}, Y{}, Nn{}, kt + 1, F1, F0);
-      it(W8{}, Y{}, Nn{}, kt + 2, F0, F1);
-      it(W8{}, Y{}, Nn{}, kt + 3, F1, F0);
+      it(W2{}, Y{}, Nn{}, kt + 0, F0, F1);
+      it(W2{}, Y{}, Nn{}, kt + 1, F1, F0);
+      it(W2{}, Y{}, Nn{}, kt + 2, F0, F1);
+      it(W2{}, Y{}, Nn{}, kt + 3, F1, F0);
     }
-    it(W8{}, Nn{}, Nn{}, kt + 0, F0, F1);
-    it(W4{}, Nn{}, Nn{}, kt + 1, F1, F0);
+    it(W2{}, Nn{}, Nn{}, kt + 0, F0, F1);
+    it(W1{}, Nn{}, Nn{}, kt + 1, F1, F0);
     it(W0{}, Nn{}, Nn{}, kt + 2, F0, F1);
     it(W0{}, Nn{}, Y{}, kt + 3, F1, F0);
   } else {
@@ -210,23 +238,23 @@ __global__ __launch_bounds__(THREADS) void wgrad_gemm_k(const T* __restrict__ A,
 
   auto step = [&](int kt, int slot) {
     const int rem = nk - 1 - kt;  // slots still in flight behind this one
-    if (rem >= 2) vm_wait<8>();
-    else if (rem == 1) vm_wait<4>();
+    if (rem >= 2) vm_wait<2 * PS>();
+    else if (rem == 1) vm_wait<PS>();
     else vm_wait<0>();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of slot kt-1 are done
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");  // no LDS read of slot kt is hoisted above the barrier
     if (kt + 3 < nk) stage(kt + 3, (slot + 3) & (NSLOT - 1));
     const char* base = smem + slot * SLOTB;
-    s16x8 bf[4];
+    s16x8 bf[FN];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) bf[j] = frag(base + boff[j]);
+    for (int j = 0; j < FN; ++j) bf[j] = frag(base + boff[j]);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const s16x8 af = frag(base + aoff[i]);
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = Mfma<T>::run(af, bf[j], acc[i][j]);
+      for (int j = 0; j < FN; ++j) acc[i][j] = Mfma<T>::run(af, bf[j], acc[i][j]);
       __builtin_amdgcn_s_setprio(0);
     }
   };
@@ -240,17 +268,87 @@ __global__ __launch_bounds__(THREADS) void wgrad_gemm_k(const T* __restrict__ A,
   }
 
   // ---- epilogue: lane holds C[16i + 4(l>>4) + e][16j + (l&15)] of the wave's 128 x 64 block
-  OT* c = C + sp * c_split + (m0 + wm * 128 + 4 * (lane >> 4)) * ldc + n0 + wn * 64 + (lane & 15);
+  OT* cbase = C + sp * c_split + m0 * ldc + n0;
+  if (wide) {
+    // Through LDS: fp32 rows of 1 KiB (16-B chunk index XOR (row & 7): the two rows a 32-lane
+    // half writes land on disjoint banks), pass p = the 128 rows of the waves with wm == p; then
+    // every thread moves whole 16-B global chunks (4 fp32 or 8 bf16/fp16 elements).
+    constexpr int RB = BN * 4;
+    constexpr int EPT = 16 / (int)sizeof(OT);  // elements per 16-B global access
+    constexpr int NCH = EPT / 4;               // fp32 LDS chunks per access
+    constexpr int IPR = BN / EPT;              // accesses per row
+    constexpr int TRIPS = 128 * IPR / G::THREADS;
+    struct alignas(16) V16 { OT e[EPT]; };
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // every LDS read of the ring is done
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+    for (int pass = 0; pass < 2; ++pass) {
+      if (wm == pass) {
 #pragma unroll
-    for (int e = 0; e < 4; ++e)
+        for (int i = 0; i < 8; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        OT* o = c + (long)(16 * i + e) * ldc + 16 * j;
-        const float v = acc[i][j][e];
-        *o = from_f<OT>(accumulate ? to_f(*o) + v : v);
+          for (int e = 0; e < 4; ++e)
+#pragma unroll
+            for (int j = 0; j < FN; ++j) {
+              const int lr = 16 * i + 4 * (lane >> 4) + e, col = wn * 16 * FN + 16 * j + (lane & 15);
+              *(float*)(smem + lr * RB + ((((col >> 2) ^ (lr & 7)) << 4) | ((col & 3) << 2))) = acc[i][j][e];
+            }
       }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int t = 0; t < TRIPS; ++t) {
+        const int q = (int)threadIdx.x + t * G::THREADS;
+        const int lr = q / IPR, it = q % IPR;
+        float v[EPT];
+#pragma unroll
+        for (int h = 0; h < NCH; ++h) {
+          const f32x4 x = *(const f32x4*)(smem + lr * RB + (((it * NCH + h) ^ (lr & 7)) << 4));
+#pragma unroll
+          for (int k = 0; k < 4; ++k) v[4 * h + k] = x[k];
+        }
+        V16* o = (V16*)(cbase + (long)(pass * 128 + lr) * ldc + it * EPT);
+        if (accumulate) {
+          const V16 old = *o;
+#pragma unroll
+          for (int k = 0; k < EPT; ++k) v[k] += to_f(old.e[k]);
+        }
+        V16 w;
+#pragma unroll
+        for (int k = 0; k < EPT; ++k) w.e[k] = from_f<OT>(v[k]);
+        *o = w;
+      }
+      if (pass == 0) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // pass-0 reads done before pass 1 writes
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+      }
+    }
+    return;
+  }
+  // (unaligned output: element stores; the accumulate test is hoisted out of the element loops —
+  //  a per-element select makes hipcc branch around every load and wait for each separately)
+  OT* c = cbase + (wm * 128 + 4 * (lane >> 4)) * ldc + wn * 16 * FN + (lane & 15);
+  if (accumulate) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          OT* o = c + (long)(16 * i + e) * ldc + 16 * j;
+          *o = from_f<OT>(to_f(*o) + acc[i][j][e]);
+        }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) c[(long)(16 * i + e) * ldc + 16 * j] = from_f<OT>(acc[i][j][e]);
+  }
 }
 
 template <typename T, typename OT, int VAR>
@@ -260,18 +358,17 @@ void launch_v(const void* a, long lda, const void* b, long ldb, void* c, long ld
                                                hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES) == hipSuccess;
   (void)attr;
   const dim3 grid((M / BM) * (N / BN), S);
-  hipLaunchKernelGGL((wgrad_gemm_k<T, OT, VAR>), grid, dim3(THREADS), LDS_BYTES, s, (const T*)a, lda, (const T*)b,
-                     ldb, (OT*)c, ldc, c_split, M, N, K, (int)accumulate);
+  const bool wide = reinterpret_cast<uintptr_t>(c) % 16 == 0 && (ldc * (long)sizeof(OT)) % 16 == 0 &&
+                    (c_split * (long)sizeof(OT)) % 16 == 0;
+  hipLaunchKernelGGL((wgrad_gemm_k<T, OT, VAR>), grid, dim3(Geo<VAR>::THREADS), LDS_BYTES, s, (const T*)a, lda,
+                     (const T*)b, ldb, (OT*)c, ldc, c_split, M, N, K, (int)accumulate, (int)wide);
 }
 
-// BLLM_WGRAD_VARIANT: 0 = fragments read after each barrier, 1 = next slot's fragments read
-// under the current slot's MFMAs (two register sets)
+constexpr int DEFAULT_VARIANT = 1;
+
 int variant() {
-  static const int v = [] {
-    const char* e = getenv("BLLM_WGRAD_VARIANT");
-    return e ? atoi(e) : 1;
-  }();
-  return v;
+  const char* e = getenv("BLLM_WGRAD_VARIANT");  // per launch (A/B in one process); ~100 ns
+  return e && *e ? atoi(e) : DEFAULT_VARIANT;
 }
 
 template <typename T, typename OT>

@@ -334,8 +334,11 @@ def test_split_k_weight_grad(gdt, accumulate):
 @pytest.mark.parametrize("odt", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("K,M,N,S", [(128, 256, 256, 1), (384, 512, 768, 1), (2048, 768, 512, 3), (1024, 256, 1024, 2)])
 @pytest.mark.parametrize("accumulate", [False, True])
-def test_wgrad_gemm(dt, odt, K, M, N, S, accumulate):
-    """Token-major MFMA dW kernel c (+)= a^T b (strided a, split-K) vs an fp32 matmul."""
+@pytest.mark.parametrize("variant", ["0", "1"])
+def test_wgrad_gemm(dt, odt, K, M, N, S, accumulate, variant, monkeypatch):
+    """Token-major MFMA dW kernel c (+)= a^T b (strided a, split-K) vs an fp32 matmul, every
+    schedule variant (BLLM_WGRAD_VARIANT is read per launch)."""
+    monkeypatch.setenv("BLLM_WGRAD_VARIANT", variant)
     a_full = torch.randn(K, M + 64, device=DEV).to(dt)
     a = a_full[:, 32:32 + M]                      # lda = M + 64, 64-B offset
     b = torch.randn(K, N, device=DEV).to(dt)
@@ -358,3 +361,20 @@ def test_wgrad_gemm_in_weight_grad_path():
     _weight_grad(dy, x, g1, False)
     g0 = (x.float().t() @ dy.float()).t()
     _close(g1, g0, torch.bfloat16, 1, name="dW")
+
+
+@pytest.mark.parametrize("accumulate", [False, True])
+def test_wgrad_gemm_unaligned_output(accumulate):
+    """An output view that is not 16-B aligned takes the element-store epilogue."""
+    K, M, N = 256, 256, 512
+    a = torch.randn(K, M, device=DEV).to(torch.bfloat16)
+    b = torch.randn(K, N, device=DEV).to(torch.bfloat16)
+    c_full = torch.randn(M, N + 8, device=DEV).to(torch.bfloat16)
+    c = c_full[:, 1:1 + N]                         # 2-B offset, row stride N + 8
+    assert c.data_ptr() % 16 != 0 and ops.wgrad_gemm_ok(a, b, c)
+    before = c_full.clone()
+    expect = a.float().t() @ b.float() + (c.float() if accumulate else 0)
+    ops.wgrad_gemm_(a, b, c, accumulate, 1)
+    err = (c.float() - expect).abs().max().item()
+    assert err <= 8e-3 * expect.abs().max().item(), err
+    assert torch.equal(c_full[:, 0], before[:, 0]) and torch.equal(c_full[:, 1 + N:], before[:, 1 + N:])
