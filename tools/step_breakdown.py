@@ -10,6 +10,10 @@ import sqlite3
 def classify(n):
     if n.startswith(("Cijk", "Custom_Cijk")):
         return "gemm (hipBLASLt)"
+    if "wgrad_gemm_k" in n:
+        return "wgrad_mfma (dW GEMM, csrc/gemm_wgrad.hip)"
+    if "sum_partials" in n:
+        return "sum_partials (split-K)"
     for k in ("adamw", "sqsum", "attn_bwd_mfma", "attn_bwd_dq", "attn_fwd", "attn_delta", "kv_reduce", "swiglu_fwd",
               "swiglu_bwd", "gelu", "rope", "norm_fwd", "norm_bwd", "col_reduce", "ce_fwd", "ce_bwd", "emb_",
               "copyBuffer", "dropout"):
@@ -25,6 +29,13 @@ def main():
     a = ap.parse_args()
     db = sqlite3.connect(a.db)
     rows = db.execute("select name,start,end from kernels order by start").fetchall()
+    # rocpd may truncate or demangle kernel names differently per table: prefer the full symbol
+    try:
+        full = dict(db.execute("select id,kernel_name from rocpd_info_kernel_symbol").fetchall())
+        ids = db.execute("select kernel_id from kernels order by start").fetchall()
+        rows = [(full.get(k[0], r[0]) or r[0], r[1], r[2]) for r, k in zip(rows, ids)]
+    except sqlite3.Error:
+        pass
     idx = [i for i, r in enumerate(rows) if a.marker in r[0]]
     seq = rows[idx[-1]:]
     span = (seq[-1][2] - seq[0][1]) / 1e6
