@@ -153,16 +153,16 @@ def wgrad_gemm_ok(a: torch.Tensor, b: torch.Tensor, c: torch.Tensor) -> bool:
             and a.data_ptr() % 16 == 0 and b.data_ptr() % 16 == 0)
 
 
-WGRAD_MAX_TILES = 4096
+WGRAD_MAX_TILES = 1 << 30
 
 
 def wgrad_gemm_preferred(M: int, N: int) -> bool:
     """Whether the MFMA dW kernel beats hipBLASLt for an [M, N] weight gradient.  Measured on
     MI355X at 16k tokens, interleaved in one process (tools/bench_wgrad.py,
-    profiles/r1_wgrad_kernel.md): 1.28-1.40 PF on the Llama-3-8B projections (1.09-1.30x
-    hipBLASLt), 1.05-1.40 PF on Llama-3.2-1B (1.07-1.32x) and 0.82-1.12 PF with split-K on GPT-2
-    (1.9-2.2x); hipBLASLt stays 2 % ahead only on the 128k-vocab LM head (8016 output tiles),
-    which therefore stays on it."""
+    profiles/r1_wgrad_kernel.md), default schedule: 1.28-1.40 PF on the Llama-3-8B projections
+    and 1.34 PF on the 128k-vocab LM head (1.09-1.33x hipBLASLt), 1.06-1.42 PF on Llama-3.2-1B
+    (1.15-1.44x) and 0.85-1.16 PF with split-K on GPT-2 (1.9-2.3x) — every measured shape, so the
+    cap only exists as a knob for future shapes."""
     return (M // WGRAD_TILE) * (N // WGRAD_TILE) <= WGRAD_MAX_TILES
 
 

@@ -36,7 +36,9 @@
 //
 // Variants (BLLM_WGRAD_VARIANT, read per launch so one process can A/B them):
 //   0  fragments read after each barrier
-//   1  next slot's fragments read under the current slot's MFMAs (default)
+//   1  next slot's fragments read under the current slot's MFMAs
+//   2  as 1, LDS-DMA issued by waves 0-3 only (see Geo::LOADERS) — default: 1.02-1.13x variant 1
+//      (Llama-3-8B gate/up 1.33 -> 1.40 PF, LM head 1.18 -> 1.34 PF)
 // Measured and dropped (tools/bench_wgrad.py, profiles/r1_wgrad_kernel.md): 4 waves of 128 x 128
 // (one wave per SIMD) -25 %; LDS-DMA pieces interleaved between MFMA groups instead of one burst
 // after the barrier -5 %.
@@ -85,8 +87,12 @@ template <int VAR> struct Geo {
   static constexpr int THREADS = NW * 64;
   static constexpr int WAVES_N = 4;                    // waves along N (2 along M)
   static constexpr int FN = BN / WAVES_N / 16;         // 16-wide n fragments per wave
-  static constexpr int DJ = (SLOTB / 1024) / NW;       // LDS-DMA pieces per operand per slot per wave
-  static constexpr int PER_STAGE = 2 * DJ;             // vmcnt units one staged slot adds
+  // Variant 2: only waves 0-3 (one per SIMD) issue the slot's LDS-DMA, so each SIMD's other
+  // wave (4-7) goes straight from the barrier to its MFMAs and keeps the matrix pipe busy while
+  // its partner spends ~60 issue cycles per piece; variants 0/1 split the pieces over all 8.
+  static constexpr int LOADERS = VAR == 2 ? 4 : 8;
+  static constexpr int DJ = (SLOTB / 1024) / LOADERS;  // LDS-DMA pieces per operand per slot per loader
+  static constexpr int PER_STAGE = 2 * DJ;             // vmcnt units one staged slot adds (loaders)
   static constexpr bool PREFETCH = VAR >= 1;           // next slot's fragments under this slot's MFMAs
 };
 
@@ -146,6 +152,7 @@ __global__ __launch_bounds__(Geo<VAR>::THREADS) void wgrad_gemm_k(const T* __res
     else glds16s(a, voffA[j], lds0 + slot * SLOTB + (wave * DJ + j) * 1024);
   };
   auto stage = [&](int kt, int slot) {
+    if (G::LOADERS < G::NW && wave >= G::LOADERS) return;  // wave-uniform (readfirstlane'd)
     const void* a = sgpr_ptr(Abase + (long)kt * BK * lda);
     const void* b = sgpr_ptr(Bbase + (long)kt * BK * ldb);
 #pragma unroll
@@ -364,7 +371,7 @@ void launch_v(const void* a, long lda, const void* b, long ldb, void* c, long ld
                      (const T*)b, ldb, (OT*)c, ldc, c_split, M, N, K, (int)accumulate, (int)wide);
 }
 
-constexpr int DEFAULT_VARIANT = 1;
+constexpr int DEFAULT_VARIANT = 2;
 
 int variant() {
   const char* e = getenv("BLLM_WGRAD_VARIANT");  // per launch (A/B in one process); ~100 ns
@@ -374,8 +381,11 @@ int variant() {
 template <typename T, typename OT>
 void launch(const void* a, long lda, const void* b, long ldb, void* c, long ldc, long c_split, int M, int N, int K,
             int S, bool accumulate, hipStream_t s) {
-  if (variant() == 0) launch_v<T, OT, 0>(a, lda, b, ldb, c, ldc, c_split, M, N, K, S, accumulate, s);
-  else launch_v<T, OT, 1>(a, lda, b, ldb, c, ldc, c_split, M, N, K, S, accumulate, s);
+  switch (variant()) {
+    case 0: launch_v<T, OT, 0>(a, lda, b, ldb, c, ldc, c_split, M, N, K, S, accumulate, s); break;
+    case 2: launch_v<T, OT, 2>(a, lda, b, ldb, c, ldc, c_split, M, N, K, S, accumulate, s); break;
+    default: launch_v<T, OT, 1>(a, lda, b, ldb, c, ldc, c_split, M, N, K, S, accumulate, s); break;
+  }
 }
 
 }  // namespace
