@@ -4,7 +4,7 @@
     python bench.py --gpus N --steps K --warmup W
     torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
 
-Each rank runs a micro-batch of 16 sequences x ``T = 1024`` (the reference clamps every Llama
+Each rank runs a micro-batch of 24 sequences x ``T = 1024`` (the reference clamps every Llama
 to ctx 1024, Models/Llama/config.py:115-124) of synthetic token ids through one full training
 step — forward, fused CE, backward, global-norm clip 1.0,
 AdamW(wd 0.1) with fp32 master weights — on random-init weights of the full Llama-3-8B
@@ -13,12 +13,12 @@ exactly K timed steps bracketed by barrier + device sync; the slowest rank's tim
 Weak scaling: per-GPU work is fixed, total tokens grow with N.
 
 Micro-batch: the reference's ``--batch_size`` default of 4 (args.py:53) was sized for a 16 GB
-T4.  One MI355X holds 288 GB, so the benchmark sizes the per-GPU micro-batch for that: B=16
-peaks at ~184 GiB on one GPU (bf16 params + fp32 master/moments + selective-checkpoint
-activations) and measured 23.3k tok/s vs 20.0k at B=4.  It also keeps FSDP's per-block
-all-gathers (416 MiB) and reduce-scatters hidden under block compute at 2 GPUs, where two
-ranks share a single xGMI link (at B=4 a block's forward is ~1.4 ms but its gather over one
-link is ~3.4 ms).  ``--batch_size 4`` reproduces the reference default.
+T4.  One MI355X holds 288 GB, so the benchmark sizes the per-GPU micro-batch for that
+(measured on one GPU, profiles/r1_llama3_8b_1gpu_v4.md): B=4 20.0k tok/s, B=16 25.0k (184 GiB
+peak), B=24 25.5k (217 GiB), B=32 25.7k (249 GiB).  B=24 keeps ~70 GB of headroom on the
+single-GPU (unsharded) run; it also keeps FSDP's per-block all-gathers (416 MiB) and
+reduce-scatters hidden under block compute at 2 GPUs, where two ranks share a single xGMI
+link.  ``--batch_size 4`` reproduces the reference default.
 """
 from __future__ import annotations
 
@@ -41,7 +41,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--model", default="llama3")
     ap.add_argument("--num_params", default="8B")
-    ap.add_argument("--batch_size", type=int, default=16, help="micro-batch per GPU (reference CLI default: 4)")
+    ap.add_argument("--batch_size", type=int, default=24, help="micro-batch per GPU (reference CLI default: 4)")
     ap.add_argument("--seq_len", type=int, default=1024)
     ap.add_argument("--actv_ckpt", default="selective", choices=["none", "selective", "full"])
     ap.add_argument("--parallel", default="fsdp", choices=["fsdp", "ddp", "zero1"])
