@@ -110,6 +110,27 @@ def _weight_grad(dy: torch.Tensor, x: torch.Tensor, gW: torch.Tensor, accumulate
     ops.sum_partials_(part, gW, accumulate)
 
 
+def _input_grad(dy: torch.Tensor, W: torch.Tensor, dx_acc: Optional[torch.Tensor] = None,
+                out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """dx = dy @ W (+ dx_acc) [+ written into / added to ``out``].  GPU shapes the MFMA kernel
+    takes (csrc/gemm_wgrad.hip, K-contiguous A) run there, else hipBLASLt."""
+    if out is not None:  # out += dy @ W
+        if ops.dgrad_gemm_enabled() and ops.gemm_nn_ok(dy, W, out):
+            ops.gemm_nn_(dy, W, out, True)
+        else:
+            out.addmm_(dy, W)
+        return out
+    if ops.dgrad_gemm_enabled() and ops.gemm_nn_ok(dy, W):
+        if dx_acc is not None:
+            dx = dx_acc.clone(memory_format=torch.contiguous_format)
+            ops.gemm_nn_(dy, W, dx, True)
+        else:
+            dx = torch.empty(dy.shape[0], W.shape[1], dtype=dy.dtype, device=dy.device)
+            ops.gemm_nn_(dy, W, dx, False)
+        return dx
+    return torch.addmm(dx_acc, dy, W) if dx_acc is not None else torch.mm(dy, W)
+
+
 # tests set this to drive the grouped LoRA path through the CPU oracles of ops.reference
 FORCE_GROUPED_LORA = False
 
@@ -216,11 +237,7 @@ class FusedLinear:
             return self._grouped_lora_backward(dy, x, xa[1], xa[2], need_dx, dx_acc, accumulate)
         dx = None
         if need_dx:
-            W = self.W()
-            if dx_acc is not None:
-                dx = torch.addmm(dx_acc, dy, W)
-            else:
-                dx = torch.mm(dy, W)
+            dx = _input_grad(dy, self.W(), dx_acc)
         if self.has_lora:
             for (c0, c1), s, t in zip(self.cols, self.specs, xa):
                 if s.lora_A is None:
@@ -264,5 +281,4 @@ class FusedLinear:
         # dx = dx_acc + s u A_cat^T (lora_up, write-only) then += dy W (beta = 1 GEMM)
         dx = torch.empty(x.shape, dtype=x.dtype, device=x.device)
         ops.lora_up_(dx, u, [P], [0], [0], sc, base=dx_acc)
-        dx.addmm_(dy, self.W())
-        return dx
+        return _input_grad(dy, self.W(), out=dx)

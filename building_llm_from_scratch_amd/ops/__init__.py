@@ -23,6 +23,7 @@ __all__ = [
     "sq_norm_multi", "adamw_step_", "attn_decode", "bias_grad_", "ext_available", "load_ext", "attention_backend",
     "lora_down", "lora_up_", "lora_wgrad", "lora_pack_t", "lora_kernel_ok", "sum_partials_",
     "wgrad_gemm_", "wgrad_gemm_ok", "wgrad_gemm_enabled", "wgrad_gemm_preferred", "wgrad_splits",
+    "gemm_nn_", "gemm_nn_ok", "dgrad_gemm_enabled",
 ]
 
 rope_tables = ref.rope_tables
@@ -192,6 +193,42 @@ def wgrad_gemm_(a, b, c, accumulate: bool = False, splits: Optional[int] = None)
         _k().wgrad_gemm_(a, b, c, bool(accumulate), S)
         return c
     r = a.float().t() @ b.float()
+    if accumulate:
+        r += c.float()
+    c.copy_(r)
+    return c
+
+
+def dgrad_gemm_enabled() -> bool:
+    """``BLLM_DGRAD_GEMM=1`` routes input gradients (dX = dY W) through the MFMA kernel
+    (``gemm_nn_``).  Off by default: measured at parity with hipBLASLt on the benchmark shapes
+    (0.95-1.05x, tools/bench_dgrad.py, profiles/r1_wgrad_kernel.md) — hipBLASLt's dX family is
+    already at 1.25-1.38 PF, unlike its dW family the kernel was written for."""
+    return os.environ.get("BLLM_DGRAD_GEMM", "0") == "1"
+
+
+def gemm_nn_ok(a: torch.Tensor, b: torch.Tensor, c: Optional[torch.Tensor] = None) -> bool:
+    """Shapes/layouts the MFMA kernel takes for c [M, N] (+)= a [M, K] b [K, N] (row-major):
+    M, N multiples of 256, K of 128, 16-B aligned unit-stride rows."""
+    if not (a.is_cuda and a.dtype in (torch.bfloat16, torch.float16) and b.dtype == a.dtype and a.dim() == 2
+            and b.dim() == 2):
+        return False
+    M, K = a.shape
+    N = b.shape[1]
+    ok = (M % WGRAD_TILE == 0 and N % WGRAD_TILE == 0 and K % WGRAD_KGRAN == 0 and K >= WGRAD_KGRAN
+          and b.shape[0] == K and a.stride(1) == 1 and b.stride(1) == 1
+          and a.stride(0) % 8 == 0 and b.stride(0) % 8 == 0
+          and a.data_ptr() % 16 == 0 and b.data_ptr() % 16 == 0)
+    return ok and (c is None or c.stride(1) == 1)
+
+
+def gemm_nn_(a, b, c, accumulate: bool = False):
+    """c (+)= a @ b with a [M, K], b [K, N] row-major, fp32 accumulation (csrc/gemm_wgrad.hip,
+    K-contiguous A images read with ds_read_b128, B images with transposed reads)."""
+    if _hip(a):
+        _k().gemm_nn_(a, b, c, bool(accumulate))
+        return c
+    r = a.float() @ b.float()
     if accumulate:
         r += c.float()
     c.copy_(r)

@@ -123,6 +123,10 @@ void lora_pack_t(DType dt, const LoraPackArgs& a, int K, int max_r, hipStream_t 
 bool wgrad_gemm_supported(int M, int N, int K, int S);
 void wgrad_gemm(DType dt, DType odt, const void* a, long lda, const void* b, long ldb, void* c, long ldc,
                 long c_split, int M, int N, int K, int S, bool accumulate, hipStream_t s);
+// same kernel with a K-contiguous A: C[M, N] (+)= A[M, K] B[K, N] (dX = dY W)
+bool gemm_nn_supported(int M, int N, int K);
+void gemm_nn(DType dt, DType odt, const void* a, long lda, const void* b, long ldb, void* c, long ldc, int M, int N,
+             int K, bool accumulate, hipStream_t s);
 
 // optim.hip
 void adamw_step(DType pdt, DType gdt, void* param, float* master, const void* grad, float* m, float* v, long n,

@@ -255,6 +255,27 @@ void wgrad_gemm_(const Tensor& a, const Tensor& b, Tensor& c, bool accumulate, i
                           stream());
 }
 
+// c [M, N] (+)= a [M, K] . b [K, N], all row-major (input gradient dX = dY W of a Linear)
+void gemm_nn_(const Tensor& a, const Tensor& b, Tensor& c, bool accumulate) {
+  TORCH_CHECK(a.is_cuda() && b.is_cuda() && c.is_cuda(), "gemm_nn: GPU tensors");
+  c10::DeviceGuard g(a.device());
+  TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && c.dim() == 2, "gemm_nn: 2-D operands");
+  const int64_t M = a.size(0), K = a.size(1), N = b.size(1);
+  TORCH_CHECK(b.size(0) == K && c.size(0) == M && c.size(1) == N, "gemm_nn: shapes");
+  TORCH_CHECK(a.scalar_type() == b.scalar_type() &&
+                  (a.scalar_type() == at::kBFloat16 || a.scalar_type() == at::kHalf), "gemm_nn: bf16/fp16 operands");
+  TORCH_CHECK(c.scalar_type() == a.scalar_type() || c.scalar_type() == at::kFloat, "gemm_nn: output dtype");
+  TORCH_CHECK(a.stride(1) == 1 && b.stride(1) == 1 && c.stride(1) == 1, "gemm_nn: unit column strides");
+  TORCH_CHECK(a.stride(0) % 8 == 0 && b.stride(0) % 8 == 0, "gemm_nn: rows must be 16-B aligned");
+  TORCH_CHECK((reinterpret_cast<uintptr_t>(a.data_ptr()) | reinterpret_cast<uintptr_t>(b.data_ptr())) % 16 == 0,
+              "gemm_nn: operands must be 16-B aligned");
+  TORCH_CHECK(a.stride(0) < (int64_t(1) << 26) && b.stride(0) < (int64_t(1) << 26), "gemm_nn: row stride too large");
+  TORCH_CHECK(M < (int64_t(1) << 31) && N < (int64_t(1) << 31) && K < (int64_t(1) << 31));
+  TORCH_CHECK(bllm::gemm_nn_supported((int)M, (int)N, (int)K), "gemm_nn: unsupported shape ", M, "x", N, "x", K);
+  bllm::gemm_nn(dt_of(a), dt_of(c), a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0), c.data_ptr(), c.stride(0),
+                (int)M, (int)N, (int)K, accumulate, stream());
+}
+
 // q [B, H, hd]; kc / vc [B, G, Tmax, hd] with the first L positions valid -> out [B, H*hd]
 Tensor attn_decode(const Tensor& q, const Tensor& kc, const Tensor& vc, int64_t L) {
   check_gpu(q, "q"); check_gpu(kc, "kcache"); check_gpu(vc, "vcache");
@@ -578,6 +599,7 @@ TORCH_LIBRARY(bllm, m) {
   m.def("bias_grad_(Tensor dy, Tensor(a!) db, bool accumulate) -> ()");
   m.def("sum_partials_(Tensor part, Tensor(a!) out, bool accumulate) -> ()");
   m.def("wgrad_gemm_(Tensor a, Tensor b, Tensor(a!) c, bool accumulate, int splits) -> ()");
+  m.def("gemm_nn_(Tensor a, Tensor b, Tensor(a!) c, bool accumulate) -> ()");
   m.def("attn_decode(Tensor q, Tensor kcache, Tensor vcache, int L) -> Tensor");
   m.def("flash_attn_fwd(Tensor qkv, int B, int T, int H, int G, int hd, bool causal, float p, int seed, int offset) -> (Tensor, Tensor)");
   m.def("flash_attn_bwd(Tensor qkv, Tensor o, Tensor lse, Tensor dout, int B, int T, int H, int G, int hd, bool causal, float p, int seed, int offset) -> Tensor");
@@ -609,6 +631,7 @@ TORCH_LIBRARY_IMPL(bllm, CUDA, m) {
   m.impl("attn_decode", &attn_decode);
   m.impl("sum_partials_", &sum_partials_);
   m.impl("wgrad_gemm_", &wgrad_gemm_);
+  m.impl("gemm_nn_", &gemm_nn_);
   m.impl("bias_grad_", &bias_grad_);
   m.impl("flash_attn_bwd", &flash_attn_bwd);
   m.impl("ce_fwd", &ce_fwd);

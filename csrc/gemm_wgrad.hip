@@ -106,7 +106,14 @@ __device__ __forceinline__ s16x8 frag(const char* p) {
 
 template <int N> __device__ __forceinline__ void vm_wait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
 
-template <typename T, typename OT, int VAR>
+// AK = false: A is [K, M] row-major (token-major dY of a weight gradient; transposed LDS reads).
+// AK = true:  A is [M, K] row-major (K-contiguous, e.g. dY of an input gradient dX = dY W):
+//             A images are [256 m][32 k] rows of 64 B, 16-B chunk c of row r stored at
+//             c ^ fA((r >> 2) & 3) with fA = {0, 2, 3, 1} (every 16-lane ds_read_b128 group then
+//             covers 16 distinct bank quads), fragments read with ds_read_b128.
+__device__ __forceinline__ int fA(int q) { return (0x78 >> (2 * q)) & 3; }
+
+template <typename T, typename OT, int VAR, bool AK = false>
 __global__ __launch_bounds__(Geo<VAR>::THREADS) void wgrad_gemm_k(const T* __restrict__ A, long lda,
                                                                   const T* __restrict__ B, long ldb,
                                                                   OT* __restrict__ C, long ldc, long c_split,
@@ -139,11 +146,16 @@ __global__ __launch_bounds__(Geo<VAR>::THREADS) void wgrad_gemm_k(const T* __res
 #pragma unroll
   for (int j = 0; j < DJ; ++j) {
     const int r = (wave * DJ + j) * 2 + (lane >> 5), c = (lane & 31) ^ swz(r);
-    voffA[j] = (uint32_t)((r * lda + 8 * c) * (long)sizeof(T));
     voffB[j] = (uint32_t)((r * ldb + 8 * c) * (long)sizeof(T));
+    if constexpr (AK) {  // piece = 16 m-rows x 64 B; lane -> row l/4, physical chunk l%4
+      const int ra = (wave * DJ + j) * 16 + (lane >> 2), ca = (lane & 3) ^ fA((ra >> 2) & 3);
+      voffA[j] = (uint32_t)((ra * lda + 8 * ca) * (long)sizeof(T));
+    } else {
+      voffA[j] = (uint32_t)((r * lda + 8 * c) * (long)sizeof(T));
+    }
   }
   const uint32_t lds0 = lds_u32(smem);
-  const T* Abase = A + (long)c_lo * KCH * lda + m0;
+  const T* Abase = AK ? A + m0 * lda + (long)c_lo * KCH : A + (long)c_lo * KCH * lda + m0;
   const T* Bbase = B + (long)c_lo * KCH * ldb + n0;
   // piece q of a stage: q even = A piece q/2, q odd = B piece q/2 (issue order A0 B0 A1 B1 ..)
   auto piece = [&](const void* a, const void* b, int q, int slot) {
@@ -153,7 +165,7 @@ __global__ __launch_bounds__(Geo<VAR>::THREADS) void wgrad_gemm_k(const T* __res
   };
   auto stage = [&](int kt, int slot) {
     if (G::LOADERS < G::NW && wave >= G::LOADERS) return;  // wave-uniform (readfirstlane'd)
-    const void* a = sgpr_ptr(Abase + (long)kt * BK * lda);
+    const void* a = sgpr_ptr(Abase + (AK ? (long)kt * BK : (long)kt * BK * lda));
     const void* b = sgpr_ptr(Bbase + (long)kt * BK * ldb);
 #pragma unroll
     for (int q = 0; q < PS; ++q) piece(a, b, q, slot);
@@ -166,7 +178,14 @@ __global__ __launch_bounds__(Geo<VAR>::THREADS) void wgrad_gemm_k(const T* __res
   const int rowb = (8 * g + qq) * ROWB + (p & 1) * 8 + (p >> 1) * 16;
   int aoff[8], boff[FN];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) aoff[i] = rowb + (wm * 16 + ((2 * i) ^ f)) * 16;
+  for (int i = 0; i < 8; ++i)
+    aoff[i] = AK ? (wm * 128 + 16 * i + (lane & 15)) * 64 + (((lane >> 4) ^ fA((lane & 15) >> 2)) << 4)
+                 : rowb + (wm * 16 + ((2 * i) ^ f)) * 16;
+  // A fragment: 8 k-values of one m row (row read) or of one m column (two transposed reads)
+  auto fragA = [&](const char* p) -> s16x8 {
+    if constexpr (AK) return *(const __attribute__((address_space(3))) s16x8*)(p);
+    else return frag(p);
+  };
 #pragma unroll
   for (int j = 0; j < FN; ++j) boff[j] = B_BASE + rowb + ((wn * 2 * FN + 2 * j) ^ f) * 16;
 
@@ -186,7 +205,7 @@ __global__ __launch_bounds__(Geo<VAR>::THREADS) void wgrad_gemm_k(const T* __res
 #pragma unroll
       for (int j = 0; j < FN; ++j) F.b[j] = frag(base + boff[j]);
 #pragma unroll
-      for (int i = 0; i < 8; ++i) F.a[i] = frag(base + aoff[i]);
+      for (int i = 0; i < 8; ++i) F.a[i] = fragA(base + aoff[i]);
     };
     // G.b first, then G.a[i] just before F.a[i]'s MFMAs: F.a[i] dies as G.a[i] arrives, so the
     // two sets cost 2 x FN B-fragments + 9 A-fragments of VGPRs, not 2 x (8 + FN).  The loop
@@ -206,7 +225,7 @@ __global__ __launch_bounds__(Geo<VAR>::THREADS) void wgrad_gemm_k(const T* __res
       }
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
-        if constexpr (!LAST) Gn.a[i] = frag(nxt + aoff[i]);
+        if constexpr (!LAST) Gn.a[i] = fragA(nxt + aoff[i]);
         __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int j = 0; j < FN; ++j) acc[i][j] = Mfma<T>::run(F.a[i], F.b[j], acc[i][j]);
@@ -258,7 +277,7 @@ __global__ __launch_bounds__(Geo<VAR>::THREADS) void wgrad_gemm_k(const T* __res
     for (int j = 0; j < FN; ++j) bf[j] = frag(base + boff[j]);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      const s16x8 af = frag(base + aoff[i]);
+      const s16x8 af = fragA(base + aoff[i]);
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int j = 0; j < FN; ++j) acc[i][j] = Mfma<T>::run(af, bf[j], acc[i][j]);
@@ -358,16 +377,16 @@ __global__ __launch_bounds__(Geo<VAR>::THREADS) void wgrad_gemm_k(const T* __res
   }
 }
 
-template <typename T, typename OT, int VAR>
+template <typename T, typename OT, int VAR, bool AK = false>
 void launch_v(const void* a, long lda, const void* b, long ldb, void* c, long ldc, long c_split, int M, int N, int K,
               int S, bool accumulate, hipStream_t s) {
-  static const bool attr = hipFuncSetAttribute((const void*)wgrad_gemm_k<T, OT, VAR>,
+  static const bool attr = hipFuncSetAttribute((const void*)wgrad_gemm_k<T, OT, VAR, AK>,
                                                hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES) == hipSuccess;
   (void)attr;
   const dim3 grid((M / BM) * (N / BN), S);
   const bool wide = reinterpret_cast<uintptr_t>(c) % 16 == 0 && (ldc * (long)sizeof(OT)) % 16 == 0 &&
                     (c_split * (long)sizeof(OT)) % 16 == 0;
-  hipLaunchKernelGGL((wgrad_gemm_k<T, OT, VAR>), grid, dim3(Geo<VAR>::THREADS), LDS_BYTES, s, (const T*)a, lda,
+  hipLaunchKernelGGL((wgrad_gemm_k<T, OT, VAR, AK>), grid, dim3(Geo<VAR>::THREADS), LDS_BYTES, s, (const T*)a, lda,
                      (const T*)b, ldb, (OT*)c, ldc, c_split, M, N, K, (int)accumulate, (int)wide);
 }
 
@@ -389,6 +408,16 @@ void launch(const void* a, long lda, const void* b, long ldb, void* c, long ldc,
 }
 
 }  // namespace
+
+bool gemm_nn_supported(int M, int N, int K) { return M > 0 && N > 0 && M % BM == 0 && N % BN == 0 && K >= KCH && K % KCH == 0; }
+
+void gemm_nn(DType dt, DType odt, const void* a, long lda, const void* b, long ldb, void* c, long ldc, int M, int N,
+             int K, bool accumulate, hipStream_t s) {
+  BLLM_DISPATCH(odt, OT, {
+    if (dt == DType::BF16) launch_v<bf16_t, OT, DEFAULT_VARIANT, true>(a, lda, b, ldb, c, ldc, 0, M, N, K, 1, accumulate, s);
+    else launch_v<f16_t, OT, DEFAULT_VARIANT, true>(a, lda, b, ldb, c, ldc, 0, M, N, K, 1, accumulate, s);
+  });
+}
 
 bool wgrad_gemm_supported(int M, int N, int K, int S) {
   return M > 0 && N > 0 && M % BM == 0 && N % BN == 0 && K >= KCH && K % KCH == 0 && S >= 1 && S <= K / KCH;

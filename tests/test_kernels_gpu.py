@@ -378,3 +378,35 @@ def test_wgrad_gemm_unaligned_output(accumulate):
     err = (c.float() - expect).abs().max().item()
     assert err <= 8e-3 * expect.abs().max().item(), err
     assert torch.equal(c_full[:, 0], before[:, 0]) and torch.equal(c_full[:, 1 + N:], before[:, 1 + N:])
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("odt", [None, torch.float32])
+@pytest.mark.parametrize("M,K,N", [(256, 128, 256), (512, 384, 768), (768, 1024, 512)])
+@pytest.mark.parametrize("accumulate", [False, True])
+def test_gemm_nn(dt, odt, M, K, N, accumulate):
+    """K-contiguous-A variant of the MFMA GEMM (dX = dY W) vs an fp32 matmul, strided A rows."""
+    a_full = torch.randn(M, K + 64, device=DEV).to(dt)
+    a = a_full[:, 32:32 + K]                      # lda = K + 64, 64-B offset
+    b = torch.randn(K, N, device=DEV).to(dt)
+    c = torch.randn(M, N, device=DEV).to(odt or dt)
+    assert ops.gemm_nn_ok(a, b, c)
+    expect = a.float() @ b.float() + (c.float() if accumulate else 0)
+    ops.gemm_nn_(a, b, c, accumulate)
+    err = (c.float() - expect).abs().max().item()
+    mag = expect.abs().max().item()
+    assert err <= (8e-3 if c.dtype != torch.float32 else 1e-4) * mag, (err, mag)
+
+
+def test_dgrad_in_linear_backward(monkeypatch):
+    """With BLLM_DGRAD_GEMM=1 FusedLinear.backward routes dX through the MFMA kernel."""
+    from building_llm_from_scratch_amd.models.linear import _input_grad
+    monkeypatch.setenv("BLLM_DGRAD_GEMM", "1")
+    dy = torch.randn(512, 768, device=DEV).to(torch.bfloat16)
+    W = torch.randn(768, 1280, device=DEV).to(torch.bfloat16)
+    assert ops.gemm_nn_ok(dy, W)
+    dx = _input_grad(dy, W)
+    _close(dx, dy.float() @ W.float(), torch.bfloat16, 1, name="dX")
+    acc = torch.randn(512, 1280, device=DEV).to(torch.bfloat16)
+    dx2 = _input_grad(dy, W, acc)
+    _close(dx2, acc.float() + dy.float() @ W.float(), torch.bfloat16, 1, name="dX+acc")

@@ -1,0 +1,53 @@
+#!/usr/bin/env python3
+"""dX GEMM micro-benchmark (GPU): dx[N, in] = dy[N, out] @ W[out, in] on the MFMA kernel with a
+K-contiguous A (csrc/gemm_wgrad.hip, ``ops.gemm_nn_``) vs hipBLASLt (``torch.mm``), on the
+input-gradient shapes of the benchmark models.  Interleaved rounds in one process, median.
+Usage: python tools/bench_dgrad.py [--tokens 24576] [--iters 10] [--rounds 3]"""
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from building_llm_from_scratch_amd import ops  # noqa: E402
+from tools.bench_wgrad import SHAPES, timeit  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--tokens", type=int, default=24576)
+    ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--models", default="llama3_8b,gpt2_774m,llama32_1b")
+    a = ap.parse_args()
+    ops.load_ext(required=True)
+    Nt = a.tokens
+    for model in a.models.split(","):
+        for name, out_f, in_f in SHAPES[model]:
+            dy = (torch.rand(Nt, out_f, device="cuda") * 2 - 1).to(torch.bfloat16)
+            W = ((torch.rand(out_f, in_f, device="cuda") * 2 - 1) * 0.05).to(torch.bfloat16)
+            d0 = torch.empty(Nt, in_f, device="cuda", dtype=torch.bfloat16)
+            d1 = torch.empty_like(d0)
+            fl = 2.0 * Nt * out_f * in_f
+            r = {"model": model, "gemm": name, "out_in": [out_f, in_f], "tokens": Nt}
+            times = {"hipblaslt_us": [], "mfma_us": []}
+            for _ in range(a.rounds):
+                times["hipblaslt_us"].append(timeit(lambda: torch.mm(dy, W, out=d0), a.iters))
+                times["mfma_us"].append(timeit(lambda: ops.gemm_nn_(dy, W, d1, False), a.iters))
+            for k, ts in times.items():
+                r[k] = sorted(ts)[len(ts) // 2]
+            torch.cuda.synchronize()
+            r["max_rel_err_vs_hipblaslt"] = round(((d1.float() - d0.float()).abs().max() / d0.float().abs().max()).item(), 5)
+            for k in list(r):
+                if k.endswith("_us"):
+                    r[k.replace("_us", "_tflops")] = round(fl / r[k] / 1e6, 1)
+                    r[k] = round(r[k], 1)
+            print(json.dumps(r), flush=True)
+            del dy, W, d0, d1
+            torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()
