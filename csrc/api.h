@@ -45,6 +45,9 @@ void attn_bwd_naive(DType dt, const void* qkv, const void* o, const float* lse, 
                     float* delta, int B, int T, int H, int G, int hd, bool causal, float p, uint64_t seed,
                     uint64_t offset, hipStream_t s);
 
+// whether the dK/dV pass needs the fp32 per-head partial buffer (GQA without the fused-head variant)
+bool attn_bwd_kv_partials(int B, int T, int H, int G);
+
 void attn_delta(DType dt, const void* o, const void* dout, float* delta, int B, int T, int H, int hd,
                 hipStream_t s);
 

@@ -100,7 +100,10 @@ template <int HD> constexpr int dkdv_buf_bytes() { return 4 * BWD_BQ * HD * 2 + 
 // of dS is folded into the final dK), 9 saddr LDS-DMA issues whose per-lane offsets are
 // precomputed.  Masking (causal diagonal, sequence tail) and dropout are compile-time variants
 // so the common interior step carries no per-element branches.
-template <typename T, int HD, bool DROP, int NBUF, int OCC>
+// FUSEG: one workgroup sweeps all H/G query heads of its kv head (dK/dV summed in registers,
+// written once in bf16: no fp32 per-head partials, no reduction kernel); otherwise one query
+// head per workgroup plus the attn_bwd_kv_reduce_k pass for GQA.
+template <typename T, int HD, bool DROP, int NBUF, int OCC, bool FUSEG = false>
 __global__ __launch_bounds__(256, OCC) void attn_bwd_mfma_k(const T* __restrict__ qkv, const T* __restrict__ dout,
                                                             const float* __restrict__ lse,
                                                             const float* __restrict__ delta, T* __restrict__ dqkv,
@@ -119,30 +122,22 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_mfma_k(const T* __restrict_
 
   // heaviest (lowest) key block first across the whole grid; all key blocks of one (b, h)
   // share lin % 8, i.e. one XCD and its L2 (Q / dO re-reads hit there)
-  const int lin = blockIdx.x, nbh = H * B_;
+  const int lin = blockIdx.x, nbh = (FUSEG ? G : H) * B_;
   const int kb = lin / nbh, bh = lin - kb * nbh;
-  const int h = bh % H, b = bh / H;
-  const int g = h / (H / G);
+  const int rep = H / G;
+  const int b = FUSEG ? bh / G : bh / H;
+  const int g = FUSEG ? bh % G : (bh % H) / rep;
+  const int h_first = FUSEG ? g * rep : bh % H, h_count = FUSEG ? rep : 1;
   const int tid = threadIdx.x, lane = tid & 63, hh = lane >> 5, l32 = lane & 31;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (scalar branches)
   const long rs = (long)(H + 2 * G) * HD;
   const long ors = (long)H * HD;
-  const T* qb_ = qkv + (long)b * T_ * rs + (long)h * HD;
   const T* kb_ = qkv + (long)b * T_ * rs + (long)(H + g) * HD;
   const T* vb_ = qkv + (long)b * T_ * rs + (long)(H + G + g) * HD;
-  const T* ob_ = dout + (long)b * T_ * ors + (long)h * HD;
-  const float* lse_ = lse + ((long)b * H + h) * T_;
-  const float* del_ = delta + ((long)b * H + h) * T_;
   const int k0 = kb * BWD_BKV;
   const int kw0 = k0 + 32 * w;
   const int mykey = kw0 + l32;
   const float scale = rsqrtf((float)HD), c = scale * kLog2eB;
-  DropSlab ds;
-  uint64_t dslab = 0;
-  if constexpr (DROP) {
-    dslab = doff + (uint64_t)(b * H + h) * T_ * T_;
-    ds.init(seed, dslab);
-  }
 
   // ---- K / V fragments of this wave's 32 keys (B operands, key = lane column)
   v8 kf[KK], vf[KK];
@@ -179,7 +174,19 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_mfma_k(const T* __restrict_
     o_t = (uint32_t)(r * ors * 2 + tc * 16);
   }
   const uint32_t smem_u = lds_u32(smem);
+  for (int hi = 0; hi < h_count; ++hi) {
+  const int h = h_first + hi;
+  const T* qb_ = qkv + (long)b * T_ * rs + (long)h * HD;
+  const T* ob_ = dout + (long)b * T_ * ors + (long)h * HD;
+  const float* lse_ = lse + ((long)b * H + h) * T_;
+  const float* del_ = delta + ((long)b * H + h) * T_;
   const float* stat_src = (lane < 32 ? lse_ : del_);
+  DropSlab ds;
+  uint64_t dslab = 0;
+  if constexpr (DROP) {
+    dslab = doff + (uint64_t)(b * H + h) * T_ * T_;
+    ds.init(seed, dslab);
+  }
 
   // DMA of one 32-query step into ring slot `slot`
   auto issue = [&](int q0, int slot) {
@@ -325,8 +332,11 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_mfma_k(const T* __restrict_
     slot = slot == NBUF - 1 ? 0 : slot + 1;
   }
 
-  // ---- MHA: write bf16 dK/dV straight into dqkv; GQA: per-head fp32 partials
-  if (mykey < T_ && H == G) {
+  }  // heads
+
+  // ---- MHA / fused GQA: write bf16 dK/dV straight into dqkv; else per-head fp32 partials
+  const int h = h_first;
+  if (mykey < T_ && (FUSEG || H == G)) {
     T* pk = dqkv + ((long)b * T_ + mykey) * rs + (long)(H + g) * HD;
     T* pv = dqkv + ((long)b * T_ + mykey) * rs + (long)(H + G + g) * HD;
 #pragma unroll
@@ -637,15 +647,27 @@ __global__ __launch_bounds__(256) void attn_bwd_kv_reduce_k(const float* __restr
 // dK/dV variant: 0 = 2-slot ring at 2 workgroups per CU (one wave's waits hide under the other
 // wave's MFMAs), 1 = 3-slot ring (prefetch distance 2) at 1 workgroup per CU.
 // BLLM_ATTN_KV_VARIANT selects one for A/B measurement.
+// 2 = as 0 with the GQA heads of a kv head fused into one workgroup (no partials / reduction).
+// Unset: 2 when the fused grid still has >= 4 workgroups per CU (measured: Llama-3-8B B=24
+// 1.51 -> 1.12 ms), else 0 (B=4 has only 256 fused workgroups: 0.25 ms unfused vs 0.35 fused).
 static int kv_variant_from_env() {
   const char* e = getenv("BLLM_ATTN_KV_VARIANT");
-  return e ? atoi(e) : 0;
+  return e ? atoi(e) : -1;
+}
+static bool fuse_gqa_heads(int B, int T_, int H, int G) {
+  static const int kv_variant = kv_variant_from_env();
+  if (H == G) return false;
+  if (kv_variant >= 0) return kv_variant == 2;
+  const long nkb = (T_ + BWD_BKV - 1) / BWD_BKV;
+  return nkb * G * (long)B >= 1024;
 }
 // dQ variant: 0 = 32-key tiles, 3-slot ring, 2 workgroups per CU; 1 = 64-key tiles, 1 per CU
 static int q_variant_from_env() {
   const char* e = getenv("BLLM_ATTN_Q_VARIANT");
   return e ? atoi(e) : 0;
 }
+
+bool attn_bwd_kv_partials(int B, int T_, int H, int G) { return H != G && !fuse_gqa_heads(B, T_, H, G); }
 
 void attn_bwd_mfma(DType dt, const void* qkv, const void* o, const float* lse, const void* dout, void* dqkv,
                    float* delta, float* dq_acc, float* dkv_part, int B, int T_, int H, int G, int hd, bool causal,
@@ -656,7 +678,9 @@ void attn_bwd_mfma(DType dt, const void* qkv, const void* o, const float* lse, c
   static const int kv_variant = kv_variant_from_env();
   static const int q_variant = q_variant_from_env();
   const int nkb = (T_ + BWD_BKV - 1) / BWD_BKV;
-  dim3 grid_kv(nkb * H * B), grid_q(((T_ + DQ_BQ - 1) / DQ_BQ) * H * B), block(256);
+  // kv variant 2 (GQA, large grids): the dK/dV workgroup sweeps the H/G heads of its kv head
+  const bool fuseg = fuse_gqa_heads(B, T_, H, G);
+  dim3 grid_kv(nkb * (fuseg ? G : H) * B), grid_q(((T_ + DQ_BQ - 1) / DQ_BQ) * H * B), block(256);
   const bool drop = p > 0.f;
 #define LAUNCH(TT, HDD)                                                                                         \
   do {                                                                                                          \
@@ -681,7 +705,17 @@ void attn_bwd_mfma(DType dt, const void* qkv, const void* o, const float* lse, c
                            (const TT*)o, (const TT*)dout, lse, delta, (TT*)dqkv, T_, H, G, B, causal, thr, ik, \
                            seed, offset);                                                                       \
     }                                                                                                           \
-    if (kv_variant == 0) {                                                                                      \
+    if (fuseg) {                                                                                                \
+      const int lds_kv = 2 * dkdv_buf_bytes<HDD>();                                                             \
+      if (drop)                                                                                                 \
+        hipLaunchKernelGGL((attn_bwd_mfma_k<TT, HDD, true, 2, 2, true>), grid_kv, block, lds_kv, s,            \
+                           (const TT*)qkv, (const TT*)dout, lse, delta, (TT*)dqkv, dkv_part, T_, H, G, B,       \
+                           causal, thr, ik, seed, offset);                                                      \
+      else                                                                                                      \
+        hipLaunchKernelGGL((attn_bwd_mfma_k<TT, HDD, false, 2, 2, true>), grid_kv, block, lds_kv, s,           \
+                           (const TT*)qkv, (const TT*)dout, lse, delta, (TT*)dqkv, dkv_part, T_, H, G, B,       \
+                           causal, thr, ik, seed, offset);                                                      \
+    } else if (kv_variant != 1) {                                                                               \
       const int lds_kv = 2 * dkdv_buf_bytes<HDD>();                                                             \
       if (drop)                                                                                                 \
         hipLaunchKernelGGL((attn_bwd_mfma_k<TT, HDD, true, 2, 2>), grid_kv, block, lds_kv, s, (const TT*)qkv,  \
@@ -709,7 +743,7 @@ void attn_bwd_mfma(DType dt, const void* qkv, const void* o, const float* lse, c
     if (hd == 128) LAUNCH(f16_t, 128); else LAUNCH(f16_t, 64);
   }
 #undef LAUNCH
-  if (H != G) {
+  if (H != G && !fuseg) {
     const long BT = (long)B * T_;
     const long groups = BT * 2L * G * hd / 4;
     const int fg = (int)((groups + 255) / 256 < 4096 ? (groups + 255) / 256 : 4096);

@@ -322,7 +322,7 @@ Tensor flash_attn_bwd(const Tensor& qkv, const Tensor& o, const Tensor& lse, con
   auto delta = at::empty({B, H, T}, qkv.options().dtype(at::kFloat));
   const bool mfma = bllm::attn_mfma_head_dim((int)hd);
   // per-query-head dK/dV partials only for GQA (MHA writes dK/dV directly); dQ is atomic-free
-  auto dkv_part = (mfma && H != G) ? at::empty({2, B * T, H, hd}, qkv.options().dtype(at::kFloat)) : Tensor();
+  auto dkv_part = (mfma && bllm::attn_bwd_kv_partials((int)B, (int)T, (int)H, (int)G)) ? at::empty({2, B * T, H, hd}, qkv.options().dtype(at::kFloat)) : Tensor();
   bllm::attn_bwd(dt_of(qkv), qkv.data_ptr(), o.data_ptr(), lse.data_ptr<float>(), dout.data_ptr(), dqkv.data_ptr(),
                  delta.data_ptr<float>(), nullptr, dkv_part.defined() ? dkv_part.data_ptr<float>() : nullptr, (int)B, (int)T, (int)H, (int)G, (int)hd, causal,
                  (float)p, (uint64_t)seed, (uint64_t)offset, stream());

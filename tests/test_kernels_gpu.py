@@ -196,6 +196,13 @@ def test_flash_attention(dt, B, T, H, G, hd, p, causal):
     _close(dqkv, dqkv0, dt, 4, name="dqkv")
 
 
+@pytest.mark.parametrize("p", [0.0, 0.1])
+@pytest.mark.parametrize("hd", [64, 128])
+def test_flash_attention_gqa_fused_heads(p, hd):
+    """Grid large enough (B*G*ceil(T/128) >= 1024) that dK/dV takes the fused-GQA-heads variant."""
+    test_flash_attention(torch.bfloat16, 128, 128, 16, 8, hd, p, True)
+
+
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("B,H,G,hd,L,Tmax", [(2, 8, 2, 128, 37, 64), (1, 4, 4, 64, 1, 16), (3, 32, 8, 128, 1000, 1024)])
 def test_attn_decode(dt, B, H, G, hd, L, Tmax):

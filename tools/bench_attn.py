@@ -31,7 +31,8 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     a = ap.parse_args()
     ops.load_ext(required=True)
-    shapes = [("llama3-8B", 4, 1024, 32, 8, 128, 0.0), ("gpt2-774M", 4, 1024, 20, 20, 64, 0.1),
+    shapes = [("llama3-8B", 4, 1024, 32, 8, 128, 0.0), ("llama3-8B-B24", 24, 1024, 32, 8, 128, 0.0),
+              ("llama3.2-1B-B24", 24, 1024, 32, 8, 64, 0.0), ("gpt2-774M", 4, 1024, 20, 20, 64, 0.1),
               ("gpt2-774M-nodrop", 4, 1024, 20, 20, 64, 0.0),
               ("gpt2-124M", 4, 1024, 12, 12, 64, 0.0)]
     res = []
