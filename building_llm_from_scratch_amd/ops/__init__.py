@@ -23,7 +23,7 @@ __all__ = [
     "sq_norm_multi", "adamw_step_", "attn_decode", "bias_grad_", "ext_available", "load_ext", "attention_backend",
     "lora_down", "lora_up_", "lora_wgrad", "lora_pack_t", "lora_kernel_ok", "sum_partials_",
     "wgrad_gemm_", "wgrad_gemm_ok", "wgrad_gemm_enabled", "wgrad_gemm_preferred", "wgrad_splits",
-    "gemm_nn_", "gemm_nn_ok", "dgrad_gemm_enabled",
+    "gemm_nn_", "gemm_nn_ok", "dgrad_gemm_enabled", "transpose2d", "dgrad_wt_enabled",
 ]
 
 rope_tables = ref.rope_tables
@@ -205,6 +205,22 @@ def dgrad_gemm_enabled() -> bool:
     (0.95-1.05x, tools/bench_dgrad.py, profiles/r1_wgrad_kernel.md) — hipBLASLt's dX family is
     already at 1.25-1.38 PF, unlike its dW family the kernel was written for."""
     return os.environ.get("BLLM_DGRAD_GEMM", "0") == "1"
+
+
+def transpose2d(a: torch.Tensor) -> torch.Tensor:
+    """Contiguous a^T for a 2-D 16-bit tensor (csrc/elementwise.hip transpose16_k: 64x64 LDS
+    tiles, 16-byte loads and stores); dims must be multiples of 8."""
+    if _hip(a):
+        return _k().transpose2d(a)
+    return a.t().contiguous()
+
+
+def dgrad_wt_enabled() -> bool:
+    """``BLLM_DGRAD_WT`` (default on): large input-gradient GEMMs dX = dY W first transpose W
+    into a scratch copy so hipBLASLt runs dX = dY (W^T)^T with both operands K-contiguous —
+    the same fast layout as the forward x W^T (tools/bench_gemm.py: 1.52-1.59 PF vs 1.30-1.38
+    PF for the dY W layout)."""
+    return os.environ.get("BLLM_DGRAD_WT", "1") == "1"
 
 
 def gemm_nn_ok(a: torch.Tensor, b: torch.Tensor, c: Optional[torch.Tensor] = None) -> bool:

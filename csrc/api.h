@@ -22,6 +22,8 @@ void layernorm_bwd(DType dt, const void* dy, const void* x, const void* w, const
 void col_reduce(const float* part, DType odt, void* out, int P, int d, bool accumulate, hipStream_t s);
 
 // elementwise.hip
+// out[C, R] = in[R, C]^T, 16-bit elements, R % 8 == 0 and C % 8 == 0
+void transpose16(const void* in, void* out, long R, long C, hipStream_t s);
 void swiglu_fwd(DType dt, const void* gu, void* act, long N, int F, hipStream_t s);
 void swiglu_bwd(DType dt, const void* gu, const void* dact, void* dgu, long N, int F, hipStream_t s);
 void gelu_fwd(DType dt, const void* f, void* g, long n, hipStream_t s);

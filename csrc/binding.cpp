@@ -154,6 +154,17 @@ Tensor dropout_bwd(const Tensor& dy, double p, int64_t seed, int64_t offset) {
   return out;
 }
 
+Tensor transpose2d(const Tensor& a) {
+  check_gpu(a, "a");
+  c10::DeviceGuard g(a.device());
+  TORCH_CHECK(a.dim() == 2 && a.is_contiguous() && a.element_size() == 2, "transpose2d: contiguous 2-D 16-bit tensor");
+  const int64_t R = a.size(0), C = a.size(1);
+  TORCH_CHECK(R % 8 == 0 && C % 8 == 0, "transpose2d: both dims must be multiples of 8");
+  auto out = at::empty({C, R}, a.options());
+  bllm::transpose16(a.data_ptr(), out.data_ptr(), R, C, stream());
+  return out;
+}
+
 Tensor swiglu_fwd(const Tensor& gu) {
   check_gpu(gu, "gu");
   c10::DeviceGuard g(gu.device());
@@ -591,6 +602,7 @@ TORCH_LIBRARY(bllm, m) {
   m.def("layernorm_bwd(Tensor dy, Tensor x, Tensor w, Tensor mean, Tensor rstd, Tensor? dx_acc, Tensor(a!)? dw_out, Tensor(b!)? db_out, bool accumulate) -> (Tensor, Tensor, Tensor)");
   m.def("dropout_add(Tensor x, Tensor a, float p, int seed, int offset) -> Tensor");
   m.def("dropout_bwd(Tensor dy, float p, int seed, int offset) -> Tensor");
+  m.def("transpose2d(Tensor a) -> Tensor");
   m.def("swiglu_fwd(Tensor gu) -> Tensor");
   m.def("swiglu_bwd(Tensor gu, Tensor dact) -> Tensor");
   m.def("gelu_fwd(Tensor f) -> Tensor");
@@ -622,6 +634,7 @@ TORCH_LIBRARY_IMPL(bllm, CUDA, m) {
   m.impl("layernorm_bwd", &layernorm_bwd);
   m.impl("dropout_add", &dropout_add);
   m.impl("dropout_bwd", &dropout_bwd);
+  m.impl("transpose2d", &transpose2d);
   m.impl("swiglu_fwd", &swiglu_fwd);
   m.impl("swiglu_bwd", &swiglu_bwd);
   m.impl("gelu_fwd", &gelu_fwd);

@@ -315,4 +315,44 @@ void sum_partials_into(DType pdt, DType odt, const void* part, void* out, long n
   });
 }
 
+// ---------------------------------------------------------------- 2-D transpose (16-bit)
+// out[C, R] = in[R, C]^T for bf16/fp16 (bit copy).  Used to give the input-gradient GEMM a
+// K-contiguous weight (dX = dY W runs in hipBLASLt's fast "both operands K-contiguous" layout).
+// 64x64 tile per workgroup through LDS: 16-byte row loads, LDS row stride 66 halves (33 dwords)
+// so the column gathers of one wave land on distinct banks, 16-byte row stores.
+constexpr int TP_T = 64, TP_LD = TP_T + 2;
+__global__ __launch_bounds__(256) void transpose16_k(const uint16_t* __restrict__ in, uint16_t* __restrict__ out,
+                                                     long R, long C) {
+  __shared__ uint16_t tile[TP_T * TP_LD];
+  const long ntc = (C + TP_T - 1) / TP_T;
+  const long r0 = (long)(blockIdx.x / ntc) * TP_T, c0 = (long)(blockIdx.x % ntc) * TP_T;
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int v = t + k * 256, row = v >> 3, cv = (v & 7) * 8;
+    uint4 x = make_uint4(0, 0, 0, 0);
+    if (r0 + row < R && c0 + cv < C) x = *reinterpret_cast<const uint4*>(in + (r0 + row) * C + c0 + cv);
+    uint32_t* d = reinterpret_cast<uint32_t*>(tile + row * TP_LD + cv);
+    d[0] = x.x; d[1] = x.y; d[2] = x.z; d[3] = x.w;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int ov = (t & 7) * 8, orow = (t >> 3) + k * 32;
+    if (c0 + orow >= C || r0 + ov >= R) continue;
+    uint16_t e[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) e[j] = tile[(ov + j) * TP_LD + orow];
+    uint4 y;
+    y.x = e[0] | ((uint32_t)e[1] << 16); y.y = e[2] | ((uint32_t)e[3] << 16);
+    y.z = e[4] | ((uint32_t)e[5] << 16); y.w = e[6] | ((uint32_t)e[7] << 16);
+    *reinterpret_cast<uint4*>(out + (c0 + orow) * R + r0 + ov) = y;
+  }
+}
+
+void transpose16(const void* in, void* out, long R, long C, hipStream_t s) {
+  const long nt = ((R + TP_T - 1) / TP_T) * ((C + TP_T - 1) / TP_T);
+  hipLaunchKernelGGL(transpose16_k, dim3((unsigned)nt), dim3(256), 0, s, (const uint16_t*)in, (uint16_t*)out, R, C);
+}
+
 }  // namespace bllm

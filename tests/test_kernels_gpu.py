@@ -417,3 +417,33 @@ def test_dgrad_in_linear_backward(monkeypatch):
     acc = torch.randn(512, 1280, device=DEV).to(torch.bfloat16)
     dx2 = _input_grad(dy, W, acc)
     _close(dx2, acc.float() + dy.float() @ W.float(), torch.bfloat16, 1, name="dX+acc")
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("R,C", [(64, 64), (8, 16), (200, 136), (4096, 1032), (6144, 4096)])
+def test_transpose2d(dt, R, C):
+    a = torch.randn(R, C, device=DEV).to(dt)
+    t = ops.transpose2d(a)
+    assert t.shape == (C, R) and t.is_contiguous()
+    assert torch.equal(t, a.t().contiguous())
+
+
+def test_dgrad_transposed_weight_path(monkeypatch):
+    """Above DGRAD_WT_MIN_TOKENS the input gradient runs on a transposed weight copy."""
+    from building_llm_from_scratch_amd.models import linear
+    monkeypatch.setenv("BLLM_DGRAD_GEMM", "0")
+    monkeypatch.setattr(linear, "DGRAD_WT_MIN_TOKENS", 256)
+    calls = []
+    orig = ops.transpose2d
+    monkeypatch.setattr(ops, "transpose2d", lambda w: calls.append(w.shape) or orig(w))
+    dy = torch.randn(512, 768, device=DEV).to(torch.bfloat16)
+    W = torch.randn(768, 1280, device=DEV).to(torch.bfloat16)
+    assert linear._dgrad_wt_ok(dy, W)
+    dx = linear._input_grad(dy, W)
+    _close(dx, dy.float() @ W.float(), torch.bfloat16, 1, name="dX")
+    acc = torch.randn(512, 1280, device=DEV).to(torch.bfloat16)
+    _close(linear._input_grad(dy, W, acc), acc.float() + dy.float() @ W.float(), torch.bfloat16, 1, name="dX+acc")
+    out = acc.clone()
+    linear._input_grad(dy, W, out=out)
+    _close(out, acc.float() + dy.float() @ W.float(), torch.bfloat16, 1, name="out+=dX")
+    assert len(calls) == 3

@@ -8,8 +8,13 @@ K-contiguous), so the choice of layout is measured rather than guessed.
 Usage: python tools/bench_gemm.py [--iters 20]"""
 import argparse
 import json
+import os
+import sys
 
 import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from building_llm_from_scratch_amd import ops  # noqa: E402
 
 
 def timeit(fn, iters):
@@ -31,6 +36,7 @@ def main():
     ap.add_argument("--tokens", type=int, default=4096)
     ap.add_argument("--backend", choices=["default", "hipblaslt", "rocblas"], default="default")
     a = ap.parse_args()
+    ops.load_ext(required=True)
     if a.backend != "default":
         torch.backends.cuda.preferred_blas_library("cublaslt" if a.backend == "hipblaslt" else "cublas")
     N = a.tokens
@@ -56,10 +62,13 @@ def main():
         dwt = torch.empty(k_in, n_out, device="cuda", dtype=dt)
         r["dwT_xTdy"] = timeit(lambda: torch.mm(x.t(), dy, out=dwt), a.iters)
         r["transpose_w"] = timeit(lambda: wt.copy_(w.t()), a.iters)
+        r["transpose_w_hip"] = timeit(lambda: ops.transpose2d(w), a.iters)
+        assert torch.equal(ops.transpose2d(w), wt)
+        r["transpose_w_hip_TBps"] = round(4 * w.numel() / r["transpose_w_hip"] / 1e9, 2)
         for k in ("fwd_xWt", "dx_dyW", "dx_dyWt_T", "dw_dyTx", "dw_xTdy_outT", "dwT_xTdy"):
             r[k + "_tflops"] = round(fl / r[k] / 1e9, 1)
         for k in list(r):
-            if isinstance(r[k], float) and not k.endswith("tflops"):
+            if isinstance(r[k], float) and not k.endswith(("tflops", "TBps")):
                 r[k] = round(r[k] * 1e3, 1)  # us
         print(json.dumps(r), flush=True)
         out.append(r)
