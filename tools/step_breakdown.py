@@ -14,6 +14,8 @@ def classify(n):
         return "wgrad_mfma (dW GEMM, csrc/gemm_wgrad.hip)"
     if "sum_partials" in n:
         return "sum_partials (split-K)"
+    if "transpose16" in n:
+        return "weight transpose (dX operand, csrc/elementwise.hip)"
     for k in ("adamw", "sqsum", "attn_bwd_mfma", "attn_bwd_dq", "attn_fwd", "attn_delta", "kv_reduce", "swiglu_fwd",
               "swiglu_bwd", "gelu", "rope", "norm_fwd", "norm_bwd", "col_reduce", "ce_fwd", "ce_bwd", "emb_",
               "copyBuffer", "dropout"):
