@@ -3,9 +3,19 @@
 // Replaces reference common_components.py:6-35 (RoPE), :78-124 (SiLU/SwiGLU),
 // GPT2.py:58-62 (nn.GELU, exact erf), and nn.Dropout.  All are HBM-bound: 16-byte
 // accesses per lane, grid-stride loops capped at 256 CUs x 8 workgroups.
+#include <cstdlib>
 #include "api.h"
 
 namespace bllm {
+
+// BLLM_SWIGLU_ROWS=0 selects the grid-stride SwiGLU kernels (A/B tuning)
+static bool swiglu_rows() {
+  static const bool v = [] {
+    const char* e = getenv("BLLM_SWIGLU_ROWS");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
 
 static inline int ew_grid(long nvec) {
   long g = (nvec + 255) / 256;
@@ -50,6 +60,81 @@ __global__ __launch_bounds__(256) void swiglu_bwd_k(const T* __restrict__ gu, co
     }
     stv<T, VEC>(dgu + r * 2 * F + c, dg);
     stv<T, VEC>(dgu + r * 2 * F + F + c, du);
+  }
+}
+
+// Row-per-workgroup variants for wide FFNs (F/VEC >= 512, e.g. Llama F=14336): no 64-bit index
+// division, U independent 16-B load pairs in flight per lane before any math (the grid-stride loop
+// above serialises load -> compute per vector).  One workgroup per token row; N rows >> 256 CUs.
+template <typename T, int VEC, int U>
+__global__ __launch_bounds__(256) void swiglu_fwd_rows_k(const T* __restrict__ gu, T* __restrict__ act, int F) {
+  const int fv = F / VEC;
+  const T* g0 = gu + (long)blockIdx.x * 2 * F;
+  const T* u0 = g0 + F;
+  T* o0 = act + (long)blockIdx.x * F;
+  for (int base = threadIdx.x; base < fv; base += 256 * U) {
+    VecN<T, VEC> g[U], u[U];
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      const int c = base + k * 256;
+      if (c < fv) {
+        g[k] = ldv<T, VEC>(g0 + c * VEC);
+        u[k] = ldv<T, VEC>(u0 + c * VEC);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      const int c = base + k * 256;
+      if (c < fv) {
+        VecN<T, VEC> o;
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) {
+          const float a = to_f(g[k].v[j]);
+          o.v[j] = from_f<T>(a / (1.f + __expf(-a)) * to_f(u[k].v[j]));
+        }
+        stv<T, VEC>(o0 + c * VEC, o);
+      }
+    }
+  }
+}
+
+template <typename T, int VEC, int U>
+__global__ __launch_bounds__(256) void swiglu_bwd_rows_k(const T* __restrict__ gu, const T* __restrict__ dact,
+                                                         T* __restrict__ dgu, int F) {
+  const int fv = F / VEC;
+  const long row = blockIdx.x;
+  const T* g0 = gu + row * 2 * F;
+  const T* u0 = g0 + F;
+  const T* d0 = dact + row * F;
+  T* dg0 = dgu + row * 2 * F;
+  T* du0 = dg0 + F;
+  for (int base = threadIdx.x; base < fv; base += 256 * U) {
+    VecN<T, VEC> g[U], u[U], d[U];
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      const int c = base + k * 256;
+      if (c < fv) {
+        g[k] = ldv<T, VEC>(g0 + c * VEC);
+        u[k] = ldv<T, VEC>(u0 + c * VEC);
+        d[k] = ldv<T, VEC>(d0 + c * VEC);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      const int c = base + k * 256;
+      if (c < fv) {
+        VecN<T, VEC> dg, du;
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) {
+          const float a = to_f(g[k].v[j]), b = to_f(u[k].v[j]), dd = to_f(d[k].v[j]);
+          const float sg = 1.f / (1.f + __expf(-a));
+          dg.v[j] = from_f<T>(dd * b * sg * (1.f + a * (1.f - sg)));
+          du.v[j] = from_f<T>(dd * a * sg);
+        }
+        stv<T, VEC>(dg0 + c * VEC, dg);
+        stv<T, VEC>(du0 + c * VEC, du);
+      }
+    }
   }
 }
 
@@ -214,16 +299,26 @@ void bias_grad(DType dt, DType odt, const void* dy, float* part, void* out, int 
 void swiglu_fwd(DType dt, const void* gu, void* act, long N, int F, hipStream_t s) {
   BLLM_DISPATCH(dt, T, {
     EW_VEC(T, F % (16 / sizeof(T)) == 0, {
-      hipLaunchKernelGGL((swiglu_fwd_k<T, VEC>), dim3(ew_grid(N * F / VEC)), dim3(256), 0, s, (const T*)gu,
-                         (T*)act, N, F);
+      if (swiglu_rows() && F / VEC >= 512 && N <= 0x7fffffffL) {
+        hipLaunchKernelGGL((swiglu_fwd_rows_k<T, VEC, 4>), dim3((unsigned)N), dim3(256), 0, s, (const T*)gu,
+                           (T*)act, F);
+      } else {
+        hipLaunchKernelGGL((swiglu_fwd_k<T, VEC>), dim3(ew_grid(N * F / VEC)), dim3(256), 0, s, (const T*)gu,
+                           (T*)act, N, F);
+      }
     });
   });
 }
 void swiglu_bwd(DType dt, const void* gu, const void* dact, void* dgu, long N, int F, hipStream_t s) {
   BLLM_DISPATCH(dt, T, {
     EW_VEC(T, F % (16 / sizeof(T)) == 0, {
-      hipLaunchKernelGGL((swiglu_bwd_k<T, VEC>), dim3(ew_grid(N * F / VEC)), dim3(256), 0, s, (const T*)gu,
-                         (const T*)dact, (T*)dgu, N, F);
+      if (swiglu_rows() && F / VEC >= 512 && N <= 0x7fffffffL) {
+        hipLaunchKernelGGL((swiglu_bwd_rows_k<T, VEC, 4>), dim3((unsigned)N), dim3(256), 0, s, (const T*)gu,
+                           (const T*)dact, (T*)dgu, F);
+      } else {
+        hipLaunchKernelGGL((swiglu_bwd_k<T, VEC>), dim3(ew_grid(N * F / VEC)), dim3(256), 0, s, (const T*)gu,
+                           (const T*)dact, (T*)dgu, N, F);
+      }
     });
   });
 }

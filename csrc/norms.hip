@@ -6,12 +6,23 @@
 // over (x, dy[, dx_acc]) in backward (one workgroup per row there).  Weight/bias gradients:
 // per-thread register accumulators for the columns a thread owns -> one fp32 partial row per
 // workgroup -> a column-reduction kernel (deterministic, no global atomics).
+#include <cstdlib>
 #include "common.h"
 
 namespace bllm {
 
 constexpr int ROWS_PER_WG = 4;  // 4 waves x 1 row
-constexpr int MAX_BWD_WG = 512;
+// backward workgroups (rows are grid-strided over them): 1024 = 4 WGs / 16 waves per CU on 256 CUs,
+// enough loads in flight for a d=4096 row pass; each WG adds one fp32 dW partial row (16 MiB at
+// d=4096), which col_reduce_k streams once.  BLLM_NORM_BWD_WG overrides (A/B tuning).
+static int max_bwd_wg() {
+  static const int v = [] {
+    const char* e = getenv("BLLM_NORM_BWD_WG");
+    const int n = e ? atoi(e) : 0;
+    return n > 0 ? n : 1024;
+  }();
+  return v;
+}
 
 template <typename T, int NV, bool LN>
 __global__ __launch_bounds__(256) void norm_fwd_k(const T* __restrict__ x, const T* __restrict__ w,
@@ -260,7 +271,8 @@ static void bwd_dispatch(const void* dy, const void* x, const void* w, const flo
 
 int norm_bwd_num_wg(int N) {
   int n = N;
-  return n < MAX_BWD_WG ? n : MAX_BWD_WG;
+  const int m = max_bwd_wg();
+  return n < m ? n : m;
 }
 
 // max supported row length per dtype (NV <= 16): 8192 (bf16/f16), 4096 (f32)

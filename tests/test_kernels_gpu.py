@@ -76,7 +76,7 @@ def test_layernorm(dt, d):
 
 
 @pytest.mark.parametrize("dt", DTYPES)
-@pytest.mark.parametrize("F", [10, 64, 1000])
+@pytest.mark.parametrize("F", [10, 64, 1000, 4104, 14336])
 def test_swiglu_gelu(dt, F):
     gu = torch.randn(33, 2 * F, device=DEV).to(dt)
     da = torch.randn(33, F, device=DEV).to(dt)

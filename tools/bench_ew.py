@@ -1,0 +1,55 @@
+"""Micro-benchmark of the HBM-bound Llama-3-8B elementwise/norm kernels at the bench shape
+(24 x 1024 tokens): SwiGLU fwd/bwd on [N, 2*14336] and RMSNorm bwd (with the residual-gradient
+add) on [N, 4096], bf16.  Prints one JSON line with us/call and achieved GB/s per op.
+Kernel-path A/B knobs are read from the environment by the extension (BLLM_SWIGLU_ROWS,
+BLLM_NORM_BWD_WG), so compare configurations by running this once per setting.
+"""
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from building_llm_from_scratch_amd import ops  # noqa: E402
+
+
+def _time(fn, iters=20):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) * 1e3 / iters
+
+
+def main():
+    ops.load_ext(required=True)
+    N, F, d = 24 * 1024, 14336, 4096
+    dev, dt = "cuda:0", torch.bfloat16
+    gu = torch.randn(N, 2 * F, device=dev).to(dt)
+    da = torch.randn(N, F, device=dev).to(dt)
+    x = torch.randn(N, d, device=dev).to(dt)
+    dy = torch.randn(N, d, device=dev).to(dt)
+    acc = torch.randn(N, d, device=dev).to(dt)
+    w = torch.randn(d, device=dev).to(dt)
+    dw = torch.zeros(d, device=dev, dtype=dt)
+    _, rstd = ops.rmsnorm_fwd(x, w, 1e-5)
+    res = {"env": {k: os.environ.get(k) for k in ("BLLM_SWIGLU_ROWS", "BLLM_NORM_BWD_WG")}}
+    for name, fn, nbytes in (
+        ("swiglu_fwd", lambda: ops.swiglu_fwd(gu), 3 * N * F * 2),
+        ("swiglu_bwd", lambda: ops.swiglu_bwd(gu, da), 5 * N * F * 2),
+        ("rmsnorm_fwd", lambda: ops.rmsnorm_fwd(x, w, 1e-5), 2 * N * d * 2),
+        ("rmsnorm_bwd", lambda: ops.rmsnorm_bwd(dy, x, w, rstd, acc, dw, True), 4 * N * d * 2),
+    ):
+        us = _time(fn)
+        res[name] = {"us": round(us, 1), "GBps": round(nbytes / us / 1e3, 1)}
+    print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()
