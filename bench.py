@@ -19,6 +19,10 @@ peak), B=24 25.5k (217 GiB), B=32 25.7k (249 GiB).  B=24 keeps ~70 GB of headroo
 single-GPU (unsharded) run; it also keeps FSDP's per-block all-gathers (416 MiB) and
 reduce-scatters hidden under block compute at 2 GPUs, where two ranks share a single xGMI
 link.  ``--batch_size 4`` reproduces the reference default.
+
+Activation checkpointing: off by default, like the reference (``--use_actv_ckpt`` is opt-in,
+args.py:76).  Same-box A/B at B=24 (profiles/r1_bench_v7_ckpt_*.log): none 26.94k tok/s at
+229 GiB peak vs selective (norm outputs recomputed) 26.74k at 217 GiB.
 """
 from __future__ import annotations
 
@@ -43,7 +47,8 @@ def parse():
     ap.add_argument("--num_params", default="8B")
     ap.add_argument("--batch_size", type=int, default=24, help="micro-batch per GPU (reference CLI default: 4)")
     ap.add_argument("--seq_len", type=int, default=1024)
-    ap.add_argument("--actv_ckpt", default="selective", choices=["none", "selective", "full"])
+    ap.add_argument("--actv_ckpt", default="none", choices=["none", "selective", "full"],
+                    help="none = the reference default (use_actv_ckpt off); selective recomputes the norms")
     ap.add_argument("--parallel", default="fsdp", choices=["fsdp", "ddp", "zero1"])
     ap.add_argument("--reshard_after_forward", type=int, default=1)
     ap.add_argument("--layers", type=int, default=None, help="(debug only) override n_layers; invalidates the metric")
