@@ -216,7 +216,7 @@ class FusedLinear:
             y.addmm_(x, W.t())
             return y, ("grouped", t, P)
         if residual is not None:
-            y = torch.addmm(residual, x, W.t())
+            y = ops.linear_residual(x, W, residual)
         elif b is not None:
             y = torch.addmm(b, x, W.t())
         else:

@@ -207,6 +207,19 @@ def dgrad_gemm_enabled() -> bool:
     return os.environ.get("BLLM_DGRAD_GEMM", "0") == "1"
 
 
+_LT_RESIDUAL = os.environ.get("BLLM_LT_RESIDUAL", "1") != "0"
+
+
+def linear_residual(x: torch.Tensor, W: torch.Tensor, C: torch.Tensor) -> torch.Tensor:
+    """``C + x @ W^T`` as one hipBLASLt matmul that reads C in its epilogue and writes a new D
+    (csrc/binding.cpp linear_residual).  ``torch.addmm(C, x, W.t())`` copies C into the output
+    first (one extra HBM pass of C).  BLLM_LT_RESIDUAL=0 selects torch.addmm (A/B)."""
+    if (_LT_RESIDUAL and _hip(x) and x.dtype in (torch.bfloat16, torch.float16) and W.dtype == x.dtype
+            and C.dtype == x.dtype and x.is_contiguous() and W.is_contiguous() and C.is_contiguous()):
+        return _k().linear_residual(x, W, C)
+    return torch.addmm(C, x, W.t())
+
+
 def transpose2d(a: torch.Tensor) -> torch.Tensor:
     """Contiguous a^T for a 2-D 16-bit tensor (csrc/elementwise.hip transpose16_k: 64x64 LDS
     tiles, 16-byte loads and stores); dims must be multiples of 8."""

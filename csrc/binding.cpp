@@ -8,6 +8,11 @@
 #include <c10/hip/HIPStream.h>
 #include <c10/core/DeviceGuard.h>
 #include <torch/library.h>
+#include <hipblaslt/hipblaslt.h>
+
+#include <map>
+#include <mutex>
+#include <tuple>
 
 #include "common.h"
 #include "api.h"
@@ -595,6 +600,86 @@ void adamw_step_(Tensor& param, const optional<Tensor>& master, const Tensor& gr
 
 }  // namespace
 
+
+// ----------------------------------------------------------------------------- residual GEMM
+// D[N, O] = x[N, K] @ W[O, K]^T + C[N, O] as ONE hipBLASLt matmul with C != D.  torch.addmm with
+// a 2-D `self` first copies C into the output and then runs a beta=1 GEMM in place (a 200 MB
+// copy kernel per o/down projection at Llama-3-8B B=24, profiles/r1_llama3_8b_1gpu_v7.md); here
+// the GEMM reads C in its epilogue.  Column-major view: D^T (O x N) = op_T(W: K x O) * x^T (K x N),
+// the same TN family torch picks for nn.Linear.  Heuristic top-1 solution, cached per shape.
+#define LT_CHECK(x)                                                                  \
+  do {                                                                               \
+    hipblasStatus_t st_ = (x);                                                       \
+    TORCH_CHECK(st_ == HIPBLAS_STATUS_SUCCESS, "hipBLASLt: ", #x, " failed (", (int)st_, ")"); \
+  } while (0)
+
+namespace {
+constexpr size_t kLtWorkspace = 64ull << 20;
+struct LtPlan {
+  hipblasLtMatmulDesc_t op = nullptr;
+  hipblasLtMatrixLayout_t a = nullptr, b = nullptr, c = nullptr;
+  hipblasLtMatmulAlgo_t algo;
+};
+std::mutex lt_mu;
+hipblasLtHandle_t lt_handle(int dev) {
+  static hipblasLtHandle_t h[64] = {};
+  std::lock_guard<std::mutex> g(lt_mu);
+  if (!h[dev]) LT_CHECK(hipblasLtCreate(&h[dev]));
+  return h[dev];
+}
+const LtPlan& lt_plan(int dev, hipDataType dt, int64_t N, int64_t K, int64_t O) {
+  static std::map<std::tuple<int, int, int64_t, int64_t, int64_t>, LtPlan> cache;
+  const auto key = std::make_tuple(dev, (int)dt, N, K, O);
+  {
+    std::lock_guard<std::mutex> g(lt_mu);
+    auto it = cache.find(key);
+    if (it != cache.end()) return it->second;
+  }
+  hipblasLtHandle_t h = lt_handle(dev);
+  LtPlan p;
+  LT_CHECK(hipblasLtMatmulDescCreate(&p.op, HIPBLAS_COMPUTE_32F, HIP_R_32F));
+  hipblasOperation_t ta = HIPBLAS_OP_T, tb = HIPBLAS_OP_N;
+  LT_CHECK(hipblasLtMatmulDescSetAttribute(p.op, HIPBLASLT_MATMUL_DESC_TRANSA, &ta, sizeof(ta)));
+  LT_CHECK(hipblasLtMatmulDescSetAttribute(p.op, HIPBLASLT_MATMUL_DESC_TRANSB, &tb, sizeof(tb)));
+  LT_CHECK(hipblasLtMatrixLayoutCreate(&p.a, dt, K, O, K));  // W [O, K] row-major
+  LT_CHECK(hipblasLtMatrixLayoutCreate(&p.b, dt, K, N, K));  // x [N, K] row-major
+  LT_CHECK(hipblasLtMatrixLayoutCreate(&p.c, dt, O, N, O));  // C, D [N, O] row-major
+  hipblasLtMatmulPreference_t pref;
+  LT_CHECK(hipblasLtMatmulPreferenceCreate(&pref));
+  uint64_t ws = kLtWorkspace;
+  LT_CHECK(hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &ws, sizeof(ws)));
+  hipblasLtMatmulHeuristicResult_t res[1];
+  int n = 0;
+  LT_CHECK(hipblasLtMatmulAlgoGetHeuristic(h, p.op, p.a, p.b, p.c, p.c, pref, 1, res, &n));
+  hipblasLtMatmulPreferenceDestroy(pref);
+  TORCH_CHECK(n > 0, "hipBLASLt: no solution for residual GEMM N=", N, " K=", K, " O=", O);
+  p.algo = res[0].algo;
+  std::lock_guard<std::mutex> g(lt_mu);
+  return cache.emplace(key, p).first->second;
+}
+}  // namespace
+
+Tensor linear_residual(const Tensor& x, const Tensor& W, const Tensor& C) {
+  check_gpu(x, "x"); check_gpu(W, "W"); check_gpu(C, "C");
+  TORCH_CHECK(x.dim() == 2 && W.dim() == 2 && C.dim() == 2, "linear_residual: 2-D operands");
+  TORCH_CHECK(x.is_contiguous() && W.is_contiguous() && C.is_contiguous(), "linear_residual: contiguous operands");
+  TORCH_CHECK(x.scalar_type() == W.scalar_type() && x.scalar_type() == C.scalar_type(), "linear_residual: one dtype");
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kHalf, "linear_residual: bf16/fp16");
+  const int64_t N = x.size(0), K = x.size(1), O = W.size(0);
+  TORCH_CHECK(W.size(1) == K && C.size(0) == N && C.size(1) == O, "linear_residual: shape mismatch");
+  c10::DeviceGuard g(x.device());
+  const int dev = x.get_device();
+  TORCH_CHECK(dev >= 0 && dev < 64);
+  const hipDataType dt = x.scalar_type() == at::kBFloat16 ? HIP_R_16BF : HIP_R_16F;
+  const LtPlan& p = lt_plan(dev, dt, N, K, O);
+  auto D = at::empty({N, O}, x.options());
+  auto ws = at::empty({(int64_t)kLtWorkspace}, x.options().dtype(at::kByte));
+  const float alpha = 1.f, beta = 1.f;
+  LT_CHECK(hipblasLtMatmul(lt_handle(dev), p.op, &alpha, W.data_ptr(), p.a, x.data_ptr(), p.b, &beta, C.data_ptr(),
+                           p.c, D.data_ptr(), p.c, &p.algo, ws.data_ptr(), kLtWorkspace, stream()));
+  return D;
+}
+
 TORCH_LIBRARY(bllm, m) {
   m.def("rmsnorm_fwd(Tensor x, Tensor w, float eps) -> (Tensor, Tensor)");
   m.def("rmsnorm_bwd(Tensor dy, Tensor x, Tensor w, Tensor rstd, Tensor? dx_acc, Tensor(a!)? dw_out, bool accumulate) -> (Tensor, Tensor)");
@@ -603,6 +688,7 @@ TORCH_LIBRARY(bllm, m) {
   m.def("dropout_add(Tensor x, Tensor a, float p, int seed, int offset) -> Tensor");
   m.def("dropout_bwd(Tensor dy, float p, int seed, int offset) -> Tensor");
   m.def("transpose2d(Tensor a) -> Tensor");
+  m.def("linear_residual(Tensor x, Tensor W, Tensor C) -> Tensor");
   m.def("swiglu_fwd(Tensor gu) -> Tensor");
   m.def("swiglu_bwd(Tensor gu, Tensor dact) -> Tensor");
   m.def("gelu_fwd(Tensor f) -> Tensor");
@@ -635,6 +721,7 @@ TORCH_LIBRARY_IMPL(bllm, CUDA, m) {
   m.impl("dropout_add", &dropout_add);
   m.impl("dropout_bwd", &dropout_bwd);
   m.impl("transpose2d", &transpose2d);
+  m.impl("linear_residual", &linear_residual);
   m.impl("swiglu_fwd", &swiglu_fwd);
   m.impl("swiglu_bwd", &swiglu_bwd);
   m.impl("gelu_fwd", &gelu_fwd);

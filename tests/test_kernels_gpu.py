@@ -447,3 +447,19 @@ def test_dgrad_transposed_weight_path(monkeypatch):
     linear._input_grad(dy, W, out=out)
     _close(out, acc.float() + dy.float() @ W.float(), torch.bfloat16, 1, name="out+=dX")
     assert len(calls) == 3
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("N,K,O", [(33, 64, 40), (256, 512, 768), (1024, 4096, 4096)])
+def test_linear_residual_hipblaslt(dt, N, K, O):
+    """C + x W^T on hipBLASLt with C != D (csrc/binding.cpp linear_residual) vs fp32 torch."""
+    x = torch.randn(N, K, device=DEV).to(dt)
+    W = (torch.randn(O, K, device=DEV) / K ** 0.5).to(dt)
+    C = torch.randn(N, O, device=DEV).to(dt)
+    C0 = C.clone()
+    y = torch.ops.bllm.linear_residual(x, W, C)
+    assert y.data_ptr() != C.data_ptr()
+    assert torch.equal(C, C0), "residual input must not be modified"
+    want = C.float().cpu() + x.float().cpu() @ W.float().cpu().t()
+    _close(y, want, dt, 2, name="linear_residual")
+    assert torch.equal(ops.linear_residual(x, W, C), y)

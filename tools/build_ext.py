@@ -102,7 +102,7 @@ def build(jobs: int = 8, clean: bool = False, debug: bool = False, verbose: bool
     link_needed = not os.path.exists(OUT) or any(os.path.getmtime(o) > os.path.getmtime(OUT) for o in objs)
     if link_needed:
         cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", OUT] + objs + [
-            f"-L{tlib}", "-lc10", "-lc10_hip", "-ltorch_cpu", "-ltorch_hip", "-ltorch", "-lamdhip64",
+            f"-L{tlib}", "-lc10", "-lc10_hip", "-ltorch_cpu", "-ltorch_hip", "-ltorch", "-lamdhip64", "-lhipblaslt",
             f"-Wl,-rpath,{tlib}"]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
