@@ -53,8 +53,8 @@ bool attn_bwd_kv_partials(int B, int T, int H, int G);
 void attn_delta(DType dt, const void* o, const void* dout, float* delta, int B, int T, int H, int hd,
                 hipStream_t s);
 
-// elementwise.hip — bias gradient (column sums), part must hold colsum_bands(N) * F floats
-int colsum_bands(int N);
+// elementwise.hip — bias gradient (column sums), part must hold colsum_bands(N, F) * F floats
+int colsum_bands(int N, int F);
 void bias_grad(DType dt, DType odt, const void* dy, float* part, void* out, int N, int F, bool accumulate,
                hipStream_t s);
 

@@ -228,7 +228,7 @@ void bias_grad_(const Tensor& dy, Tensor& db, bool accumulate) {
   TORCH_CHECK(dy.dim() == 2 && db.dim() == 1 && db.size(0) == dy.size(1), "bias_grad: shapes");
   const int N = (int)dy.size(0), F = (int)dy.size(1);
   TORCH_CHECK(F % (16 / (int)dy.element_size()) == 0, "bias_grad: F must be a multiple of 16 bytes");
-  auto part = at::empty({bllm::colsum_bands(N), F}, dy.options().dtype(at::kFloat));
+  auto part = at::empty({bllm::colsum_bands(N, F), F}, dy.options().dtype(at::kFloat));
   bllm::bias_grad(dt_of(dy), dt_of(db), dy.data_ptr(), part.data_ptr<float>(), db.data_ptr(), N, F, accumulate,
                   stream());
 }

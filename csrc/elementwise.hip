@@ -265,7 +265,17 @@ __global__ __launch_bounds__(256) void colsum_partial_k(const T* __restrict__ dy
   float acc[VEC];
 #pragma unroll
   for (int j = 0; j < VEC; ++j) acc[j] = 0.f;
-  for (int r = r0; r < r1; ++r) {
+  int r = r0;
+  for (; r + 4 <= r1; r += 4) {  // 4 independent 16-B loads in flight per lane
+    Vec16<T> v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = ld16(dy + (long)(r + k) * F + cv * VEC);
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) acc[j] += to_f(v[k].v[j]);
+  }
+  for (; r < r1; ++r) {
     const Vec16<T> v = ld16(dy + (long)r * F + cv * VEC);
 #pragma unroll
     for (int j = 0; j < VEC; ++j) acc[j] += to_f(v.v[j]);
@@ -275,12 +285,22 @@ __global__ __launch_bounds__(256) void colsum_partial_k(const T* __restrict__ dy
   for (int j = 0; j < VEC; ++j) o[j] = acc[j];
 }
 
-int colsum_bands(int N) { return N >= 16 * 256 ? 256 : (N + 15) / 16; }
+// row bands: narrow outputs (F <= 2048, e.g. GPT-2's 1280-wide biases: one 160-lane workgroup
+// per band) get 4x more bands so enough waves stream dy; partials stay small (1024 x F fp32)
+int colsum_bands(int N, int F) {
+  static const int small_cap = [] {  // BLLM_COLSUM_BANDS=<n> overrides the narrow-output cap (A/B)
+    const char* e = getenv("BLLM_COLSUM_BANDS");
+    const int n = e ? atoi(e) : 0;
+    return n > 0 ? n : 1024;
+  }();
+  const int cap = F <= 2048 ? small_cap : 256;
+  return N >= 16 * cap ? cap : (N + 15) / 16;
+}
 
 // dy [N, F] (F % (16/sizeof(T)) == 0), out [F] in dtype odt (written, or added when accumulate)
 void bias_grad(DType dt, DType odt, const void* dy, float* part, void* out, int N, int F, bool accumulate,
                hipStream_t s) {
-  const int P = colsum_bands(N);
+  const int P = colsum_bands(N, F);
   const int rows_per = (N + P - 1) / P;
   BLLM_DISPATCH(dt, T, {
     constexpr int VEC = 16 / sizeof(T);

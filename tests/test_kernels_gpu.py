@@ -215,7 +215,7 @@ def test_attn_decode(dt, B, H, G, hd, L, Tmax):
 
 
 @pytest.mark.parametrize("dt", DTYPES)
-@pytest.mark.parametrize("N,F", [(4096, 3840), (7, 64), (300, 5120)])
+@pytest.mark.parametrize("N,F", [(4096, 3840), (7, 64), (300, 5120), (16390, 1280)])
 @pytest.mark.parametrize("acc", [False, True])
 def test_bias_grad(dt, N, F, acc):
     dy = torch.randn(N, F, device=DEV).to(dt)

@@ -1,6 +1,6 @@
 """Micro-benchmark of the HBM-bound Llama-3-8B elementwise/norm kernels at the bench shape
 (24 x 1024 tokens): SwiGLU fwd/bwd on [N, 2*14336] and RMSNorm bwd (with the residual-gradient
-add) on [N, 4096], bf16.  Prints one JSON line with us/call and achieved GB/s per op.
+add) on [N, 4096], bf16; plus the GPT2-774M bias-gradient column sums ([N, 1280], [N, 5120]).  Prints one JSON line with us/call and achieved GB/s per op.
 Kernel-path A/B knobs are read from the environment by the extension (BLLM_SWIGLU_ROWS,
 BLLM_NORM_BWD_WG), so compare configurations by running this once per setting.
 """
@@ -39,12 +39,18 @@ def main():
     w = torch.randn(d, device=dev).to(dt)
     dw = torch.zeros(d, device=dev, dtype=dt)
     _, rstd = ops.rmsnorm_fwd(x, w, 1e-5)
+    g1 = torch.randn(N, 1280, device=dev).to(dt)     # GPT2-774M out/fc2 bias grads
+    g5 = torch.randn(N, 5120, device=dev).to(dt)     # GPT2-774M fc1 bias grad
+    db1 = torch.zeros(1280, device=dev, dtype=dt)
+    db5 = torch.zeros(5120, device=dev, dtype=dt)
     res = {"env": {k: os.environ.get(k) for k in ("BLLM_SWIGLU_ROWS", "BLLM_NORM_BWD_WG")}}
     for name, fn, nbytes in (
         ("swiglu_fwd", lambda: ops.swiglu_fwd(gu), 3 * N * F * 2),
         ("swiglu_bwd", lambda: ops.swiglu_bwd(gu, da), 5 * N * F * 2),
         ("rmsnorm_fwd", lambda: ops.rmsnorm_fwd(x, w, 1e-5), 2 * N * d * 2),
         ("rmsnorm_bwd", lambda: ops.rmsnorm_bwd(dy, x, w, rstd, acc, dw, True), 4 * N * d * 2),
+        ("bias_grad_1280", lambda: ops.bias_grad_(g1, db1, True), N * 1280 * 2),
+        ("bias_grad_5120", lambda: ops.bias_grad_(g5, db5, True), N * 5120 * 2),
     ):
         us = _time(fn)
         res[name] = {"us": round(us, 1), "GBps": round(nbytes / us / 1e3, 1)}
