@@ -221,10 +221,11 @@ def get_config(model: str, num_params: str,
     if model.startswith("llama"):
         cfg = _llama(model, num_params)
         if context_length is not None and cfg.context_length != context_length:
-            cfg = cfg.replace(
-                rope_base=rescale_theta(cfg.rope_base, cfg.context_length, context_length),
-                context_length=context_length,
-            )
+            # Llama-2's attention always builds its tables with theta 10000 at the clamped
+            # ctx and never reads rope_base (reference Llama2.py:34,86): no rescale there
+            base = cfg.rope_base if model == "llama2" else \
+                rescale_theta(cfg.rope_base, cfg.context_length, context_length)
+            cfg = cfg.replace(rope_base=base, context_length=context_length)
         return cfg
     raise ValueError(f"Unsupported model '{model}'")
 
