@@ -1,28 +1,42 @@
 #!/usr/bin/env python3
-"""Headline benchmark: whole-node training tokens/s, Llama-3-8B bf16 FSDP (BASELINE.json).
+"""Headline benchmark (BASELINE.json): whole-node training tokens/s, Llama-3-8B bf16 FSDP
+full-shard + activation checkpointing, at 1/2/4/8 MI355X.
 
     python bench.py --gpus N --steps K --warmup W
-    torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
 
-Each rank runs a micro-batch of 24 sequences x ``T = 1024`` (the reference clamps every Llama
-to ctx 1024, Models/Llama/config.py:115-124) of synthetic token ids through one full training
-step — forward, fused CE, backward, global-norm clip 1.0,
-AdamW(wd 0.1) with fp32 master weights — on random-init weights of the full Llama-3-8B
-architecture.  Nothing is skipped inside the timed region.  W untimed warm-up steps, then
-exactly K timed steps bracketed by barrier + device sync; the slowest rank's time is used.
-Weak scaling: per-GPU work is fixed, total tokens grow with N.
+Every run — N=1 included — initialises a process group (RCCL; gloo with ``--device cpu``) and
+trains through the SAME ``FSDPEngine`` (parallel/fsdp.py).  At N=1 that engine behaves like
+torch FSDP at world size 1, which clamps FULL_SHARD to NO_SHARD (torch/distributed/fsdp/
+_init_utils.py:426-437): the single rank's shard is the whole flat, so no collective runs.
 
-Micro-batch: the reference's ``--batch_size`` default of 4 (args.py:53) was sized for a 16 GB
-T4.  One MI355X holds 288 GB, so the benchmark sizes the per-GPU micro-batch for that
-(measured on one GPU, profiles/r1_llama3_8b_1gpu_v4.md): B=4 20.0k tok/s, B=16 25.0k (184 GiB
-peak), B=24 25.5k (217 GiB), B=32 25.7k (249 GiB).  B=24 keeps ~70 GB of headroom on the
-single-GPU (unsharded) run; it also keeps FSDP's per-block all-gathers (416 MiB) and
-reduce-scatters hidden under block compute at 2 GPUs, where two ranks share a single xGMI
-link.  ``--batch_size 4`` reproduces the reference default.
+One step = forward, fused CE, backward (with full activation-checkpoint recompute: only each
+block's input is saved, every block's forward is re-run in backward — the reference's
+``checkpoint_sequential(segments=n_layers)``, Llama3.py:198-199), global-norm clip 1.0 (one
+scalar all-reduce) and AdamW(wd 0.1) with fp32 master weights on this rank's shard, on
+random-init weights of the full architecture and synthetic token ids.  W untimed warm-up
+steps, then exactly K timed steps bracketed by barrier + device sync; the slowest rank's time
+is reported.  Weak scaling: the per-GPU micro-batch is fixed, total tokens grow with N.
 
-Activation checkpointing: off by default, like the reference (``--use_actv_ckpt`` is opt-in,
-args.py:76).  Same-box A/B at B=24 (profiles/r1_bench_v7_ckpt_*.log): none 26.94k tok/s at
-229 GiB peak vs selective (norm outputs recomputed) 26.74k at 217 GiB.
+Micro-batch: the reference's ``--batch_size`` default 4 (args.py:53) was sized for a 16 GB T4;
+one MI355X holds 288 GB, so each rank runs 24 x 1024 tokens (``--batch_size 4`` reproduces the
+reference default).
+
+``mfu`` counts model FLOPs only (6·N_nonemb + 12·L·d·T per token, no recompute); ``hfu`` adds
+the re-run forward of full checkpointing (x 4/3).  Peak is 2.5 PF dense bf16.
+
+Other BASELINE configs (``--preset``; each prints one JSON line of its own):
+  gpt2_774m_ddp          #2  GPT2-774M pretrain, DDP, bf16, dropout 0.1
+  llama32_1b_lora_alpaca #4  Llama-3.2-1B Alpaca instruction finetune, LoRA r=16 a=32: variable
+                             length batches through the reference collate (pad to batch max,
+                             -100 masking) from synthetic Alpaca-shaped records, DataLoader in
+                             the timed loop; tokens counted like the reference's tokens_seen
+                             (padded B x T)
+  llama2_7b_fsdp_mp      #5  Llama-2-7B pretrain, FSDP full shard (params, grads AND optimizer
+                             state sharded = ZeRO-3, a superset of the ZeRO optimizer) +
+                             ``--mixed_precision bf16`` policy
+``--device cpu`` runs a tiny config of the same model family on gloo (multi-process plumbing
+check only; never a headline number).
 """
 from __future__ import annotations
 
@@ -31,118 +45,230 @@ import json
 import os
 import sys
 import time
+from datetime import timedelta
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 BASELINE_TOKENS_PER_S = None  # the reference publishes no number
+METRIC = "tokens/sec (whole node) Llama-3-8B bf16 FSDP at 1/2/4/8 MI355X"
+PEAK_BF16 = 2.5e15
+
+PRESETS = {
+    "llama3_8b_fsdp": dict(model="llama3", num_params="8B", parallel="fsdp", actv_ckpt="full", batch_size=24,
+                           data="pretrain", mixed_precision=None, lora_rank=0),
+    "gpt2_774m_ddp": dict(model="GPT2", num_params="774M", parallel="ddp", actv_ckpt="none", batch_size=24,
+                          data="pretrain", mixed_precision=None, lora_rank=0),
+    "llama32_1b_lora_alpaca": dict(model="llama3_2", num_params="1B", parallel="ddp", actv_ckpt="none",
+                                   batch_size=24, data="alpaca", mixed_precision=None, lora_rank=16),
+    "llama2_7b_fsdp_mp": dict(model="llama2", num_params="7B", parallel="fsdp", actv_ckpt="none", batch_size=24,
+                              data="pretrain", mixed_precision="bf16", lora_rank=0),
+}
+NICE = {"llama3": "Llama-3-8B", "GPT2": "GPT2-774M", "llama3_2": "Llama-3.2-1B", "llama2": "Llama-2-7B"}
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--model", default="llama3")
-    ap.add_argument("--num_params", default="8B")
-    ap.add_argument("--batch_size", type=int, default=24, help="micro-batch per GPU (reference CLI default: 4)")
+    ap.add_argument("--preset", default="llama3_8b_fsdp", choices=sorted(PRESETS))
+    ap.add_argument("--model", default=None)
+    ap.add_argument("--num_params", default=None)
+    ap.add_argument("--batch_size", type=int, default=None, help="micro-batch per GPU (reference CLI default: 4)")
     ap.add_argument("--seq_len", type=int, default=1024)
-    ap.add_argument("--actv_ckpt", default="none", choices=["none", "selective", "full"],
-                    help="none = the reference default (use_actv_ckpt off); selective recomputes the norms")
-    ap.add_argument("--parallel", default="fsdp", choices=["fsdp", "ddp", "zero1"])
+    ap.add_argument("--actv_ckpt", default=None, choices=["none", "selective", "full"],
+                    help="full = reference checkpoint_sequential semantics (headline); selective recomputes norms")
+    ap.add_argument("--parallel", default=None, choices=["fsdp", "ddp", "zero1"])
+    ap.add_argument("--mixed_precision", default=None, choices=["bf16", "fp16", "bf16_hybrid", "fp32"])
+    ap.add_argument("--lora_rank", type=int, default=None)
+    ap.add_argument("--lora_alpha", type=int, default=32)
     ap.add_argument("--reshard_after_forward", type=int, default=1)
     ap.add_argument("--layers", type=int, default=None, help="(debug only) override n_layers; invalidates the metric")
-    ap.add_argument("--profile", action="store_true", help="print a per-phase timing breakdown")
-    ap.add_argument("--lora_rank", type=int, default=0, help="LoRA finetune benchmark (freeze base, rank r)")
-    ap.add_argument("--lora_alpha", type=int, default=32)
+    ap.add_argument("--profile", action="store_true", help="print a per-phase timing breakdown to stderr")
     ap.add_argument("--overlap_optimizer", action="store_true",
                     help="run AdamW on a side HIP stream under the next forward")
-    return ap.parse_args()
+    ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
+                    help="cpu: tiny config on gloo (distributed plumbing check, not a measurement)")
+    ap.add_argument("--pg_timeout_min", type=float, default=20.0)
+    a = ap.parse_args(argv)
+    for k, v in PRESETS[a.preset].items():
+        if getattr(a, k, None) is None:
+            setattr(a, k, v)
+    return a
 
 
-def main():
-    a = parse()
+def init_dist(a):
+    """Process group for every N (world 1 included) with a collective timeout, so a wedged
+    collective raises instead of hanging the node."""
     import torch
     import torch.distributed as dist
-    from building_llm_from_scratch_amd import ops
-    from building_llm_from_scratch_amd.config import get_config
-    from building_llm_from_scratch_amd.models import build_model
-    from building_llm_from_scratch_amd.parallel import setup_engine
-    from building_llm_from_scratch_amd.train.optim import FusedAdamW
-
-    launched = "WORLD_SIZE" in os.environ and "RANK" in os.environ  # torchrun
+    launched = "WORLD_SIZE" in os.environ and "RANK" in os.environ
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     assert world == a.gpus, f"--gpus {a.gpus} but WORLD_SIZE={world} (launch with torchrun for N>1)"
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    distributed = launched or world > 1
-    if distributed:
+    if a.device == "cuda":
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
+    else:
+        dev = torch.device("cpu")
+    kw = dict(timeout=timedelta(minutes=a.pg_timeout_min))
+    if dev.type == "cuda":
+        kw["device_id"] = dev
+    backend = "nccl" if dev.type == "cuda" else "gloo"
+    if launched:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=dev)
-    ops.load_ext(required=True)
+        dist.init_process_group(backend, **kw)
+    else:
+        import socket
+        with socket.socket() as s:
+            s.bind(("127.0.0.1", 0))
+            port = s.getsockname()[1]
+        dist.init_process_group(backend, init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1, **kw)
+    return dist, dev, world, rank
 
-    cfg = get_config(a.model, a.num_params, context_length=a.seq_len).replace(dtype=torch.bfloat16)
+
+def build_config(a, dev):
+    import torch
+    from building_llm_from_scratch_amd.config import get_config
+    from building_llm_from_scratch_amd.parallel.mixed_precision import get_policy
+    cfg = get_config(a.model, a.num_params, context_length=a.seq_len)
+    dtype = get_policy(a.mixed_precision).param_dtype if a.mixed_precision else torch.bfloat16
+    if dev.type == "cpu":  # plumbing-size model, fp32 (the CPU path has no bf16 kernels)
+        a.seq_len = min(a.seq_len, 32)
+        a.batch_size = min(a.batch_size, 2)
+        cfg = cfg.replace(n_layers=2, emb_dim=64, n_heads=4, n_kv_groups=2 if cfg.is_llama else 4, hidden_dim=128,
+                          vocab_size=512, context_length=a.seq_len)
+        dtype = torch.float32
+    cfg = cfg.replace(dtype=dtype)
     if a.layers:
         cfg = cfg.replace(n_layers=a.layers)
+    return cfg
+
+
+def alpaca_loader(a, cfg, rank, world):
+    """Synthetic Alpaca records -> InstructionDataset -> reference collate (variable T)."""
+    from functools import partial
+
+    import torch
+    from torch.utils.data import DataLoader
+
+    from building_llm_from_scratch_amd.data.datasets import InstructionDataset, custom_collate_fn
+    from building_llm_from_scratch_amd.data.synthetic import alpaca_records
+    from building_llm_from_scratch_amd.data.tokenizer import build_tokenizer
+    tok = build_tokenizer(a.model, cfg, None)
+    recs = alpaca_records(4096, seed=123)[rank::world]
+    ds = InstructionDataset(recs, tok)
+    collate = partial(custom_collate_fn, pad_token_id=cfg.eos_id, allowed_max_length=cfg.context_length)
+    g = torch.Generator().manual_seed(1000 + rank)
+    dl = DataLoader(ds, batch_size=a.batch_size, shuffle=True, drop_last=True, collate_fn=collate,
+                    num_workers=2, pin_memory=torch.cuda.is_available(), generator=g, persistent_workers=True)
+
+    def forever():
+        while True:
+            yield from dl
+    return forever()
+
+
+def main(argv=None):
+    a = parse(argv)
+    import torch
+    from building_llm_from_scratch_amd import ops
+    from building_llm_from_scratch_amd.models import build_model, replace_linear_with_lora
+    from building_llm_from_scratch_amd.parallel import setup_engine
+    from building_llm_from_scratch_amd.parallel.mixed_precision import get_policy
+    from building_llm_from_scratch_amd.train.optim import FusedAdamW
+
+    dist, dev, world, rank = init_dist(a)
+    cuda = dev.type == "cuda"
+    if cuda:
+        ops.load_ext(required=True)
+    sync = torch.cuda.synchronize if cuda else (lambda: None)
+
+    cfg = build_config(a, dev)
     torch.manual_seed(123)
     model = build_model(cfg, use_actv_ckpt=a.actv_ckpt, device=dev)
     if a.lora_rank:
-        from building_llm_from_scratch_amd.models import replace_linear_with_lora
         for p in model.parameters():
             p.requires_grad = False
         replace_linear_with_lora(model, rank=a.lora_rank, alpha=a.lora_alpha)
-    engine = setup_engine(model, a.parallel if distributed else "local", device=dev,
+    reduce = get_policy(a.mixed_precision).reduce_dtype if a.mixed_precision else None
+    engine = setup_engine(model, a.parallel, device=dev, reduce_dtype=reduce,
                           reshard_after_forward=bool(a.reshard_after_forward))
     opt = FusedAdamW(model, lr=3e-4, weight_decay=0.1, engine=engine, overlap=a.overlap_optimizer)
     B, T = a.batch_size, a.seq_len
-    g = torch.Generator(device=dev)
-    g.manual_seed(1000 + rank)
-    data = [torch.randint(0, cfg.vocab_size, (B, T + 1), device=dev, generator=g) for _ in range(4)]
+
+    if a.data == "alpaca":
+        batches = alpaca_loader(a, cfg, rank, world)
+
+        def next_batch(i):
+            x, y = next(batches)
+            return x.to(dev, non_blocking=True), y.to(dev, non_blocking=True)
+    else:
+        g = torch.Generator(device=dev)
+        g.manual_seed(1000 + rank)
+        data = [torch.randint(0, cfg.vocab_size, (B, T + 1), device=dev, generator=g) for _ in range(4)]
+
+        def next_batch(i):
+            b = data[i % len(data)]
+            return b[:, :-1], b[:, 1:]
+
+    tokens = 0
 
     def step(i):
-        batch = data[i % len(data)]
+        nonlocal tokens
+        x, y = next_batch(i)
         opt.zero_grad()
-        loss = model(batch[:, :-1], batch[:, 1:])
+        loss = model(x, y)
         loss.backward()
         opt.clip_grad_norm_(1.0)
         opt.step()
+        tokens += x.numel()
         return loss
 
     for i in range(a.warmup):
         loss = step(i)
-    torch.cuda.synchronize()
-    if distributed:
-        dist.barrier()
-    torch.cuda.synchronize()
+    sync()
+    dist.barrier()
+    sync()
+    tokens = 0
     t0 = time.perf_counter()
     for i in range(a.steps):
-        loss = step(i)
-    torch.cuda.synchronize()
-    if distributed:
-        dist.barrier()
-    torch.cuda.synchronize()
+        loss = step(a.warmup + i)
+    sync()
+    dist.barrier()
+    sync()
     elapsed = time.perf_counter() - t0
-    el = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-    if distributed:
-        dist.all_reduce(el, op=dist.ReduceOp.MAX)
-    elapsed = el.item()
-    tokens = world * B * T * a.steps
-    tps = tokens / elapsed
+    red = torch.tensor([elapsed, float(tokens)], device=dev, dtype=torch.float64)
+    el = red[:1].clone()
+    dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    tok = red[1:].clone()
+    dist.all_reduce(tok, op=dist.ReduceOp.SUM)
+    elapsed, total_tokens = el.item(), tok.item()
+    tps = total_tokens / elapsed
     ms = 1000 * elapsed / a.steps
-    flops_tok = cfg.train_flops_per_token(T)
-    if a.actv_ckpt == "full":
-        flops_tok *= 4.0 / 3.0
-    mfu = tps / world * flops_tok / 2.5e15
-    if a.profile and rank == 0:
-        prof = profile_phases(model, opt, data[0], dev)
-        print(json.dumps({"profile_ms": prof}), file=sys.stderr)
+    T_eff = total_tokens / (world * a.steps * B)           # mean padded length (alpaca); == T otherwise
+    flops_tok = cfg.train_flops_per_token(int(round(T_eff)))
+    if a.lora_rank:  # frozen base: no weight-gradient GEMMs (2 of the 6 N FLOPs per param)
+        flops_tok -= 2.0 * (cfg.num_params() - cfg.vocab_size * cfg.emb_dim)
+    mfu = tps / world * flops_tok / PEAK_BF16
+    recompute = 4.0 / 3.0 if a.actv_ckpt == "full" else 1.0
+    prof = profile_phases(model, opt, next_batch, dev) if (a.profile and rank == 0 and cuda) else None
     if rank == 0:
+        headline = a.preset == "llama3_8b_fsdp" and cuda and not a.layers
+        name = NICE.get(a.model, f"{cfg.name}-{cfg.size}")
+        if cuda:
+            dtype = "bf16" if cfg.dtype == torch.bfloat16 else str(cfg.dtype).replace("torch.", "")
+        else:
+            dtype = "fp32"
+        metric = METRIC if headline else (
+            f"tokens/sec (whole node) {name} {dtype} {a.parallel.upper()}"
+            + (f" LoRA r={a.lora_rank} Alpaca finetune" if a.lora_rank else "")
+            + (f" mixed_precision={a.mixed_precision}" if a.mixed_precision else "")
+            + (" [cpu plumbing, tiny config]" if not cuda else ""))
         out = {
-            "metric": ("tokens/sec (whole node) Llama-3-8B bf16 FSDP" if (a.model, a.num_params) == ("llama3", "8B")
-                       else f"tokens/sec (whole node) {cfg.name}-{cfg.size} bf16 {a.parallel}"
-                       + (f" LoRA r={a.lora_rank}" if a.lora_rank else "")),
+            "metric": metric,
             "value": round(tps, 1),
             "unit": "tokens/s",
             "n_gpus": world,
@@ -152,35 +278,44 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": (tps / BASELINE_TOKENS_PER_S) if BASELINE_TOKENS_PER_S else None,
-            "dtype": "bf16",
-            "data": "synthetic token ids (Gutenberg-pretraining shape), random-init weights",
+            "dtype": dtype,
+            "data": ("synthetic Alpaca-shaped records, offline byte tokenizer, reference collate (variable T)"
+                     if a.data == "alpaca" else "synthetic token ids (Gutenberg-pretraining shape)")
+                    + ", random-init weights",
             "config": {
-                "model": f"{cfg.name}-{cfg.size}" + (f" ({cfg.n_layers} layers, INVALID)" if a.layers else ""),
+                "model": name + (f" ({cfg.n_layers} layers, INVALID)" if a.layers else "")
+                + ("" if cuda else " (tiny cpu config, INVALID as a measurement)"),
                 "global_batch": world * B,
                 "micro_batch_per_gpu": B,
-                "seq_len": T,
+                "seq_len": T if a.data != "alpaca" else f"variable (mean {T_eff:.0f}, max {cfg.context_length})",
                 "parallelism": f"{a.parallel}{world}",
-                "engine": type(engine).__name__,
+                "engine": type(engine).__name__ + (" (world 1: no-shard)" if getattr(engine, "no_shard", False)
+                                                   else ""),
                 "actv_ckpt": a.actv_ckpt,
+                "mixed_precision": a.mixed_precision,
+                "lora": {"rank": a.lora_rank, "alpha": a.lora_alpha} if a.lora_rank else None,
                 "optimizer": "AdamW fp32 master, wd 0.1, clip 1.0",
             },
-            "mfu_dense_bf16": round(mfu, 4),
-            "peak_mem_gib": round(torch.cuda.max_memory_allocated(dev) / 2**30, 1),
+            "mfu": round(mfu, 4),
+            "hfu": round(mfu * recompute, 4),
+            "peak_mem_gib": round(torch.cuda.max_memory_allocated(dev) / 2**30, 1) if cuda else None,
             "final_loss": round(float(loss.item()), 4),
         }
-        print(json.dumps(out))
-    if distributed:
-        dist.destroy_process_group()
+        if prof is not None:
+            out["profile_ms"] = prof
+        print(json.dumps(out), flush=True)
+    dist.destroy_process_group()
 
 
-def profile_phases(model, opt, batch, dev, n=3):
+def profile_phases(model, opt, next_batch, dev, n=3):
     import torch
     ev = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
     res = {"fwd": 0.0, "bwd": 0.0, "clip+opt": 0.0}
-    for _ in range(n):
+    for i in range(n):
+        x, y = next_batch(i)
         e = [ev() for _ in range(4)]
         e[0].record()
-        loss = model(batch[:, :-1], batch[:, 1:])
+        loss = model(x, y)
         e[1].record()
         loss.backward()
         e[2].record()

@@ -77,6 +77,13 @@ def build_model(config, rank, device, args):
         if rank == 0:
             n = sum(p.numel() for p in model.parameters() if p.requires_grad)
             logger.info(f"Total trainable LoRA parameters: {n:,}")
+    if getattr(args, "resume", None):
+        # weights go in BEFORE the engine shards / buckets them and before the optimizer
+        # copies its fp32 master from them (loading later would be reverted by the next step)
+        from .train.checkpoint import load_model
+        load_model(model, args.resume)
+        if rank == 0:
+            logger.info(f"Resumed weights from {args.resume}")
     pol = precision_policy(args)
     reduce = pol.reduce_dtype if pol is not None else None
     if pol is not None and rank == 0:

@@ -12,6 +12,7 @@ from __future__ import annotations
 import argparse
 import os
 import warnings
+from datetime import timedelta
 from functools import partial
 from pathlib import Path
 
@@ -91,8 +92,15 @@ def build_parser() -> argparse.ArgumentParser:
     x.add_argument("--synthetic_data", action="store_true",
                    help="generate Gutenberg-/Alpaca-shaped data into --data_dir if it is empty")
     x.add_argument("--sample_tokens", type=int, default=200)
-    x.add_argument("--resume", type=str, default=None, help="model_pg_*.pth to resume from (+ trainer_state)")
-    x.add_argument("--save_resume_state", action="store_true")
+    x.add_argument("--resume", type=str, default=None,
+                   help="model_pg_*.pth to resume from (+ its .state.pt written by --save_resume_state)")
+    x.add_argument("--save_resume_state", action="store_true",
+                   help="write optimizer / step / RNG / data-position state next to every checkpoint")
+    x.add_argument("--num_workers", type=int, default=2, help="DataLoader workers (reference train.py:167,195)")
+    x.add_argument("--token_cache", type=str, default=None,
+                   help="memmapped token cache dir (default <output_dir>/token_cache; 'none' disables)")
+    x.add_argument("--pg_timeout_min", type=float, default=30.0,
+                   help="collective timeout (minutes): a wedged RCCL/gloo collective raises instead of hanging")
     x.add_argument("--bucket_mb", type=float, default=256.0, help="DDP all-reduce bucket size")
     x.add_argument("--no_reshard_after_forward", action="store_true",
                    help="FSDP: keep gathered params from forward to backward (ZeRO-2 style)")
@@ -123,10 +131,11 @@ def ddp_setup(rank: int, world_size: int, args):
     os.environ.setdefault("MASTER_PORT", "12355")
     device = _device_for(args, int(os.environ.get("LOCAL_RANK", rank)))
     backend = args.backend or ("nccl" if device.type == "cuda" else "gloo")
+    timeout = timedelta(minutes=getattr(args, "pg_timeout_min", 30.0))
     if backend == "nccl":
-        dist.init_process_group("nccl", rank=rank, world_size=world_size, device_id=device)
+        dist.init_process_group("nccl", rank=rank, world_size=world_size, device_id=device, timeout=timeout)
     else:
-        dist.init_process_group("gloo", rank=rank, world_size=world_size)
+        dist.init_process_group("gloo", rank=rank, world_size=world_size, timeout=timeout)
     return device
 
 
@@ -149,7 +158,7 @@ def main(rank: int, args):
     from .builder import build_components
     from .data.datasets import custom_collate_fn
     from .data.loaders import DataloaderIF, DataloaderPT
-    from .train.checkpoint import load_model, load_resume_state
+    from .train.checkpoint import load_resume_state, rank_state_path, resume_state_path
     from .train.trainer import DynamicLossScaler, Trainer
 
     world = getattr(args, "world_size", 1)
@@ -160,8 +169,6 @@ def main(rank: int, args):
 
     utils.set_seed(args.seed)
     config, model, optimizer, tokenizer, engine = build_components(rank, device, args)
-    if args.resume:
-        load_model(model, args.resume)
 
     _prepare_data(args, config, rank)
     if args.run_type == "multi_gpu":
@@ -179,7 +186,14 @@ def main(rank: int, args):
         collate = partial(custom_collate_fn, pad_token_id=config["eos_id"], allowed_max_length=config["context_length"])
         loader = DataloaderIF(collate_func=collate, **kw)
     else:
-        loader = DataloaderPT(stride=config["context_length"], eos_text=config["eos_text"], collate_func=None, **kw)
+        cache = None if args.token_cache == "none" else (args.token_cache or os.path.join(args.output_dir, "token_cache"))
+        loader = DataloaderPT(stride=config["context_length"], eos_text=config["eos_text"], collate_func=None,
+                              cache_dir=cache, **kw)
+        # rank 0 tokenises every file once into the memmapped cache; the others map it
+        if cache and rank == 0:
+            loader.pretokenize(all_files)
+        if cache and args.run_type == "multi_gpu":
+            dist.barrier()
 
     out_dir = Path(args.output_dir)
     out_dir.mkdir(parents=True, exist_ok=True)
@@ -190,12 +204,19 @@ def main(rank: int, args):
                       engine=engine, metrics_file=args.metrics_file,
                       loss_scaler=DynamicLossScaler() if config.dtype == torch.float16 else None,
                       max_steps=args.max_steps, sample_tokens=args.sample_tokens,
-                      save_resume=args.save_resume_state, world_size=world, profile_steps=args.profile_steps)
-    if args.resume:
-        st_path = Path(args.resume).with_name("trainer_state_" + Path(args.resume).stem.split("_")[-1] + ".pt")
-        if st_path.exists() or Path(str(st_path).replace(".pt", f".rank{rank}.pt")).exists():
-            trainer.load_trainer_state(load_resume_state(st_path, optimizer, rank, world))
+                      save_resume=args.save_resume_state, world_size=world, profile_steps=args.profile_steps,
+                      num_workers=args.num_workers, seed=args.seed)
     trainer.generate_and_print_sample("Every effort moves you", temperature=1.0, top_k=5, memory_check=True)
+    if args.resume:
+        # after the start-up sample: the restored host RNG state is the one saved at the checkpoint
+        st_path = resume_state_path(args.resume)
+        if rank_state_path(st_path, rank, world).exists():
+            trainer.load_trainer_state(load_resume_state(st_path, optimizer, rank, world))
+            if rank == 0:
+                logger.info(f"Resumed optimizer / step / data position from {st_path} (step {trainer.global_step})")
+        elif rank == 0:
+            logger.warning(f"--resume: no optimizer state next to {args.resume} ({st_path.name}); "
+                           "continuing from the weights only with fresh AdamW moments and step 0")
     if args.finetune:
         train_losses, val_losses, tokens_seen, lrs = trainer.finetune_model(n_epochs=args.n_epochs)
     else:

@@ -13,33 +13,66 @@
 from __future__ import annotations
 
 import hashlib
+import os
+import warnings
 from typing import Dict, List, Optional, Sequence, Tuple
 
+import numpy as np
 import torch
 from torch.utils.data import Dataset
 
 _TOKEN_CACHE: Dict[Tuple[str, int, str], torch.Tensor] = {}
 
 
-def tokenize_cached(text: str, tokenizer, allowed_special=frozenset({"<|endoftext|>"})) -> torch.Tensor:
+def _tokenizer_tag(tokenizer) -> str:
+    return f"{type(tokenizer).__name__}-{getattr(tokenizer, 'n_vocab', getattr(tokenizer, 'vocab_size', 0))}"
+
+
+def token_cache_path(text: str, tokenizer, allowed_special, cache_dir: str) -> str:
+    h = hashlib.sha1(text.encode("utf-8", errors="ignore"))
+    h.update(("|" + _tokenizer_tag(tokenizer) + "|" + ",".join(sorted(allowed_special))).encode())
+    return os.path.join(cache_dir, h.hexdigest() + ".u32")
+
+
+def tokenize_cached(text: str, tokenizer, allowed_special=frozenset({"<|endoftext|>"}),
+                    cache_dir: Optional[str] = None) -> torch.Tensor:
+    """Token ids of ``text`` as one int32 tensor.  With ``cache_dir`` the stream is tokenised
+    once into a flat uint32 file (written atomically) and every later call — other ranks,
+    later epochs, a resumed run — memory-maps it instead of re-tokenising (reference
+    dataset.py:26 re-tokenises every file every epoch, plus once more to count steps)."""
     key = (hashlib.sha1(text.encode("utf-8", errors="ignore")).hexdigest(), id(tokenizer),
            ",".join(sorted(allowed_special)))
     hit = _TOKEN_CACHE.get(key)
-    if hit is None:
+    if hit is not None:
+        return hit
+    path = token_cache_path(text, tokenizer, allowed_special, cache_dir) if cache_dir else None
+    if path and os.path.exists(path):
+        arr = np.memmap(path, dtype=np.uint32, mode="r")
+        with warnings.catch_warnings():       # read-only memmap: windows are only ever read
+            warnings.simplefilter("ignore")
+            hit = torch.from_numpy(arr.view(np.int32)) if arr.size else torch.zeros(0, dtype=torch.int32)
+    else:
         ids = tokenizer.encode(text, allowed_special=set(allowed_special))
         hit = torch.tensor(ids, dtype=torch.int32)
-        if len(_TOKEN_CACHE) > 64:
-            _TOKEN_CACHE.clear()
-        _TOKEN_CACHE[key] = hit
+        if path:
+            os.makedirs(cache_dir, exist_ok=True)
+            tmp = f"{path}.{os.getpid()}.tmp"
+            hit.numpy().astype(np.uint32).tofile(tmp)
+            os.replace(tmp, path)
+    if len(_TOKEN_CACHE) > 64:
+        _TOKEN_CACHE.clear()
+    _TOKEN_CACHE[key] = hit
     return hit
 
 
 class DatasetPT(Dataset):
     def __init__(self, txt: str, tokenizer, max_length: int, stride: int,
-                 allowed_special=frozenset({"<|endoftext|>"}), token_ids: Optional[torch.Tensor] = None):
+                 allowed_special=frozenset({"<|endoftext|>"}), token_ids: Optional[torch.Tensor] = None,
+                 cache_dir: Optional[str] = None):
         self.max_length = max_length
         self.stride = stride
-        self.tokens = token_ids if token_ids is not None else tokenize_cached(txt, tokenizer, allowed_special)
+        self.tokens = token_ids if token_ids is not None else \
+            tokenize_cached(txt, tokenizer, allowed_special, cache_dir)
         n = self.tokens.numel()
         self.starts = list(range(0, max(n - max_length, 0), stride))
 

@@ -5,7 +5,10 @@ Semantics kept: raw text split by characters ``train_ratio`` / rest; train loade
 with ``drop_last=True``, val loader in order; multi-GPU uses a ``DistributedSampler`` (which
 shuffles, seed 0, pads by repetition) with ``set_epoch`` called by the trainer.
 Differences: the instruction pad id defaults to the model's eos id (SURVEY §2.8 defect 7),
-and ``get_total_steps_epoch`` reuses cached tokenisation.
+``get_total_steps_epoch`` reuses cached tokenisation (``cache_dir``: a memory-mapped uint32
+token stream per text, written once), worker processes are used under DistributedSampler too,
+and the single-process shuffle takes an explicit ``generator`` so a resumed run replays the
+same batch order (trainer seeds it per (epoch, file)).
 """
 from __future__ import annotations
 
@@ -23,14 +26,29 @@ def _is_dist() -> bool:
     return torch.distributed.is_available() and torch.distributed.is_initialized()
 
 
+def _make_loader(owner, ds, shuffle, drop_last, num_workers, generator):
+    workers = dict(num_workers=num_workers, persistent_workers=False)
+    if num_workers > 0:
+        workers["prefetch_factor"] = 4
+    if owner.run_type == "multi_gpu" and _is_dist():
+        # DistributedSampler(shuffle=True, seed=0) + set_epoch: identical order on resume
+        return DataLoader(ds, batch_size=owner.batch_size, pin_memory=owner.pin_memory, shuffle=False,
+                          drop_last=drop_last, sampler=DistributedSampler(ds, shuffle=shuffle),
+                          collate_fn=owner.collate_func, **workers)
+    return DataLoader(ds, batch_size=owner.batch_size, pin_memory=owner.pin_memory, shuffle=shuffle,
+                      drop_last=drop_last, collate_fn=owner.collate_func,
+                      generator=generator if shuffle else None, **workers)
+
+
 class DataloaderPT:
     def __init__(self, tokenizer, batch_size, max_length, stride, eos_text="<|endoftext|>",
                  dataset_name="gutenberg", run_type="single_gpu", train_ratio=0.90,
-                 collate_func=None, pin_memory=None):
+                 collate_func=None, pin_memory=None, cache_dir=None):
         self.tokenizer = tokenizer
         self.batch_size = batch_size
         self.max_length = max_length
         self.stride = stride
+        self.cache_dir = cache_dir
         self.train_ratio = train_ratio
         self.run_type = run_type
         self.collate_func = collate_func
@@ -40,23 +58,26 @@ class DataloaderPT:
         # allow the model's eos text as a special token (fixes SURVEY §2.8 defect 13)
         self.allowed_special = frozenset({"<|endoftext|>", eos_text})
 
-    def create_dataloader(self, txt, shuffle=True, drop_last=True, num_workers=0):
+    def create_dataloader(self, txt, shuffle=True, drop_last=True, num_workers=0, generator=None):
         if self.dataset_name != "gutenberg":
             raise NotImplementedError(f"Dataset '{self.dataset_name}' not supported.")
-        ds = DatasetPT(txt, self.tokenizer, self.max_length, self.stride, self.allowed_special)
-        if self.run_type == "multi_gpu" and _is_dist():
-            return DataLoader(ds, batch_size=self.batch_size, pin_memory=self.pin_memory,
-                              shuffle=False, drop_last=drop_last, sampler=DistributedSampler(ds),
-                              collate_fn=self.collate_func)
-        return DataLoader(ds, batch_size=self.batch_size, pin_memory=self.pin_memory, shuffle=shuffle,
-                          drop_last=drop_last, num_workers=num_workers, collate_fn=self.collate_func,
-                          persistent_workers=False)
+        ds = DatasetPT(txt, self.tokenizer, self.max_length, self.stride, self.allowed_special,
+                       cache_dir=self.cache_dir)
+        return _make_loader(self, ds, shuffle, drop_last, num_workers, generator)
 
-    def create_dataloaders(self, text_data, num_workers=0):
+    def create_dataloaders(self, text_data, num_workers=0, generator=None):
         split = int(self.train_ratio * len(text_data))
-        train = self.create_dataloader(text_data[:split], drop_last=True, shuffle=True, num_workers=num_workers)
+        train = self.create_dataloader(text_data[:split], drop_last=True, shuffle=True, num_workers=num_workers,
+                                       generator=generator)
         val = self.create_dataloader(text_data[split:], drop_last=False, shuffle=False, num_workers=num_workers)
         return train, val
+
+    def pretokenize(self, data_files):
+        """Tokenise every file's train/val split into the memmap cache (call on one rank,
+        then barrier: the other ranks map the files instead of re-tokenising)."""
+        for fp in data_files:
+            text = read_text_file(fp) + " " + self.eos_text + " "
+            self.create_dataloaders(text, num_workers=0)
 
     def get_total_steps_epoch(self, data_files):
         n = 0
@@ -83,21 +104,21 @@ class DataloaderIF:
         if self.dataset_name not in ("alpaca",):
             raise ValueError(f"Dataset '{self.dataset_name}' is not supported.")
 
-    def create_dataloader(self, data, shuffle=True, drop_last=True, num_workers=0):
+    def create_dataloader(self, data, shuffle=True, drop_last=True, num_workers=0, generator=None):
         ds = InstructionDataset(data, self.tokenizer)
-        if self.run_type == "multi_gpu" and _is_dist():
-            return DataLoader(ds, batch_size=self.batch_size, pin_memory=self.pin_memory, shuffle=False,
-                              drop_last=drop_last, sampler=DistributedSampler(ds), collate_fn=self.collate_func)
-        return DataLoader(ds, batch_size=self.batch_size, pin_memory=self.pin_memory, shuffle=shuffle,
-                          drop_last=drop_last, num_workers=num_workers, collate_fn=self.collate_func)
+        return _make_loader(self, ds, shuffle, drop_last, num_workers, generator)
 
-    def create_dataloaders(self, data, num_workers=0):
+    def create_dataloaders(self, data, num_workers=0, generator=None):
         if not isinstance(data, list):
             raise TypeError("Data must be a list of instruction-format samples.")
         split = int(self.train_ratio * len(data))
-        train = self.create_dataloader(data[:split], shuffle=True, drop_last=True, num_workers=num_workers)
+        train = self.create_dataloader(data[:split], shuffle=True, drop_last=True, num_workers=num_workers,
+                                       generator=generator)
         val = self.create_dataloader(data[split:], shuffle=False, drop_last=False, num_workers=num_workers)
         return train, val
+
+    def pretokenize(self, data_files):
+        pass
 
     def get_total_steps_epoch(self, data_files):
         n = 0

@@ -80,6 +80,16 @@ _ANTONYMS = [("hot", "cold"), ("big", "small"), ("fast", "slow"), ("happy", "sad
 
 
 def make_alpaca_json(path: str, n_records: int = 1000, seed: int = 123) -> str:
+    recs = alpaca_records(n_records, seed)
+    os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+    with open(path, "w", encoding="utf-8") as f:
+        json.dump(recs, f, indent=1)
+    return path
+
+
+def alpaca_records(n_records: int = 1000, seed: int = 123) -> list:
+    """Alpaca-shaped {instruction, input, output} records (reference Datasets/Alpaca/download.py
+    fetches tatsu-lab's alpaca_data.json; no network here)."""
     rng = random.Random(seed)
     lex = _lexicon(rng, 800)
     recs = []
@@ -97,10 +107,7 @@ def make_alpaca_json(path: str, n_records: int = 1000, seed: int = 123) -> str:
             words = rng.choices(lex, k=rng.randint(4, 12))
             recs.append({"instruction": "Rewrite the sentence in reverse word order.",
                          "input": " ".join(words), "output": " ".join(reversed(words)) + "."})
-    os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
-    with open(path, "w", encoding="utf-8") as f:
-        json.dump(recs, f, indent=1)
-    return path
+    return recs
 
 
 if __name__ == "__main__":  # python -m building_llm_from_scratch_amd.data.synthetic OUT_DIR

@@ -33,6 +33,9 @@ class LocalEngine:
     world_size = 1
     rank = 0
 
+    def __init__(self, model=None):
+        self.model = model
+
     def pre_forward(self, unit):
         pass
 
@@ -47,6 +50,10 @@ class LocalEngine:
 
     def finish_backward(self):
         pass
+
+    @torch.no_grad()
+    def load_full_state_dict(self, sd, strict: bool = True):
+        return self.model.load_state_dict(sd, strict=strict)
 
     @contextmanager
     def params_resident(self):

@@ -22,7 +22,7 @@ def setup_engine(model, kind: str = "local", device=None, reduce_dtype=None, buc
     device = torch.device(device) if device is not None else model.device
     if kind in ("local", "single", "single_gpu"):
         model.flatten(device=device)
-        eng = LocalEngine()
+        eng = LocalEngine(model)
         model.set_engine(eng)
         return eng
     if kind == "ddp":
@@ -30,7 +30,7 @@ def setup_engine(model, kind: str = "local", device=None, reduce_dtype=None, buc
         return DDPEngine(model, device, reduce_dtype=reduce_dtype, bucket_mb=bucket_mb, pg=process_group)
     if kind == "zero1":
         from .zero import ZeroEngine
-        return ZeroEngine(model, device, reduce_dtype=reduce_dtype, pg=process_group)
+        return ZeroEngine(model, device, reduce_dtype=reduce_dtype, bucket_mb=bucket_mb, pg=process_group)
     if kind == "fsdp":
         from .fsdp import FSDPEngine
         return FSDPEngine(model, device, reduce_dtype=reduce_dtype,

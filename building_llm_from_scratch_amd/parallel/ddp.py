@@ -32,7 +32,9 @@ class DDPEngine(LocalEngine):
         dtype = next(model.parameters()).dtype
         self.arena = Arena(model, device, dtype, self.world_size, bucket_mb * 2 ** 20)
         self.reduce_dtype = reduce_dtype if reduce_dtype not in (None, dtype) else None
-        if broadcast:
+        # a single rank has nothing to average with: no broadcast, no all-reduce (same hooks)
+        self.no_comm = self.world_size == 1
+        if broadcast and not self.no_comm:
             self._broadcast_params()
         self.grad_prescale = 1.0 / self.world_size
         self.sync_grads = True
@@ -55,7 +57,7 @@ class DDPEngine(LocalEngine):
             self._works = []
 
     def post_backward(self, unit):
-        if not self.sync_grads or unit.index not in self.arena.bucket_of:
+        if self.no_comm or not self.sync_grads or unit.index not in self.arena.bucket_of:
             return
         b = self.arena.bucket_of[unit.index]
         self._pending[b] -= 1
@@ -72,7 +74,7 @@ class DDPEngine(LocalEngine):
             self._works.append((dist.all_reduce(g, group=self.pg, async_op=True), None, None))
 
     def finish_backward(self):
-        if self.sync_grads:
+        if self.sync_grads and not self.no_comm:
             for b, n in enumerate(self._pending):
                 if n > 0:  # units that saw no backward this step (e.g. frozen paths)
                     self._launch(b)
@@ -82,6 +84,11 @@ class DDPEngine(LocalEngine):
                     g.copy_(tmp)
         self._works = []
         self._started = False
+
+    @torch.no_grad()
+    def load_full_state_dict(self, sd, strict: bool = True):
+        self.model.rctx.sync_all_params()
+        return self.model.load_state_dict(sd, strict=strict)
 
     # ------------------------------------------------------------------ optimizer
     def optimizer_slots(self, model):

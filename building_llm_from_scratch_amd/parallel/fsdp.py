@@ -17,8 +17,14 @@ every model family:
     full gradient is reduce-scattered asynchronously into its gradient shard and freed;
   * gradient clipping: shard-local sum of squares + one scalar all-reduce;
   * checkpoint: full state dict gathered unit by unit to rank 0 with the reference key names.
-Mixed precision: the flats hold the compute dtype (``--mixed_precision`` or ``--data_type``),
-gradients are reduced in that dtype (reference bf16 policy), master weights stay fp32.
+Mixed precision: the flats hold the policy's ``param_dtype``; gradients are reduce-scattered
+in its ``reduce_dtype`` (one cast each way when it differs, e.g. ``bf16_hybrid``: fp32 params,
+bf16 collectives — reference datautils/mixed_precision.py:24-28); master weights stay fp32.
+
+World size 1: like torch FSDP, which clamps FULL_SHARD to NO_SHARD when there is a single
+rank (torch/distributed/fsdp/_init_utils.py:426-437), the shard IS the full flat: nothing is
+freed, gathered or reduce-scattered (a world-1 collective is a device copy of every unit per
+pass).  It is the same engine class, hooks and optimizer slots as at N>1.
 """
 from __future__ import annotations
 
@@ -56,7 +62,9 @@ class FSDPEngine(LocalEngine):
         self.reshard_after_forward = reshard_after_forward
         self.grad_prescale = 1.0 / self.world_size
         self.is_cuda = self.device.type == "cuda"
+        self.no_shard = self.world_size == 1
         dtype = next(model.parameters()).dtype
+        self.reduce_dtype = reduce_dtype if reduce_dtype not in (None, dtype) else None
         model.flatten(device=device, dtype=dtype, pad_to=self.world_size * ALIGN)
         self.units = model.units
         W, r = self.world_size, self.rank
@@ -64,10 +72,16 @@ class FSDPEngine(LocalEngine):
             st = u.state
             st["bufs"] = []
             for fb in u.buffers():
-                dist.broadcast(fb.data, src=0, group=pg)          # identical init on every rank
                 n = fb.numel // W
-                fb.shard = fb.data[r * n:(r + 1) * n].clone()
                 fb.nbytes = fb.data.untyped_storage().size()
+                if self.no_shard:
+                    fb.shard = fb.data
+                    if fb is u.train:
+                        fb.grad_shard = fb.grad
+                    st["bufs"].append(fb)
+                    continue
+                dist.broadcast(fb.data, src=0, group=pg)          # identical init on every rank
+                fb.shard = fb.data[r * n:(r + 1) * n].clone()
                 if fb is u.train:
                     fb.grad_shard = torch.zeros(n, dtype=fb.grad.dtype, device=device)
                     fb.grad_nbytes = fb.grad.untyped_storage().size()
@@ -75,7 +89,7 @@ class FSDPEngine(LocalEngine):
                     _free(fb.grad)
                 _free(fb.data)
                 st["bufs"].append(fb)
-            st["gathered"] = False
+            st["gathered"] = self.no_shard
             st["gather_work"] = None
         self._rs_works: List = []
         self._in_backward = False
@@ -98,6 +112,8 @@ class FSDPEngine(LocalEngine):
     # ------------------------------------------------------------------ gather / reshard
     def _issue_gather(self, u, async_op: bool):
         st = u.state
+        if self.no_shard:
+            return
         if st["gathered"] or st["gather_work"] is not None:
             return
         works = []
@@ -122,6 +138,8 @@ class FSDPEngine(LocalEngine):
 
     def _reshard(self, u):
         st = u.state
+        if self.no_shard:
+            return
         if st["gather_work"] is not None:
             self._wait_gather(u)
         for fb in st["bufs"]:
@@ -154,19 +172,27 @@ class FSDPEngine(LocalEngine):
         if prv >= 0:
             self._issue_gather(self.units[prv], async_op=True)
         fb = unit.train
-        if fb is not None:
+        if fb is not None and not self.no_shard:
             _alloc(fb.grad, fb.grad_nbytes)
             for s, e in fb.gaps:
                 fb.grad[s:e].zero_()
 
     def post_backward(self, unit):
         fb = unit.train
-        if fb is not None:
-            w = dist.reduce_scatter_tensor(fb.grad_shard, fb.grad, group=self.pg, async_op=True)
+        if fb is not None and not self.no_shard:
+            if self.reduce_dtype is not None:
+                # reduce in the policy's dtype: cast the full gradient, reduce-scatter into a
+                # reduce-dtype shard, cast back into the (param-dtype) gradient shard on retire
+                full = fb.grad.to(self.reduce_dtype)
+                part = torch.empty(fb.grad_shard.numel(), dtype=self.reduce_dtype, device=full.device)
+                w = dist.reduce_scatter_tensor(part, full, group=self.pg, async_op=True)
+                self._rs_works.append((w, fb, full, part))
+            else:
+                w = dist.reduce_scatter_tensor(fb.grad_shard, fb.grad, group=self.pg, async_op=True)
+                self._rs_works.append((w, fb, None, None))
             # the full gradient is released only after the reduce-scatter completed: freeing it
             # now would hand the block back to the compute stream's allocator pool while RCCL
             # may still be reading it (288 GB leaves room to hold them until the end of backward)
-            self._rs_works.append((w, fb))
             self._retire_rs(keep=2)
         self._reshard(unit)
 
@@ -174,10 +200,11 @@ class FSDPEngine(LocalEngine):
         """Wait for and free all but the ``keep`` most recent reduce-scatters (bounded memory
         without stalling the stream on the one just issued)."""
         while len(self._rs_works) > keep:
-            w, fb = self._rs_works.pop(0)
+            w, fb, full, part = self._rs_works.pop(0)
             w.wait()
-            if fb is not None:
-                _free(fb.grad)
+            if part is not None:
+                fb.grad_shard.copy_(part)
+            _free(fb.grad)
 
     def finish_backward(self):
         self._retire_rs(keep=0)
@@ -189,7 +216,8 @@ class FSDPEngine(LocalEngine):
                 for u in self.units if u.train is not None]
 
     def all_reduce_grad_sq_norm(self, sq: torch.Tensor) -> torch.Tensor:
-        dist.all_reduce(sq, group=self.pg)
+        if not self.no_shard:
+            dist.all_reduce(sq, group=self.pg)
         return sq
 
     # the next forward starts with the embedding (1 GiB bf16 for Llama-3-8B) and the first
@@ -220,6 +248,31 @@ class FSDPEngine(LocalEngine):
                 self._reshard(u)
 
     # ------------------------------------------------------------------ checkpoint
+    @torch.no_grad()
+    def load_full_state_dict(self, sd: Dict[str, torch.Tensor], strict: bool = True):
+        """Scatter a full (reference-named) state dict into this rank's shards, unit by unit
+        (never more than one gathered unit alive).  Buffers (mask / cos / sin) are ignored:
+        they are recomputed, never stored.  Call ``optimizer.reload_master()`` afterwards."""
+        self.model.rctx.sync_all_params()
+        names = {id(p): n for n, p in self.model.named_parameters()}
+        missing = []
+        W, r = self.world_size, self.rank
+        for u in self.units:
+            self._wait_gather(u)
+            for fb in u.state["bufs"]:
+                for p in fb.params:
+                    k = names[id(p)]
+                    if k not in sd:
+                        missing.append(k)
+                        continue
+                    fb.view(fb.data, p).copy_(sd[k].to(dtype=fb.dtype).view(p.shape))
+                if not self.no_shard:
+                    n = fb.numel // W
+                    fb.shard.copy_(fb.data[r * n:(r + 1) * n])
+            self._reshard(u)
+        if strict and missing:
+            raise KeyError(f"missing keys in state dict: {missing[:8]}{'...' if len(missing) > 8 else ''}")
+
     def full_state_dict(self) -> Optional[Dict[str, torch.Tensor]]:
         """Gather unit by unit; rank 0 receives the reference-named CPU state dict."""
         self.model.rctx.sync_all_params()

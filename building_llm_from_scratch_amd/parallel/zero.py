@@ -7,7 +7,9 @@ greedy partition, then ONE BROADCAST PER PARAMETER re-syncs weights (SURVEY §2.
 Here: per arena bucket, the gradient is REDUCE-SCATTERED (half the bytes of an all-reduce)
 asynchronously as soon as the bucket's units finish backward; each rank runs the fused
 AdamW on its contiguous 1/world shard (fp32 master + moments only for that shard); then one
-all-gather per bucket rebuilds the full bf16 parameters in place.
+all-gather per bucket rebuilds the full bf16 parameters in place.  With a mixed-precision
+policy whose ``reduce_dtype`` differs from the parameter dtype (``bf16_hybrid``), each bucket's
+gradient is cast once, reduce-scattered in the reduce dtype and cast back into the shard.
 """
 from __future__ import annotations
 
@@ -29,13 +31,19 @@ class ZeroEngine(LocalEngine):
         self.rank = dist.get_rank(pg)
         self.model = model
         dtype = next(model.parameters()).dtype
+        self.reduce_dtype = reduce_dtype if reduce_dtype not in (None, dtype) else None
         self.arena = Arena(model, device, dtype, self.world_size, bucket_mb * 2 ** 20)
-        dist.broadcast(self.arena.param, src=0, group=pg)
-        for u in model.units:
-            if u.frozen is not None:
-                dist.broadcast(u.frozen.data, src=0, group=pg)
+        self.no_comm = self.world_size == 1      # one rank: its shard is the whole bucket
+        if not self.no_comm:
+            dist.broadcast(self.arena.param, src=0, group=pg)
+            for u in model.units:
+                if u.frozen is not None:
+                    dist.broadcast(u.frozen.data, src=0, group=pg)
         self.grad_shards = []
         for b in range(len(self.arena.buckets)):
+            if self.no_comm:
+                self.grad_shards.append(self.arena.bucket_grad(b))
+                continue
             n = self.arena.bucket_grad(b).numel() // self.world_size
             self.grad_shards.append(torch.zeros(n, dtype=dtype, device=device))
         self.grad_prescale = 1.0 / self.world_size
@@ -64,15 +72,26 @@ class ZeroEngine(LocalEngine):
             self._launch(b)
 
     def _launch(self, b):
-        w = dist.reduce_scatter_tensor(self.grad_shards[b], self.arena.bucket_grad(b), group=self.pg, async_op=True)
-        self._works.append(w)
+        if self.no_comm:
+            return
+        g = self.arena.bucket_grad(b)
+        if self.reduce_dtype is not None:
+            full = g.to(self.reduce_dtype)
+            part = torch.empty(self.grad_shards[b].numel(), dtype=self.reduce_dtype, device=g.device)
+            w = dist.reduce_scatter_tensor(part, full, group=self.pg, async_op=True)
+            self._works.append((w, b, full, part))
+        else:
+            w = dist.reduce_scatter_tensor(self.grad_shards[b], g, group=self.pg, async_op=True)
+            self._works.append((w, b, None, None))
 
     def finish_backward(self):
         for b, n in enumerate(self._pending):
             if n > 0:
                 self._launch(b)
-        for w in self._works:
+        for w, b, full, part in self._works:
             w.wait()
+            if part is not None:
+                self.grad_shards[b].copy_(part)
         self._works = []
         self._started = False
 
@@ -81,10 +100,13 @@ class ZeroEngine(LocalEngine):
                         tuple(self.arena.buckets[b])) for b in range(len(self.arena.buckets))]
 
     def all_reduce_grad_sq_norm(self, sq: torch.Tensor) -> torch.Tensor:
-        dist.all_reduce(sq, group=self.pg)
+        if not self.no_comm:
+            dist.all_reduce(sq, group=self.pg)
         return sq
 
     def after_slot_update(self, slot):
+        if self.no_comm:
+            return
         # one all-gather per bucket, issued right behind that bucket's AdamW (on the optimizer
         # stream when overlapped); unit i's next forward waits only for its own bucket
         b = self.arena.bucket_of[slot.units[0]]
@@ -108,6 +130,14 @@ class ZeroEngine(LocalEngine):
         self.model.rctx.sync_all_params()
         self.sync()
         yield
+
+    @torch.no_grad()
+    def load_full_state_dict(self, sd, strict: bool = True):
+        """Parameters are replicated: load into the (arena-backed) parameter views; call
+        ``optimizer.reload_master()`` afterwards."""
+        self.sync()
+        self.model.rctx.sync_all_params()
+        return self.model.load_state_dict(sd, strict=strict)
 
     def full_state_dict(self):
         self.model.rctx.sync_all_params()

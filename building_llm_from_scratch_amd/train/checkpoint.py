@@ -4,9 +4,12 @@
   ``torch.save`` of a plain, prefix-free ``state_dict`` (reference train.py:231-257) —
   identical key names (incl. the ``att.mask|cos|sin`` buffers and fp32 RMSNorm weights).
   Rank 0 writes; under FSDP the full state dict is gathered unit by unit to rank 0.
-* Extension (off unless ``--resume`` / ``save_resume_state``): ``trainer_state_{step}.pt``
-  with optimizer state (fp32 master, exp_avg, exp_avg_sq per flat slot), step, LR, RNG and
-  loss history.  The reference has no resume path at all.
+* Extension (off unless ``--save_resume_state``): next to every ``<name>.pth`` a
+  ``<name>.state.pt`` (``.rank{r}`` per rank when world > 1) with the optimizer state (fp32
+  master, exp_avg, exp_avg_sq per flat slot — rank-local shards under ZeRO / FSDP), global
+  step, LR, host RNGs, the model's dropout RNG counter, the data position (epoch, file, batch)
+  and loss history.  ``--resume <name>.pth`` loads the weights BEFORE the engine shards them
+  and the optimizer is built, then this state.  The reference has no resume path at all.
 """
 from __future__ import annotations
 
@@ -34,6 +37,15 @@ def save_model(model, path, engine=None, rank: int = 0):
         os.replace(tmp, path)
 
 
+def resume_state_path(ckpt_path) -> Path:
+    p = Path(ckpt_path)
+    return p.with_name(p.stem + ".state.pt")
+
+
+def load_state(path) -> dict:
+    return torch.load(path, map_location="cpu", weights_only=True)
+
+
 def load_model(model, path, strict: bool = True):
     sd = torch.load(path, map_location="cpu", weights_only=True)
     return model.load_state_dict(sd, strict=strict)
@@ -49,16 +61,19 @@ def save_resume_state(path, optimizer, trainer_state: dict, rank: int = 0, world
         "rng": _rng_state(),
         "world": world,
     }
+    p = rank_state_path(path, rank, world)
+    tmp = str(p) + ".tmp"
+    torch.save(st, tmp)
+    os.replace(tmp, p)
+
+
+def rank_state_path(path, rank: int = 0, world: int = 1) -> Path:
     p = Path(path)
-    if world > 1:
-        p = p.with_name(p.stem + f".rank{rank}" + p.suffix)
-    torch.save(st, p)
+    return p.with_name(p.stem + f".rank{rank}" + p.suffix) if world > 1 else p
 
 
 def load_resume_state(path, optimizer, rank: int = 0, world: int = 1) -> dict:
-    p = Path(path)
-    if world > 1:
-        p = p.with_name(p.stem + f".rank{rank}" + p.suffix)
+    p = rank_state_path(path, rank, world)
     st = torch.load(p, map_location="cpu", weights_only=True)
     assert st["world"] == world, "resume requires the same world size"
     for s, saved in zip(optimizer.slots, st["optim"]):

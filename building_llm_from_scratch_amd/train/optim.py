@@ -135,6 +135,17 @@ class FusedAdamW(torch.optim.Optimizer):
         ops.adamw_step_(s.param.reshape(-1), st.get("master"), s.grad.reshape(-1), st["exp_avg"],
                         st["exp_avg_sq"], lr, b1, b2, eps, wd, st["step"], self._gscale)
 
+    @torch.no_grad()
+    def reload_master(self):
+        """Re-seed the fp32 master copies from the (just loaded) parameters.  Needed whenever
+        weights are loaded after the optimizer was built: ``step`` writes master -> param, so a
+        stale master would silently revert the load."""
+        self.synchronize()
+        for s in self.slots:
+            st = self.state[s.param]
+            if "master" in st:
+                st["master"].copy_(s.param.detach().reshape(-1).float())
+
     def synchronize(self):
         """Block the current stream until every overlapped update has been applied."""
         if self.overlap:

@@ -16,6 +16,7 @@ loss guard, optional ``max_steps`` and resume state.
 """
 from __future__ import annotations
 
+import itertools
 import math
 import time
 from pathlib import Path
@@ -26,7 +27,7 @@ import torch.distributed as dist
 
 from ..logger import MetricsWriter, setup_logger
 from ..utils.misc import read_json_file, read_text_file, text_to_token_ids, token_ids_to_text
-from .checkpoint import save_model, save_resume_state
+from .checkpoint import resume_state_path, save_model, save_resume_state
 from .generate import generate_cached
 
 logger = setup_logger("train")
@@ -60,7 +61,7 @@ class Trainer:
                  print_sample_iter=1, eval_iter=1, engine=None, max_grad_norm=1.0, metrics_file=None,
                  loss_scaler: Optional[DynamicLossScaler] = None, max_steps: Optional[int] = None,
                  sample_tokens: int = 200, save_resume: bool = False, world_size: int = 1,
-                 profile_steps: Optional[str] = None):
+                 profile_steps: Optional[str] = None, num_workers: int = 0, seed: int = 123):
         self.config = config
         self.model = model
         self.optimizer = optimizer
@@ -93,6 +94,12 @@ class Trainer:
         self.total_training_steps = 1
         self.lr_increment = 0.0
         self.stop = False
+        self.num_workers = num_workers
+        self.seed = seed
+        # data position: (epoch, file index, train batches of that file consumed); saved with
+        # the resume state so a resumed run continues with the very next batch
+        self.pos = (0, 0, 0)
+        self._resume_pos = None
         # torch.profiler window "first:last" (global steps, inclusive) -> chrome trace per rank
         self.profile_steps = None
         if profile_steps:
@@ -171,9 +178,14 @@ class Trainer:
         self.tokens_seen += input_batch.numel() * self.world_size
         return loss
 
-    def train_epoch(self, epoch_no, train_loader, val_loader, start_context="Every effort moves you"):
+    def train_epoch(self, epoch_no, train_loader, val_loader, start_context="Every effort moves you",
+                    file_index: int = 0, skip_batches: int = 0):
         self.model.train()
-        for input_batch, target_batch in train_loader:
+        it = iter(train_loader)
+        if skip_batches:
+            it = itertools.islice(it, skip_batches, None)
+        for bi, (input_batch, target_batch) in enumerate(it, start=skip_batches):
+            self.pos = (epoch_no, file_index, bi + 1)
             loss = self.train_batch(input_batch, target_batch)
             if self.global_step % self.eval_freq == 0:
                 lv = float(loss.item())
@@ -221,17 +233,27 @@ class Trainer:
         except Exception:  # pragma: no cover
             return None
 
-    def train_model(self, n_epochs):
+    def _loop(self, n_epochs, read, start_context):
         self._setup_schedule(n_epochs)
         pbar = self._progress(n_epochs * len(self.data_files))
+        start = self._resume_pos or (0, 0, 0)
         try:
             for epoch in range(n_epochs):
-                for fp in self.data_files:
-                    raw = read_text_file(fp) + " " + self.config["eos_text"] + " "
-                    train_loader, val_loader = self.loaderObj.create_dataloaders(raw, num_workers=0)
+                for fi, fp in enumerate(self.data_files):
+                    if (epoch, fi) < start[:2]:
+                        if pbar is not None:
+                            pbar.update(1)
+                        continue
+                    skip = start[2] if (epoch, fi) == start[:2] else 0
+                    # per-(epoch, file) shuffle seed: the order does not depend on how many
+                    # random numbers were drawn before (sampling, dropout), so resume replays it
+                    g = torch.Generator().manual_seed(self.seed * 1_000_003 + epoch * 1009 + fi)
+                    train_loader, val_loader = self.loaderObj.create_dataloaders(
+                        read(fp), num_workers=self.num_workers, generator=g)
                     if hasattr(train_loader.sampler, "set_epoch"):
                         train_loader.sampler.set_epoch(epoch)
-                    self.train_epoch(epoch, train_loader, val_loader)
+                    self.train_epoch(epoch, train_loader, val_loader, start_context=start_context,
+                                     file_index=fi, skip_batches=skip)
                     if pbar is not None:
                         pbar.update(1)
                     if self.stop:
@@ -240,24 +262,12 @@ class Trainer:
             self.save_checkpoint(f"model_pg_{self.global_step}_interrupted.pth")
         return self._results()
 
+    def train_model(self, n_epochs):
+        eos = self.config["eos_text"]
+        return self._loop(n_epochs, lambda fp: read_text_file(fp) + " " + eos + " ", "Every effort moves you")
+
     def finetune_model(self, n_epochs):
-        self._setup_schedule(n_epochs)
-        pbar = self._progress(n_epochs * len(self.data_files))
-        try:
-            for epoch in range(n_epochs):
-                for fp in self.data_files:
-                    data = read_json_file(fp)
-                    train_loader, val_loader = self.loaderObj.create_dataloaders(data, num_workers=0)
-                    if hasattr(train_loader.sampler, "set_epoch"):
-                        train_loader.sampler.set_epoch(epoch)
-                    self.train_epoch(epoch, train_loader, val_loader, start_context=ALPACA_CONTEXT)
-                    if pbar is not None:
-                        pbar.update(1)
-                    if self.stop:
-                        return self._results()
-        except KeyboardInterrupt:
-            self.save_checkpoint(f"model_pg_{self.global_step}_interrupted.pth")
-        return self._results()
+        return self._loop(n_epochs, read_json_file, ALPACA_CONTEXT)
 
     def _results(self):
         return self.train_losses, self.val_losses, self.track_tokens_seen, self.track_lrs
@@ -282,19 +292,33 @@ class Trainer:
         path = self.save_dir / file_name
         save_model(self.model, path, self.engine, self.rank)
         if self.save_resume:
-            save_resume_state(self.save_dir / f"trainer_state_{self.global_step}.pt", self.optimizer,
-                              dict(global_step=self.global_step, tokens_seen=self.tokens_seen,
-                                   train_losses=self.train_losses, val_losses=self.val_losses,
-                                   track_lrs=self.track_lrs, track_tokens_seen=self.track_tokens_seen),
+            save_resume_state(resume_state_path(path), self.optimizer, self.trainer_state(),
                               self.rank, self.world_size)
         if self.rank == 0:
             logger.info(f"Checkpoint saved: {path}")
         if self._dist():
             dist.barrier()
 
+    _STATE_KEYS = ("global_step", "tokens_seen", "train_losses", "val_losses", "track_lrs", "track_tokens_seen")
+
+    def trainer_state(self) -> dict:
+        st = {k: getattr(self, k) for k in self._STATE_KEYS}
+        rc = self.model.rctx
+        st.update(pos=list(self.pos), rng_seed=int(rc.seed), rng_offset=int(rc._offset),
+                  loss_scale=(self.loss_scaler.scale if self.loss_scaler else None),
+                  loss_scale_clean=(self.loss_scaler.clean if self.loss_scaler else None))
+        return st
+
     def load_trainer_state(self, st: dict):
-        for k in ("global_step", "tokens_seen", "train_losses", "val_losses", "track_lrs", "track_tokens_seen"):
+        for k in self._STATE_KEYS:
             setattr(self, k, st[k])
+        if "pos" in st:
+            self.pos = tuple(st["pos"])
+            self._resume_pos = self.pos
+            rc = self.model.rctx
+            rc.seed, rc._offset = st["rng_seed"], st["rng_offset"]
+            if self.loss_scaler is not None and st.get("loss_scale") is not None:
+                self.loss_scaler.scale, self.loss_scaler.clean = st["loss_scale"], st["loss_scale_clean"]
 
     @torch.no_grad()
     def calc_loss_loader(self, data_loader, num_batches=None):

@@ -55,20 +55,6 @@ def test_finetune_llama_lora_debug(tmp_path):
     assert "trf_blocks.0.att.W_query.lora.A" in sd and "out_head.lora.B" in sd
 
 
-def test_resume_roundtrip(tmp_path):
-    out = tmp_path / "ckpt"
-    base = ["--model", "GPT2", "--num_params", "124M", "--debug", "--data_dir", str(tmp_path / "data"),
-            "--synthetic_data", "--output_dir", str(out), "--n_epochs", "1", "--eval_freq", "100",
-            "--print_sample_iter", "100", "--batch_size", "2", "--device", "cpu", "--no_plot",
-            "--save_resume_state", "--sample_tokens", "2"]
-    _run(base + ["--max_steps", "3", "--save_ckpt_freq", "2"], tmp_path)
-    assert (out / "trainer_state_2.pt").exists()
-    st = torch.load(out / "trainer_state_2.pt", weights_only=True)
-    assert st["trainer"]["global_step"] == 2 and st["optim"][0]["step"] == 3
-    _run(base + ["--max_steps", "5", "--save_ckpt_freq", "100", "--resume", str(out / "model_pg_2.pth")], tmp_path)
-    assert (out / "model_pg_final.pth").exists()
-
-
 @pytest.mark.parametrize("mode", [["--use_fsdp"], ["--use_zero_opt"], []])
 def test_multi_process_spawn_gloo(tmp_path, mode):
     """--run_type multi_gpu self-spawns (reference mp.spawn path) — here 2 CPU ranks on gloo."""
