@@ -42,10 +42,12 @@ def compute_dtype(args) -> torch.dtype:
 def build_config(args):
     cfg = get_config(args.model, args.num_params, context_length=getattr(args, "context_length", 1024) or 1024)
     cfg = cfg.replace(dtype=compute_dtype(args))
-    if args.load_weights and args.model == "GPT2":
-        cfg = cfg.replace(qkv_bias=True)
     if args.debug:
         cfg = debug_config(cfg)
+    # after --debug (the reference applies its debug qkv_bias=False last, build_components.py:
+    # 69-80, which makes --debug --load_weights unloadable: HF GPT-2 always has qkv biases)
+    if args.load_weights and args.model == "GPT2":
+        cfg = cfg.replace(qkv_bias=True)
     return cfg
 
 

@@ -199,7 +199,7 @@ class _BlockFn(torch.autograd.Function):
         if isinstance(saved, tuple) and len(saved) == 3 and isinstance(saved[0], str) \
                 and saved[0] == "__recompute__":
             _, x, replay = saved
-            _, saved = comp.forward(x, save=True, replay=replay)
+            _, saved = comp.forward(x, save=True, replay=replay, recompute=True)
         dx = comp.backward(dy.contiguous(), saved)
         ctx.saved = None
         eng.post_backward(comp.unit)

@@ -138,7 +138,9 @@ class GPTBlockCompute(UnitCompute):
         m, _ = self.proj.forward(ops.gelu_fwd(f))
         return x2 + m
 
-    def forward(self, x, save, replay=None):
+    def forward(self, x, save, replay=None, recompute=False):
+        """``recompute`` (activation-checkpoint re-run in backward): the MLP output projection
+        and the last residual are skipped — backward never reads the block output."""
         rc, cfg, b = self.rctx, self.rctx.cfg, self.block
         B, T = rc.B, rc.T
         N, d = B * T, cfg.emb_dim
@@ -160,8 +162,11 @@ class GPTBlockCompute(UnitCompute):
         h2, m2, r2 = self._ln(x2, b.norm2)
         f, xa_fc = self.fc.forward(h2)
         g = ops.gelu_fwd(f)
-        m, xa_pr = self.proj.forward(g)
-        x3 = ops.dropout_add(x2, m, p, rc.seed, offs[2])
+        if recompute:
+            x3, xa_pr = None, self.proj.lora_state(g)
+        else:
+            m, xa_pr = self.proj.forward(g)
+            x3 = ops.dropout_add(x2, m, p, rc.seed, offs[2])
         if not save:
             # full-recompute mode: _BlockFn keeps ``offs`` as the replay token so the
             # recomputed forward regenerates identical dropout masks
@@ -170,7 +175,7 @@ class GPTBlockCompute(UnitCompute):
                      p=p, offs=offs, xa=(xa_qkv, xa_o, xa_fc, xa_pr))
         if rc.actv_ckpt == "none":
             saved.update(h1=h1, h2=h2)
-        return x3.view(B, T, d), saved
+        return (x3.view(B, T, d) if x3 is not None else None), saved
 
     def backward(self, dy, s):
         rc, cfg, u, b = self.rctx, self.rctx.cfg, self.unit, self.block

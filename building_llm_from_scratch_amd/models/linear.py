@@ -235,6 +235,18 @@ class FusedLinear:
                 xa.append(t)
         return y, xa
 
+    def lora_state(self, x: torch.Tensor):
+        """Only the LoRA intermediate ``x A`` that ``backward`` needs (what ``forward`` would
+        return as its second value) without the base GEMM: the activation-checkpoint recompute
+        of a block's LAST projection needs it, but never that projection's output."""
+        if not self.has_lora:
+            return None
+        u = self.unit
+        if self._grouped_lora(x):
+            P = ops.lora_pack_t([u.data(s.lora_A) for s in self.lora_specs])
+            return ("grouped", ops.lora_down(x, [P], [0], [x.shape[1]], [0], self.lora_R), P)
+        return [torch.mm(x, u.data(s.lora_A)) if s.lora_A is not None else None for s in self.specs]
+
     # ------------------------------------------------------------------ bwd
     def backward(self, dy: torch.Tensor, x: torch.Tensor, xa, need_dx: bool = True,
                  accumulate: bool = False, dx_acc: Optional[torch.Tensor] = None):

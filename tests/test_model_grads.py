@@ -63,11 +63,14 @@ def test_gpt2_grads(qkv_bias, ckpt):
     _compare(m, lambda sd: gpt2_loss(sd, cfg, idx, tgt), idx, tgt)
 
 
+@pytest.mark.parametrize("ckpt", ["none", "full"])
 @pytest.mark.parametrize("family", ["llama", "gpt2"])
-def test_lora_grads(family):
+def test_lora_grads(family, ckpt):
+    """``full`` also covers the recompute's skipped last projection: its LoRA intermediate is
+    rebuilt without the base GEMM (FusedLinear.lora_state)."""
     torch.manual_seed(0)
     cfg = _small_llama() if family == "llama" else _small_gpt2()
-    m = build_model(cfg)
+    m = build_model(cfg, use_actv_ckpt=ckpt)
     for p in m.parameters():
         p.requires_grad = False
     replace_linear_with_lora(m, rank=4, alpha=8)
@@ -103,10 +106,11 @@ def test_logits_path_matches_loss_path():
     assert torch.allclose(last[:, 0], logits[:, -1].detach(), atol=1e-5)
 
 
+@pytest.mark.parametrize("ckpt", ["none", "full"])
 @pytest.mark.parametrize("family", ["llama", "gpt2"])
-def test_grouped_lora_path_grads(family, monkeypatch):
+def test_grouped_lora_path_grads(family, monkeypatch, ckpt):
     """The grouped LoRA plumbing (pack / down / up / wgrad, as the HIP kernels run it) driven
     through the CPU oracles gives the eager-autograd gradients."""
     from building_llm_from_scratch_amd.models import linear
     monkeypatch.setattr(linear, "FORCE_GROUPED_LORA", True)
-    test_lora_grads(family)
+    test_lora_grads(family, ckpt)
