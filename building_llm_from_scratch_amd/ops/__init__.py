@@ -108,13 +108,15 @@ def rope_(qkv, cos, sin, T: int, H: int, G: int, hd: int, inverse: bool = False,
 
 
 def attention_backend(dtype: torch.dtype, device_type: str = "cuda") -> str:
+    """Every GPU dtype runs a flash kernel (bf16/fp16: attn_mfma.hip; fp32: attn_f32.hip on the
+    f32 MFMA; other head dims: attn_naive.hip) -- [B,H,T,T] is never materialised."""
     if device_type != "cuda":
         return "reference"
-    return "hip" if dtype in (torch.bfloat16, torch.float16) else "reference-fp32"
+    return "hip" if dtype in (torch.bfloat16, torch.float16, torch.float32) else "reference"
 
 
 def flash_attn_fwd(qkv, B, T, H, G, hd, causal=True, dropout_p=0.0, seed=0, offset=0):
-    if qkv.device.type == "cuda" and qkv.dtype in (torch.bfloat16, torch.float16):
+    if qkv.device.type == "cuda" and qkv.dtype in (torch.bfloat16, torch.float16, torch.float32):
         load_ext(required=True)
         return _k().flash_attn_fwd(qkv, B, T, H, G, hd, causal, float(dropout_p), int(seed), int(offset))
     return ref.flash_attn_fwd(qkv, B, T, H, G, hd, causal, dropout_p, seed, offset)
@@ -286,7 +288,7 @@ def attn_decode(q, kcache, vcache, L: int):
 
 
 def flash_attn_bwd(qkv, o, lse, do, B, T, H, G, hd, causal=True, dropout_p=0.0, seed=0, offset=0):
-    if qkv.device.type == "cuda" and qkv.dtype in (torch.bfloat16, torch.float16):
+    if qkv.device.type == "cuda" and qkv.dtype in (torch.bfloat16, torch.float16, torch.float32):
         load_ext(required=True)
         return _k().flash_attn_bwd(qkv, o, lse, do, B, T, H, G, hd, causal, float(dropout_p),
                                    int(seed), int(offset))

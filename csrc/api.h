@@ -47,6 +47,14 @@ void attn_bwd_naive(DType dt, const void* qkv, const void* o, const float* lse, 
                     float* delta, int B, int T, int H, int G, int hd, bool causal, float p, uint64_t seed,
                     uint64_t offset, hipStream_t s);
 
+// attn_f32.hip: fp32 flash attention on v_mfma_f32_32x32x2_f32 (head dims 64 / 128)
+bool attn_f32_head_dim(int hd);
+void attn_fwd_f32(const float* qkv, float* o, float* lse, int B, int T, int H, int G, int hd, bool causal, float p,
+                  uint64_t seed, uint64_t offset, hipStream_t s);
+void attn_bwd_f32(const float* qkv, const float* o, const float* lse, const float* dout, float* dqkv, float* delta,
+                  int B, int T, int H, int G, int hd, bool causal, float p, uint64_t seed, uint64_t offset,
+                  hipStream_t s);
+
 // whether the dK/dV pass needs the fp32 per-head partial buffer (GQA without the fused-head variant)
 bool attn_bwd_kv_partials(int B, int T, int H, int G);
 

@@ -315,8 +315,8 @@ std::tuple<Tensor, Tensor> flash_attn_fwd(const Tensor& qkv, int64_t B, int64_t 
                                           int64_t hd, bool causal, double p, int64_t seed, int64_t offset) {
   check_gpu(qkv, "qkv");
   c10::DeviceGuard g(qkv.device());
-  TORCH_CHECK(qkv.scalar_type() == at::kBFloat16 || qkv.scalar_type() == at::kHalf,
-              "flash_attn: bf16/fp16 only");
+  TORCH_CHECK(qkv.scalar_type() == at::kBFloat16 || qkv.scalar_type() == at::kHalf ||
+              qkv.scalar_type() == at::kFloat, "flash_attn: bf16/fp16/fp32 only");
   TORCH_CHECK(qkv.dim() == 2 && qkv.size(0) == B * T && qkv.size(1) == (H + 2 * G) * hd);
   TORCH_CHECK(H % G == 0, "flash_attn: n_heads must be a multiple of n_kv_groups");
   TORCH_CHECK(bllm::attn_supported_head_dim((int)hd), "flash_attn: unsupported head_dim ", hd);
@@ -332,13 +332,16 @@ Tensor flash_attn_bwd(const Tensor& qkv, const Tensor& o, const Tensor& lse, con
                       int64_t offset) {
   check_gpu(qkv, "qkv"); check_gpu(o, "o"); check_gpu(lse, "lse"); check_gpu(dout, "dout");
   c10::DeviceGuard g(qkv.device());
-  TORCH_CHECK(qkv.scalar_type() == at::kBFloat16 || qkv.scalar_type() == at::kHalf);
+  TORCH_CHECK(qkv.scalar_type() == at::kBFloat16 || qkv.scalar_type() == at::kHalf ||
+              qkv.scalar_type() == at::kFloat);
+  TORCH_CHECK(o.scalar_type() == qkv.scalar_type() && dout.scalar_type() == qkv.scalar_type(), "flash_attn_bwd: dtypes");
+  TORCH_CHECK(qkv.is_contiguous() && o.is_contiguous() && dout.is_contiguous(), "flash_attn_bwd: contiguous inputs");
   TORCH_CHECK(qkv.dim() == 2 && qkv.size(0) == B * T && qkv.size(1) == (H + 2 * G) * hd);
   TORCH_CHECK(o.sizes() == dout.sizes() && o.size(0) == B * T && o.size(1) == H * hd);
   TORCH_CHECK(bllm::attn_supported_head_dim((int)hd), "flash_attn: unsupported head_dim ", hd);
   auto dqkv = at::empty_like(qkv);
   auto delta = at::empty({B, H, T}, qkv.options().dtype(at::kFloat));
-  const bool mfma = bllm::attn_mfma_head_dim((int)hd);
+  const bool mfma = qkv.scalar_type() != at::kFloat && bllm::attn_mfma_head_dim((int)hd);
   // per-query-head dK/dV partials only for GQA (MHA writes dK/dV directly); dQ is atomic-free
   auto dkv_part = (mfma && bllm::attn_bwd_kv_partials((int)B, (int)T, (int)H, (int)G)) ? at::empty({2, B * T, H, hd}, qkv.options().dtype(at::kFloat)) : Tensor();
   bllm::attn_bwd(dt_of(qkv), qkv.data_ptr(), o.data_ptr(), lse.data_ptr<float>(), dout.data_ptr(), dqkv.data_ptr(),

@@ -177,7 +177,7 @@ def test_adamw_and_norm(pdt):
     assert math.isclose(sq.item(), sq0.item(), rel_tol=1e-4)
 
 
-@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16, torch.float32])
 @pytest.mark.parametrize("B,T,H,G,hd", [(2, 64, 4, 4, 64), (1, 200, 8, 2, 128), (2, 33, 4, 2, 64),
                                          (1, 10, 16, 8, 2), (2, 256, 4, 1, 128), (1, 512, 8, 2, 128),
                                          (1, 300, 2, 2, 128), (1, 96, 3, 3, 64)])
@@ -194,6 +194,42 @@ def test_flash_attention(dt, B, T, H, G, hd, p, causal):
     dqkv0 = ref.flash_attn_bwd(qkv.cpu().float(), o0, lse0, do.cpu().float(), B, T, H, G, hd, causal, p, 99,
                                12345)
     _close(dqkv, dqkv0, dt, 4, name="dqkv")
+
+
+def test_flash_attention_fp32_is_flash_not_materialised():
+    """GPT-2 in the reference's default fp32 (args.py:77) at T = 4096, 12 heads: the fp32 kernels'
+    footprint is O(T) -- the materialised oracle would need 12 x 4096^2 x 4 B = 805 MB per sequence."""
+    B, T, H, hd = 2, 4096, 12, 64
+    qkv = torch.randn(B * T, 3 * H * hd, device=DEV)
+    torch.cuda.synchronize()
+    torch.cuda.reset_peak_memory_stats()
+    base = torch.cuda.memory_allocated()
+    o, lse = ops.flash_attn_fwd(qkv, B, T, H, H, hd, True, 0.1, 3, 0)
+    dq = ops.flash_attn_bwd(qkv, o, lse, torch.randn_like(o), B, T, H, H, hd, True, 0.1, 3, 0)
+    torch.cuda.synchronize()
+    extra = torch.cuda.max_memory_allocated() - base
+    assert extra < 3 * qkv.numel() * 4, extra
+    assert torch.isfinite(dq).all()
+
+
+@pytest.mark.parametrize("T", [1024, 2048, 4096, 8192])
+@pytest.mark.parametrize("H,G,hd,p", [(32, 8, 128, 0.0), (12, 12, 64, 0.1)])
+def test_flash_attention_long_context(T, H, G, hd, p):
+    """The bench shape (Llama-3-8B: 32 q / 8 kv heads x 128) and GPT-2 (hd 64, dropout) at
+    T = 1k..8k (``--context_length``); fp32 reference evaluated on the GPU (the [H,T,T] scores
+    of the oracle fit in HBM; the kernels never form them)."""
+    B = 1
+    g = torch.Generator(device=DEV).manual_seed(T + hd)
+    qkv = torch.randn(B * T, (H + 2 * G) * hd, device=DEV, generator=g).to(torch.bfloat16)
+    do = torch.randn(B * T, H * hd, device=DEV, generator=g).to(torch.bfloat16)
+    o, lse = ops.flash_attn_fwd(qkv, B, T, H, G, hd, True, p, 7, 4242)
+    o0, lse0 = ref.flash_attn_fwd(qkv.float(), B, T, H, G, hd, True, p, 7, 4242)
+    _close(o, o0, torch.bfloat16, 2, name="o")
+    _close(lse, lse0, torch.float32, 1000, name="lse")
+    dqkv = ops.flash_attn_bwd(qkv, o, lse, do, B, T, H, G, hd, True, p, 7, 4242)
+    del o0
+    dqkv0 = ref.flash_attn_bwd(qkv.float(), o.float(), lse0, do.float(), B, T, H, G, hd, True, p, 7, 4242)
+    _close(dqkv, dqkv0, torch.bfloat16, 4, name="dqkv")
 
 
 @pytest.mark.parametrize("p", [0.0, 0.1])
