@@ -23,7 +23,9 @@ one MI355X holds 288 GB, so each rank runs 24 x 1024 tokens (``--batch_size 4`` 
 reference default).
 
 ``mfu`` counts model FLOPs only (6·N_nonemb + 12·L·d·T per token, no recompute); ``hfu`` adds
-the re-run forward of full checkpointing (x 4/3).  Peak is 2.5 PF dense bf16.
+what the hardware also executes under full checkpointing: each block's forward re-run minus its
+last projection, which the recompute skips (config.recompute_flops_per_token).  Peak is 2.5 PF
+dense bf16.
 
 Other BASELINE configs (``--preset``; each prints one JSON line of its own):
   gpt2_774m_ddp          #2  GPT2-774M pretrain, DDP, bf16, dropout 0.1
@@ -253,7 +255,8 @@ def main(argv=None):
     if a.lora_rank:  # frozen base: no weight-gradient GEMMs (2 of the 6 N FLOPs per param)
         flops_tok -= 2.0 * (cfg.num_params() - cfg.vocab_size * cfg.emb_dim)
     mfu = tps / world * flops_tok / PEAK_BF16
-    recompute = 4.0 / 3.0 if a.actv_ckpt == "full" else 1.0
+    extra = cfg.recompute_flops_per_token(int(round(T_eff))) if a.actv_ckpt == "full" else 0.0
+    recompute = (flops_tok + extra) / flops_tok
     prof = profile_phases(model, opt, next_batch, dev) if (a.profile and rank == 0 and cuda) else None
     if rank == 0:
         headline = a.preset == "llama3_8b_fsdp" and cuda and not a.layers

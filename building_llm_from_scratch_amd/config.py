@@ -143,6 +143,16 @@ class ModelConfig:
         n = self.num_params() - n_emb
         return 6.0 * n + 12.0 * self.n_layers * self.emb_dim * T
 
+    def recompute_flops_per_token(self, seq_len: Optional[int] = None) -> float:
+        """Extra FLOPs of full activation checkpointing: every block's forward re-run in
+        backward, minus its last projection (down / c_proj), whose output backward never reads
+        (models/llama.py, gpt2.py ``recompute``)."""
+        T = seq_len or self.context_length
+        d, F = self.emb_dim, self.hidden_dim
+        kv = self.n_kv_groups * self.head_dim
+        proj = d * (d + 2 * kv) + d * d + (2 * d * F if self.is_llama else d * F)
+        return self.n_layers * (2.0 * proj + 4.0 * d * T)
+
 
 # ---------------------------------------------------------------------------
 # GPT-2 registry (reference Models/GPT2/config.py)

@@ -17,12 +17,14 @@ MI355X execution (per block, N = B*T rows, all bf16 with fp32 accumulation):
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn as nn
 
 from .. import ops
 from .base import BaseLM, UnitCompute, cached_attention
-from .linear import FusedLinear
+from .linear import FusedLinear, _dgrad_wt_ok, _weight_grad
 
 
 # ---------------------------------------------------------------------------
@@ -213,8 +215,20 @@ class LlamaBlockCompute(UnitCompute):
         return dx.view(B, T, d)
 
 
+# logits chunk budget of the fused head + CE (bytes of one [rows, V] chunk)
+LOGIT_CHUNK_BYTES = int(os.environ.get("BLLM_LOGIT_CHUNK_MB", "2048")) * 2 ** 20
+MIN_CHUNK_ROWS = 256  # chunk rows are a multiple of this (token-major dW kernel K granule)
+
+
 class HeadComputeMixin:
-    """final norm + LM head + fused cross-entropy (reference train.py:88-92)."""
+    """final norm + LM head + fused cross-entropy (reference train.py:88-92).
+
+    Training forward (``forward_loss`` with ``save``): the head GEMM, CE forward, CE backward and
+    both head gradient GEMMs run chunk by chunk over the tokens, so the [N, V] logits never exist
+    at once (Llama-3-8B, 24k tokens: 6.3 GB of bf16 logits -> 2 GiB chunks, 3 of them; 6 chunks
+    of 1 GiB measured +5 ms / step, profiles/r2_llama3_8b_fsdp_full_v3.md).  The loss
+    gradient is taken for dloss = 1 and scaled by the real dloss in backward (dh and dW, one
+    pass each) -- exact for any dloss, including fp16 loss scaling."""
 
     ignore_index = -100
 
@@ -242,9 +256,40 @@ class HeadComputeMixin:
         dx = self._norm_bwd(dh, (x2d,) + ns)
         return dx.view(self.rctx.B, self.rctx.T, -1)
 
+    def _fused_ok(self, h) -> bool:
+        return not self.head.has_lora and self.head.b_params is None
+
+    def _fused_loss(self, x2d, h, ns, targets, nvalid):
+        W = self.head.W()                                          # [V, d]
+        N, V = h.shape[0], W.shape[0]
+        rows = max(MIN_CHUNK_ROWS, LOGIT_CHUNK_BYTES // (V * h.element_size()) // MIN_CHUNK_ROWS * MIN_CHUNK_ROWS)
+        gW = None
+        if self.head.unit.trainable(self.head.W_params[0]):
+            gW = torch.empty(W.shape, dtype=self.head.unit.train.grad.dtype, device=W.device)
+        dh = torch.empty_like(h)
+        Wd = W
+        if _dgrad_wt_ok(h[:rows], W):   # one K-contiguous copy of W for every chunk's dX GEMM
+            Wd = ops.transpose2d(W).t()
+        scale = (1.0 / nvalid).reshape(1)
+        total = torch.zeros(1, dtype=torch.float32, device=h.device)
+        for s0 in range(0, N, rows):
+            hc, tc = h[s0:s0 + rows], targets[s0:s0 + rows]
+            logits = torch.mm(hc, W.t())
+            lrow, lse = ops.ce_fwd(logits, tc, self.ignore_index)
+            total += lrow.sum()
+            dl = ops.ce_bwd_(logits, tc, lse, scale, self.ignore_index)   # in place
+            torch.mm(dl, Wd, out=dh[s0:s0 + rows])
+            if gW is not None:
+                _weight_grad(dl, hc, gW, accumulate=s0 > 0)
+            del logits, dl
+        return total[0] / nvalid, (x2d, ns, dh, gW, "fused")
+
     def forward_loss(self, x, targets, save):
         x2d = x.reshape(-1, x.shape[-1])
         h, ns = self._norm_fwd(x2d)
+        if save and self._fused_ok(h):
+            nvalid = (targets != self.ignore_index).sum().to(torch.float32).clamp_(min=1.0)
+            return self._fused_loss(x2d, h, ns, targets, nvalid)
         logits, xa = self.head.forward(h)
         rows, lse = ops.ce_fwd(logits, targets, self.ignore_index)
         # a batch whose targets are all ignore_index (e.g. prompts longer than the context in
@@ -256,6 +301,18 @@ class HeadComputeMixin:
         return loss, (x2d, h, ns, xa, logits, lse, targets, nvalid)
 
     def backward_loss(self, dloss, saved):
+        if saved[-1] == "fused":
+            x2d, ns, dh, gW, _ = saved
+            dls = dloss.float().reshape(1)
+            dh.mul_(dls)
+            if gW is not None:
+                g = self.head.unit.fused_grad(self.head.W_params)
+                if self.rctx.accumulate:
+                    g.add_(gW * dls)
+                else:
+                    torch.mul(gW, dls, out=g)
+            dx = self._norm_bwd(dh, (x2d,) + ns)
+            return dx.view(self.rctx.B, self.rctx.T, -1)
         x2d, h, ns, xa, logits, lse, targets, nvalid = saved
         scale = (dloss.float() / nvalid).reshape(1)
         dlogits = ops.ce_bwd_(logits, targets, lse, scale, self.ignore_index)  # in place

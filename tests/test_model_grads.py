@@ -114,3 +114,32 @@ def test_grouped_lora_path_grads(family, monkeypatch, ckpt):
     from building_llm_from_scratch_amd.models import linear
     monkeypatch.setattr(linear, "FORCE_GROUPED_LORA", True)
     test_lora_grads(family, ckpt)
+
+
+@pytest.mark.parametrize("family", ["llama", "gpt2"])
+def test_fused_chunked_head_ce(family, monkeypatch):
+    """Head + CE fused chunk by chunk (logits never materialised whole): several chunks, a
+    chunk boundary inside the sequence, ignore_index targets, and a non-unit dloss (fp16 loss
+    scaling path) all give the eager-autograd gradients."""
+    from building_llm_from_scratch_amd.models import llama
+    monkeypatch.setattr(llama, "MIN_CHUNK_ROWS", 8)
+    monkeypatch.setattr(llama, "LOGIT_CHUNK_BYTES", 8 * 97 * 4)   # 8 rows of fp32 logits per chunk
+    torch.manual_seed(0)
+    cfg = _small_llama() if family == "llama" else _small_gpt2()
+    m = build_model(cfg)
+    idx = torch.randint(0, cfg.vocab_size, (3, 13))
+    tgt = torch.randint(0, cfg.vocab_size, (3, 13))
+    tgt[1, :5] = -100
+    if family == "llama":
+        cos, sin = ops.rope_tables(cfg.head_dim, cfg.context_length, cfg.rope_base, cfg.rope_freq)
+        fn = lambda sd: llama_loss(sd, cfg, idx, tgt, cos, sin)  # noqa: E731
+    else:
+        fn = lambda sd: gpt2_loss(sd, cfg, idx, tgt)  # noqa: E731
+    _compare(m, fn, idx, tgt)
+    # dloss != 1: gradients scale exactly (unit backwards overwrite the flat gradients)
+    (m(idx, tgt) * 4.0).backward()
+    g4 = {n: p.grad.clone() for n, p in m.named_parameters() if p.grad is not None}
+    m(idx, tgt).backward()
+    g1 = {n: p.grad.clone() for n, p in m.named_parameters() if p.grad is not None}
+    for n in g1:
+        assert torch.allclose(g4[n], 4.0 * g1[n], rtol=1e-5, atol=1e-6), n

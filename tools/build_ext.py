@@ -126,7 +126,8 @@ def build_host(verbose: bool = False):
         out = os.path.join(ROOT, "building_llm_from_scratch_amd", "_" + f[:-4] + suffix)
         cmd = [os.environ.get("CXX", "g++"), "-O3", "-std=c++17", "-shared", "-fPIC", "-fvisibility=hidden",
                f"-I{pybind11.get_include()}", f"-I{sysconfig.get_paths()['include']}", src, "-o", out]
-        if not os.path.exists(out) or os.path.getmtime(src) > os.path.getmtime(out):
+        deps = [src] + [os.path.join(hdir, h) for h in os.listdir(hdir) if h.endswith(".h")]
+        if not os.path.exists(out) or max(os.path.getmtime(d) for d in deps) > os.path.getmtime(out):
             r = subprocess.run(cmd, capture_output=True, text=True)
             if r.returncode != 0:
                 raise RuntimeError(f"host build failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
