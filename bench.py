@@ -86,6 +86,7 @@ def parse(argv=None):
     ap.add_argument("--lora_rank", type=int, default=None)
     ap.add_argument("--lora_alpha", type=int, default=32)
     ap.add_argument("--reshard_after_forward", type=int, default=1)
+    ap.add_argument("--fsdp_prefetch", type=int, default=1, help="FSDP units all-gathered ahead")
     ap.add_argument("--layers", type=int, default=None, help="(debug only) override n_layers; invalidates the metric")
     ap.add_argument("--profile", action="store_true", help="print a per-phase timing breakdown to stderr")
     ap.add_argument("--overlap_optimizer", action="store_true",
@@ -117,7 +118,9 @@ def init_dist(a):
         dev = torch.device("cpu")
     kw = dict(timeout=timedelta(minutes=a.pg_timeout_min))
     if dev.type == "cuda":
+        from building_llm_from_scratch_amd.parallel import nccl_pg_options
         kw["device_id"] = dev
+        kw["pg_options"] = nccl_pg_options()
     backend = "nccl" if dev.type == "cuda" else "gloo"
     if launched:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -197,7 +200,7 @@ def main(argv=None):
         replace_linear_with_lora(model, rank=a.lora_rank, alpha=a.lora_alpha)
     reduce = get_policy(a.mixed_precision).reduce_dtype if a.mixed_precision else None
     engine = setup_engine(model, a.parallel, device=dev, reduce_dtype=reduce,
-                          reshard_after_forward=bool(a.reshard_after_forward))
+                          reshard_after_forward=bool(a.reshard_after_forward), prefetch=a.fsdp_prefetch)
     opt = FusedAdamW(model, lr=3e-4, weight_decay=0.1, engine=engine, overlap=a.overlap_optimizer)
     B, T = a.batch_size, a.seq_len
 

@@ -102,6 +102,7 @@ def build_parser() -> argparse.ArgumentParser:
     x.add_argument("--pg_timeout_min", type=float, default=30.0,
                    help="collective timeout (minutes): a wedged RCCL/gloo collective raises instead of hanging")
     x.add_argument("--bucket_mb", type=float, default=256.0, help="DDP all-reduce bucket size")
+    x.add_argument("--fsdp_prefetch", type=int, default=1, help="FSDP: units all-gathered ahead of the computing one")
     x.add_argument("--no_reshard_after_forward", action="store_true",
                    help="FSDP: keep gathered params from forward to backward (ZeRO-2 style)")
     x.add_argument("--no_plot", action="store_true")
@@ -133,7 +134,9 @@ def ddp_setup(rank: int, world_size: int, args):
     backend = args.backend or ("nccl" if device.type == "cuda" else "gloo")
     timeout = timedelta(minutes=getattr(args, "pg_timeout_min", 30.0))
     if backend == "nccl":
-        dist.init_process_group("nccl", rank=rank, world_size=world_size, device_id=device, timeout=timeout)
+        from .parallel import nccl_pg_options
+        dist.init_process_group("nccl", rank=rank, world_size=world_size, device_id=device, timeout=timeout,
+                                pg_options=nccl_pg_options())
     else:
         dist.init_process_group("gloo", rank=rank, world_size=world_size, timeout=timeout)
     return device

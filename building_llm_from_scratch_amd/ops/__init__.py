@@ -350,12 +350,13 @@ def embedding_bwd(idx, dx, grad_wte, grad_wpe, T: int, accumulate: bool = False)
 
 # --------------------------------------------------------------------------- LoRA
 def lora_kernel_ok(x: torch.Tensor, ranks, widths) -> bool:
-    """Whether the fused LoRA kernels (csrc/lora.hip) take a group: bf16/fp16 on the GPU,
-    N % 64 == 0 tokens, every rank a multiple of 16 (<= 64) and every column width (input and
-    member outputs) a multiple of 32.  Otherwise the caller uses the hipBLASLt GEMM path."""
+    """Whether the fused LoRA kernels (csrc/lora.hip) take a group: bf16/fp16 on the GPU, any
+    token count (row tails are bounds-checked: variable-length instruction batches), every rank
+    a multiple of 16 (<= 64) and every column width (input and member outputs) a multiple of 32.
+    Otherwise the caller uses the hipBLASLt GEMM path."""
     if x.device.type != "cuda" or x.dtype not in (torch.bfloat16, torch.float16):
         return False
-    if x.dim() != 2 or x.shape[0] % 64 or x.shape[1] % 32:
+    if x.dim() != 2 or x.shape[0] < 1 or x.shape[1] % 32:
         return False
     return all(r % 16 == 0 and 0 < r <= 64 for r in ranks) and all(w % 32 == 0 for w in widths)
 

@@ -16,8 +16,21 @@ import torch
 from ..models.base import LocalEngine
 
 
+def nccl_pg_options():
+    """RCCL process-group options: collectives on HIGH-priority HIP streams, so a prefetched
+    all-gather / reduce-scatter kernel is scheduled ahead of queued compute kernels instead of
+    waiting behind them (the overlap FSDP / DDP rely on)."""
+    import torch.distributed as dist
+    try:
+        opts = dist.ProcessGroupNCCL.Options()
+        opts.is_high_priority_stream = True
+        return opts
+    except (AttributeError, RuntimeError):  # torch built without NCCL/RCCL
+        return None
+
+
 def setup_engine(model, kind: str = "local", device=None, reduce_dtype=None, bucket_mb: float = 256.0,
-                 reshard_after_forward: bool = True, process_group=None):
+                 reshard_after_forward: bool = True, process_group=None, prefetch: int = 1):
     """Flatten ``model`` onto ``device`` and attach the requested engine; returns it."""
     device = torch.device(device) if device is not None else model.device
     if kind in ("local", "single", "single_gpu"):
@@ -34,5 +47,5 @@ def setup_engine(model, kind: str = "local", device=None, reduce_dtype=None, buc
     if kind == "fsdp":
         from .fsdp import FSDPEngine
         return FSDPEngine(model, device, reduce_dtype=reduce_dtype,
-                          reshard_after_forward=reshard_after_forward, pg=process_group)
+                          reshard_after_forward=reshard_after_forward, pg=process_group, prefetch=prefetch)
     raise ValueError(f"unknown parallel engine '{kind}'")

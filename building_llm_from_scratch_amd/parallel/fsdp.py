@@ -53,13 +53,17 @@ def _alloc(t: torch.Tensor, nbytes: int):
 
 class FSDPEngine(LocalEngine):
     def __init__(self, model, device, reduce_dtype: Optional[torch.dtype] = None,
-                 reshard_after_forward: bool = True, pg=None):
+                 reshard_after_forward: bool = True, pg=None, prefetch: int = 1):
         self.pg = pg
         self.world_size = dist.get_world_size(pg)
         self.rank = dist.get_rank(pg)
         self.model = model
         self.device = torch.device(device)
         self.reshard_after_forward = reshard_after_forward
+        # units gathered ahead of the one computing (forward: i+1..i+prefetch, backward:
+        # i-1..i-prefetch); each extra unit costs one gathered unit of memory (Llama-3-8B block:
+        # 436 MB bf16) and buys slack when a gather is slower than one unit's compute
+        self.prefetch = max(1, int(prefetch))
         self.grad_prescale = 1.0 / self.world_size
         self.is_cuda = self.device.type == "cuda"
         self.no_shard = self.world_size == 1
@@ -149,8 +153,7 @@ class FSDPEngine(LocalEngine):
     # ------------------------------------------------------------------ hooks
     def pre_forward(self, unit):
         self._wait_gather(unit)
-        nxt = unit.index + 1
-        if nxt < len(self.units):
+        for nxt in range(unit.index + 1, min(unit.index + 1 + self.prefetch, len(self.units))):
             self._issue_gather(self.units[nxt], async_op=True)
 
     def post_forward(self, unit):
@@ -168,8 +171,7 @@ class FSDPEngine(LocalEngine):
             self._in_backward = True
             self._rs_works = []
         self._wait_gather(unit)
-        prv = unit.index - 1
-        if prv >= 0:
+        for prv in range(unit.index - 1, max(unit.index - 1 - self.prefetch, -1), -1):
             self._issue_gather(self.units[prv], async_op=True)
         fb = unit.train
         if fb is not None and not self.no_shard:

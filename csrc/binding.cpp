@@ -431,7 +431,7 @@ Tensor lora_down(const Tensor& x, at::TensorList ws, at::IntArrayRef c0, at::Int
   c10::DeviceGuard g(x.device());
   TORCH_CHECK(x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kHalf, "lora_down: bf16/fp16 only");
   const int64_t N = x.size(0);
-  TORCH_CHECK(N % 16 == 0 && R % 16 == 0 && R > 0, "lora_down: N and R must be multiples of 16");
+  TORCH_CHECK(N > 0 && R % 16 == 0 && R > 0, "lora_down: N > 0 and R a multiple of 16 required");
   TORCH_CHECK(ws.size() == c0.size() && ws.size() == lens.size() && ws.size() == ocol.size());
   auto out = at::empty({N, R}, x.options());
   bllm::LoraDownArgs a{};
@@ -465,7 +465,7 @@ void lora_up_(Tensor& y, const Tensor& t, at::TensorList us, at::IntArrayRef c0,
   c10::DeviceGuard g(y.device());
   TORCH_CHECK(y.scalar_type() == t.scalar_type() && (y.scalar_type() == at::kBFloat16 || y.scalar_type() == at::kHalf));
   const int64_t N = y.size(0);
-  TORCH_CHECK(t.size(0) == N && N % 64 == 0, "lora_up: N must be a multiple of 64");
+  TORCH_CHECK(t.size(0) == N && N > 0, "lora_up: t rows must match y");
   TORCH_CHECK(us.size() == c0.size() && us.size() == toff.size() && (int)us.size() <= bllm::LORA_MAX);
   bllm::LoraUpArgs a{};
   a.y = y.data_ptr(); a.ldy = y.stride(0); a.t = t.data_ptr(); a.ldt = t.stride(0); a.scale = (float)scale;
@@ -502,7 +502,7 @@ void lora_wgrad(const Tensor& p, const Tensor& q, at::TensorList gs, at::IntArra
   c10::DeviceGuard g(p.device());
   TORCH_CHECK(p.scalar_type() == q.scalar_type() && (p.scalar_type() == at::kBFloat16 || p.scalar_type() == at::kHalf));
   const int64_t N = p.size(0);
-  TORCH_CHECK(q.size(0) == N && N % 64 == 0, "lora_wgrad: N must be a multiple of 64");
+  TORCH_CHECK(q.size(0) == N && N > 0, "lora_wgrad: p / q token counts differ");
   TORCH_CHECK(gs.size() == pa.size() && gs.size() == qb.size() && (int)gs.size() <= bllm::LORA_MAX && !gs.empty());
   bllm::LoraWgradArgs a{};
   a.p = p.data_ptr(); a.ldp = p.stride(0); a.q = q.data_ptr(); a.ldq = q.stride(0);

@@ -58,14 +58,16 @@ template <typename T> __device__ __forceinline__ float from_bits(short b) {
 // MFMA: A = X rows (lane: X[row l&15][k 8(l>>4)..+8], one 16-B load), B[k][col] = W[col][k]
 // (W rows are k-contiguous -> one 16-B load per column tile).
 template <typename T>
-__global__ __launch_bounds__(512) void lora_down_k(LoraDownArgs a) {
+__global__ __launch_bounds__(512) void lora_down_k(LoraDownArgs a, int N) {
   constexpr int NW = 8;
   __shared__ float red[NW][16][4 * 16 + 1];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int ch = blockIdx.y;
   const int nt = a.nt[ch];
   const long row0 = (long)blockIdx.x * 16;
-  const T* x = (const T*)a.x + (row0 + (lane & 15)) * a.ldx + a.c0[ch] + 8 * (lane >> 4);
+  // rows past the token count (last block of an N % 16 != 0 batch) read row N-1, never stored
+  const long xr = row0 + (lane & 15) < N ? row0 + (lane & 15) : N - 1;
+  const T* x = (const T*)a.x + xr * a.ldx + a.c0[ch] + 8 * (lane >> 4);
   const T* w = (const T*)a.w[ch] + (long)(lane & 15) * a.ldw[ch] + 8 * (lane >> 4);
   const long wstep = 16 * a.ldw[ch];
   f32x4 acc[4];
@@ -102,6 +104,7 @@ __global__ __launch_bounds__(512) void lora_down_k(LoraDownArgs a) {
   T* out = (T*)a.out + row0 * a.ldo + a.ocol[ch];
   for (int e = threadIdx.x; e < 16 * cols; e += NW * 64) {
     const int r = e / cols, c = e - r * cols;
+    if (row0 + r >= N) continue;
     float v = 0.f;
 #pragma unroll
     for (int q = 0; q < NW; ++q) v += red[q][r][c];
@@ -119,7 +122,7 @@ __global__ __launch_bounds__(512) void lora_down_k(LoraDownArgs a) {
 // U^T . T^T (B fragment = a 16-B global read of a t row); the fp32 tile is re-laid through a
 // per-wave LDS buffer so every lane stores 16 contiguous bytes.
 template <typename T>
-__global__ __launch_bounds__(256) void lora_up_k(LoraUpArgs a, int rows) {
+__global__ __launch_bounds__(256) void lora_up_k(LoraUpArgs a, int rows, int N) {
   constexpr int BN = 128, RP = 64 + 8, EP = BN + 4;
   __shared__ __attribute__((aligned(16))) short us[BN * RP];
   __shared__ __attribute__((aligned(16))) float eps_[4 * 16 * EP];
@@ -159,7 +162,9 @@ __global__ __launch_bounds__(256) void lora_up_k(LoraUpArgs a, int rows) {
     __syncthreads();
     for (int rt = 0; rt < rows / 64; ++rt) {
       const long row0 = (long)blockIdx.x * rows + rt * 64 + wave * 16;
-      const T* t = (const T*)a.t + (row0 + (lane & 15)) * a.ldt + a.toff[m] + j0;
+      if (row0 >= N) break;  // wave-uniform: this wave's remaining tiles are past the tokens
+      const long tr = row0 + (lane & 15) < N ? row0 + (lane & 15) : N - 1;
+      const T* t = (const T*)a.t + tr * a.ldt + a.toff[m] + j0;
       f32x4 acc[8];
 #pragma unroll
       for (int q = 0; q < 8; ++q) acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -182,7 +187,7 @@ __global__ __launch_bounds__(256) void lora_up_k(LoraUpArgs a, int rows) {
 #pragma unroll
       for (int p = 0; p < 4; ++p) {
         const int row = (lane >> 4) + 4 * p;
-        if (!col_ok) continue;
+        if (!col_ok || row0 + row >= N) continue;
         const long g = (row0 + row) * a.ldy + a.c0[m] + cb + c8;
         const f32x4 v0 = *reinterpret_cast<const f32x4*>(&ep[row * EP + c8]);
         const f32x4 v1 = *reinterpret_cast<const f32x4*>(&ep[row * EP + c8 + 4]);
@@ -235,7 +240,7 @@ __global__ __launch_bounds__(256) void lora_wgrad_k(LoraWgradArgs a, int N) {
   const int r = a.r[m], len = a.len[m];
   const int b0 = bx * 64;
   const int S = gridDim.y, split = blockIdx.y;
-  const int nchunks = N / 64;
+  const int nchunks = (N + 63) / 64;
   const int c_lo = (int)((long)nchunks * split / S), c_hi = (int)((long)nchunks * (split + 1) / S);
   const T* Q = (const T*)a.q + a.qb[m];
   const T* P = (const T*)a.p + a.pa[m];
@@ -251,8 +256,9 @@ __global__ __launch_bounds__(256) void lora_wgrad_k(LoraWgradArgs a, int N) {
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const long n = (long)ck * 64 + sn + 32 * h;
-      qv[h] = q_ok ? ld8(Q + n * a.ldq + b0 + sc) : zero;
-      pv[h] = p_ok ? ld8(P + n * a.ldp + sc) : zero;
+      const bool n_ok = n < N;  // tail chunk of an N % 64 != 0 batch: zero tokens
+      qv[h] = q_ok && n_ok ? ld8(Q + n * a.ldq + b0 + sc) : zero;
+      pv[h] = p_ok && n_ok ? ld8(P + n * a.ldp + sc) : zero;
     }
   };
   // tr-read addresses: lane 4q+p of each 16-lane group -> row q, columns 4p..4p+3 of the block
@@ -329,9 +335,9 @@ __global__ __launch_bounds__(256) void lora_pack_t_k(LoraPackArgs a, int K) {
 
 // ----------------------------------------------------------------------------- launchers
 void lora_down(DType dt, const LoraDownArgs& a, int N, hipStream_t s) {
-  dim3 grid(N / 16, a.n);
-  if (dt == DType::BF16) hipLaunchKernelGGL(lora_down_k<bf16_t>, grid, dim3(512), 0, s, a);
-  else hipLaunchKernelGGL(lora_down_k<f16_t>, grid, dim3(512), 0, s, a);
+  dim3 grid(ceil_div(N, 16), a.n);
+  if (dt == DType::BF16) hipLaunchKernelGGL(lora_down_k<bf16_t>, grid, dim3(512), 0, s, a, N);
+  else hipLaunchKernelGGL(lora_down_k<f16_t>, grid, dim3(512), 0, s, a, N);
 }
 
 void lora_up(DType dt, const LoraUpArgs& a, int N, int max_len, hipStream_t s) {
@@ -339,16 +345,16 @@ void lora_up(DType dt, const LoraUpArgs& a, int N, int max_len, hipStream_t s) {
   int col_blocks = 0;
   for (int m = 0; m < a.n; ++m) col_blocks += ceil_div(a.len[m], 128);
   int rows = 256;
-  while (rows > 64 && ((long)N / rows * col_blocks < 1024 || N % rows)) rows /= 2;
-  dim3 grid(N / rows, ceil_div(max_len, 128), a.n);
-  if (dt == DType::BF16) hipLaunchKernelGGL(lora_up_k<bf16_t>, grid, dim3(256), 0, s, a, rows);
-  else hipLaunchKernelGGL(lora_up_k<f16_t>, grid, dim3(256), 0, s, a, rows);
+  while (rows > 64 && (long)ceil_div(N, rows) * col_blocks < 1024) rows /= 2;
+  dim3 grid(ceil_div(N, rows), ceil_div(max_len, 128), a.n);
+  if (dt == DType::BF16) hipLaunchKernelGGL(lora_up_k<bf16_t>, grid, dim3(256), 0, s, a, rows, N);
+  else hipLaunchKernelGGL(lora_up_k<f16_t>, grid, dim3(256), 0, s, a, rows, N);
 }
 
 int lora_wgrad_splits(int blocks, int N) {
   // aim for >= 2 blocks per CU; every split keeps at least 4 chunks of 64 tokens
   int S = ceil_div(512, blocks > 0 ? blocks : 1);
-  const int max_s = (N / 64) / 4;
+  const int max_s = ceil_div(N, 64) / 4;
   if (S > max_s) S = max_s;
   return S < 1 ? 1 : S;
 }

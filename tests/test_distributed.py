@@ -96,7 +96,7 @@ def _worker(rank, world, kind, family, lora, ckpt, out, store, opts=None):
             for p in m.parameters():
                 p.data.normal_()
         eng = setup_engine(m, kind, device="cpu", bucket_mb=opts.get("bucket_mb", 0.05),
-                           reduce_dtype=opts.get("reduce_dtype"))
+                           reduce_dtype=opts.get("reduce_dtype"), prefetch=opts.get("prefetch", 1))
         opt = FusedAdamW(m, lr=opts.get("lr", 1e-2), weight_decay=0.1, engine=eng)
         if opts.get("load"):
             _, init = _build(family, lora, ckpt, odd=opts.get("odd", False), dtype=opts.get("dtype"))
@@ -159,10 +159,11 @@ def test_world4_lora_fsdp():
     _check(_spawn(4, "fsdp", "llama", True, opts=dict(rows=8)), ref_sd, ref_losses)
 
 
-@pytest.mark.parametrize("kind", ["ddp", "fsdp"])
-def test_world4_full_actv_ckpt(kind):
+@pytest.mark.parametrize("kind,prefetch", [("ddp", 1), ("fsdp", 1), ("fsdp", 3)])
+def test_world4_full_actv_ckpt(kind, prefetch):
+    """(fsdp, 3): three units gathered ahead in forward and in backward."""
     ref_sd, ref_losses = _reference("gpt2", False, rows=8)
-    _check(_spawn(4, kind, "gpt2", False, ckpt="full", opts=dict(rows=8)), ref_sd, ref_losses)
+    _check(_spawn(4, kind, "gpt2", False, ckpt="full", opts=dict(rows=8, prefetch=prefetch)), ref_sd, ref_losses)
 
 
 @pytest.mark.parametrize("kind", ["ddp", "zero1", "fsdp"])

@@ -270,10 +270,12 @@ def _up_only(t, Bs, c0, offs, s, N, M):
 
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("r", [16, 64])
-def test_lora_kernels(dt, r):
+@pytest.mark.parametrize("N", [1024, 1000, 37, 9288])
+def test_lora_kernels(dt, r, N):
     """pack / down / up / wgrad against fp32 matmuls, Q/K/V-style group (3 members, unequal
-    widths), including split-N partial reduction, accumulation and transposed grad views."""
-    N, K = 1024, 512
+    widths), including split-N partial reduction, accumulation and transposed grad views; token
+    counts that are not multiples of 16 / 64 (variable-length Alpaca batches: 24 x 387 = 9288)."""
+    K = 512
     outs = [512, 128, 128]
     c0 = [0, 512, 640]
     M = sum(outs)
