@@ -19,8 +19,10 @@ steps, then exactly K timed steps bracketed by barrier + device sync; the slowes
 is reported.  Weak scaling: the per-GPU micro-batch is fixed, total tokens grow with N.
 
 Micro-batch: the reference's ``--batch_size`` default 4 (args.py:53) was sized for a 16 GB T4;
-one MI355X holds 288 GB, so each rank runs 24 x 1024 tokens (``--batch_size 4`` reproduces the
-reference default).
+one MI355X holds 288 GB, so each rank runs 40 x 1024 tokens (``--batch_size 4`` reproduces the
+reference default).  With full checkpointing only block inputs are kept, so memory barely grows
+with B (same box, profiles/r2_bsweep.md): B=24 21.93k tok/s at 130.6 GiB, B=32 22.26k at 134.2,
+B=40 22.40k at 137.8 -- larger GEMM row counts and fewer LM-head chunk tails per token.
 
 ``mfu`` counts model FLOPs only (6·N_nonemb + 12·L·d·T per token, no recompute); ``hfu`` adds
 what the hardware also executes under full checkpointing: each block's forward re-run minus its
@@ -57,7 +59,7 @@ METRIC = "tokens/sec (whole node) Llama-3-8B bf16 FSDP at 1/2/4/8 MI355X"
 PEAK_BF16 = 2.5e15
 
 PRESETS = {
-    "llama3_8b_fsdp": dict(model="llama3", num_params="8B", parallel="fsdp", actv_ckpt="full", batch_size=24,
+    "llama3_8b_fsdp": dict(model="llama3", num_params="8B", parallel="fsdp", actv_ckpt="full", batch_size=40,
                            data="pretrain", mixed_precision=None, lora_rank=0),
     "gpt2_774m_ddp": dict(model="GPT2", num_params="774M", parallel="ddp", actv_ckpt="none", batch_size=24,
                           data="pretrain", mixed_precision=None, lora_rank=0),

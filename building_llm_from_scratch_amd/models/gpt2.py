@@ -173,7 +173,7 @@ class GPTBlockCompute(UnitCompute):
             return x3.view(B, T, d), offs
         saved = dict(x=x2d, m1=m1, r1=r1, qkv=qkv, o=o, lse=lse, x2=x2, m2=m2, r2=r2, f=f, g=g,
                      p=p, offs=offs, xa=(xa_qkv, xa_o, xa_fc, xa_pr))
-        if rc.actv_ckpt == "none":
+        if rc.actv_ckpt == "none" or recompute:  # the recompute's norm outputs live one block
             saved.update(h1=h1, h2=h2)
         return (x3.view(B, T, d) if x3 is not None else None), saved
 
