@@ -410,6 +410,25 @@ class BaseLM(nn.Module):
             x = c.infer(x, B, t, pos, kv)
         return comps[-1].infer(x, B, t)
 
+    def decode_graph_ok(self, cache) -> bool:
+        """Whether :meth:`forward_cached_dev` runs on this model / cache (GPU, bf16/fp16, head
+        dim 64/128, cache <= 8192 positions)."""
+        dev = self._anchor.device if self._anchor is not None else torch.device("cpu")
+        kc = cache[0][0]
+        return (dev.type == "cuda" and kc.dtype in (torch.bfloat16, torch.float16)
+                and self.cfg.head_dim in (64, 128) and kc.shape[2] <= 8192)
+
+    @torch.no_grad()
+    def forward_cached_dev(self, idx: torch.Tensor, cache, pos_t: torch.Tensor) -> torch.Tensor:
+        """One decode token per row (idx [B, 1]) at the position held in ``pos_t`` (int32 on the
+        device): no host-side position, no host sync, so the whole step can be captured in a HIP
+        graph once and replayed per token (train/generate.py)."""
+        comps = self._comps
+        x = comps[0].infer_dev(idx, pos_t)
+        for c, kv in zip(comps[1:-1], cache):
+            x = c.infer_dev(x, pos_t, kv)
+        return comps[-1].infer(x, idx.shape[0], 1)
+
     def sync_params(self):
         """Make the current stream wait for every in-flight (overlapped) optimizer update."""
         self._rctx.sync_all_params()

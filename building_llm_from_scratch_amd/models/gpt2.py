@@ -86,6 +86,12 @@ class GPTEmbedCompute(UnitCompute):
         wpe = self.unit.data(self.m.pos_emb.weight)
         return (wte[idx.reshape(-1)].view(B, t, -1) + wpe[pos:pos + t]).reshape(B * t, -1)
 
+    def infer_dev(self, idx, pos_t):
+        """One decode token per row, position in device memory (graph-replayable)."""
+        wte = self.unit.data(self.m.tok_emb.weight)
+        wpe = self.unit.data(self.m.pos_emb.weight)
+        return wte.index_select(0, idx.reshape(-1)) + wpe.index_select(0, pos_t)
+
     def backward(self, dx, saved):
         idx, p, off = saved
         rc = self.rctx
@@ -126,6 +132,18 @@ class GPTBlockCompute(UnitCompute):
     def _ln(self, x, norm):
         u = self.unit
         return ops.layernorm_fwd(x, u.data(norm.weight), u.data(norm.bias), 1e-5)
+
+    def infer_dev(self, x2d, pos_t, kv):
+        """Decode step with the position in device memory: K/V appended and attended by one
+        kernel (csrc/attn_decode.hip APPEND), so the step can be captured in a HIP graph."""
+        cfg, b = self.rctx.cfg, self.block
+        H = cfg.n_heads
+        qkv, _ = self.qkv.forward(self._ln(x2d, b.norm1)[0])
+        a, _ = self.o.forward(ops.attn_decode_append(qkv, kv[0], kv[1], pos_t, H, H))
+        x2 = x2d + a
+        f, _ = self.fc.forward(self._ln(x2, b.norm2)[0])
+        m, _ = self.proj.forward(ops.gelu_fwd(f))
+        return x2 + m
 
     def infer(self, x2d, B, t, pos, kv):
         cfg, b = self.rctx.cfg, self.block

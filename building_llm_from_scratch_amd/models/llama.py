@@ -115,6 +115,10 @@ class LlamaEmbedCompute(UnitCompute):
         W = self.unit.data(self.m.tok_emb.weight)
         return ops.embedding_fwd(idx.reshape(-1).contiguous(), W, None, idx.shape[1])
 
+    def infer_dev(self, idx, pos_t):
+        W = self.unit.data(self.m.tok_emb.weight)
+        return ops.embedding_fwd(idx.reshape(-1).contiguous(), W, None, 1)
+
 
 class LlamaBlockCompute(UnitCompute):
     def __init__(self, rctx, block: TransformerBlock, i: int):
@@ -167,6 +171,22 @@ class LlamaBlockCompute(UnitCompute):
             if rc.actv_ckpt == "none" or recompute:  # the recompute's norm outputs live one block
                 saved.update(h1=h1, h2=h2)
         return (x3.view(B, T, d) if x3 is not None else None), saved
+
+    def infer_dev(self, x2d, pos_t, kv):
+        """Decode step with the position in device memory (RoPE reads it, the decode kernel
+        appends K/V at it): capturable in a HIP graph and replayed once per generated token."""
+        cfg, u, b = self.rctx.cfg, self.unit, self.block
+        H, G, hd, eps = cfg.n_heads, cfg.n_kv_groups, cfg.head_dim, cfg.norm_eps
+        cos, sin = self.rctx.rope
+        h1, _ = ops.rmsnorm_fwd(x2d, u.data(b.norm1.weight), eps)
+        qkv, _ = self.qkv.forward(h1)
+        ops.rope_dev_(qkv, cos, sin, H, G, hd, pos_t)
+        o = ops.attn_decode_append(qkv, kv[0], kv[1], pos_t, H, G)
+        x2, _ = self.o.forward(o, residual=x2d)
+        h2, _ = ops.rmsnorm_fwd(x2, u.data(b.norm2.weight), eps)
+        gu, _ = self.gu.forward(h2)
+        x3, _ = self.down.forward(ops.swiglu_fwd(gu), residual=x2)
+        return x3
 
     def infer(self, x2d, B, t, pos, kv):
         cfg, u, b = self.rctx.cfg, self.unit, self.block

@@ -122,6 +122,19 @@ def flash_attn_fwd(qkv, B, T, H, G, hd, causal=True, dropout_p=0.0, seed=0, offs
     return ref.flash_attn_fwd(qkv, B, T, H, G, hd, causal, dropout_p, seed, offset)
 
 
+def rope_dev_(qkv, cos, sin, H: int, G: int, hd: int, pos_t):
+    """RoPE of one decode token per row at the position stored in ``pos_t`` (int32, device)."""
+    load_ext(required=True)
+    _k().rope_dev_(qkv, cos, sin, H, G, hd, pos_t)
+    return qkv
+
+
+def attn_decode_append(qkv, kc, vc, pos_t, H: int, G: int):
+    """Append the rows' new K/V to the caches at ``pos_t`` and attend over pos + 1 keys."""
+    load_ext(required=True)
+    return _k().attn_decode_append(qkv, kc, vc, pos_t, H, G)
+
+
 def bias_grad_(dy, db, accumulate: bool = False):
     """db (+)= dy.sum(0) (fp32 accumulation, deterministic)."""
     if _hip(dy) and dy.shape[1] * dy.element_size() % 16 == 0:

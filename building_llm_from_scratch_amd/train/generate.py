@@ -8,9 +8,20 @@ Same contract: sliding window of ``context_size`` tokens, optional top-k thresho
 * :func:`generate_cached` — KV-cache decode: one prefill of the window, then one token per
   forward through the HIP decode-attention kernel over the cache (the window slides by
   re-prefilling, exactly reproducing the reference's conditioning).  Under FSDP the parameters
-  are gathered once for the whole sample instead of once per token.
+  are gathered once for the whole sample instead of once per token.  Tokens go into a
+  preallocated buffer and the all-rows-eos stop test runs every ``EOS_CHECK_EVERY`` tokens (the
+  output is cut at the first all-eos step, so the result is identical): the host never waits
+  on the GPU per token, so each token's ~12 launches per layer queue up behind the previous
+  token's kernels instead of running while the GPU idles.
+* On the GPU the single-token step (every layer: norm, QKV GEMM, RoPE, K/V append + decode
+  attention, projections, MLP, head) is captured ONCE per sample into a HIP graph
+  (``torch.cuda.CUDAGraph``) with the position kept in device memory, and replayed per token:
+  one graph launch instead of ~12 kernel launches per layer (the decode loop is launch-bound
+  below Llama-3-8B size).  ``BLLM_DECODE_GRAPH=0`` runs it eagerly.
 """
 from __future__ import annotations
+
+import os
 
 from typing import Optional
 
@@ -28,6 +39,40 @@ def _sample(logits, temperature, top_k, generator):
     return torch.argmax(logits, dim=-1, keepdim=True)
 
 
+EOS_CHECK_EVERY = int(os.environ.get("BLLM_EOS_CHECK_EVERY", "16"))
+
+
+def _graph_enabled() -> bool:
+    return os.environ.get("BLLM_DECODE_GRAPH", "1") != "0"
+
+
+class DecodeGraph:
+    """A model's single-token decode step (``forward_cached_dev``) captured into a HIP graph.
+    Capture runs with the position set to the cache's LAST slot, so the warm-up / capture
+    passes only write that slot, which every later decode step overwrites before reading it."""
+
+    def __init__(self, model, cache, B: int, device):
+        Tmax = cache[0][0].shape[2]
+        self.idx = torch.zeros(B, 1, dtype=torch.long, device=device)
+        self.pos = torch.full((1,), Tmax - 1, dtype=torch.int32, device=device)
+        cur = torch.cuda.current_stream(device)
+        side = torch.cuda.Stream(device)
+        side.wait_stream(cur)
+        with torch.cuda.stream(side):          # warm-up: hipBLASLt heuristics, allocator pool
+            for _ in range(2):
+                model.forward_cached_dev(self.idx, cache, self.pos)
+        cur.wait_stream(side)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self.logits = model.forward_cached_dev(self.idx, cache, self.pos)
+
+    def step(self, idx_next: torch.Tensor, pos: int) -> torch.Tensor:
+        self.idx.copy_(idx_next)
+        self.pos.fill_(pos)
+        self.graph.replay()
+        return self.logits
+
+
 @torch.no_grad()
 def generate_cached(model, idx: torch.Tensor, max_new_tokens: int, context_size: int, temperature: float = 0.0,
                     top_k: Optional[int] = None, eos_id: Optional[int] = None,
@@ -36,30 +81,49 @@ def generate_cached(model, idx: torch.Tensor, max_new_tokens: int, context_size:
     model.eval()
     device = next(model.parameters()).device
     idx = idx.to(device)
-    B = idx.shape[0]
+    B, T0 = idx.shape
+    out = torch.empty(B, T0 + max(max_new_tokens, 0), dtype=idx.dtype, device=device)
+    out[:, :T0] = idx
+    n = checked = T0
     eng = model.rctx.engine
     resident = eng.params_resident() if hasattr(eng, "params_resident") else _null()
     with resident:
         cache = model.new_kv_cache(B, context_size)
         cond = idx[:, -context_size:]
-        logits = model.forward_cached(cond, cache, 0)
+        logits = model.forward_cached(cond, cache, 0) if max_new_tokens > 0 else None
         pos = cond.shape[1]
+        dec = None
+        if max_new_tokens > 8 and _graph_enabled() and hasattr(model, "decode_graph_ok") \
+                and model.decode_graph_ok(cache):
+            logits = logits.clone()            # the prefill output must survive the capture
+            dec = DecodeGraph(model, cache, B, device)
         for i in range(max_new_tokens):
             idx_next = _sample(logits, temperature, top_k, generator)
-            if eos_id is not None and bool((idx_next == eos_id).all()):
-                break
-            idx = torch.cat((idx, idx_next), dim=1)
-            if i == max_new_tokens - 1:
+            out[:, n] = idx_next[:, 0]
+            n += 1
+            last = i == max_new_tokens - 1
+            if eos_id is not None and (n - checked >= EOS_CHECK_EVERY or last):
+                # reference semantics (generate.py:68-70): stop before the first step at which
+                # EVERY row sampled eos; later tokens were speculative and are dropped
+                alleos = (out[:, checked:n] == eos_id).all(dim=0)
+                if bool(alleos.any()):
+                    n = checked + int(alleos.nonzero()[0, 0])
+                    break
+                checked = n
+            if last:
                 break
             if pos >= context_size:          # window full: slide by re-prefilling
-                cond = idx[:, -context_size:]
+                cond = out[:, n - context_size:n]
                 logits = model.forward_cached(cond, cache, 0)
                 pos = context_size
+            elif dec is not None:
+                logits = dec.step(idx_next, pos)
+                pos += 1
             else:
                 logits = model.forward_cached(idx_next, cache, pos)
                 pos += 1
     model.train(was_training)
-    return idx
+    return out[:, :n]
 
 
 class _null:

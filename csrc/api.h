@@ -31,7 +31,7 @@ void gelu_bwd(DType dt, const void* f, const void* dg, void* df, long n, hipStre
 void dropout_add(DType dt, const void* x, const void* a, void* out, long n, float p, uint64_t seed, uint64_t offset,
                  hipStream_t s);
 void rope(DType dt, void* qkv, const float* cosT, const float* sinT, long N, int T, int H, int G, int hd,
-          bool inverse, int pos_offset, hipStream_t s);
+          bool inverse, int pos_offset, hipStream_t s, const int* pos_dev = nullptr);
 
 // attention (attn_fwd.hip / attn_bwd.hip / attn_naive.hip)
 bool attn_supported_head_dim(int hd);
@@ -72,6 +72,11 @@ void sum_partials_into(DType pdt, DType odt, const void* part, void* out, long n
 
 // attn_decode.hip — single-query attention over a [B, G, Tmax, hd] KV cache
 int attn_decode_max_len();
+// graph-replayable decode step: q / new k / new v read from the packed qkv rows [B, (H+2G)*hd],
+// the position from device memory (*pos), new k/v appended to the caches at *pos, attention
+// over the pos + 1 keys -> out [B, H*hd]
+void attn_decode_append(DType dt, const void* qkv, void* kc, void* vc, void* out, const int* pos, int B, int H,
+                        int G, int hd, int Tmax, hipStream_t s);
 void attn_decode(DType dt, const void* q, const void* kc, const void* vc, void* out, int B, int H, int G, int hd,
                  int Tmax, int L, hipStream_t s);
 

@@ -20,10 +20,15 @@ namespace bllm {
 constexpr int DEC_THREADS = 256;
 constexpr int DEC_MAXL = 8192;  // LDS score buffer (32 KiB)
 
-template <typename T, int HD>
-__global__ __launch_bounds__(DEC_THREADS) void attn_decode_k(const T* __restrict__ q, const T* __restrict__ kc,
-                                                             const T* __restrict__ vc, T* __restrict__ out,
-                                                             int H, int G, int Tmax, int L, float scale) {
+// APPEND (graph-replayed decode, the position known only on the device): q, the new key and
+// the new value come from the packed qkv row of the token (row stride qs); L = *pos + 1 and key
+// L - 1 is read from that row, while the first query head of each kv group also writes it into
+// the caches at row *pos (no block of this launch reads cache row *pos, so no ordering needed).
+template <typename T, int HD, bool APPEND>
+__global__ __launch_bounds__(DEC_THREADS) void attn_decode_k(const T* __restrict__ q, T* __restrict__ kc,
+                                                             T* __restrict__ vc, T* __restrict__ out,
+                                                             int H, int G, int Tmax, int L, float scale,
+                                                             const int* __restrict__ pos, long qs) {
   constexpr int VEC = 8;               // elements per 16-B load
   constexpr int NC = HD / VEC;         // 16-B chunks per row
   constexpr int KPH = DEC_THREADS / NC;  // key phases in the output pass
@@ -33,9 +38,22 @@ __global__ __launch_bounds__(DEC_THREADS) void attn_decode_k(const T* __restrict
   const int bh = blockIdx.x, h = bh % H, b = bh / H;
   const int g = h / (H / G);
   const int tid = threadIdx.x;
-  const T* qr = q + ((long)b * H + h) * HD;
-  const T* kb = kc + ((long)b * G + g) * (long)Tmax * HD;
-  const T* vb = vc + ((long)b * G + g) * (long)Tmax * HD;
+  const T* qr = APPEND ? q + (long)b * qs + (long)h * HD : q + ((long)b * H + h) * HD;
+  T* kb = kc + ((long)b * G + g) * (long)Tmax * HD;
+  T* vb = vc + ((long)b * G + g) * (long)Tmax * HD;
+  const T* knew = nullptr;
+  const T* vnew = nullptr;
+  if constexpr (APPEND) {
+    const int p = *pos;
+    L = p + 1;
+    knew = q + (long)b * qs + (long)(H + g) * HD;
+    vnew = q + (long)b * qs + (long)(H + G + g) * HD;
+    if (h % (H / G) == 0 && tid < 2 * (HD / 8)) {  // one block per kv group appends k and v
+      const int c = tid % (HD / 8);
+      if (tid < HD / 8) st16(kb + (long)p * HD + c * 8, ld16(knew + c * 8));
+      else st16(vb + (long)p * HD + c * 8, ld16(vnew + c * 8));
+    }
+  }
   const float c = scale * 1.4426950408889634f;
 
   float qf[HD];
@@ -48,7 +66,7 @@ __global__ __launch_bounds__(DEC_THREADS) void attn_decode_k(const T* __restrict
   // 1. scores (log2 domain)
   float mx = -INFINITY;
   for (int k = tid; k < L; k += DEC_THREADS) {
-    const T* kr = kb + (long)k * HD;
+    const T* kr = (APPEND && k == L - 1) ? knew : kb + (long)k * HD;
     float s = 0.f;
 #pragma unroll
     for (int i = 0; i < NC; ++i) {
@@ -87,7 +105,7 @@ __global__ __launch_bounds__(DEC_THREADS) void attn_decode_k(const T* __restrict
 #pragma unroll
   for (int j = 0; j < VEC; ++j) acc[j] = 0.f;
   for (int k = kp; k < L; k += KPH) {
-    const Vec16<T> v = ld16(vb + (long)k * HD + ci * VEC);
+    const Vec16<T> v = ld16(((APPEND && k == L - 1) ? vnew : vb + (long)k * HD) + ci * VEC);
     const float p = sc[k];
 #pragma unroll
     for (int j = 0; j < VEC; ++j) acc[j] += p * to_f(v.v[j]);
@@ -109,8 +127,23 @@ void attn_decode(DType dt, const void* q, const void* kc, const void* vc, void* 
                  int Tmax, int L, hipStream_t s) {
   const float scale = 1.f / sqrtf((float)hd);
   dim3 grid(B * H), block(DEC_THREADS);
-#define L_(TT, HDD) hipLaunchKernelGGL((attn_decode_k<TT, HDD>), grid, block, 0, s, (const TT*)q, (const TT*)kc, \
-                                       (const TT*)vc, (TT*)out, H, G, Tmax, L, scale)
+#define L_(TT, HDD) hipLaunchKernelGGL((attn_decode_k<TT, HDD, false>), grid, block, 0, s, (const TT*)q, (TT*)kc, \
+                                       (TT*)vc, (TT*)out, H, G, Tmax, L, scale, nullptr, 0L)
+  if (dt == DType::BF16) {
+    if (hd == 128) L_(bf16_t, 128); else L_(bf16_t, 64);
+  } else {
+    if (hd == 128) L_(f16_t, 128); else L_(f16_t, 64);
+  }
+#undef L_
+}
+
+void attn_decode_append(DType dt, const void* qkv, void* kc, void* vc, void* out, const int* pos, int B, int H,
+                        int G, int hd, int Tmax, hipStream_t s) {
+  const float scale = 1.f / sqrtf((float)hd);
+  const long qs = (long)(H + 2 * G) * hd;
+  dim3 grid(B * H), block(DEC_THREADS);
+#define L_(TT, HDD) hipLaunchKernelGGL((attn_decode_k<TT, HDD, true>), grid, block, 0, s, (const TT*)qkv, (TT*)kc, \
+                                       (TT*)vc, (TT*)out, H, G, Tmax, 0, scale, pos, qs)
   if (dt == DType::BF16) {
     if (hd == 128) L_(bf16_t, 128); else L_(bf16_t, 64);
   } else {

@@ -220,6 +220,19 @@ void rope_(Tensor& qkv, const Tensor& cos, const Tensor& sin, int64_t T, int64_t
              (int)G, (int)hd, inverse, (int)pos_offset, stream());
 }
 
+// graph-replayable RoPE of one decode token: position = pos_offset + *pos (device int32)
+void rope_dev_(Tensor& qkv, const Tensor& cos, const Tensor& sin, int64_t H, int64_t G, int64_t hd,
+               const Tensor& pos) {
+  check_gpu(qkv, "qkv"); check_gpu(cos, "cos"); check_gpu(sin, "sin"); check_gpu(pos, "pos");
+  c10::DeviceGuard g(qkv.device());
+  TORCH_CHECK(qkv.dim() == 2 && qkv.size(1) == (H + 2 * G) * hd && hd % 2 == 0);
+  TORCH_CHECK(cos.scalar_type() == at::kFloat && sin.scalar_type() == at::kFloat && cos.size(1) == hd / 2);
+  TORCH_CHECK(pos.scalar_type() == at::kInt && pos.numel() == 1, "rope_dev_: pos must be one int32");
+  // T = 1: every row is one token at position *pos (the caller keeps *pos < cos.size(0))
+  bllm::rope(dt_of(qkv), qkv.data_ptr(), cos.data_ptr<float>(), sin.data_ptr<float>(), qkv.size(0), 1, (int)H,
+             (int)G, (int)hd, false, 0, stream(), pos.data_ptr<int>());
+}
+
 // ------------------------------------------------------------------ attention
 // db (+)= dy.sum(0): dy [N, F] bf16/fp16/fp32, db [F] any float dtype (written in place)
 void bias_grad_(const Tensor& dy, Tensor& db, bool accumulate) {
@@ -292,6 +305,26 @@ void gemm_nn_(const Tensor& a, const Tensor& b, Tensor& c, bool accumulate) {
   TORCH_CHECK(bllm::gemm_nn_supported((int)M, (int)N, (int)K), "gemm_nn: unsupported shape ", M, "x", N, "x", K);
   bllm::gemm_nn(dt_of(a), dt_of(c), a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0), c.data_ptr(), c.stride(0),
                 (int)M, (int)N, (int)K, accumulate, stream());
+}
+
+// qkv [B, (H+2G)*hd] (one decode token per row); kc / vc [B, G, Tmax, hd] valid below *pos;
+// appends the token's k / v at *pos and attends over pos + 1 keys -> out [B, H*hd]
+Tensor attn_decode_append(const Tensor& qkv, Tensor& kc, Tensor& vc, const Tensor& pos, int64_t H, int64_t G) {
+  check_gpu(qkv, "qkv"); check_gpu(kc, "kcache"); check_gpu(vc, "vcache"); check_gpu(pos, "pos");
+  c10::DeviceGuard g(qkv.device());
+  TORCH_CHECK(qkv.scalar_type() == at::kBFloat16 || qkv.scalar_type() == at::kHalf, "attn_decode_append: bf16/fp16");
+  TORCH_CHECK(kc.scalar_type() == qkv.scalar_type() && vc.scalar_type() == qkv.scalar_type());
+  TORCH_CHECK(kc.dim() == 4 && vc.sizes() == kc.sizes() && kc.is_contiguous() && vc.is_contiguous());
+  TORCH_CHECK(qkv.dim() == 2 && qkv.is_contiguous() && H % G == 0 && kc.size(1) == G, "attn_decode_append: shapes");
+  const int64_t B = qkv.size(0), hd = kc.size(3), Tmax = kc.size(2);
+  TORCH_CHECK(qkv.size(1) == (H + 2 * G) * hd && kc.size(0) == B, "attn_decode_append: qkv / cache mismatch");
+  TORCH_CHECK(hd == 64 || hd == 128, "attn_decode_append: head_dim 64 or 128");
+  TORCH_CHECK(Tmax <= bllm::attn_decode_max_len(), "attn_decode_append: cache longer than the LDS score buffer");
+  TORCH_CHECK(pos.scalar_type() == at::kInt && pos.numel() == 1, "attn_decode_append: pos must be one int32");
+  auto out = at::empty({B, H * hd}, qkv.options());
+  bllm::attn_decode_append(dt_of(qkv), qkv.data_ptr(), kc.data_ptr(), vc.data_ptr(), out.data_ptr(),
+                           pos.data_ptr<int>(), (int)B, (int)H, (int)G, (int)hd, (int)Tmax, stream());
+  return out;
 }
 
 // q [B, H, hd]; kc / vc [B, G, Tmax, hd] with the first L positions valid -> out [B, H*hd]
@@ -743,6 +776,8 @@ TORCH_LIBRARY(bllm, m) {
   m.def("wgrad_gemm_(Tensor a, Tensor b, Tensor(a!) c, bool accumulate, int splits) -> ()");
   m.def("gemm_nn_(Tensor a, Tensor b, Tensor(a!) c, bool accumulate) -> ()");
   m.def("attn_decode(Tensor q, Tensor kcache, Tensor vcache, int L) -> Tensor");
+  m.def("attn_decode_append(Tensor qkv, Tensor(a!) kcache, Tensor(b!) vcache, Tensor pos, int H, int G) -> Tensor");
+  m.def("rope_dev_(Tensor(a!) qkv, Tensor cos, Tensor sin, int H, int G, int hd, Tensor pos) -> ()");
   m.def("flash_attn_fwd(Tensor qkv, int B, int T, int H, int G, int hd, bool causal, float p, int seed, int offset) -> (Tensor, Tensor)");
   m.def("flash_attn_bwd(Tensor qkv, Tensor o, Tensor lse, Tensor dout, int B, int T, int H, int G, int hd, bool causal, float p, int seed, int offset) -> Tensor");
   m.def("ce_fwd(Tensor logits, Tensor targets, int ignore_index) -> (Tensor, Tensor)");
@@ -773,6 +808,8 @@ TORCH_LIBRARY_IMPL(bllm, CUDA, m) {
   m.impl("rope_", &rope_);
   m.impl("flash_attn_fwd", &flash_attn_fwd);
   m.impl("attn_decode", &attn_decode);
+  m.impl("attn_decode_append", &attn_decode_append);
+  m.impl("rope_dev_", &rope_dev_);
   m.impl("sum_partials_", &sum_partials_);
   m.impl("wgrad_gemm_", &wgrad_gemm_);
   m.impl("gemm_nn_", &gemm_nn_);

@@ -197,11 +197,13 @@ __global__ __launch_bounds__(256) void dropout_add_k(const T* __restrict__ x, co
 template <typename T>
 __global__ __launch_bounds__(256) void rope_k(T* __restrict__ qkv, const float* __restrict__ cosT,
                                               const float* __restrict__ sinT, long N, int T_, int nh_rot,
-                                              int row_stride, int hd, int pos_offset, float sgn) {
+                                              int row_stride, int hd, int pos_offset, float sgn,
+                                              const int* __restrict__ pos_dev) {
   // one thread = 8 rotation pairs (two 16-B vectors of the head, 8 fp32 cos/sin each);
   // 32-bit index math (N * heads * chunks < 2^31 for every supported shape)
   static_assert(sizeof(T) == 2, "16-bit element types (fp32 uses rope_scalar_k)");
   const int half = hd / 2;
+  if (pos_dev) pos_offset += *pos_dev;  // graph-replayed decode: position read at run time
   const int cpb = half / 8;  // chunks of 8 pairs per head
   const int per_row = nh_rot * cpb;
   const int total = (int)(N * per_row);
@@ -234,8 +236,10 @@ __global__ __launch_bounds__(256) void rope_k(T* __restrict__ qkv, const float* 
 template <typename T>
 __global__ __launch_bounds__(256) void rope_scalar_k(T* __restrict__ qkv, const float* __restrict__ cosT,
                                                      const float* __restrict__ sinT, long N, int T_, int nh_rot,
-                                                     int row_stride, int hd, int pos_offset, float sgn) {
+                                                     int row_stride, int hd, int pos_offset, float sgn,
+                                                     const int* __restrict__ pos_dev) {
   const int half = hd / 2;
+  if (pos_dev) pos_offset += *pos_dev;
   const long total = N * nh_rot * half;
   for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
     const int k = (int)(i % half);
@@ -370,7 +374,7 @@ void dropout_add(DType dt, const void* x, const void* a, void* out, long n, floa
   });
 }
 void rope(DType dt, void* qkv, const float* cosT, const float* sinT, long N, int T_, int H, int G, int hd,
-          bool inverse, int pos_offset, hipStream_t s) {
+          bool inverse, int pos_offset, hipStream_t s, const int* pos_dev) {
   const int nh = H + G, stride = (H + 2 * G) * hd;
   const float sgn = inverse ? -1.f : 1.f;
   BLLM_DISPATCH(dt, T, {
@@ -378,14 +382,14 @@ void rope(DType dt, void* qkv, const float* cosT, const float* sinT, long N, int
       if ((hd / 2) % 8 == 0) {
         long tot = N * nh * (hd / 16);
         hipLaunchKernelGGL(rope_k<T>, dim3(ew_grid(tot)), dim3(256), 0, s, (T*)qkv, cosT, sinT, N, T_, nh, stride,
-                           hd, pos_offset, sgn);
+                           hd, pos_offset, sgn, pos_dev);
         return;
       }
     }
     {
       long tot = N * nh * (hd / 2);
       hipLaunchKernelGGL(rope_scalar_k<T>, dim3(ew_grid(tot)), dim3(256), 0, s, (T*)qkv, cosT, sinT, N, T_, nh,
-                         stride, hd, pos_offset, sgn);
+                         stride, hd, pos_offset, sgn, pos_dev);
     }
   });
 }

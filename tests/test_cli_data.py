@@ -311,3 +311,25 @@ def test_generate_cached_matches_recompute(model, size, G):
     a = generate(m, idx, 12, 24, temperature=1.0, top_k=5, generator=g1)
     b = generate_cached(m, idx, 12, 24, temperature=1.0, top_k=5, generator=g2)
     assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("check_every", [1, 4, 16])
+@pytest.mark.parametrize("rows", [1, 2])
+def test_generate_cached_eos_stop_matches_reference(check_every, rows, monkeypatch):
+    """Deferred all-rows-eos test (every ``EOS_CHECK_EVERY`` tokens) cuts the output exactly
+    where the reference's per-token check stops (generate.py:68-70), for eos hits early, late,
+    at a check boundary and never."""
+    from building_llm_from_scratch_amd.train import generate as G
+    monkeypatch.setattr(G, "EOS_CHECK_EVERY", check_every)
+    cfg = get_config("llama3_2", "1B").replace(context_length=24, emb_dim=64, n_heads=4, n_kv_groups=2,
+                                              hidden_dim=96, n_layers=2, vocab_size=7, dtype=torch.float32)
+    torch.manual_seed(1)
+    m = build_model(cfg)
+    m.flatten()
+    idx = torch.randint(0, 7, (rows, 3))
+    free = G.generate(m, idx, 40, 24)                  # greedy, no eos: a short-vocab sequence
+    for eos in range(7):
+        ref = G.generate(m, idx, 40, 24, eos_id=eos)
+        got = G.generate_cached(m, idx, 40, 24, eos_id=eos)
+        assert torch.equal(ref, got), (eos, ref.shape, got.shape)
+    assert free.shape[1] == 43

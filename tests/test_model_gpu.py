@@ -116,6 +116,53 @@ def test_kv_cache_decode_matches_full_forward(name):
             assert _rel(lg, full[:, p]) < 2e-2, p
 
 
+@pytest.mark.parametrize("name", ["llama_hd64", "llama_hd128", "gpt2"])
+def test_device_position_decode_matches_full_forward(name):
+    """forward_cached_dev (position in device memory, fused K/V append + decode attention,
+    device-side RoPE) reproduces the full forward's logits, eagerly and replayed from a HIP graph."""
+    from building_llm_from_scratch_amd.train.generate import DecodeGraph
+    ops.load_ext(required=True)
+    cfg = _cfgs()[name].replace(dtype=torch.bfloat16)
+    torch.manual_seed(0)
+    m = build_model(cfg, device="cuda")
+    m.flatten()
+    m.eval()
+    idx = torch.randint(0, cfg.vocab_size, (2, 40), device="cuda")
+    with torch.no_grad():
+        full = m(idx).float()
+        for graph in (False, True):
+            cache = m.new_kv_cache(2, cfg.context_length)
+            m.forward_cached(idx[:, :24], cache, 0)
+            dec = DecodeGraph(m, cache, 2, idx.device) if graph else None
+            pos_t = torch.zeros(1, dtype=torch.int32, device="cuda")
+            for p in range(24, 40):
+                if graph:
+                    lg = dec.step(idx[:, p:p + 1], p)
+                else:
+                    pos_t.fill_(p)
+                    lg = m.forward_cached_dev(idx[:, p:p + 1], cache, pos_t)
+                assert _rel(lg, full[:, p]) < 2e-2, (graph, p)
+
+
+@pytest.mark.parametrize("name", ["llama_hd128", "gpt2"])
+def test_generate_graph_matches_eager(name, monkeypatch):
+    """The whole sample (top-k 5, temperature 1, seeded) is token-identical with and without the
+    HIP-graph decode step."""
+    from building_llm_from_scratch_amd.train import generate as G
+    ops.load_ext(required=True)
+    cfg = _cfgs()[name].replace(dtype=torch.bfloat16)
+    torch.manual_seed(0)
+    m = build_model(cfg, device="cuda")
+    m.flatten()
+    idx = torch.randint(0, cfg.vocab_size, (1, 6), device="cuda")
+    outs = []
+    for flag in ("0", "1"):
+        monkeypatch.setenv("BLLM_DECODE_GRAPH", flag)
+        g = torch.Generator(device="cuda").manual_seed(5)
+        outs.append(G.generate_cached(m, idx, 60, cfg.context_length, temperature=1.0, top_k=5, generator=g))
+    assert torch.equal(outs[0], outs[1])
+
+
 @pytest.mark.parametrize("name", ["llama_hd128", "gpt2"])
 def test_training_is_bitwise_deterministic(name):
     """Two identical runs (same seed, same data) must give bit-identical parameters: every
