@@ -96,6 +96,10 @@ def parse(argv=None):
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
                     help="cpu: tiny config on gloo (distributed plumbing check, not a measurement)")
     ap.add_argument("--pg_timeout_min", type=float, default=20.0)
+    ap.add_argument("--tunableop", default=None,
+                    help="PyTorch TunableOp results CSV (every hipBLASLt + rocBLAS solution timed per GEMM "
+                         "shape), e.g. configs/tunableop_llama3_8b_b40_mi355x.csv: +0.6 %% on the headline "
+                         "(profiles/r2_tunableop_*.log); read-only, shapes not in the file keep the heuristic")
     a = ap.parse_args(argv)
     for k, v in PRESETS[a.preset].items():
         if getattr(a, k, None) is None:
@@ -180,6 +184,13 @@ def alpaca_loader(a, cfg, rank, world):
 
 def main(argv=None):
     a = parse(argv)
+    if a.tunableop:  # must be set before the first GEMM; TunableOp reads <name><device ordinal>.csv
+        import tempfile
+        d = tempfile.mkdtemp(prefix="bllm_tunableop_")
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        os.symlink(os.path.abspath(a.tunableop), os.path.join(d, f"results{local}.csv"))
+        os.environ.update(PYTORCH_TUNABLEOP_ENABLED="1", PYTORCH_TUNABLEOP_TUNING="0",
+                          PYTORCH_TUNABLEOP_FILENAME=os.path.join(d, "results%d.csv"))
     import torch
     from building_llm_from_scratch_amd import ops
     from building_llm_from_scratch_amd.models import build_model, replace_linear_with_lora
