@@ -83,6 +83,9 @@ def parse(argv=None):
     ap.add_argument("--seq_len", type=int, default=1024)
     ap.add_argument("--actv_ckpt", default=None, choices=["none", "selective", "full"],
                     help="full = reference checkpoint_sequential semantics (headline); selective recomputes norms")
+    ap.add_argument("--ckpt_segments", type=int, default=None,
+                    help="full mode: checkpoint_sequential segments (default n_layers = the reference's "
+                         "--use_actv_ckpt; fewer segments recompute fewer blocks)")
     ap.add_argument("--parallel", default=None, choices=["fsdp", "ddp", "zero1"])
     ap.add_argument("--mixed_precision", default=None, choices=["bf16", "fp16", "bf16_hybrid", "fp32"])
     ap.add_argument("--lora_rank", type=int, default=None)
@@ -207,6 +210,9 @@ def main(argv=None):
     cfg = build_config(a, dev)
     torch.manual_seed(123)
     model = build_model(cfg, use_actv_ckpt=a.actv_ckpt, device=dev)
+    if a.ckpt_segments:
+        model.set_actv_ckpt(a.actv_ckpt, a.ckpt_segments)
+    n_ckpt = sum(model.rctx.block_mode(i) == "full" for i in range(cfg.n_layers))
     if a.lora_rank:
         for p in model.parameters():
             p.requires_grad = False
@@ -271,7 +277,8 @@ def main(argv=None):
     if a.lora_rank:  # frozen base: no weight-gradient GEMMs (2 of the 6 N FLOPs per param)
         flops_tok -= 2.0 * (cfg.num_params() - cfg.vocab_size * cfg.emb_dim)
     mfu = tps / world * flops_tok / PEAK_BF16
-    extra = cfg.recompute_flops_per_token(int(round(T_eff))) if a.actv_ckpt == "full" else 0.0
+    # recomputed blocks only (checkpoint_sequential leaves the last segment un-checkpointed)
+    extra = cfg.recompute_flops_per_token(int(round(T_eff))) * n_ckpt / cfg.n_layers
     recompute = (flops_tok + extra) / flops_tok
     prof = profile_phases(model, opt, next_batch, dev) if (a.profile and rank == 0 and cuda) else None
     if rank == 0:
@@ -311,6 +318,10 @@ def main(argv=None):
                 "engine": type(engine).__name__ + (" (world 1: no-shard)" if getattr(engine, "no_shard", False)
                                                    else ""),
                 "actv_ckpt": a.actv_ckpt,
+                "ckpt_blocks": f"{n_ckpt}/{cfg.n_layers} recomputed"
+                + (f" (checkpoint_sequential segments={a.ckpt_segments})" if a.ckpt_segments
+                   else (" (checkpoint_sequential segments=n_layers, as the reference)"
+                         if a.actv_ckpt == "full" else "")),
                 "mixed_precision": a.mixed_precision,
                 "lora": {"rank": a.lora_rank, "alpha": a.lora_alpha} if a.lora_rank else None,
                 "optimizer": "AdamW fp32 master, wd 0.1, clip 1.0",

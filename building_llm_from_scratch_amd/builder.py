@@ -65,6 +65,8 @@ def build_model(config, rank, device, args):
     misc.start_memory_tracking()
     ckpt = getattr(args, "actv_ckpt_mode", None) or ("full" if args.use_actv_ckpt else "none")
     model = _build_model(config, use_actv_ckpt=ckpt, device=device)
+    if getattr(args, "actv_ckpt_segments", None):
+        model.set_actv_ckpt(ckpt, args.actv_ckpt_segments)
     if rank == 0:
         logger.info(f"Total parameters: {misc.get_num_params(model):,}")
         misc.model_memory_size(model, config.dtype)

@@ -81,6 +81,9 @@ def build_parser() -> argparse.ArgumentParser:
     x.add_argument("--context_length", type=int, default=1024, help="Llama ctx clamp (reference: fixed 1024)")
     x.add_argument("--actv_ckpt_mode", choices=["none", "selective", "full"], default=None,
                    help="granularity; --use_actv_ckpt alone = full (reference semantics)")
+    x.add_argument("--actv_ckpt_segments", type=int, default=None,
+                   help="full mode: checkpoint_sequential segments (default n_layers = reference); "
+                        "fewer segments recompute fewer blocks for more memory")
     x.add_argument("--tokenizer_path", type=str, default=None)
     x.add_argument("--weights_path", type=str, default=None)
     x.add_argument("--max_steps", type=int, default=None)

@@ -10,7 +10,11 @@ gives exact control over:
   * what each block saves for backward (``actv_ckpt``: ``none`` | ``selective`` — recompute
     only the norm outputs, the cheapest memory-bound ops; everything a GEMM or the attention
     kernel produced is kept, which 288 GB of HBM affords | ``full`` — save the block input
-    only, the reference's ``checkpoint_sequential(segments=n_layers)`` semantics);
+    only, the reference's ``checkpoint_sequential(blocks, segments=n_layers)`` semantics
+    (Llama3.py:199, GPT2.py:116): every block of the first ``segments - 1`` segments is
+    recomputed in backward, the last segment runs without checkpointing.  ``ckpt_segments``
+    (default n_layers, exactly the reference) trades recompute for memory; the recompute is
+    per block either way, so only one block's activations are ever rebuilt at a time);
   * where distributed hooks fire (``engine.pre_forward/post_forward/pre_backward/
     post_backward`` per unit — FSDP gathers and reduce-scatters, DDP bucket all-reduce);
   * fused head + cross-entropy: ``model(idx, targets)`` returns the mean loss without
@@ -68,6 +72,7 @@ class RunCtx:
     def __init__(self, cfg, actv_ckpt: str = "none"):
         self.cfg = cfg
         self.actv_ckpt = actv_ckpt
+        self.ckpt_segments = None      # full mode: checkpoint_sequential segments (None = n_layers)
         self.training = True
         self.engine = LocalEngine()
         self.accumulate = False        # micro-batch gradient accumulation: add into grads
@@ -80,6 +85,16 @@ class RunCtx:
         # unit index -> HIP event recorded after that unit's optimizer update (the update
         # runs on a side stream, overlapped with the next forward; see train/optim.py)
         self.param_ready: dict = {}
+
+    def block_mode(self, i: int) -> str:
+        """Checkpoint mode of block ``i``.  ``full`` follows torch's checkpoint_sequential:
+        segment size n // s, the first s - 1 segments checkpointed, the rest (the last segment
+        plus the remainder) run plainly -- with s = n_layers only the last block is not."""
+        if self.actv_ckpt != "full":
+            return self.actv_ckpt
+        n = self.cfg.n_layers
+        s = max(1, min(int(self.ckpt_segments or n), n))
+        return "full" if i < (n // s) * (s - 1) else "none"
 
     def wait_param_ready(self, unit_index: int):
         ev = self.param_ready.pop(unit_index, None)
@@ -104,6 +119,7 @@ class UnitCompute:
     """Hand-written forward/backward of one unit over a :class:`FlatUnit`."""
 
     name = "unit"
+    index = -1   # block index (blocks only)
 
     def __init__(self, rctx: RunCtx):
         self.rctx = rctx
@@ -183,7 +199,7 @@ class _BlockFn(torch.autograd.Function):
     def forward(ctx, x, comp):
         eng = comp.rctx.engine
         eng.pre_forward(comp.unit)
-        full = comp.rctx.actv_ckpt == "full"
+        full = comp.rctx.block_mode(comp.index) == "full"
         y, saved = comp.forward(x, save=not full)
         eng.post_forward(comp.unit)
         ctx.comp = comp
@@ -271,9 +287,10 @@ class BaseLM(nn.Module):
     def rctx(self) -> RunCtx:
         return self._rctx
 
-    def set_actv_ckpt(self, mode: str):
+    def set_actv_ckpt(self, mode: str, segments=None):
         assert mode in ("none", "selective", "full")
         self._rctx.actv_ckpt = mode
+        self._rctx.ckpt_segments = segments
         self.use_actv_ckpt = mode != "none"
 
     def set_engine(self, engine):

@@ -113,6 +113,7 @@ class GPTBlockCompute(UnitCompute):
         super().__init__(rctx)
         self.block = block
         self.name = f"blocks.{i}"
+        self.index = i
         a, f = block.att, block.ff
         self.qkv = FusedLinear([a.W_query, a.W_key, a.W_value])
         self.o = FusedLinear([a.out_proj])
@@ -191,7 +192,7 @@ class GPTBlockCompute(UnitCompute):
             return x3.view(B, T, d), offs
         saved = dict(x=x2d, m1=m1, r1=r1, qkv=qkv, o=o, lse=lse, x2=x2, m2=m2, r2=r2, f=f, g=g,
                      p=p, offs=offs, xa=(xa_qkv, xa_o, xa_fc, xa_pr))
-        if rc.actv_ckpt == "none" or recompute:  # the recompute's norm outputs live one block
+        if rc.block_mode(self.index) == "none" or recompute:  # the recompute's norm outputs live one block
             saved.update(h1=h1, h2=h2)
         return (x3.view(B, T, d) if x3 is not None else None), saved
 

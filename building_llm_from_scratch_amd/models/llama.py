@@ -125,6 +125,7 @@ class LlamaBlockCompute(UnitCompute):
         super().__init__(rctx)
         self.block = block
         self.name = f"trf_blocks.{i}"
+        self.index = i
         a, f = block.att, block.ff
         self.qkv = FusedLinear([a.W_query, a.W_key, a.W_value])
         self.o = FusedLinear([a.out_proj])
@@ -168,7 +169,7 @@ class LlamaBlockCompute(UnitCompute):
         if save:
             saved = dict(x=x2d, r1=r1, qkv=qkv, o=o, lse=lse, x2=x2, r2=r2, gu=gu, act=act,
                          xa=(xa_qkv, xa_o, xa_gu, xa_dn))
-            if rc.actv_ckpt == "none" or recompute:  # the recompute's norm outputs live one block
+            if rc.block_mode(self.index) == "none" or recompute:  # the recompute's norm outputs live one block
                 saved.update(h1=h1, h2=h2)
         return (x3.view(B, T, d) if x3 is not None else None), saved
 

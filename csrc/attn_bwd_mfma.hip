@@ -62,6 +62,21 @@ template <int HD> __device__ __forceinline__ int t_off(int r, int col) {
   if constexpr (HD == 128) return r * 256 + ((c64 ^ (r & 3)) << 6) + w;
   else return r * 128 + ((c64 ^ ((r >> 1) & 1)) << 6) + w;
 }
+// ONE image of a [rows][HD] tile serving both 16-B row reads (ds_read_b128, S / dP operands)
+// and hardware-transposed reads (ds_read_b64_tr_b16, dV^T / dK^T operands): chunk ch of row r at
+// ch ^ f(r).  HD 128 (256-B rows): f = ((r&3)<<2) | ((r>>2)&3)  (cdna_hip_programming.md T10 (b)).
+// HD 64 (128-B rows): f = (((r>>1)&1)<<2) | ((r>>2)&3) -- over the 8 same-parity rows of every
+// b128 lane group f is a permutation of 0..7 (row reads conflict-free), and rows r, r+2 of an
+// aligned 4-row block differ in bit 2 (the 4-chunk block a transposed half-wave read touches),
+// so a 32-lane transposed read hits 32 distinct bank pairs.  Depends on r & 15 only.
+template <int HD> __device__ __forceinline__ int dual_f(int r) {
+  if constexpr (HD == 128) return ((r & 3) << 2) | ((r >> 2) & 3);
+  else return (((r >> 1) & 1) << 2) | ((r >> 2) & 3);
+}
+template <int HD> __device__ __forceinline__ int dual_off(int r, int ch) {
+  return r * (HD * 2) + ((ch ^ dual_f<HD>(r)) << 4);
+}
+
 // dS image [32 q][128 keys] bf16: 16-B chunk XOR by q
 __device__ __forceinline__ int ds_off(int q, int key) {
   return q * 256 + ((((key >> 3) ^ (q & 15))) << 4) + ((key & 7) << 1);
@@ -93,7 +108,9 @@ constexpr float kLog2eB = 1.4426950408889634f;
 
 // LDS bytes of one ring slot of the dK/dV kernel: Q rows, Q^T image, dO rows, dO^T image,
 // and a per-wave copy of the step's lse/delta (so each wave's stats DMA is its own)
-template <int HD> constexpr int dkdv_buf_bytes() { return 4 * BWD_BQ * HD * 2 + 4 * 256; }
+template <int HD, bool DUAL = false> constexpr int dkdv_buf_bytes() {
+  return (DUAL ? 2 : 4) * BWD_BQ * HD * 2 + 4 * 256;
+}
 
 // Instruction budget per 32-query step (per wave): 32 MFMAs, 16 b128 + 32 tr_b64 LDS reads at
 // loop-invariant per-lane offsets (+ a per-slot base), ~60 VALU of softmax math (the 1/sqrt(d)
@@ -103,7 +120,10 @@ template <int HD> constexpr int dkdv_buf_bytes() { return 4 * BWD_BQ * HD * 2 + 
 // FUSEG: one workgroup sweeps all H/G query heads of its kv head (dK/dV summed in registers,
 // written once in bf16: no fp32 per-head partials, no reduction kernel); otherwise one query
 // head per workgroup plus the attn_bwd_kv_reduce_k pass for GQA.
-template <typename T, int HD, bool DROP, int NBUF, int OCC, bool FUSEG = false>
+// DUAL: Q and dO each staged as ONE dual-use image (dual_off) instead of a row image plus a
+// transposed image: half the LDS and DMA per step, which buys a 4-slot ring (three steps in
+// flight) at two workgroups per CU -- the 2-slot version waits on its DMA ~60 % of wave cycles.
+template <typename T, int HD, bool DROP, int NBUF, int OCC, bool FUSEG = false, bool DUAL = false>
 __global__ __launch_bounds__(256, OCC) void attn_bwd_mfma_k(const T* __restrict__ qkv, const T* __restrict__ dout,
                                                             const float* __restrict__ lse,
                                                             const float* __restrict__ delta, T* __restrict__ dqkv,
@@ -115,9 +135,10 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_mfma_k(const T* __restrict_
   constexpr int IMG = BWD_BQ * ROWB;            // bytes of one [32][HD] image
   constexpr int PPW = IMG / 1024 / 4;           // 1-KiB DMA pieces per wave per image
   constexpr int PROWS = 256 / CH;               // rows between a wave's consecutive pieces
-  constexpr int BUF = dkdv_buf_bytes<HD>();
-  constexpr int NPW = 4 * PPW + 1;              // DMA instructions per wave per step
-  static_assert(NBUF == 2 || NBUF == 3, "ring depth");
+  constexpr int BUF = dkdv_buf_bytes<HD, DUAL>();
+  constexpr int NIMG = DUAL ? 2 : 4;            // LDS images per step
+  constexpr int NPW = NIMG * PPW + 1;           // DMA instructions per wave per step
+  static_assert(NBUF >= 2 && NBUF <= 4, "ring depth");
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   // heaviest (lowest) key block first across the whole grid; all key blocks of one (b, h)
@@ -165,7 +186,9 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_mfma_k(const T* __restrict_
     const int P = w * 64 + lane;
     const int r = P / CH, pc = P % CH;
     int rc;
-    if constexpr (HD == 128) rc = pc ^ (r & 15); else rc = pc ^ ((r >> 1) & 7);
+    if constexpr (DUAL) rc = pc ^ dual_f<HD>(r);
+    else if constexpr (HD == 128) rc = pc ^ (r & 15);
+    else rc = pc ^ ((r >> 1) & 7);
     const int c64 = (pc >> 2) ^ (HD == 128 ? (r & 3) : ((r >> 1) & 1));
     const int tc = c64 * 4 + (pc & 3);
     q_r = (uint32_t)(r * rs * 2 + rc * 16);
@@ -173,6 +196,9 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_mfma_k(const T* __restrict_
     o_r = (uint32_t)(r * ors * 2 + rc * 16);
     o_t = (uint32_t)(r * ors * 2 + tc * 16);
   }
+  // image offsets inside a slot: Q rows, Q^T, dO rows, dO^T (DUAL: Q at 0, dO at IMG)
+  constexpr int IQT = DUAL ? 0 : IMG, IOR = DUAL ? IMG : 2 * IMG, IOT = DUAL ? IMG : 3 * IMG;
+  constexpr int ISTAT = NIMG * IMG;
   const uint32_t smem_u = lds_u32(smem);
   for (int hi = 0; hi < h_count; ++hi) {
   const int h = h_first + hi;
@@ -198,9 +224,9 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_mfma_k(const T* __restrict_
         const void* os = sgpr_ptr(ob_ + (long)(q0 + j * PROWS) * ors);
         const uint32_t pd = (w + 4 * j) * 1024;
         glds16s(qs, q_r, base + pd);
-        glds16s(qs, q_t, base + IMG + pd);
-        glds16s(os, o_r, base + 2 * IMG + pd);
-        glds16s(os, o_t, base + 3 * IMG + pd);
+        if constexpr (!DUAL) glds16s(qs, q_t, base + IQT + pd);
+        glds16s(os, o_r, base + IOR + pd);
+        if constexpr (!DUAL) glds16s(os, o_t, base + IOT + pd);
       }
     } else {  // sequence tail: clamp rows (rows >= T_ are masked in the step)
       char* lb = smem + slot * BUF;
@@ -209,22 +235,26 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_mfma_k(const T* __restrict_
         const int P = (w + 4 * j) * 64 + lane;
         const int r = P / CH, pc = P % CH;
         int rc;
-        if constexpr (HD == 128) rc = pc ^ (r & 15); else rc = pc ^ ((r >> 1) & 7);
+        if constexpr (DUAL) rc = pc ^ dual_f<HD>(r);
+        else if constexpr (HD == 128) rc = pc ^ (r & 15);
+        else rc = pc ^ ((r >> 1) & 7);
         const int c64 = (pc >> 2) ^ (HD == 128 ? (r & 3) : ((r >> 1) & 1));
         const int tc = c64 * 4 + (pc & 3);
         const uint32_t pd = (w + 4 * j) * 1024;
         const int rr = min(q0 + r, T_ - 1);
         glds16(qb_ + (long)rr * rs + rc * 8, lb + pd);
-        glds16(qb_ + (long)rr * rs + tc * 8, lb + IMG + pd);
-        glds16(ob_ + (long)rr * ors + rc * 8, lb + 2 * IMG + pd);
-        glds16(ob_ + (long)rr * ors + tc * 8, lb + 3 * IMG + pd);
+        if constexpr (!DUAL) glds16(qb_ + (long)rr * rs + tc * 8, lb + IQT + pd);
+        glds16(ob_ + (long)rr * ors + rc * 8, lb + IOR + pd);
+        if constexpr (!DUAL) glds16(ob_ + (long)rr * ors + tc * 8, lb + IOT + pd);
       }
     }
-    glds4(stat_src + min(q0 + l32, T_ - 1), smem + slot * BUF + 4 * IMG + w * 256);
+    glds4(stat_src + min(q0 + l32, T_ - 1), smem + slot * BUF + ISTAT + w * 256);
   };
-  // after step i: wait for step i+1's DMA (NBUF = 3 may leave step i+2's in flight)
+  // wait until step i+1's DMA landed, leaving the later issued steps (up to NBUF-2) in flight
   auto ring_wait = [&](int i, int nsteps) {
-    if constexpr (NBUF == 3) {
+    if constexpr (NBUF == 4) {
+      if (i + 3 < nsteps) wait_vm<2 * NPW>(); else if (i + 2 < nsteps) wait_vm<NPW>(); else wait_vm0();
+    } else if constexpr (NBUF == 3) {
       if (i + 2 < nsteps) wait_vm<NPW>(); else wait_vm0();
     } else {
       wait_vm0();
@@ -237,7 +267,10 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_mfma_k(const T* __restrict_
 #pragma unroll
   for (int j = 0; j < NBUF - 1; ++j)
     if (j < nsteps) issue(qstart + j * BWD_BQ, j);
-  if constexpr (NBUF == 3) {
+  // step 0 landed; steps 1 .. min(nsteps, NBUF-1)-1 may still fly
+  if constexpr (NBUF == 4) {
+    if (nsteps > 2) wait_vm<2 * NPW>(); else if (nsteps > 1) wait_vm<NPW>(); else wait_vm0();
+  } else if constexpr (NBUF == 3) {
     if (nsteps > 1) wait_vm<NPW>(); else wait_vm0();
   } else {
     wait_vm0();
@@ -271,9 +304,9 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_mfma_k(const T* __restrict_
       f32x16 sacc = f32x16{}, dpacc = f32x16{};
 #pragma unroll
       for (int kk = 0; kk < KK; ++kk) {
-        const int ro = r_off<HD>(l32_, kk * 2 + hh_);
+        const int ro = DUAL ? dual_off<HD>(l32_, kk * 2 + hh_) : r_off<HD>(l32_, kk * 2 + hh_);
         sacc = MFb<T>::mma(*reinterpret_cast<const v8*>(S + ro), kf[kk], sacc);
-        dpacc = MFb<T>::mma(*reinterpret_cast<const v8*>(S + 2 * IMG + ro), vf[kk], dpacc);
+        dpacc = MFb<T>::mma(*reinterpret_cast<const v8*>(S + IOR + ro), vf[kk], dpacc);
       }
       // rows of this lane's accumulator registers: q = q0 + (r&3) + 8(r>>2) + 4hh
       if (edge) {  // uniform branch: -inf the masked scores (causal diagonal, sequence tail)
@@ -284,7 +317,7 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_mfma_k(const T* __restrict_
           if ((causal && mykey > q) || q >= T_ || mykey >= T_) sacc[r] = -INFINITY;
         }
       }
-      const float* LS = reinterpret_cast<const float*>(S + 4 * IMG + w * 256);
+      const float* LS = reinterpret_cast<const float*>(S + ISTAT + w * 256);
 #pragma unroll
       for (int gq = 0; gq < 4; ++gq) {
         const f32x4 L4 = *reinterpret_cast<const f32x4*>(LS + 8 * gq + 4 * hh_);
@@ -320,10 +353,19 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_mfma_k(const T* __restrict_
         }
 #pragma unroll
         for (int dt = 0; dt < DT; ++dt) {
-          const int o = t_off<HD>(4 * hh_ + qrow, dt * 32 + glb * 16 + pcol * 4) + s2 * 16 * ROWB;
-          const v8 ao = tr8<v8>(S + 3 * IMG, o, o + 8 * ROWB);
+          int olo, ohi;
+          if constexpr (DUAL) {
+            // lane 4q+p of a 16-lane group: row 4hh+q (+8), columns dt*32 + glb*16 + 4p .. +3
+            const int row = 4 * hh_ + qrow + s2 * 16, ch = dt * 4 + glb * 2 + (pcol >> 1);
+            olo = dual_off<HD>(row, ch) + 8 * (pcol & 1);
+            ohi = dual_off<HD>(row + 8, ch) + 8 * (pcol & 1);
+          } else {
+            olo = t_off<HD>(4 * hh_ + qrow, dt * 32 + glb * 16 + pcol * 4) + s2 * 16 * ROWB;
+            ohi = olo + 8 * ROWB;
+          }
+          const v8 ao = tr8<v8>(S + IOT, olo, ohi);
           dv[dt] = MFb<T>::mma(ao, pf, dv[dt]);
-          const v8 aq = tr8<v8>(S + IMG, o, o + 8 * ROWB);
+          const v8 aq = tr8<v8>(S + IQT, olo, ohi);
           dk[dt] = MFb<T>::mma(aq, df, dk[dt]);
         }
       }
@@ -662,6 +704,14 @@ static bool fuse_gqa_heads(int B, int T_, int H, int G) {
   return nkb * G * (long)B >= 1024;
 }
 // dQ variant: 0 = 32-key tiles, 3-slot ring, 2 workgroups per CU; 1 = 64-key tiles, 1 per CU
+// dK/dV staging: 1 = one dual-use LDS image per Q / dO tile and a 4-slot ring (DUAL kernels),
+// 0 = separate row and transposed images, 2-slot ring.  Unset: dual at hd 128 (Llama-3-8B
+// B=24 backward 1.143 -> 1.100 ms), separate images at hd 64 (Llama-3.2-1B 0.548 vs 0.568 ms);
+// BLLM_ATTN_KV_DUAL overrides.
+static int kv_dual_from_env() {
+  const char* e = getenv("BLLM_ATTN_KV_DUAL");
+  return e ? atoi(e) : -1;
+}
 static int q_variant_from_env() {
   const char* e = getenv("BLLM_ATTN_Q_VARIANT");
   return e ? atoi(e) : 0;
@@ -677,6 +727,8 @@ void attn_bwd_mfma(DType dt, const void* qkv, const void* o, const float* lse, c
   const float ik = drop_inv_keep(p);
   static const int kv_variant = kv_variant_from_env();
   static const int q_variant = q_variant_from_env();
+  static const int kv_dual_env = kv_dual_from_env();
+  const bool kv_dual = kv_dual_env >= 0 ? kv_dual_env != 0 : hd == 128;
   const int nkb = (T_ + BWD_BKV - 1) / BWD_BKV;
   // kv variant 2 (GQA, large grids): the dK/dV workgroup sweeps the H/G heads of its kv head
   const bool fuseg = fuse_gqa_heads(B, T_, H, G);
@@ -705,7 +757,27 @@ void attn_bwd_mfma(DType dt, const void* qkv, const void* o, const float* lse, c
                            (const TT*)o, (const TT*)dout, lse, delta, (TT*)dqkv, T_, H, G, B, causal, thr, ik, \
                            seed, offset);                                                                       \
     }                                                                                                           \
-    if (fuseg) {                                                                                                \
+    if (fuseg && kv_dual) {                                                                                     \
+      const int lds_kv = 4 * dkdv_buf_bytes<HDD, true>();                                                       \
+      if (drop)                                                                                                 \
+        hipLaunchKernelGGL((attn_bwd_mfma_k<TT, HDD, true, 4, 2, true, true>), grid_kv, block, lds_kv, s,      \
+                           (const TT*)qkv, (const TT*)dout, lse, delta, (TT*)dqkv, dkv_part, T_, H, G, B,       \
+                           causal, thr, ik, seed, offset);                                                      \
+      else                                                                                                      \
+        hipLaunchKernelGGL((attn_bwd_mfma_k<TT, HDD, false, 4, 2, true, true>), grid_kv, block, lds_kv, s,     \
+                           (const TT*)qkv, (const TT*)dout, lse, delta, (TT*)dqkv, dkv_part, T_, H, G, B,       \
+                           causal, thr, ik, seed, offset);                                                      \
+    } else if (kv_dual && kv_variant != 1) {                                                                    \
+      const int lds_kv = 4 * dkdv_buf_bytes<HDD, true>();                                                       \
+      if (drop)                                                                                                 \
+        hipLaunchKernelGGL((attn_bwd_mfma_k<TT, HDD, true, 4, 2, false, true>), grid_kv, block, lds_kv, s,     \
+                           (const TT*)qkv, (const TT*)dout, lse, delta, (TT*)dqkv, dkv_part, T_, H, G, B,       \
+                           causal, thr, ik, seed, offset);                                                      \
+      else                                                                                                      \
+        hipLaunchKernelGGL((attn_bwd_mfma_k<TT, HDD, false, 4, 2, false, true>), grid_kv, block, lds_kv, s,    \
+                           (const TT*)qkv, (const TT*)dout, lse, delta, (TT*)dqkv, dkv_part, T_, H, G, B,       \
+                           causal, thr, ik, seed, offset);                                                      \
+    } else if (fuseg) {                                                                                         \
       const int lds_kv = 2 * dkdv_buf_bytes<HDD>();                                                             \
       if (drop)                                                                                                 \
         hipLaunchKernelGGL((attn_bwd_mfma_k<TT, HDD, true, 2, 2, true>), grid_kv, block, lds_kv, s,            \

@@ -143,3 +143,49 @@ def test_fused_chunked_head_ce(family, monkeypatch):
     g1 = {n: p.grad.clone() for n, p in m.named_parameters() if p.grad is not None}
     for n in g1:
         assert torch.allclose(g4[n], 4.0 * g1[n], rtol=1e-5, atol=1e-6), n
+
+
+def _torch_ckpt_blocks(n, segments):
+    """Blocks torch.utils.checkpoint.checkpoint_sequential(fns, segments, x) re-runs in
+    backward: it checkpoints ``segments - 1`` chunks of ``n // segments`` and runs the rest
+    plainly (the reference's --use_actv_ckpt call passes segments = n_layers)."""
+    size = n // segments
+    return [i for i in range(n) if i < size * (segments - 1)]
+
+
+@pytest.mark.parametrize("n,segments", [(5, None), (5, 2), (5, 3), (4, 4), (6, 1), (32, None), (32, 2)])
+def test_ckpt_segments_match_checkpoint_sequential(n, segments):
+    cfg = _small_llama().replace(n_layers=n)
+    m = build_model(cfg, use_actv_ckpt="full")
+    m.set_actv_ckpt("full", segments)
+    got = [i for i in range(n) if m.rctx.block_mode(i) == "full"]
+    assert got == _torch_ckpt_blocks(n, segments or n)
+
+
+@pytest.mark.parametrize("segments", [None, 2, 3])
+@pytest.mark.parametrize("family", ["llama", "gpt2"])
+def test_ckpt_segments_grads(family, segments):
+    """Gradients are exact for every segmentation, and exactly the checkpointed blocks re-run
+    their forward in backward."""
+    torch.manual_seed(0)
+    cfg = (_small_llama() if family == "llama" else _small_gpt2()).replace(n_layers=5)
+    m = build_model(cfg, use_actv_ckpt="full")
+    m.set_actv_ckpt("full", segments)
+    recomputed = []
+    for comp in m.computes:
+        if comp.index >= 0:
+            fwd = comp.forward
+
+            def spy(x, save, replay=None, recompute=False, _f=fwd, _i=comp.index):
+                if recompute:
+                    recomputed.append(_i)
+                return _f(x, save, replay=replay, recompute=recompute)
+            comp.forward = spy
+    idx = torch.randint(0, cfg.vocab_size, (2, 16))
+    tgt = torch.randint(0, cfg.vocab_size, (2, 16))
+    if family == "llama":
+        cos, sin = ops.rope_tables(cfg.head_dim, cfg.context_length, cfg.rope_base, cfg.rope_freq)
+        _compare(m, lambda sd: llama_loss(sd, cfg, idx, tgt, cos, sin), idx, tgt)
+    else:
+        _compare(m, lambda sd: gpt2_loss(sd, cfg, idx, tgt), idx, tgt)
+    assert sorted(recomputed) == _torch_ckpt_blocks(5, segments or 5)
