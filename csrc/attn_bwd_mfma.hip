@@ -95,10 +95,9 @@ template <typename T> __device__ __forceinline__ uint32_t pk2(float a, float b) 
 template <typename v8> __device__ __forceinline__ v8 tr8(const char* base, int off_lo, int off_hi) {
   const s16x4 r1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + off_lo));
   const s16x4 r2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + off_hi));
-  short tmp[8] = {r1[0], r1[1], r1[2], r1[3], r2[0], r2[1], r2[2], r2[3]};
-  v8 a;
-  __builtin_memcpy(&a, tmp, 16);
-  return a;
+  // whole-register concatenation (an element-wise short[8] build made hipcc emit a v_bfi per
+  // fragment and wait for the read right there)
+  return __builtin_bit_cast(v8, __builtin_shufflevector(r1, r2, 0, 1, 2, 3, 4, 5, 6, 7));
 }
 }  // namespace
 

@@ -22,6 +22,8 @@
 // Attention-probability dropout (GPT-2) uses the stateless counter hash of common.h.
 #include <float.h>
 #include <stdlib.h>
+
+#include <type_traits>
 #include "api.h"
 
 namespace bllm {
@@ -47,6 +49,7 @@ template <> struct MF<f16_t> {
 };
 
 constexpr float kLog2e = 1.4426950408889634f;
+constexpr float kRescaleThr = 8.f;  // deferred online-softmax rescale threshold (log2 units)
 constexpr int FWD_BQ = 128;  // queries per workgroup
 // keys per tile (FWD_BK), LDS ring depth and workgroups per CU are template parameters
 
@@ -209,42 +212,48 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd_mfma_k(const T* __restrict_
   }
   __builtin_amdgcn_s_barrier();
   int t = 0, buf = 0;
-  for (; t < nact; ++t) {
-    if (t + NBUF - 1 < ntiles) issue(t + NBUF - 1, buf == 0 ? NBUF - 1 : buf - 1);
-    const int k0 = t * FWD_BK;
-    const char* kb = smem + buf * 2 * TILE_B;
-    const char* vb = kb + TILE_B;
-    // ---- S^T = K Q^T for the 32-key sub-tiles
-    f32x16 s[NKT];
+  // One K/V tile.  NV = 32-key sub-tiles this wave can see (< NKT only on causal-diagonal or
+  // tail tiles: even waves' diagonal tile has its upper half above every query), EDGE = some
+  // visible key is masked.  Instantiated per (NV, EDGE) so each path is straight-line code.
+  auto body = [&](auto nv_c, auto edge_c, int k0, const char* kb, const char* vb) {
+    constexpr int NV = decltype(nv_c)::value;
+    constexpr bool EDGE = decltype(edge_c)::value;
+    // ---- S^T = K Q^T for the visible 32-key sub-tiles
+    f32x16 s[NV];
+    {
 #pragma unroll
-    for (int kt = 0; kt < NKT; ++kt) {
-      s[kt] = f32x16{};
+      for (int kt = 0; kt < NV; ++kt) {
+        s[kt] = f32x16{};
 #pragma unroll
-      for (int kk = 0; kk < KK; ++kk)
-        s[kt] = MF<T>::mma(*reinterpret_cast<const v8*>(kb + kt * 32 * ROWB + koff[kk]), qf[kk], s[kt]);
-    }
-    // ---- mask (uniform branch: causal diagonal / tail tiles only), online softmax
-    const bool edge = (causal && k0 + FWD_BK - 1 > wq_lo) || k0 + FWD_BK > T_ || wq_hi >= T_;
-    if (edge) {
-#pragma unroll
-      for (int kt = 0; kt < NKT; ++kt) {
-        const int kb0 = k0 + kt * 32 + 4 * hh;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int key = kb0 + (r & 3) + 8 * (r >> 2);
-          if ((causal && key > qi) || key >= T_) s[kt][r] = -INFINITY;
-        }
+        for (int kk = 0; kk < KK; ++kk)
+          s[kt] = MF<T>::mma(*reinterpret_cast<const v8*>(kb + kt * 32 * ROWB + koff[kk]), qf[kk], s[kt]);
       }
     }
+    // ---- mask: key k0 + 4hh + off is visible iff off <= lim (one compare + select each)
+    if constexpr (EDGE) {
+      const int lim = (causal ? min(qi, T_ - 1) : T_ - 1) - (k0 + 4 * hh);
+#pragma unroll
+      for (int kt = 0; kt < NV; ++kt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if (kt * 32 + (r & 3) + 8 * (r >> 2) > lim) s[kt][r] = -INFINITY;
+    }
+    // ---- online softmax
     float mx = -INFINITY;
 #pragma unroll
-    for (int kt = 0; kt < NKT; ++kt)
+    for (int kt = 0; kt < NV; ++kt)
 #pragma unroll
       for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s[kt][r]);
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64)) * c;
-    const float mn = fmaxf(m, mx);
-    // lazy rescale: only when some lane's running max moved
-    if (__builtin_amdgcn_ballot_w64(mn > m)) {
+    {  // other half's max: one v_permlane32_swap (no LDS round trip / lgkmcnt wait)
+      const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
+      mx = fmaxf(mx, fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]))) * c;
+    }
+    // deferred rescale: only when some lane's max grew by more than kRescaleThr (log2 units);
+    // until then P is exponentiated against the stale max and stays below 2^kRescaleThr
+    // (fp32 O / l accumulators; bf16 P keeps its relative precision), and the epilogue's
+    // lse = m + log2(l) is exact for whatever m the sums were taken against
+    if (__builtin_amdgcn_ballot_w64(mx > m + kRescaleThr)) {
+      const float mn = fmaxf(m, mx);
       const float alpha = __builtin_amdgcn_exp2f(m - mn);
       l *= alpha;
 #pragma unroll
@@ -253,7 +262,7 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd_mfma_k(const T* __restrict_
     }
     float ls = 0.f;
 #pragma unroll
-    for (int kt = 0; kt < NKT; ++kt)
+    for (int kt = 0; kt < NV; ++kt)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const float p = __builtin_amdgcn_exp2f(fmaf(s[kt][r], c, -m));
@@ -266,7 +275,7 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd_mfma_k(const T* __restrict_
       const uint64_t rowbase = dslab + (uint64_t)qi * T_;
       if (dpair) {
 #pragma unroll
-        for (int kt = 0; kt < NKT; ++kt)
+        for (int kt = 0; kt < NV; ++kt)
 #pragma unroll
           for (int r = 0; r < 16; r += 2) {
             const int key = k0 + kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
@@ -276,7 +285,7 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd_mfma_k(const T* __restrict_
           }
       } else {
 #pragma unroll
-        for (int kt = 0; kt < NKT; ++kt)
+        for (int kt = 0; kt < NV; ++kt)
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
             const int key = k0 + kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
@@ -286,7 +295,7 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd_mfma_k(const T* __restrict_
     }
     // ---- O^T += V^T P^T: P fragments packed from the accumulators, V^T by transposed reads
 #pragma unroll
-    for (int kt = 0; kt < NKT; ++kt)
+    for (int kt = 0; kt < NV; ++kt)
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) {
         v8 pf;
@@ -301,12 +310,29 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd_mfma_k(const T* __restrict_
           const int off = voff[dt] + (kt * 32 + s2 * 16) * ROWB;
           const s16x4 r1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(vb + off));
           const s16x4 r2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(vb + off + 8 * ROWB));
-          short tmp[8] = {r1[0], r1[1], r1[2], r1[3], r2[0], r2[1], r2[2], r2[3]};
-          v8 va;
-          __builtin_memcpy(&va, tmp, 16);
+          const v8 va = __builtin_bit_cast(v8, __builtin_shufflevector(r1, r2, 0, 1, 2, 3, 4, 5, 6, 7));
           o[dt] = MF<T>::mma(va, pf, o[dt]);
         }
       }
+  };
+  using Ic1 = std::integral_constant<int, 1>;
+  using IcN = std::integral_constant<int, NKT>;
+  using Yes = std::true_type;
+  using No = std::false_type;
+  for (; t < nact; ++t) {
+    if (t + NBUF - 1 < ntiles) issue(t + NBUF - 1, buf == 0 ? NBUF - 1 : buf - 1);
+    const int k0 = t * FWD_BK;
+    const char* kb = smem + buf * 2 * TILE_B;
+    const char* vb = kb + TILE_B;
+    // wave-uniform: causal diagonal / sequence tail tiles need masking
+    const bool edge = (causal && k0 + FWD_BK - 1 > wq_lo) || k0 + FWD_BK > T_ || wq_hi >= T_;
+    if (!edge) {
+      body(IcN{}, No{}, k0, kb, vb);
+    } else {
+      const int kvis = min(causal ? wq_hi : T_ - 1, T_ - 1) - k0;  // >= 0 for an active tile
+      if (NKT == 1 || kvis >= 32) body(IcN{}, Yes{}, k0, kb, vb);
+      else body(Ic1{}, Yes{}, k0, kb, vb);
+    }
     ring_wait(t);  // the DMA of tile t+1 has landed (asm-issued, so drained by hand)
     buf = buf == NBUF - 1 ? 0 : buf + 1;
   }
@@ -351,15 +377,15 @@ void attn_fwd_mfma(DType dt, const void* qkv, void* o, float* lse, int B, int T_
   const float ik = drop_inv_keep(p);
   static const int fwd_variant = fwd_variant_from_env();
   dim3 grid(((T_ + FWD_BQ - 1) / FWD_BQ) * H * B), block(256);
-#define LAUNCH_V(TT, HDD, BK, NB, OC)                                                                         \
+#define LAUNCH_V(TT, HDD, BK, NB, OC)                                                                     \
   do {                                                                                                        \
     const int lds = NB * 2 * BK * HDD * 2;                                                                    \
     if (p > 0.f)                                                                                              \
-      hipLaunchKernelGGL((attn_fwd_mfma_k<TT, HDD, true, BK, NB, OC>), grid, block, lds, s, (const TT*)qkv,   \
-                         (TT*)o, lse, T_, H, G, B, causal, thr, ik, seed, offset);                            \
+      hipLaunchKernelGGL((attn_fwd_mfma_k<TT, HDD, true, BK, NB, OC>), grid, block, lds, s,               \
+                         (const TT*)qkv, (TT*)o, lse, T_, H, G, B, causal, thr, ik, seed, offset);            \
     else                                                                                                      \
-      hipLaunchKernelGGL((attn_fwd_mfma_k<TT, HDD, false, BK, NB, OC>), grid, block, lds, s, (const TT*)qkv,  \
-                         (TT*)o, lse, T_, H, G, B, causal, thr, ik, seed, offset);                            \
+      hipLaunchKernelGGL((attn_fwd_mfma_k<TT, HDD, false, BK, NB, OC>), grid, block, lds, s,              \
+                         (const TT*)qkv, (TT*)o, lse, T_, H, G, B, causal, thr, ik, seed, offset);            \
   } while (0)
 #define LAUNCH(TT, HDD)                                                                                       \
   do {                                                                                                        \

@@ -196,6 +196,31 @@ def test_flash_attention(dt, B, T, H, G, hd, p, causal):
     _close(dqkv, dqkv0, dt, 4, name="dqkv")
 
 
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("hd,step", [(128, 0.35), (128, 0.6), (64, 0.5)])
+def test_flash_attention_deferred_rescale(dt, hd, step):
+    """Scores that grow tile by tile (key j scaled by step * (j // 64) along the query
+    direction): each query's running max rises by 4-10 log2 units per 64-key tile, so the
+    forward both defers (rise < kRescaleThr) and takes the rescale branch mid-sequence --
+    random data almost never exercises the deferred path."""
+    B, T, H, G = 1, 512, 4, 2
+    g = torch.Generator(device=DEV).manual_seed(hd)
+    u = torch.randn(hd, device=DEV, generator=g)
+    q = u + 0.3 * torch.randn(B * T, H, hd, device=DEV, generator=g)
+    a = step * (torch.arange(T, device=DEV) // 64).float() / (hd ** 0.5) * 8.0
+    k = a[:, None, None] * u + 0.3 * torch.randn(B * T, G, hd, device=DEV, generator=g)
+    v = torch.randn(B * T, G, hd, device=DEV, generator=g)
+    qkv = torch.cat([q, k, v], 1).reshape(B * T, (H + 2 * G) * hd).to(dt)
+    do = torch.randn(B * T, H * hd, device=DEV, generator=g).to(dt)
+    o, lse = ops.flash_attn_fwd(qkv, B, T, H, G, hd, True, 0.0, 1, 0)
+    o0, lse0 = ref.flash_attn_fwd(qkv.float(), B, T, H, G, hd, True, 0.0, 1, 0)
+    _close(o, o0, dt, 2, name="o")
+    _close(lse, lse0, torch.float32, 1000, name="lse")
+    dqkv = ops.flash_attn_bwd(qkv, o, lse, do, B, T, H, G, hd, True, 0.0, 1, 0)
+    dqkv0 = ref.flash_attn_bwd(qkv.float(), o0, lse0, do.float(), B, T, H, G, hd, True, 0.0, 1, 0)
+    _close(dqkv, dqkv0, dt, 4, name="dqkv")
+
+
 def test_flash_attention_fp32_is_flash_not_materialised():
     """GPT-2 in the reference's default fp32 (args.py:77) at T = 4096, 12 heads: the fp32 kernels'
     footprint is O(T) -- the materialised oracle would need 12 x 4096^2 x 4 B = 805 MB per sequence."""

@@ -29,21 +29,30 @@ def timeit(fn, iters):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--shapes", default="", help="comma-separated shape names (default: all)")
+    ap.add_argument("--noncausal", action="store_true", help="full (non-causal) attention")
+    ap.add_argument("--T", type=int, default=None, help="override the sequence length")
     a = ap.parse_args()
     ops.load_ext(required=True)
     shapes = [("llama3-8B", 4, 1024, 32, 8, 128, 0.0), ("llama3-8B-B24", 24, 1024, 32, 8, 128, 0.0),
               ("llama3.2-1B-B24", 24, 1024, 32, 8, 64, 0.0), ("gpt2-774M", 4, 1024, 20, 20, 64, 0.1),
               ("gpt2-774M-nodrop", 4, 1024, 20, 20, 64, 0.0),
               ("gpt2-124M", 4, 1024, 12, 12, 64, 0.0)]
+    if a.shapes:
+        keep = a.shapes.split(",")
+        shapes = [sh for sh in shapes if sh[0] in keep]
+    causal = not a.noncausal
     res = []
     for name, B, T, H, G, hd, p in shapes:
+        if a.T:
+            B, T = max(1, B * T // a.T), a.T
         qkv = torch.randn(B * T, (H + 2 * G) * hd, device="cuda", dtype=torch.bfloat16)
         do = torch.randn(B * T, H * hd, device="cuda", dtype=torch.bfloat16)
-        o, lse = ops.flash_attn_fwd(qkv, B, T, H, G, hd, True, p, 1, 0)
-        tf = timeit(lambda: ops.flash_attn_fwd(qkv, B, T, H, G, hd, True, p, 1, 0), a.iters)
-        tb = timeit(lambda: ops.flash_attn_bwd(qkv, o, lse, do, B, T, H, G, hd, True, p, 1, 0), a.iters)
-        flop = 2 * 2 * B * H * T * T * hd / 2  # causal: two matmuls, half the square
-        res.append(dict(shape=name, fwd_ms=round(tf, 4), bwd_ms=round(tb, 4),
+        o, lse = ops.flash_attn_fwd(qkv, B, T, H, G, hd, causal, p, 1, 0)
+        tf = timeit(lambda: ops.flash_attn_fwd(qkv, B, T, H, G, hd, causal, p, 1, 0), a.iters)
+        tb = timeit(lambda: ops.flash_attn_bwd(qkv, o, lse, do, B, T, H, G, hd, causal, p, 1, 0), a.iters)
+        flop = 2 * 2 * B * H * T * T * hd / (2 if causal else 1)  # two matmuls (causal: half the square)
+        res.append(dict(shape=name, B=B, T=T, causal=causal, fwd_ms=round(tf, 4), bwd_ms=round(tb, 4),
                         fwd_tflops=round(flop / tf / 1e9, 1), bwd_tflops_5mm=round(2.5 * flop / tb / 1e9, 1)))
     for r in res:
         print(json.dumps(r))
