@@ -2,9 +2,12 @@
 in-tree ``_C.so``), CPU tensors -> ``ops.reference`` (plain PyTorch).
 
 There is deliberately NO silent fallback for GPU tensors: if the extension is not built,
-every op on a GPU tensor raises.  The single documented exception is fp32 *attention* on
-the GPU (the flash-attention kernels are bf16/fp16 MFMA kernels); fp32 GPU runs go through
-the reference attention math, which ``ops.attention_backend(dtype)`` reports.
+every op on a GPU tensor raises (fp32 attention included: csrc/attn_f32.hip).
+
+Kernel debug mode (``BLLM_KERNEL_DEBUG=1`` with ``tools/build_ext.py --debug``): every
+``torch.ops.bllm`` call is followed by a device synchronisation and a read of the kernels'
+debug word, so a failed device-side check (token id / CE target / decode position out of
+range, common.h ``BLLM_DASSERT``) raises at the op that caused it, like a launch-blocking run.
 """
 from __future__ import annotations
 
@@ -14,7 +17,7 @@ from typing import List, Optional
 import torch
 
 from . import reference as ref
-from ._ext import ext_available, load_ext
+from ._ext import ext_available, kernel_debug, load_ext
 
 __all__ = [
     "rmsnorm_fwd", "rmsnorm_bwd", "layernorm_fwd", "layernorm_bwd", "dropout_add", "dropout_bwd",
@@ -36,8 +39,31 @@ def _hip(t: torch.Tensor) -> bool:
     return False
 
 
+DEBUG_CODES = {1: "embedding token id outside [0, vocab)", 2: "cross-entropy target outside [0, V)",
+               3: "decode cache position outside [0, Tmax)", 4: "rope device position negative"}
+
+
+class _CheckedOps:
+    """torch.ops.bllm with a synchronise + device-check after every call (kernel debug mode)."""
+
+    def __getattr__(self, name):
+        op = getattr(torch.ops.bllm, name)
+
+        def call(*args, **kwargs):
+            out = op(*args, **kwargs)
+            torch.cuda.synchronize()
+            code = torch.ops.bllm.debug_error()
+            if code:
+                raise RuntimeError(f"bllm kernel check failed in {name}: {DEBUG_CODES.get(code, code)}")
+            return out
+        return call
+
+
+_CHECKED = _CheckedOps()
+
+
 def _k():
-    return torch.ops.bllm
+    return _CHECKED if kernel_debug() else torch.ops.bllm
 
 
 # --------------------------------------------------------------------------- norms

@@ -87,8 +87,13 @@ void ce_bwd(DType dt, void* logits, const int64_t* tgt, const float* lse, const 
             long ignore_index, hipStream_t s);
 
 // embedding.hip
+// kernel debug mode (common.h BLLM_DASSERT): first failed check code of each TU, reset on read
+unsigned int debug_take_embedding();
+unsigned int debug_take_loss();
+unsigned int debug_take_attn_decode();
+unsigned int debug_take_elementwise();
 void embedding_fwd(DType dt, const int64_t* idx, const void* wte, const void* wpe, void* out, long N, int d, int T,
-                   float p, uint64_t seed, uint64_t offset, hipStream_t s);
+                   float p, uint64_t seed, uint64_t offset, long vocab, hipStream_t s);
 void embedding_bwd_tok(DType dt, const int64_t* sorted, const int64_t* perm, const void* dx, void* grad, long N, int d,
                        bool accumulate, hipStream_t s);
 void embedding_bwd_pos(DType dt, const void* dx, void* grad, int B, int T, int d, bool accumulate, hipStream_t s);

@@ -17,6 +17,8 @@
 
 namespace bllm {
 
+BLLM_DEBUG_WORD(attn_decode)
+
 constexpr int DEC_THREADS = 256;
 constexpr int DEC_MAXL = 8192;  // LDS score buffer (32 KiB)
 
@@ -44,7 +46,12 @@ __global__ __launch_bounds__(DEC_THREADS) void attn_decode_k(const T* __restrict
   const T* knew = nullptr;
   const T* vnew = nullptr;
   if constexpr (APPEND) {
-    const int p = *pos;
+    int p = *pos;
+    BLLM_DASSERT(p >= 0 && p < Tmax && p < DEC_MAXL, DBG_DECODE_POS);
+#ifdef BLLM_KERNEL_DEBUG
+    p = p < 0 ? 0 : (p >= Tmax ? Tmax - 1 : p);
+    p = p >= DEC_MAXL ? DEC_MAXL - 1 : p;
+#endif
     L = p + 1;
     knew = q + (long)b * qs + (long)(H + g) * HD;
     vnew = q + (long)b * qs + (long)(H + G + g) * HD;

@@ -421,7 +421,7 @@ Tensor embedding_fwd(const Tensor& idx, const Tensor& wte, const optional<Tensor
   }
   auto out = at::empty({N, d}, wte.options());
   bllm::embedding_fwd(dt_of(wte), idx.data_ptr<int64_t>(), wte.data_ptr(), pe, out.data_ptr(), N, (int)d, (int)T,
-                      (float)p, (uint64_t)seed, (uint64_t)offset, stream());
+                      (float)p, (uint64_t)seed, (uint64_t)offset, (long)wte.size(0), stream());
   return out;
 }
 
@@ -757,7 +757,27 @@ Tensor linear_residual(const Tensor& x, const Tensor& W, const Tensor& C) {
   return D;
 }
 
+// ------------------------------------------------------------------ kernel debug mode
+// First failed device-side check since the last call (common.h DebugCode; 0 = none), over every
+// instrumented translation unit; always 0 in release builds (the checks are compiled away).
+int64_t debug_error() {
+  const unsigned codes[] = {bllm::debug_take_embedding(), bllm::debug_take_loss(), bllm::debug_take_attn_decode(),
+                            bllm::debug_take_elementwise()};
+  for (unsigned c : codes)
+    if (c) return (int64_t)c;
+  return 0;
+}
+bool kernel_debug_build() {
+#ifdef BLLM_KERNEL_DEBUG
+  return true;
+#else
+  return false;
+#endif
+}
+
 TORCH_LIBRARY(bllm, m) {
+  m.def("debug_error() -> int", &debug_error);
+  m.def("kernel_debug_build() -> bool", &kernel_debug_build);
   m.def("rmsnorm_fwd(Tensor x, Tensor w, float eps) -> (Tensor, Tensor)");
   m.def("rmsnorm_bwd(Tensor dy, Tensor x, Tensor w, Tensor rstd, Tensor? dx_acc, Tensor(a!)? dw_out, bool accumulate) -> (Tensor, Tensor)");
   m.def("layernorm_fwd(Tensor x, Tensor w, Tensor b, float eps) -> (Tensor, Tensor, Tensor)");

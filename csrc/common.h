@@ -198,6 +198,39 @@ __device__ __forceinline__ void glds16s(const void* sbase, uint32_t voff, uint32
 
 inline int ceil_div(long a, long b) { return (int)((a + b - 1) / b); }
 
+// ---- kernel debug mode (tools/build_ext.py --debug -> _C_debug.so, loaded when
+// BLLM_KERNEL_DEBUG=1).  BLLM_DASSERT records the first failed check of a translation unit in a
+// device word with a vector atomic and lets the kernel run on (no trap: a fault would take the
+// whole device down); ops/__init__.py synchronises after every op in debug mode and raises with
+// the check's name (bllm::debug_error).  Release builds compile every check away.
+enum DebugCode : unsigned int {
+  DBG_OK = 0,
+  DBG_EMB_INDEX = 1,     // embedding: token id outside [0, vocab)
+  DBG_CE_TARGET = 2,     // cross-entropy: target outside [0, V) and != ignore_index
+  DBG_DECODE_POS = 3,    // decode: cache position outside [0, Tmax) or beyond the LDS score buffer
+  DBG_ROPE_POS = 4,      // rope: device position negative
+};
+#ifdef BLLM_KERNEL_DEBUG
+#define BLLM_DEBUG_WORD(tu)                                                                        \
+  static __device__ unsigned int bllm_dbg_word;                                                     \
+  unsigned int debug_take_##tu() {                                                                  \
+    unsigned int v = 0, z = 0;                                                                      \
+    if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(bllm_dbg_word), sizeof(v)) != hipSuccess) return 0;     \
+    if (v) (void)hipMemcpyToSymbol(HIP_SYMBOL(bllm_dbg_word), &z, sizeof(z));                       \
+    return v;                                                                                       \
+  }
+#define BLLM_DASSERT(cond, code)                                   \
+  do {                                                             \
+    if (!(cond)) atomicCAS(&bllm_dbg_word, 0u, (unsigned)(code));  \
+  } while (0)
+#else
+#define BLLM_DEBUG_WORD(tu) \
+  unsigned int debug_take_##tu() { return 0; }
+#define BLLM_DASSERT(cond, code) \
+  do {                           \
+  } while (0)
+#endif
+
 }  // namespace bllm
 
 #define BLLM_DISPATCH(dt, T, ...)                                  \

@@ -8,6 +8,8 @@
 
 namespace bllm {
 
+BLLM_DEBUG_WORD(elementwise)
+
 // BLLM_SWIGLU_ROWS=0 selects the grid-stride SwiGLU kernels (A/B tuning)
 static bool swiglu_rows() {
   static const bool v = [] {
@@ -203,7 +205,10 @@ __global__ __launch_bounds__(256) void rope_k(T* __restrict__ qkv, const float* 
   // 32-bit index math (N * heads * chunks < 2^31 for every supported shape)
   static_assert(sizeof(T) == 2, "16-bit element types (fp32 uses rope_scalar_k)");
   const int half = hd / 2;
-  if (pos_dev) pos_offset += *pos_dev;  // graph-replayed decode: position read at run time
+  if (pos_dev) {
+    BLLM_DASSERT(*pos_dev >= 0, DBG_ROPE_POS);
+    pos_offset += *pos_dev;
+  }  // graph-replayed decode: position read at run time
   const int cpb = half / 8;  // chunks of 8 pairs per head
   const int per_row = nh_rot * cpb;
   const int total = (int)(N * per_row);
@@ -239,7 +244,10 @@ __global__ __launch_bounds__(256) void rope_scalar_k(T* __restrict__ qkv, const 
                                                      int row_stride, int hd, int pos_offset, float sgn,
                                                      const int* __restrict__ pos_dev) {
   const int half = hd / 2;
-  if (pos_dev) pos_offset += *pos_dev;
+  if (pos_dev) {
+    BLLM_DASSERT(*pos_dev >= 0, DBG_ROPE_POS);
+    pos_offset += *pos_dev;
+  }
   const long total = N * nh_rot * half;
   for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
     const int k = (int)(i % half);

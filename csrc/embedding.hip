@@ -11,17 +11,24 @@
 
 namespace bllm {
 
+BLLM_DEBUG_WORD(embedding)
+
 template <typename T, int VEC>
 __global__ __launch_bounds__(256) void emb_fwd_k(const int64_t* __restrict__ idx, const T* __restrict__ wte,
                                                  const T* __restrict__ wpe, T* __restrict__ out, long N, int d,
                                                  int T_, uint64_t seed, uint64_t offset, uint32_t thr,
-                                                 float inv_keep, bool drop) {
+                                                 float inv_keep, bool drop, long vocab) {
   const int dv = d / VEC;
   const long total = N * dv;
   for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
     const long r = i / dv;
     const int c = (int)(i - r * dv) * VEC;
-    VecN<T, VEC> a = ldv<T, VEC>(wte + idx[r] * d + c), o;
+    long tok = idx[r];
+    BLLM_DASSERT(tok >= 0 && tok < vocab, DBG_EMB_INDEX);
+#ifdef BLLM_KERNEL_DEBUG
+    tok = tok < 0 ? 0 : (tok >= vocab ? vocab - 1 : tok);  // keep the debug run in bounds
+#endif
+    VecN<T, VEC> a = ldv<T, VEC>(wte + tok * d + c), o;
     VecN<T, VEC> b;
     if (wpe) b = ldv<T, VEC>(wpe + (long)(r % T_) * d + c);
     uint32_t bits[VEC];
@@ -108,13 +115,13 @@ static inline int grid_of(long n) {
 }
 
 void embedding_fwd(DType dt, const int64_t* idx, const void* wte, const void* wpe, void* out, long N, int d,
-                   int T_, float p, uint64_t seed, uint64_t offset, hipStream_t s) {
+                   int T_, float p, uint64_t seed, uint64_t offset, long vocab, hipStream_t s) {
   const uint32_t thr = drop_threshold16(p);
   const float inv_keep = drop_inv_keep(p);
   BLLM_DISPATCH(dt, T, {
     EMB_VEC(T, d, {
       hipLaunchKernelGGL((emb_fwd_k<T, VEC>), dim3(grid_of(N * d / VEC)), dim3(256), 0, s, idx, (const T*)wte,
-                         (const T*)wpe, (T*)out, N, d, T_, seed, offset, thr, inv_keep, p > 0.f);
+                         (const T*)wpe, (T*)out, N, d, T_, seed, offset, thr, inv_keep, p > 0.f, vocab);
     });
   });
 }

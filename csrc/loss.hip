@@ -11,6 +11,8 @@
 
 namespace bllm {
 
+BLLM_DEBUG_WORD(loss)
+
 template <typename T>
 __device__ __forceinline__ void online_add(float x, float& m, float& s) {
   if (x > m) {
@@ -67,7 +69,11 @@ __global__ __launch_bounds__(256) void ce_fwd_k(const T* __restrict__ logits, co
     for (int i = 0; i < 4; ++i) S += sm[i] == -FLT_MAX ? 0.f : ss[i] * __expf(sm[i] - M);
     const float l = M + __logf(S);
     lse_out[row] = l;
-    const long t = tgt[row];
+    long t = tgt[row];
+    BLLM_DASSERT(t == ignore_index || (t >= 0 && t < V), DBG_CE_TARGET);
+#ifdef BLLM_KERNEL_DEBUG
+    if (t != ignore_index && (t < 0 || t >= V)) t = ignore_index;
+#endif
     loss[row] = (t == ignore_index) ? 0.f : l - to_f(p[t]);
   }
 }

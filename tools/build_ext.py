@@ -9,6 +9,9 @@
   same SONAME as /opt/rocm's) so one runtime instance is used in-process.
 
 Incremental (mtime + flags hash), parallel (``-j``).  No hipify, no CUDA sources.
+``--debug`` builds the kernel-debug variant ``_C_debug.so`` instead (-O1 -g and
+-DBLLM_KERNEL_DEBUG: device-side bounds checks, common.h ``BLLM_DASSERT``), loaded in place of
+``_C.so`` when ``BLLM_KERNEL_DEBUG=1`` (ops then synchronise and check after every call).
 Usage: ``python tools/build_ext.py [-j N] [--clean] [--debug]``.
 """
 from __future__ import annotations
@@ -26,6 +29,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "csrc")
 BUILD = os.path.join(ROOT, "build", "obj")
 OUT = os.path.join(ROOT, "building_llm_from_scratch_amd", "_C.so")
+OUT_DEBUG = os.path.join(ROOT, "building_llm_from_scratch_amd", "_C_debug.so")
 ARCH = os.environ.get("BLLM_ARCH", "gfx950")
 
 
@@ -65,11 +69,13 @@ def _run(cmd, obj, flags):
 def build(jobs: int = 8, clean: bool = False, debug: bool = False, verbose: bool = False) -> str:
     hipcc = _hipcc()
     tdir, tinc, tlib, abi = _torch_paths()
-    if clean and os.path.isdir(BUILD):
-        shutil.rmtree(BUILD)
-    os.makedirs(BUILD, exist_ok=True)
+    bdir = BUILD + "_debug" if debug else BUILD
+    out = OUT_DEBUG if debug else OUT
+    if clean and os.path.isdir(bdir):
+        shutil.rmtree(bdir)
+    os.makedirs(bdir, exist_ok=True)
     headers = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
-    opt = ["-O1", "-g"] if debug else ["-O3"]
+    opt = ["-O1", "-DBLLM_KERNEL_DEBUG=1"] if debug else ["-O3"]
     common = [f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", "-munsafe-fp-atomics",
               "-Wno-unused-result", f"-I{CSRC}"] + opt
     jobs_list = []
@@ -77,12 +83,13 @@ def build(jobs: int = 8, clean: bool = False, debug: bool = False, verbose: bool
     for f in sorted(os.listdir(CSRC)):
         src = os.path.join(CSRC, f)
         if f.endswith(".hip"):
-            obj = os.path.join(BUILD, f + ".o")
+            obj = os.path.join(bdir, f + ".o")
             cmd = [hipcc] + common + ["-c", src, "-o", obj]
         elif f.endswith(".cpp"):
-            obj = os.path.join(BUILD, f + ".o")
+            obj = os.path.join(bdir, f + ".o")
             py_inc = sysconfig.get_paths()["include"]
-            cmd = [hipcc, "-std=c++17", "-fPIC", "-O2", f"-I{CSRC}", f"-I{py_inc}"] + [f"-I{i}" for i in tinc] + [
+            cmd = [hipcc, "-std=c++17", "-fPIC", "-O2", f"-I{CSRC}", f"-I{py_inc}"] + (
+                ["-DBLLM_KERNEL_DEBUG=1"] if debug else []) + [f"-I{i}" for i in tinc] + [
                 f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-DUSE_ROCM=1", "-D__HIP_PLATFORM_AMD__=1",
                 "-DTORCH_API_INCLUDE_EXTENSION_H", "-DTORCH_EXTENSION_NAME=_C", "-Wno-deprecated-declarations",
                 "-c", src, "-o", obj]
@@ -99,18 +106,18 @@ def build(jobs: int = 8, clean: bool = False, debug: bool = False, verbose: bool
                 obj, err = fu.result()
                 if verbose:
                     print(f"[build] {os.path.basename(obj)}" + (f"\n{err}" if err.strip() else ""))
-    link_needed = not os.path.exists(OUT) or any(os.path.getmtime(o) > os.path.getmtime(OUT) for o in objs)
+    link_needed = not os.path.exists(out) or any(os.path.getmtime(o) > os.path.getmtime(out) for o in objs)
     if link_needed:
-        cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", OUT] + objs + [
+        cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out] + objs + [
             f"-L{tlib}", "-lc10", "-lc10_hip", "-ltorch_cpu", "-ltorch_hip", "-ltorch", "-lamdhip64", "-lhipblaslt",
             f"-Wl,-rpath,{tlib}"]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
         if verbose:
-            print(f"[build] linked {OUT}")
+            print(f"[build] linked {out}")
     build_host(verbose=verbose)
-    return OUT
+    return out
 
 
 def build_host(verbose: bool = False):
