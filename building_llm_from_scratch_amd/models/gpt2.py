@@ -174,7 +174,9 @@ class GPTBlockCompute(UnitCompute):
         x2d = x.reshape(N, d)
         h1, m1, r1 = self._ln(x2d, b.norm1)
         qkv, xa_qkv = self.qkv.forward(h1)
-        o, lse = ops.flash_attn_fwd(qkv, B, T, H, H, hd, True, p, rc.seed, offs[0])
+        # attention-dropout keep bits for the backward (only when this forward saves for it)
+        km = ops.attn_keep_mask(qkv, B, T, H, hd, p) if save else None
+        o, lse = ops.flash_attn_fwd(qkv, B, T, H, H, hd, True, p, rc.seed, offs[0], keep_mask=km)
         a, xa_o = self.o.forward(o)
         x2 = ops.dropout_add(x2d, a, p, rc.seed, offs[1])
         del a
@@ -190,7 +192,7 @@ class GPTBlockCompute(UnitCompute):
             # full-recompute mode: _BlockFn keeps ``offs`` as the replay token so the
             # recomputed forward regenerates identical dropout masks
             return x3.view(B, T, d), offs
-        saved = dict(x=x2d, m1=m1, r1=r1, qkv=qkv, o=o, lse=lse, x2=x2, m2=m2, r2=r2, f=f, g=g,
+        saved = dict(x=x2d, m1=m1, r1=r1, qkv=qkv, o=o, lse=lse, km=km, x2=x2, m2=m2, r2=r2, f=f, g=g,
                      p=p, offs=offs, xa=(xa_qkv, xa_o, xa_fc, xa_pr))
         if rc.block_mode(self.index) == "none" or recompute:  # the recompute's norm outputs live one block
             saved.update(h1=h1, h2=h2)
@@ -219,7 +221,8 @@ class GPTBlockCompute(UnitCompute):
         da = ops.dropout_bwd(dx2, p, rc.seed, offs[1])
         d_o = self.o.backward(da, s["o"], xa_o, accumulate=acc)
         del da
-        dqkv = ops.flash_attn_bwd(s["qkv"], s["o"], s["lse"], d_o, B, T, H, H, hd, True, p, rc.seed, offs[0])
+        dqkv = ops.flash_attn_bwd(s["qkv"], s["o"], s["lse"], d_o, B, T, H, H, hd, True, p, rc.seed, offs[0],
+                                  keep_mask=s.get("km"))
         del d_o
         h1 = s["h1"] if "h1" in s else self._ln(s["x"], b.norm1)[0]
         dh1 = self.qkv.backward(dqkv, h1, xa_qkv, accumulate=acc)

@@ -26,7 +26,7 @@ __all__ = [
     "sq_norm_multi", "adamw_step_", "attn_decode", "bias_grad_", "ext_available", "load_ext", "attention_backend",
     "lora_down", "lora_up_", "lora_wgrad", "lora_pack_t", "lora_kernel_ok", "sum_partials_",
     "wgrad_gemm_", "wgrad_gemm_ok", "wgrad_gemm_enabled", "wgrad_gemm_preferred", "wgrad_splits",
-    "gemm_nn_", "gemm_nn_ok", "dgrad_gemm_enabled", "transpose2d", "dgrad_wt_enabled",
+    "gemm_nn_", "gemm_nn_ok", "dgrad_gemm_enabled", "transpose2d", "dgrad_wt_enabled", "attn_keep_mask",
 ]
 
 rope_tables = ref.rope_tables
@@ -141,10 +141,21 @@ def attention_backend(dtype: torch.dtype, device_type: str = "cuda") -> str:
     return "hip" if dtype in (torch.bfloat16, torch.float16, torch.float32) else "reference"
 
 
-def flash_attn_fwd(qkv, B, T, H, G, hd, causal=True, dropout_p=0.0, seed=0, offset=0):
+def attn_keep_mask(qkv, B: int, T: int, H: int, hd: int, dropout_p: float):
+    """Buffer for the attention-dropout keep bits (int32 [B*H, ceil(T/32), T]) that the forward
+    kernel fills and the backward kernels read instead of re-hashing every (query, key), or None
+    where the kernels hash (no dropout, fp32, CPU, head dims without MFMA kernels)."""
+    if dropout_p <= 0.0 or qkv.device.type != "cuda" or qkv.dtype not in (torch.bfloat16, torch.float16) \
+            or hd not in (64, 128):
+        return None
+    return torch.empty(B * H, (T + 31) // 32, T, dtype=torch.int32, device=qkv.device)
+
+
+def flash_attn_fwd(qkv, B, T, H, G, hd, causal=True, dropout_p=0.0, seed=0, offset=0, keep_mask=None):
     if qkv.device.type == "cuda" and qkv.dtype in (torch.bfloat16, torch.float16, torch.float32):
         load_ext(required=True)
-        return _k().flash_attn_fwd(qkv, B, T, H, G, hd, causal, float(dropout_p), int(seed), int(offset))
+        return _k().flash_attn_fwd(qkv, B, T, H, G, hd, causal, float(dropout_p), int(seed), int(offset),
+                                   keep_mask)
     return ref.flash_attn_fwd(qkv, B, T, H, G, hd, causal, dropout_p, seed, offset)
 
 
@@ -326,11 +337,14 @@ def attn_decode(q, kcache, vcache, L: int):
     return ref.attn_decode(q, kcache, vcache, L)
 
 
-def flash_attn_bwd(qkv, o, lse, do, B, T, H, G, hd, causal=True, dropout_p=0.0, seed=0, offset=0):
+def flash_attn_bwd(qkv, o, lse, do, B, T, H, G, hd, causal=True, dropout_p=0.0, seed=0, offset=0,
+                   keep_mask=None):
+    """``keep_mask``: the buffer the matching forward filled (``attn_keep_mask``), or None to
+    regenerate the dropout bits from the counter hash (identical result)."""
     if qkv.device.type == "cuda" and qkv.dtype in (torch.bfloat16, torch.float16, torch.float32):
         load_ext(required=True)
         return _k().flash_attn_bwd(qkv, o, lse, do, B, T, H, G, hd, causal, float(dropout_p),
-                                   int(seed), int(offset))
+                                   int(seed), int(offset), keep_mask)
     return ref.flash_attn_bwd(qkv, o, lse, do, B, T, H, G, hd, causal, dropout_p, seed, offset)
 
 

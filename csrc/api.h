@@ -33,13 +33,18 @@ void dropout_add(DType dt, const void* x, const void* a, void* out, long n, floa
 void rope(DType dt, void* qkv, const float* cosT, const float* sinT, long N, int T, int H, int G, int hd,
           bool inverse, int pos_offset, hipStream_t s, const int* pos_dev = nullptr);
 
-// attention (attn_fwd.hip / attn_bwd.hip / attn_naive.hip)
+// attention (attn.hip dispatch; attn_mfma.hip / attn_bwd_mfma.hip / attn_f32.hip / attn_naive.hip)
+// keep_mask (dropout > 0, bf16/fp16 MFMA kernels only, else nullptr): the forward writes the
+// attention-dropout keep bits, uint32 words [B*H][ceil(T/32)][T] (bit j of word (kw, q) = key
+// 32kw + j), the backward kernels read them instead of re-hashing every (q, key).  Words of
+// tiles above the causal diagonal are never written or read.
 bool attn_supported_head_dim(int hd);
+bool attn_keep_mask_ok(DType dt, int hd);
 void attn_fwd(DType dt, const void* qkv, void* o, float* lse, int B, int T, int H, int G, int hd, bool causal,
-              float p, uint64_t seed, uint64_t offset, hipStream_t s);
+              float p, uint64_t seed, uint64_t offset, uint32_t* keep_mask, hipStream_t s);
 void attn_bwd(DType dt, const void* qkv, const void* o, const float* lse, const void* dout, void* dqkv, float* delta,
               float* dq_acc, float* dkv_part, int B, int T, int H, int G, int hd, bool causal, float p, uint64_t seed,
-              uint64_t offset, hipStream_t s);
+              uint64_t offset, const uint32_t* keep_mask, hipStream_t s);
 bool attn_mfma_head_dim(int hd);
 void attn_fwd_naive(DType dt, const void* qkv, void* o, float* lse, int B, int T, int H, int G, int hd, bool causal,
                     float p, uint64_t seed, uint64_t offset, hipStream_t s);

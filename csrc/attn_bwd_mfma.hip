@@ -107,8 +107,8 @@ constexpr float kLog2eB = 1.4426950408889634f;
 
 // LDS bytes of one ring slot of the dK/dV kernel: Q rows, Q^T image, dO rows, dO^T image,
 // and a per-wave copy of the step's lse/delta (so each wave's stats DMA is its own)
-template <int HD, bool DUAL = false> constexpr int dkdv_buf_bytes() {
-  return (DUAL ? 2 : 4) * BWD_BQ * HD * 2 + 4 * 256;
+template <int HD, bool DUAL = false, bool MASK = false> constexpr int dkdv_buf_bytes() {
+  return (DUAL ? 2 : 4) * BWD_BQ * HD * 2 + 4 * 256 + (MASK ? 4 * 256 : 0);
 }
 
 // Instruction budget per 32-query step (per wave): 32 MFMAs, 16 b128 + 32 tr_b64 LDS reads at
@@ -122,21 +122,26 @@ template <int HD, bool DUAL = false> constexpr int dkdv_buf_bytes() {
 // DUAL: Q and dO each staged as ONE dual-use image (dual_off) instead of a row image plus a
 // transposed image: half the LDS and DMA per step, which buys a 4-slot ring (three steps in
 // flight) at two workgroups per CU -- the 2-slot version waits on its DMA ~60 % of wave cycles.
-template <typename T, int HD, bool DROP, int NBUF, int OCC, bool FUSEG = false, bool DUAL = false>
+// MASK (with DROP): the dropout keep bits come from the forward's keep mask -- one more 4-byte
+// DMA per wave and step brings the 32 words (queries of the step, this wave's 32 keys) into the
+// slot -- instead of one counter hash per (query, key) element.
+template <typename T, int HD, bool DROP, int NBUF, int OCC, bool FUSEG = false, bool DUAL = false, bool MASK = false>
 __global__ __launch_bounds__(256, OCC) void attn_bwd_mfma_k(const T* __restrict__ qkv, const T* __restrict__ dout,
                                                             const float* __restrict__ lse,
                                                             const float* __restrict__ delta, T* __restrict__ dqkv,
                                                             float* __restrict__ dkv_part, int T_, int H, int G, int B_,
                                                             bool causal, uint32_t thr, float inv_keep,
-                                                            uint64_t seed, uint64_t doff) {
+                                                            uint64_t seed, uint64_t doff,
+                                                            const uint32_t* __restrict__ kmask) {
   typedef typename MFb<T>::v8 v8;
   constexpr int KK = HD / 16, DT = HD / 32, CH = HD / 8, ROWB = HD * 2;
   constexpr int IMG = BWD_BQ * ROWB;            // bytes of one [32][HD] image
   constexpr int PPW = IMG / 1024 / 4;           // 1-KiB DMA pieces per wave per image
   constexpr int PROWS = 256 / CH;               // rows between a wave's consecutive pieces
-  constexpr int BUF = dkdv_buf_bytes<HD, DUAL>();
+  static_assert(!MASK || DROP, "keep mask only with dropout");
+  constexpr int BUF = dkdv_buf_bytes<HD, DUAL, MASK>();
   constexpr int NIMG = DUAL ? 2 : 4;            // LDS images per step
-  constexpr int NPW = NIMG * PPW + 1;           // DMA instructions per wave per step
+  constexpr int NPW = NIMG * PPW + 1 + (MASK ? 1 : 0);  // DMA instructions per wave per step
   static_assert(NBUF >= 2 && NBUF <= 4, "ring depth");
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
@@ -198,6 +203,8 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_mfma_k(const T* __restrict_
   // image offsets inside a slot: Q rows, Q^T, dO rows, dO^T (DUAL: Q at 0, dO at IMG)
   constexpr int IQT = DUAL ? 0 : IMG, IOR = DUAL ? IMG : 2 * IMG, IOT = DUAL ? IMG : 3 * IMG;
   constexpr int ISTAT = NIMG * IMG;
+  constexpr int IMASK = ISTAT + 4 * 256;         // per-wave keep-mask words (MASK)
+  const long kw_row = (long)((T_ + 31) / 32) * T_;  // keep-mask words per (b, h)
   const uint32_t smem_u = lds_u32(smem);
   for (int hi = 0; hi < h_count; ++hi) {
   const int h = h_first + hi;
@@ -248,6 +255,9 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_mfma_k(const T* __restrict_
       }
     }
     glds4(stat_src + min(q0 + l32, T_ - 1), smem + slot * BUF + ISTAT + w * 256);
+    if constexpr (MASK)  // words (q0 .. q0+31, this wave's key word); the upper half duplicates
+      glds4(kmask + (long)(b * H + h) * kw_row + (long)min(kw0 >> 5, (T_ - 1) >> 5) * T_ + min(q0 + l32, T_ - 1),
+            smem + slot * BUF + IMASK + w * 256);
   };
   // wait until step i+1's DMA landed, leaving the later issued steps (up to NBUF-2) in flight
   auto ring_wait = [&](int i, int nsteps) {
@@ -321,14 +331,22 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_mfma_k(const T* __restrict_
       for (int gq = 0; gq < 4; ++gq) {
         const f32x4 L4 = *reinterpret_cast<const f32x4*>(LS + 8 * gq + 4 * hh_);
         const f32x4 D4 = *reinterpret_cast<const f32x4*>(LS + 32 + 8 * gq + 4 * hh_);
+        uint4 M4 = {0u, 0u, 0u, 0u};
+        if constexpr (MASK) M4 = *reinterpret_cast<const uint4*>(S + IMASK + w * 256 + 4 * (8 * gq + 4 * hh_));
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int r = 4 * gq + j;
           const float p = __builtin_amdgcn_exp2f(fmaf(sacc[r], c, -L4[j]));
           float dp = dpacc[r], pd = p;
           if constexpr (DROP) {
-            const int q = q0 + 8 * gq + 4 * hh + j;
-            const bool keep = ds.bits16(dslab + (uint64_t)q * T_ + mykey) >= thr;
+            bool keep;
+            if constexpr (MASK) {
+              const uint32_t mw = j == 0 ? M4.x : j == 1 ? M4.y : j == 2 ? M4.z : M4.w;
+              keep = (mw >> l32_) & 1u;
+            } else {
+              const int q = q0 + 8 * gq + 4 * hh + j;
+              keep = ds.bits16(dslab + (uint64_t)q * T_ + mykey) >= thr;
+            }
             pd = keep ? p * inv_keep : 0.f;
             dp = keep ? dp * inv_keep : 0.f;
           }
@@ -415,23 +433,31 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_mfma_k(const T* __restrict_
 // K transposed (dQ^T += K^T dS^T), V rows (dP^T = V dO^T).  The query is the lane column, so
 // lse / delta are per-lane scalars; 1/sqrt(d) is applied once to the final dQ.
 constexpr int DQ_BQ = 128;
-template <int HD, int BK> constexpr int dq_buf_bytes() { return 3 * BK * HD * 2; }
+template <int HD, int BK, bool MASK = false> constexpr int dq_buf_bytes() {
+  return 3 * BK * HD * 2 + (MASK ? 4 * 256 : 0);
+}
 
-template <typename T, int HD, bool DROP, int DQ_BK, int NBUF, int OCC>
+// MASK (with DROP): keep bits from the forward's keep mask (one 4-byte DMA per wave and tile:
+// the words of the wave's 32 queries for each 32-key sub-tile) instead of the counter hash.
+template <typename T, int HD, bool DROP, int DQ_BK, int NBUF, int OCC, bool MASK = false>
 __global__ __launch_bounds__(256, OCC) void attn_bwd_dq_k(const T* __restrict__ qkv, const T* __restrict__ out,
                                                         const T* __restrict__ dout,
                                                         const float* __restrict__ lse,
                                                         float* __restrict__ delta, T* __restrict__ dqkv,
                                                         int T_, int H, int G, int B_, bool causal, uint32_t thr,
-                                                        float inv_keep, uint64_t seed, uint64_t doff) {
+                                                        float inv_keep, uint64_t seed, uint64_t doff,
+                                                        const uint32_t* __restrict__ kmask) {
   typedef typename MFb<T>::v8 v8;
   constexpr int KK = HD / 16, DT = HD / 32, CH = HD / 8, ROWB = HD * 2;
   constexpr int IMG = DQ_BK * ROWB;             // bytes of one [BK][HD] image
   constexpr int LD = DQ_BK * CH / 256;          // 1-KiB pieces per wave per image
   constexpr int NKT = DQ_BK / 32;               // 32-key MFMA tiles per step
-  constexpr int BUF = dq_buf_bytes<HD, DQ_BK>();
+  constexpr int BUF = dq_buf_bytes<HD, DQ_BK, MASK>();
   static_assert(NBUF == 2 || NBUF == 3, "ring depth");
-  constexpr int NPW = 3 * LD;                   // DMA instructions per wave per step
+  static_assert(!MASK || DROP, "keep mask only with dropout");
+  static_assert(DQ_BK / 32 <= 2, "mask words: one lane half per 32-key sub-tile");
+  constexpr int NPW = 3 * LD + (MASK ? 1 : 0);  // DMA instructions per wave per step
+  constexpr int MOFF = 3 * IMG;                 // per-wave keep-mask words (MASK)
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   // heaviest (last, for causal) query block first; one (b, h) per XCD residue
@@ -513,9 +539,14 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_dq_k(const T* __restrict__ 
   }
   const uint32_t smem_u = lds_u32(smem);
 
+  const long kw_row = (long)((T_ + 31) / 32) * T_;  // keep-mask words per (b, h)
   auto issue = [&](int t, int slot) {
     const int k0 = t * DQ_BK;
     const uint32_t base = smem_u + slot * BUF;
+    if constexpr (MASK) {  // lane half kt: words (wave's queries, key word t*NKT + kt)
+      const int kw = min(t * NKT + (NKT == 2 ? hh : 0), (T_ - 1) >> 5);
+      glds4(kmask + (long)(b * H + h) * kw_row + (long)kw * T_ + qc, smem + slot * BUF + MOFF + w * 256);
+    }
     if (k0 + DQ_BK <= T_) {
       const void* ks = sgpr_ptr(kb_ + (long)k0 * rs);
       const void* vs = sgpr_ptr(vb_ + (long)k0 * rs);
@@ -590,7 +621,15 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_dq_k(const T* __restrict__ 
           if ((causal && key > qi) || key >= T_ || qi >= T_) sc[kt][r] = -INFINITY;
         }
     }
-    if constexpr (DROP) {
+    if constexpr (MASK) {
+#pragma unroll
+      for (int kt = 0; kt < NKT; ++kt) {
+        const uint32_t mw = *reinterpret_cast<const uint32_t*>(KR + MOFF + w * 256 + 4 * (kt * 32 + l32)) >> (4 * hh);
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          dp[kt][r] = ((mw >> ((r & 3) + 8 * (r >> 2))) & 1u) ? dp[kt][r] * inv_keep : 0.f;
+      }
+    } else if constexpr (DROP) {
       const uint64_t rowbase = dslab + (uint64_t)qi * T_;
       if (dpair) {
 #pragma unroll
@@ -718,12 +757,61 @@ static int q_variant_from_env() {
 
 bool attn_bwd_kv_partials(int B, int T_, int H, int G) { return H != G && !fuse_gqa_heads(B, T_, H, G); }
 
+// launch helpers: one instantiation per (ring, occupancy, fused heads, dual images) and per
+// dropout form (none / counter hash / forward keep mask)
+struct BwdArgs {
+  const void *qkv, *o, *dout;
+  const float* lse;
+  float *delta, *dkv_part;
+  void* dqkv;
+  int T_, H, G, B;
+  bool causal;
+  uint32_t thr;
+  float ik;
+  uint64_t seed, offset;
+  const uint32_t* kmask;
+  hipStream_t s;
+};
+template <typename TT, int HDD, bool DROP, int BK, int NB, int OC, bool MASK>
+static void launch_dq1(const BwdArgs& a, dim3 grid) {
+  constexpr int lds = NB * dq_buf_bytes<HDD, BK, MASK>();
+  hipLaunchKernelGGL((attn_bwd_dq_k<TT, HDD, DROP, BK, NB, OC, MASK>), grid, dim3(256), lds, a.s, (const TT*)a.qkv, (const TT*)a.o, (const TT*)a.dout, a.lse, a.delta, (TT*)a.dqkv, a.T_, a.H,
+                     a.G, a.B, a.causal, a.thr, a.ik, a.seed, a.offset, a.kmask);
+}
+template <typename TT, int HDD, int BK, int NB, int OC>
+static void launch_dq(const BwdArgs& a, bool drop, dim3 grid) {
+  if (drop && a.kmask) launch_dq1<TT, HDD, true, BK, NB, OC, true>(a, grid);
+  else if (drop) launch_dq1<TT, HDD, true, BK, NB, OC, false>(a, grid);
+  else launch_dq1<TT, HDD, false, BK, NB, OC, false>(a, grid);
+}
+template <typename TT, int HDD, bool DROP, int NB, int OC, bool FG, bool DU, bool MASK>
+static void launch_kv1(const BwdArgs& a, dim3 grid) {
+  constexpr int lds = NB * dkdv_buf_bytes<HDD, DU, MASK>();
+  hipLaunchKernelGGL((attn_bwd_mfma_k<TT, HDD, DROP, NB, OC, FG, DU, MASK>), grid, dim3(256), lds, a.s, (const TT*)a.qkv, (const TT*)a.dout, a.lse, a.delta,
+                     (TT*)a.dqkv, a.dkv_part, a.T_, a.H, a.G, a.B, a.causal, a.thr, a.ik, a.seed, a.offset, a.kmask);
+}
+template <typename TT, int HDD, int NB, int OC, bool FG, bool DU>
+static void launch_kv(const BwdArgs& a, bool drop, dim3 grid) {
+  if (drop && a.kmask) launch_kv1<TT, HDD, true, NB, OC, FG, DU, true>(a, grid);
+  else if (drop) launch_kv1<TT, HDD, true, NB, OC, FG, DU, false>(a, grid);
+  else launch_kv1<TT, HDD, false, NB, OC, FG, DU, false>(a, grid);
+}
+template <typename TT, int HDD>
+static void launch_bwd(const BwdArgs& a, bool drop, int q_variant, int kv_variant, bool fuseg, bool kv_dual,
+                       dim3 grid_q, dim3 grid_kv) {
+  if (q_variant == 0) launch_dq<TT, HDD, 32, 3, 2>(a, drop, grid_q);
+  else launch_dq<TT, HDD, 64, 3, 1>(a, drop, grid_q);
+  if (fuseg && kv_dual) launch_kv<TT, HDD, 4, 2, true, true>(a, drop, grid_kv);
+  else if (kv_dual && kv_variant != 1) launch_kv<TT, HDD, 4, 2, false, true>(a, drop, grid_kv);
+  else if (fuseg) launch_kv<TT, HDD, 2, 2, true, false>(a, drop, grid_kv);
+  else if (kv_variant != 1) launch_kv<TT, HDD, 2, 2, false, false>(a, drop, grid_kv);
+  else launch_kv<TT, HDD, 3, 1, false, false>(a, drop, grid_kv);
+}
+
 void attn_bwd_mfma(DType dt, const void* qkv, const void* o, const float* lse, const void* dout, void* dqkv,
                    float* delta, float* dq_acc, float* dkv_part, int B, int T_, int H, int G, int hd, bool causal,
-                   float p, uint64_t seed, uint64_t offset, hipStream_t s) {
+                   float p, uint64_t seed, uint64_t offset, const uint32_t* keep_mask, hipStream_t s) {
   (void)dq_acc;
-  const uint32_t thr = drop_threshold16(p);
-  const float ik = drop_inv_keep(p);
   static const int kv_variant = kv_variant_from_env();
   static const int q_variant = q_variant_from_env();
   static const int kv_dual_env = kv_dual_from_env();
@@ -731,89 +819,17 @@ void attn_bwd_mfma(DType dt, const void* qkv, const void* o, const float* lse, c
   const int nkb = (T_ + BWD_BKV - 1) / BWD_BKV;
   // kv variant 2 (GQA, large grids): the dK/dV workgroup sweeps the H/G heads of its kv head
   const bool fuseg = fuse_gqa_heads(B, T_, H, G);
-  dim3 grid_kv(nkb * (fuseg ? G : H) * B), grid_q(((T_ + DQ_BQ - 1) / DQ_BQ) * H * B), block(256);
+  dim3 grid_kv(nkb * (fuseg ? G : H) * B), grid_q(((T_ + DQ_BQ - 1) / DQ_BQ) * H * B);
   const bool drop = p > 0.f;
-#define LAUNCH(TT, HDD)                                                                                         \
-  do {                                                                                                          \
-    if (q_variant == 0) {                                                                                       \
-      const int lds_q = 3 * dq_buf_bytes<HDD, 32>();                                                            \
-      if (drop)                                                                                                 \
-        hipLaunchKernelGGL((attn_bwd_dq_k<TT, HDD, true, 32, 3, 2>), grid_q, block, lds_q, s, (const TT*)qkv,  \
-                           (const TT*)o, (const TT*)dout, lse, delta, (TT*)dqkv, T_, H, G, B, causal, thr, ik, \
-                           seed, offset);                                                                       \
-      else                                                                                                      \
-        hipLaunchKernelGGL((attn_bwd_dq_k<TT, HDD, false, 32, 3, 2>), grid_q, block, lds_q, s, (const TT*)qkv, \
-                           (const TT*)o, (const TT*)dout, lse, delta, (TT*)dqkv, T_, H, G, B, causal, thr, ik, \
-                           seed, offset);                                                                       \
-    } else {                                                                                                    \
-      const int lds_q = 3 * dq_buf_bytes<HDD, 64>();                                                            \
-      if (drop)                                                                                                 \
-        hipLaunchKernelGGL((attn_bwd_dq_k<TT, HDD, true, 64, 3, 1>), grid_q, block, lds_q, s, (const TT*)qkv,  \
-                           (const TT*)o, (const TT*)dout, lse, delta, (TT*)dqkv, T_, H, G, B, causal, thr, ik, \
-                           seed, offset);                                                                       \
-      else                                                                                                      \
-        hipLaunchKernelGGL((attn_bwd_dq_k<TT, HDD, false, 64, 3, 1>), grid_q, block, lds_q, s, (const TT*)qkv, \
-                           (const TT*)o, (const TT*)dout, lse, delta, (TT*)dqkv, T_, H, G, B, causal, thr, ik, \
-                           seed, offset);                                                                       \
-    }                                                                                                           \
-    if (fuseg && kv_dual) {                                                                                     \
-      const int lds_kv = 4 * dkdv_buf_bytes<HDD, true>();                                                       \
-      if (drop)                                                                                                 \
-        hipLaunchKernelGGL((attn_bwd_mfma_k<TT, HDD, true, 4, 2, true, true>), grid_kv, block, lds_kv, s,      \
-                           (const TT*)qkv, (const TT*)dout, lse, delta, (TT*)dqkv, dkv_part, T_, H, G, B,       \
-                           causal, thr, ik, seed, offset);                                                      \
-      else                                                                                                      \
-        hipLaunchKernelGGL((attn_bwd_mfma_k<TT, HDD, false, 4, 2, true, true>), grid_kv, block, lds_kv, s,     \
-                           (const TT*)qkv, (const TT*)dout, lse, delta, (TT*)dqkv, dkv_part, T_, H, G, B,       \
-                           causal, thr, ik, seed, offset);                                                      \
-    } else if (kv_dual && kv_variant != 1) {                                                                    \
-      const int lds_kv = 4 * dkdv_buf_bytes<HDD, true>();                                                       \
-      if (drop)                                                                                                 \
-        hipLaunchKernelGGL((attn_bwd_mfma_k<TT, HDD, true, 4, 2, false, true>), grid_kv, block, lds_kv, s,     \
-                           (const TT*)qkv, (const TT*)dout, lse, delta, (TT*)dqkv, dkv_part, T_, H, G, B,       \
-                           causal, thr, ik, seed, offset);                                                      \
-      else                                                                                                      \
-        hipLaunchKernelGGL((attn_bwd_mfma_k<TT, HDD, false, 4, 2, false, true>), grid_kv, block, lds_kv, s,    \
-                           (const TT*)qkv, (const TT*)dout, lse, delta, (TT*)dqkv, dkv_part, T_, H, G, B,       \
-                           causal, thr, ik, seed, offset);                                                      \
-    } else if (fuseg) {                                                                                         \
-      const int lds_kv = 2 * dkdv_buf_bytes<HDD>();                                                             \
-      if (drop)                                                                                                 \
-        hipLaunchKernelGGL((attn_bwd_mfma_k<TT, HDD, true, 2, 2, true>), grid_kv, block, lds_kv, s,            \
-                           (const TT*)qkv, (const TT*)dout, lse, delta, (TT*)dqkv, dkv_part, T_, H, G, B,       \
-                           causal, thr, ik, seed, offset);                                                      \
-      else                                                                                                      \
-        hipLaunchKernelGGL((attn_bwd_mfma_k<TT, HDD, false, 2, 2, true>), grid_kv, block, lds_kv, s,           \
-                           (const TT*)qkv, (const TT*)dout, lse, delta, (TT*)dqkv, dkv_part, T_, H, G, B,       \
-                           causal, thr, ik, seed, offset);                                                      \
-    } else if (kv_variant != 1) {                                                                               \
-      const int lds_kv = 2 * dkdv_buf_bytes<HDD>();                                                             \
-      if (drop)                                                                                                 \
-        hipLaunchKernelGGL((attn_bwd_mfma_k<TT, HDD, true, 2, 2>), grid_kv, block, lds_kv, s, (const TT*)qkv,  \
-                           (const TT*)dout, lse, delta, (TT*)dqkv, dkv_part, T_, H, G, B, causal, thr, ik,     \
-                           seed, offset);                                                                       \
-      else                                                                                                      \
-        hipLaunchKernelGGL((attn_bwd_mfma_k<TT, HDD, false, 2, 2>), grid_kv, block, lds_kv, s, (const TT*)qkv, \
-                           (const TT*)dout, lse, delta, (TT*)dqkv, dkv_part, T_, H, G, B, causal, thr, ik,     \
-                           seed, offset);                                                                       \
-    } else {                                                                                                    \
-      const int lds_kv = 3 * dkdv_buf_bytes<HDD>();                                                             \
-      if (drop)                                                                                                 \
-        hipLaunchKernelGGL((attn_bwd_mfma_k<TT, HDD, true, 3, 1>), grid_kv, block, lds_kv, s, (const TT*)qkv,  \
-                           (const TT*)dout, lse, delta, (TT*)dqkv, dkv_part, T_, H, G, B, causal, thr, ik,     \
-                           seed, offset);                                                                       \
-      else                                                                                                      \
-        hipLaunchKernelGGL((attn_bwd_mfma_k<TT, HDD, false, 3, 1>), grid_kv, block, lds_kv, s, (const TT*)qkv, \
-                           (const TT*)dout, lse, delta, (TT*)dqkv, dkv_part, T_, H, G, B, causal, thr, ik,     \
-                           seed, offset);                                                                       \
-    }                                                                                                           \
-  } while (0)
+  const BwdArgs a{qkv, o, dout, lse, delta, dkv_part, dqkv, T_, H, G, B, causal, drop_threshold16(p),
+                  drop_inv_keep(p), seed, offset, drop ? keep_mask : nullptr, s};
   if (dt == DType::BF16) {
-    if (hd == 128) LAUNCH(bf16_t, 128); else LAUNCH(bf16_t, 64);
+    if (hd == 128) launch_bwd<bf16_t, 128>(a, drop, q_variant, kv_variant, fuseg, kv_dual, grid_q, grid_kv);
+    else launch_bwd<bf16_t, 64>(a, drop, q_variant, kv_variant, fuseg, kv_dual, grid_q, grid_kv);
   } else {
-    if (hd == 128) LAUNCH(f16_t, 128); else LAUNCH(f16_t, 64);
+    if (hd == 128) launch_bwd<f16_t, 128>(a, drop, q_variant, kv_variant, fuseg, kv_dual, grid_q, grid_kv);
+    else launch_bwd<f16_t, 64>(a, drop, q_variant, kv_variant, fuseg, kv_dual, grid_q, grid_kv);
   }
-#undef LAUNCH
   if (H != G && !fuseg) {
     const long BT = (long)B * T_;
     const long groups = BT * 2L * G * hd / 4;

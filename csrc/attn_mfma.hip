@@ -84,7 +84,7 @@ template <typename T, int HD, bool DROP, int FWD_BK, int NBUF, int OCC>
 __global__ __launch_bounds__(256, OCC) void attn_fwd_mfma_k(const T* __restrict__ qkv, T* __restrict__ out,
                                                           float* __restrict__ lse, int T_, int H, int G, int B_,
                                                           bool causal, uint32_t thr, float inv_keep, uint64_t seed,
-                                                          uint64_t doff) {
+                                                          uint64_t doff, uint32_t* __restrict__ kmask) {
   typedef typename MF<T>::v8 v8;
   constexpr int KK = HD / 16;               // k-steps of the QK^T product
   constexpr int DT = HD / 32;               // 32-row tiles of O^T
@@ -212,6 +212,23 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd_mfma_k(const T* __restrict_
   }
   __builtin_amdgcn_s_barrier();
   int t = 0, buf = 0;
+  // dropout keep-mask words of the last computed tile (kmask != nullptr): stored at the top of
+  // the next iteration, BEFORE that iteration's DMA issue -- vector memory completes in order,
+  // so the ring's counted waits are not lengthened by the stores
+  uint32_t kw_pend[NKT];
+  int kw_n = 0, kw_t = 0;
+  const long kw_row = (long)((T_ + 31) / 32) * T_;  // words per (b, h)
+  auto flush_mask = [&]() {
+    if constexpr (DROP) {
+      if (kmask != nullptr && hh == 0 && qi < T_) {
+        uint32_t* mrow = kmask + (long)(b * H + h) * kw_row + qi;
+#pragma unroll
+        for (int kt = 0; kt < NKT; ++kt)
+          if (kt < kw_n) mrow[(long)(kw_t * NKT + kt) * T_] = kw_pend[kt];
+      }
+      kw_n = 0;
+    }
+  };
   // One K/V tile.  NV = 32-key sub-tiles this wave can see (< NKT only on causal-diagonal or
   // tail tiles: even waves' diagonal tile has its upper half above every query), EDGE = some
   // visible key is masked.  Instantiated per (NV, EDGE) so each path is straight-line code.
@@ -271,27 +288,39 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd_mfma_k(const T* __restrict_
       }
     l += ls;
     if constexpr (DROP) {
-      // keys (r, r+1) with r even are adjacent: one hash serves both when the row base is even
+      // keys (r, r+1) with r even are adjacent: one hash serves both when the row base is even.
+      // The keep bits also go to the backward's mask (bit (r&3) + 8(r>>2) + 4hh of the word of
+      // this query and 32-key sub-tile; the two lane halves' bits are merged by one swap).
       const uint64_t rowbase = dslab + (uint64_t)qi * T_;
-      if (dpair) {
 #pragma unroll
-        for (int kt = 0; kt < NV; ++kt)
+      for (int kt = 0; kt < NV; ++kt) {
+        uint32_t kbits = 0;
+        if (dpair) {
 #pragma unroll
           for (int r = 0; r < 16; r += 2) {
             const int key = k0 + kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
             const uint32_t hv = ds.pair_hash((rowbase + key) >> 1);
-            s[kt][r] = (hv & 0xFFFFu) >= thr ? s[kt][r] * inv_keep : 0.f;
-            s[kt][r + 1] = (hv >> 16) >= thr ? s[kt][r + 1] * inv_keep : 0.f;
+            const bool k0b = (hv & 0xFFFFu) >= thr, k1b = (hv >> 16) >= thr;
+            s[kt][r] = k0b ? s[kt][r] * inv_keep : 0.f;
+            s[kt][r + 1] = k1b ? s[kt][r + 1] * inv_keep : 0.f;
+            kbits |= ((uint32_t)k0b << ((r & 3) + 8 * (r >> 2))) | ((uint32_t)k1b << (((r + 1) & 3) + 8 * (r >> 2)));
           }
-      } else {
-#pragma unroll
-        for (int kt = 0; kt < NV; ++kt)
+        } else {
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
             const int key = k0 + kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
-            s[kt][r] = ds.bits16(rowbase + key) >= thr ? s[kt][r] * inv_keep : 0.f;
+            const bool kb = ds.bits16(rowbase + key) >= thr;
+            s[kt][r] = kb ? s[kt][r] * inv_keep : 0.f;
+            kbits |= (uint32_t)kb << ((r & 3) + 8 * (r >> 2));
           }
+        }
+        if (kmask != nullptr) {
+          const uint32_t mine = kbits << (4 * hh);
+          const auto sw = __builtin_amdgcn_permlane32_swap(mine, mine, false, false);
+          kw_pend[kt] = mine | sw[0] | sw[1];
+        }
       }
+      kw_n = NV;
     }
     // ---- O^T += V^T P^T: P fragments packed from the accumulators, V^T by transposed reads
 #pragma unroll
@@ -320,8 +349,10 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd_mfma_k(const T* __restrict_
   using Yes = std::true_type;
   using No = std::false_type;
   for (; t < nact; ++t) {
+    flush_mask();  // keep bits of tile t - 1
     if (t + NBUF - 1 < ntiles) issue(t + NBUF - 1, buf == 0 ? NBUF - 1 : buf - 1);
     const int k0 = t * FWD_BK;
+    kw_t = t;
     const char* kb = smem + buf * 2 * TILE_B;
     const char* vb = kb + TILE_B;
     // wave-uniform: causal diagonal / sequence tail tiles need masking
@@ -336,6 +367,7 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd_mfma_k(const T* __restrict_
     ring_wait(t);  // the DMA of tile t+1 has landed (asm-issued, so drained by hand)
     buf = buf == NBUF - 1 ? 0 : buf + 1;
   }
+  flush_mask();
   for (; t < ntiles; ++t) {  // wave done (causal): keep the DMA ring and barriers going
     if (t + NBUF - 1 < ntiles) issue(t + NBUF - 1, buf == 0 ? NBUF - 1 : buf - 1);
     ring_wait(t);
@@ -372,7 +404,7 @@ static int fwd_variant_from_env() {
 }
 
 void attn_fwd_mfma(DType dt, const void* qkv, void* o, float* lse, int B, int T_, int H, int G, int hd, bool causal,
-                   float p, uint64_t seed, uint64_t offset, hipStream_t s) {
+                   float p, uint64_t seed, uint64_t offset, uint32_t* keep_mask, hipStream_t s) {
   const uint32_t thr = drop_threshold16(p);
   const float ik = drop_inv_keep(p);
   static const int fwd_variant = fwd_variant_from_env();
@@ -382,10 +414,10 @@ void attn_fwd_mfma(DType dt, const void* qkv, void* o, float* lse, int B, int T_
     const int lds = NB * 2 * BK * HDD * 2;                                                                    \
     if (p > 0.f)                                                                                              \
       hipLaunchKernelGGL((attn_fwd_mfma_k<TT, HDD, true, BK, NB, OC>), grid, block, lds, s,               \
-                         (const TT*)qkv, (TT*)o, lse, T_, H, G, B, causal, thr, ik, seed, offset);            \
+                         (const TT*)qkv, (TT*)o, lse, T_, H, G, B, causal, thr, ik, seed, offset, keep_mask); \
     else                                                                                                      \
       hipLaunchKernelGGL((attn_fwd_mfma_k<TT, HDD, false, BK, NB, OC>), grid, block, lds, s,              \
-                         (const TT*)qkv, (TT*)o, lse, T_, H, G, B, causal, thr, ik, seed, offset);            \
+                         (const TT*)qkv, (TT*)o, lse, T_, H, G, B, causal, thr, ik, seed, offset, nullptr); \
   } while (0)
 #define LAUNCH(TT, HDD)                                                                                       \
   do {                                                                                                        \

@@ -344,8 +344,20 @@ Tensor attn_decode(const Tensor& q, const Tensor& kc, const Tensor& vc, int64_t 
   return out;
 }
 
+// keep_mask: optional uint32 [B*H, ceil(T/32), T] the forward fills with the dropout keep bits
+// (dropout > 0, bf16/fp16) and the backward reads (api.h attn_fwd)
+static uint32_t* keep_mask_ptr(const optional<Tensor>& m, const Tensor& qkv, int64_t B, int64_t T, int64_t H,
+                               int64_t hd, double p) {
+  if (!m.has_value() || p <= 0.0 || !bllm::attn_keep_mask_ok(dt_of(qkv), (int)hd)) return nullptr;
+  check_gpu(*m, "keep_mask");
+  TORCH_CHECK(m->scalar_type() == at::kInt && m->numel() == B * H * ((T + 31) / 32) * T,
+              "flash_attn: keep_mask must be int32 [B*H, ceil(T/32), T]");
+  return reinterpret_cast<uint32_t*>(m->data_ptr<int32_t>());
+}
+
 std::tuple<Tensor, Tensor> flash_attn_fwd(const Tensor& qkv, int64_t B, int64_t T, int64_t H, int64_t G,
-                                          int64_t hd, bool causal, double p, int64_t seed, int64_t offset) {
+                                          int64_t hd, bool causal, double p, int64_t seed, int64_t offset,
+                                          const optional<Tensor>& keep_mask) {
   check_gpu(qkv, "qkv");
   c10::DeviceGuard g(qkv.device());
   TORCH_CHECK(qkv.scalar_type() == at::kBFloat16 || qkv.scalar_type() == at::kHalf ||
@@ -356,13 +368,14 @@ std::tuple<Tensor, Tensor> flash_attn_fwd(const Tensor& qkv, int64_t B, int64_t 
   auto o = at::empty({B * T, H * hd}, qkv.options());
   auto lse = at::empty({B, H, T}, qkv.options().dtype(at::kFloat));
   bllm::attn_fwd(dt_of(qkv), qkv.data_ptr(), o.data_ptr(), lse.data_ptr<float>(), (int)B, (int)T, (int)H, (int)G,
-                 (int)hd, causal, (float)p, (uint64_t)seed, (uint64_t)offset, stream());
+                 (int)hd, causal, (float)p, (uint64_t)seed, (uint64_t)offset,
+                 keep_mask_ptr(keep_mask, qkv, B, T, H, hd, p), stream());
   return {o, lse};
 }
 
 Tensor flash_attn_bwd(const Tensor& qkv, const Tensor& o, const Tensor& lse, const Tensor& dout, int64_t B,
                       int64_t T, int64_t H, int64_t G, int64_t hd, bool causal, double p, int64_t seed,
-                      int64_t offset) {
+                      int64_t offset, const optional<Tensor>& keep_mask) {
   check_gpu(qkv, "qkv"); check_gpu(o, "o"); check_gpu(lse, "lse"); check_gpu(dout, "dout");
   c10::DeviceGuard g(qkv.device());
   TORCH_CHECK(qkv.scalar_type() == at::kBFloat16 || qkv.scalar_type() == at::kHalf ||
@@ -379,7 +392,7 @@ Tensor flash_attn_bwd(const Tensor& qkv, const Tensor& o, const Tensor& lse, con
   auto dkv_part = (mfma && bllm::attn_bwd_kv_partials((int)B, (int)T, (int)H, (int)G)) ? at::empty({2, B * T, H, hd}, qkv.options().dtype(at::kFloat)) : Tensor();
   bllm::attn_bwd(dt_of(qkv), qkv.data_ptr(), o.data_ptr(), lse.data_ptr<float>(), dout.data_ptr(), dqkv.data_ptr(),
                  delta.data_ptr<float>(), nullptr, dkv_part.defined() ? dkv_part.data_ptr<float>() : nullptr, (int)B, (int)T, (int)H, (int)G, (int)hd, causal,
-                 (float)p, (uint64_t)seed, (uint64_t)offset, stream());
+                 (float)p, (uint64_t)seed, (uint64_t)offset, keep_mask_ptr(keep_mask, qkv, B, T, H, hd, p), stream());
   return dqkv;
 }
 
@@ -798,8 +811,8 @@ TORCH_LIBRARY(bllm, m) {
   m.def("attn_decode(Tensor q, Tensor kcache, Tensor vcache, int L) -> Tensor");
   m.def("attn_decode_append(Tensor qkv, Tensor(a!) kcache, Tensor(b!) vcache, Tensor pos, int H, int G) -> Tensor");
   m.def("rope_dev_(Tensor(a!) qkv, Tensor cos, Tensor sin, int H, int G, int hd, Tensor pos) -> ()");
-  m.def("flash_attn_fwd(Tensor qkv, int B, int T, int H, int G, int hd, bool causal, float p, int seed, int offset) -> (Tensor, Tensor)");
-  m.def("flash_attn_bwd(Tensor qkv, Tensor o, Tensor lse, Tensor dout, int B, int T, int H, int G, int hd, bool causal, float p, int seed, int offset) -> Tensor");
+  m.def("flash_attn_fwd(Tensor qkv, int B, int T, int H, int G, int hd, bool causal, float p, int seed, int offset, Tensor(a!)? keep_mask=None) -> (Tensor, Tensor)");
+  m.def("flash_attn_bwd(Tensor qkv, Tensor o, Tensor lse, Tensor dout, int B, int T, int H, int G, int hd, bool causal, float p, int seed, int offset, Tensor? keep_mask=None) -> Tensor");
   m.def("ce_fwd(Tensor logits, Tensor targets, int ignore_index) -> (Tensor, Tensor)");
   m.def("ce_bwd_(Tensor(a!) logits, Tensor targets, Tensor lse, Tensor scale, int ignore_index) -> ()");
   m.def("embedding_fwd(Tensor idx, Tensor wte, Tensor? wpe, int T, float p, int seed, int offset) -> Tensor");

@@ -196,6 +196,35 @@ def test_flash_attention(dt, B, T, H, G, hd, p, causal):
     _close(dqkv, dqkv0, dt, 4, name="dqkv")
 
 
+@pytest.mark.parametrize("hd", [64, 128])
+@pytest.mark.parametrize("B,T,H,G", [(2, 256, 4, 4), (1, 200, 4, 2), (2, 33, 2, 2), (1, 1024, 4, 1)])
+@pytest.mark.parametrize("causal", [True, False])
+def test_flash_attention_keep_mask(hd, B, T, H, G, causal):
+    """The forward's dropout keep bits (word (kw, q), bit j = key 32kw + j) equal the counter
+    hash of the oracle for every (query, key) the softmax covers, and a backward reading them is
+    bit-identical to one that re-hashes."""
+    p, seed, offset = 0.1, 99, 12345
+    qkv = torch.randn(B * T, (H + 2 * G) * hd, device=DEV).to(torch.bfloat16)
+    do = torch.randn(B * T, H * hd, device=DEV).to(torch.bfloat16)
+    km = ops.attn_keep_mask(qkv, B, T, H, hd, p)
+    assert km is not None
+    o, lse = ops.flash_attn_fwd(qkv, B, T, H, G, hd, causal, p, seed, offset, keep_mask=km)
+    o2, lse2 = ops.flash_attn_fwd(qkv, B, T, H, G, hd, causal, p, seed, offset)
+    assert torch.equal(o, o2) and torch.equal(lse, lse2)
+    KW = (T + 31) // 32
+    bits = (km.view(B * H, KW, T).permute(0, 2, 1).unsqueeze(-1).to(torch.int64)
+            >> torch.arange(32, device=DEV)) & 1                        # [BH, T(q), KW, 32]
+    got = bits.reshape(B * H, T, KW * 32)[:, :, :T].bool()
+    want = ref.drop_keep_mask(seed, offset, B * H * T * T, p, device=DEV).view(B * H, T, T)
+    cover = torch.ones(T, T, dtype=torch.bool, device=DEV)
+    if causal:
+        cover = cover.tril()
+    assert torch.equal(got[:, cover], want[:, cover])
+    d1 = ops.flash_attn_bwd(qkv, o, lse, do, B, T, H, G, hd, causal, p, seed, offset, keep_mask=km)
+    d2 = ops.flash_attn_bwd(qkv, o, lse, do, B, T, H, G, hd, causal, p, seed, offset)
+    assert torch.equal(d1, d2)
+
+
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("hd,step", [(128, 0.35), (128, 0.6), (64, 0.5)])
 def test_flash_attention_deferred_rescale(dt, hd, step):

@@ -32,6 +32,8 @@ def main():
     ap.add_argument("--shapes", default="", help="comma-separated shape names (default: all)")
     ap.add_argument("--noncausal", action="store_true", help="full (non-causal) attention")
     ap.add_argument("--T", type=int, default=None, help="override the sequence length")
+    ap.add_argument("--no_mask", action="store_true",
+                    help="dropout shapes: re-hash the keep bits in backward instead of reading the forward's mask")
     a = ap.parse_args()
     ops.load_ext(required=True)
     shapes = [("llama3-8B", 4, 1024, 32, 8, 128, 0.0), ("llama3-8B-B24", 24, 1024, 32, 8, 128, 0.0),
@@ -48,11 +50,13 @@ def main():
             B, T = max(1, B * T // a.T), a.T
         qkv = torch.randn(B * T, (H + 2 * G) * hd, device="cuda", dtype=torch.bfloat16)
         do = torch.randn(B * T, H * hd, device="cuda", dtype=torch.bfloat16)
-        o, lse = ops.flash_attn_fwd(qkv, B, T, H, G, hd, causal, p, 1, 0)
-        tf = timeit(lambda: ops.flash_attn_fwd(qkv, B, T, H, G, hd, causal, p, 1, 0), a.iters)
-        tb = timeit(lambda: ops.flash_attn_bwd(qkv, o, lse, do, B, T, H, G, hd, causal, p, 1, 0), a.iters)
+        km = None if a.no_mask else ops.attn_keep_mask(qkv, B, T, H, hd, p)
+        o, lse = ops.flash_attn_fwd(qkv, B, T, H, G, hd, causal, p, 1, 0, keep_mask=km)
+        tf = timeit(lambda: ops.flash_attn_fwd(qkv, B, T, H, G, hd, causal, p, 1, 0, keep_mask=km), a.iters)
+        tb = timeit(lambda: ops.flash_attn_bwd(qkv, o, lse, do, B, T, H, G, hd, causal, p, 1, 0, keep_mask=km),
+                    a.iters)
         flop = 2 * 2 * B * H * T * T * hd / (2 if causal else 1)  # two matmuls (causal: half the square)
-        res.append(dict(shape=name, B=B, T=T, causal=causal, fwd_ms=round(tf, 4), bwd_ms=round(tb, 4),
+        res.append(dict(shape=name, B=B, T=T, causal=causal, keep_mask=km is not None, fwd_ms=round(tf, 4), bwd_ms=round(tb, 4),
                         fwd_tflops=round(flop / tf / 1e9, 1), bwd_tflops_5mm=round(2.5 * flop / tb / 1e9, 1)))
     for r in res:
         print(json.dumps(r))
