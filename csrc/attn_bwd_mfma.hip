@@ -23,6 +23,8 @@
 // reads (ds_read_b64_tr_b16).  Causal: only tiles at/below the diagonal; heaviest first.
 #include <float.h>
 #include <stdlib.h>
+#include <type_traits>
+
 #include "api.h"
 
 namespace bllm {
@@ -125,7 +127,13 @@ template <int HD, bool DUAL = false, bool MASK = false> constexpr int dkdv_buf_b
 // MASK (with DROP): the dropout keep bits come from the forward's keep mask -- one more 4-byte
 // DMA per wave and step brings the 32 words (queries of the step, this wave's 32 keys) into the
 // slot -- instead of one counter hash per (query, key) element.
-template <typename T, int HD, bool DROP, int NBUF, int OCC, bool FUSEG = false, bool DUAL = false, bool MASK = false>
+// VLDS: the V fragments (B operands of dP = dO V^T) live in LDS -- [32 keys][HD] per wave,
+// 16-B chunks XOR-swizzled by row (r_off) -- instead of 32 VGPRs for the whole kernel: at hd 128
+// K + V fragments (64) + dK/dV accumulators (128) + S/dP (32) leave too little of the 256 VGPRs
+// two waves per SIMD allow, and hipcc spilled the fragments to scratch, reloading them every
+// step behind an s_waitcnt vmcnt(0) that also drained the Q/dO DMA ring.
+template <typename T, int HD, bool DROP, int NBUF, int OCC, bool FUSEG = false, bool DUAL = false, bool MASK = false,
+          bool VLDS = false>
 __global__ __launch_bounds__(256, OCC) void attn_bwd_mfma_k(const T* __restrict__ qkv, const T* __restrict__ dout,
                                                             const float* __restrict__ lse,
                                                             const float* __restrict__ delta, T* __restrict__ dqkv,
@@ -165,19 +173,28 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_mfma_k(const T* __restrict_
   const float scale = rsqrtf((float)HD), c = scale * kLog2eB;
 
   // ---- K / V fragments of this wave's 32 keys (B operands, key = lane column)
-  v8 kf[KK], vf[KK];
+  constexpr int VOFF = NBUF * BUF;              // VLDS: per-wave V rows after the ring
+  v8 kf[KK], vf[VLDS ? 1 : KK];
   {
     const int kr = mykey < T_ ? mykey : T_ - 1;
 #pragma unroll
     for (int kk = 0; kk < KK; ++kk) {
       kf[kk] = *reinterpret_cast<const v8*>(kb_ + (long)kr * rs + kk * 16 + hh * 8);
-      vf[kk] = *reinterpret_cast<const v8*>(vb_ + (long)kr * rs + kk * 16 + hh * 8);
+      const v8 vv = *reinterpret_cast<const v8*>(vb_ + (long)kr * rs + kk * 16 + hh * 8);
+      if constexpr (VLDS)
+        *reinterpret_cast<v8*>(smem + VOFF + w * 32 * ROWB + r_off<HD>(l32, kk * 2 + hh)) = vv;
+      else
+        vf[kk] = vv;
     }
     // consume the fragments here: the compiler then retires these loads before the loop and
     // inserts no vmcnt waits inside it (it cannot see the asm-issued DMA, whose counts the
     // loop manages itself)
 #pragma unroll
-    for (int kk = 0; kk < KK; ++kk) asm volatile("" ::"v"(kf[kk]), "v"(vf[kk]));
+    for (int kk = 0; kk < KK; ++kk) asm volatile("" ::"v"(kf[kk]));
+    if constexpr (!VLDS) {
+#pragma unroll
+      for (int kk = 0; kk < KK; ++kk) asm volatile("" ::"v"(vf[kk]));
+    }
   }
   f32x16 dk[DT], dv[DT];
 #pragma unroll
@@ -315,15 +332,24 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_mfma_k(const T* __restrict_
       for (int kk = 0; kk < KK; ++kk) {
         const int ro = DUAL ? dual_off<HD>(l32_, kk * 2 + hh_) : r_off<HD>(l32_, kk * 2 + hh_);
         sacc = MFb<T>::mma(*reinterpret_cast<const v8*>(S + ro), kf[kk], sacc);
-        dpacc = MFb<T>::mma(*reinterpret_cast<const v8*>(S + IOR + ro), vf[kk], dpacc);
+        v8 vk;
+        if constexpr (VLDS) vk = *reinterpret_cast<const v8*>(smem + VOFF + w * 32 * ROWB + r_off<HD>(l32_, kk * 2 + hh_));
+        else vk = vf[kk];
+        dpacc = MFb<T>::mma(*reinterpret_cast<const v8*>(S + IOR + ro), vk, dpacc);
       }
-      // rows of this lane's accumulator registers: q = q0 + (r&3) + 8(r>>2) + 4hh
-      if (edge) {  // uniform branch: -inf the masked scores (causal diagonal, sequence tail)
+      // rows of this lane's accumulator registers: q = q0 + 4hh + off, off = (r&3) + 8(r>>2);
+      // visible iff lo <= off <= hi (causal: q >= key; q < T; key < T)
+      if (edge) {
+        // (the empty volatile asm keeps hipcc from if-converting this rare branch into
+        // per-step selects on every element)
+        asm volatile("" ::: "memory");
         const int qb0 = q0 + 4 * hh;
+        const int lo = causal ? mykey - qb0 : -(1 << 30);
+        const int hi = mykey < T_ ? T_ - 1 - qb0 : -(1 << 30);
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const int q = qb0 + (r & 3) + 8 * (r >> 2);
-          if ((causal && mykey > q) || q >= T_ || mykey >= T_) sacc[r] = -INFINITY;
+          const int off = (r & 3) + 8 * (r >> 2);
+          if (off < lo || off > hi) sacc[r] = -INFINITY;
         }
       }
       const float* LS = reinterpret_cast<const float*>(S + ISTAT + w * 256);
@@ -750,6 +776,13 @@ static int kv_dual_from_env() {
   const char* e = getenv("BLLM_ATTN_KV_DUAL");
   return e ? atoi(e) : -1;
 }
+// V fragments in LDS (VLDS kernels, with the dual images and a 2-slot ring).  Unset: on at
+// hd 128 (no spills; Llama-3-8B B=24 backward 1.158 -> 1.009 ms), off at hd 64 (no register
+// pressure there); BLLM_ATTN_KV_VLDS overrides.
+static int kv_vlds_from_env() {
+  const char* e = getenv("BLLM_ATTN_KV_VLDS");
+  return e ? atoi(e) : -1;
+}
 static int q_variant_from_env() {
   const char* e = getenv("BLLM_ATTN_Q_VARIANT");
   return e ? atoi(e) : 0;
@@ -784,24 +817,27 @@ static void launch_dq(const BwdArgs& a, bool drop, dim3 grid) {
   else if (drop) launch_dq1<TT, HDD, true, BK, NB, OC, false>(a, grid);
   else launch_dq1<TT, HDD, false, BK, NB, OC, false>(a, grid);
 }
-template <typename TT, int HDD, bool DROP, int NB, int OC, bool FG, bool DU, bool MASK>
+template <typename TT, int HDD, bool DROP, int NB, int OC, bool FG, bool DU, bool MASK, bool VL>
 static void launch_kv1(const BwdArgs& a, dim3 grid) {
-  constexpr int lds = NB * dkdv_buf_bytes<HDD, DU, MASK>();
-  hipLaunchKernelGGL((attn_bwd_mfma_k<TT, HDD, DROP, NB, OC, FG, DU, MASK>), grid, dim3(256), lds, a.s, (const TT*)a.qkv, (const TT*)a.dout, a.lse, a.delta,
+  constexpr int lds = NB * dkdv_buf_bytes<HDD, DU, MASK>() + (VL ? BWD_BKV * HDD * 2 : 0);
+  hipLaunchKernelGGL((attn_bwd_mfma_k<TT, HDD, DROP, NB, OC, FG, DU, MASK, VL>), grid, dim3(256), lds, a.s, (const TT*)a.qkv, (const TT*)a.dout, a.lse, a.delta,
                      (TT*)a.dqkv, a.dkv_part, a.T_, a.H, a.G, a.B, a.causal, a.thr, a.ik, a.seed, a.offset, a.kmask);
 }
-template <typename TT, int HDD, int NB, int OC, bool FG, bool DU>
+template <typename TT, int HDD, int NB, int OC, bool FG, bool DU, bool VL = false>
 static void launch_kv(const BwdArgs& a, bool drop, dim3 grid) {
-  if (drop && a.kmask) launch_kv1<TT, HDD, true, NB, OC, FG, DU, true>(a, grid);
-  else if (drop) launch_kv1<TT, HDD, true, NB, OC, FG, DU, false>(a, grid);
-  else launch_kv1<TT, HDD, false, NB, OC, FG, DU, false>(a, grid);
+  if (drop && a.kmask) launch_kv1<TT, HDD, true, NB, OC, FG, DU, true, VL>(a, grid);
+  else if (drop) launch_kv1<TT, HDD, true, NB, OC, FG, DU, false, VL>(a, grid);
+  else launch_kv1<TT, HDD, false, NB, OC, FG, DU, false, VL>(a, grid);
 }
 template <typename TT, int HDD>
 static void launch_bwd(const BwdArgs& a, bool drop, int q_variant, int kv_variant, bool fuseg, bool kv_dual,
-                       dim3 grid_q, dim3 grid_kv) {
+                       bool kv_vlds, dim3 grid_q, dim3 grid_kv) {
   if (q_variant == 0) launch_dq<TT, HDD, 32, 3, 2>(a, drop, grid_q);
   else launch_dq<TT, HDD, 64, 3, 1>(a, drop, grid_q);
-  if (fuseg && kv_dual) launch_kv<TT, HDD, 4, 2, true, true>(a, drop, grid_kv);
+  if (kv_vlds && kv_dual) {  // dual images, 2-slot ring, V fragments in LDS
+    if (fuseg) launch_kv<TT, HDD, 2, 2, true, true, true>(a, drop, grid_kv);
+    else launch_kv<TT, HDD, 2, 2, false, true, true>(a, drop, grid_kv);
+  } else if (fuseg && kv_dual) launch_kv<TT, HDD, 4, 2, true, true>(a, drop, grid_kv);
   else if (kv_dual && kv_variant != 1) launch_kv<TT, HDD, 4, 2, false, true>(a, drop, grid_kv);
   else if (fuseg) launch_kv<TT, HDD, 2, 2, true, false>(a, drop, grid_kv);
   else if (kv_variant != 1) launch_kv<TT, HDD, 2, 2, false, false>(a, drop, grid_kv);
@@ -816,6 +852,8 @@ void attn_bwd_mfma(DType dt, const void* qkv, const void* o, const float* lse, c
   static const int q_variant = q_variant_from_env();
   static const int kv_dual_env = kv_dual_from_env();
   const bool kv_dual = kv_dual_env >= 0 ? kv_dual_env != 0 : hd == 128;
+  static const int kv_vlds_env = kv_vlds_from_env();
+  const bool kv_vlds = kv_vlds_env >= 0 ? kv_vlds_env > 0 : hd == 128;
   const int nkb = (T_ + BWD_BKV - 1) / BWD_BKV;
   // kv variant 2 (GQA, large grids): the dK/dV workgroup sweeps the H/G heads of its kv head
   const bool fuseg = fuse_gqa_heads(B, T_, H, G);
@@ -824,11 +862,11 @@ void attn_bwd_mfma(DType dt, const void* qkv, const void* o, const float* lse, c
   const BwdArgs a{qkv, o, dout, lse, delta, dkv_part, dqkv, T_, H, G, B, causal, drop_threshold16(p),
                   drop_inv_keep(p), seed, offset, drop ? keep_mask : nullptr, s};
   if (dt == DType::BF16) {
-    if (hd == 128) launch_bwd<bf16_t, 128>(a, drop, q_variant, kv_variant, fuseg, kv_dual, grid_q, grid_kv);
-    else launch_bwd<bf16_t, 64>(a, drop, q_variant, kv_variant, fuseg, kv_dual, grid_q, grid_kv);
+    if (hd == 128) launch_bwd<bf16_t, 128>(a, drop, q_variant, kv_variant, fuseg, kv_dual, kv_vlds, grid_q, grid_kv);
+    else launch_bwd<bf16_t, 64>(a, drop, q_variant, kv_variant, fuseg, kv_dual, kv_vlds, grid_q, grid_kv);
   } else {
-    if (hd == 128) launch_bwd<f16_t, 128>(a, drop, q_variant, kv_variant, fuseg, kv_dual, grid_q, grid_kv);
-    else launch_bwd<f16_t, 64>(a, drop, q_variant, kv_variant, fuseg, kv_dual, grid_q, grid_kv);
+    if (hd == 128) launch_bwd<f16_t, 128>(a, drop, q_variant, kv_variant, fuseg, kv_dual, kv_vlds, grid_q, grid_kv);
+    else launch_bwd<f16_t, 64>(a, drop, q_variant, kv_variant, fuseg, kv_dual, kv_vlds, grid_q, grid_kv);
   }
   if (H != G && !fuseg) {
     const long BT = (long)B * T_;
