@@ -147,20 +147,19 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd_mfma_k(const T* __restrict_
   int voff[DT];
 #pragma unroll
   for (int dt = 0; dt < DT; ++dt) voff[dt] = v_off<HD>(4 * hh + qrow, dt * 32 + gl * 16 + pcol * 4);
-  uint32_t kgo[LD], vgo[LD];
-  int prow[LD], pkc[LD], pvc[LD];
-#pragma unroll
-  for (int i = 0; i < LD; ++i) {
-    const int P = (w * LD + i) * 64 + lane;
-    const int r = P / CH, pc = P % CH;
-    int kc16;
+  // DMA piece i of this lane: row P / CH, physical 16-B chunk P % CH (P = (w LD + i) 64 + lane);
+  // the source chunk carries the image's XOR swizzle.  Recomputed at every issue from an opaque
+  // copy of the lane id (a few full-rate VALU): kept in VGPRs across the loop they were spilled
+  // at hd 128, and each scratch reload's vmcnt(0) serialised the DMA pieces.
+  const uint32_t rs2 = (uint32_t)rs * 2u;  // row stride in bytes (< 2^24 for every shape)
+  auto piece = [&](int i, int ln, int& r, int& kc16, int& vc16) {
+    const int P = (w * LD + i) * 64 + ln;
+    r = P / CH;
+    const int pc = P % CH;
     if constexpr (HD == 128) kc16 = pc ^ (r & 15); else kc16 = pc ^ ((r >> 1) & 7);
     const int c64 = (pc >> 2) ^ (HD == 128 ? (r & 3) : ((r >> 1) & 1));
-    const int vc16 = c64 * 4 + (pc & 3);
-    prow[i] = r; pkc[i] = kc16; pvc[i] = vc16;
-    kgo[i] = (uint32_t)(r * rs * 2 + kc16 * 16);
-    vgo[i] = (uint32_t)(r * rs * 2 + vc16 * 16);
-  }
+    vc16 = c64 * 4 + (pc & 3);
+  };
   const uint32_t smem_u = lds_u32(smem);
 
   const int kend = causal ? min(T_, q0 + FWD_BQ) : T_;
@@ -173,27 +172,33 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd_mfma_k(const T* __restrict_
   auto issue = [&](int t, int buf) {
     const int k0 = t * FWD_BK;
     const uint32_t base = smem_u + buf * 2 * TILE_B;
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
     if (k0 + FWD_BK <= T_) {
       const void* ks = sgpr_ptr(kbase + (long)k0 * rs);
       const void* vs = sgpr_ptr(vbase + (long)k0 * rs);
 #pragma unroll
       for (int i = 0; i < LD; ++i) {
+        int r, kc16, vc16;
+        piece(i, ln, r, kc16, vc16);
+        const uint32_t ro = __umul24((uint32_t)r, rs2);
         const uint32_t pd = (w * LD + i) * 1024;
-        glds16s(ks, kgo[i], base + pd);
-        glds16s(vs, vgo[i], base + TILE_B + pd);
+        glds16s(ks, ro + kc16 * 16, base + pd);
+        glds16s(vs, ro + vc16 * 16, base + TILE_B + pd);
       }
     } else {  // sequence tail: clamp rows (masked / multiplied by P = 0 later)
       char* kb = smem + buf * 2 * TILE_B;
 #pragma unroll
       for (int i = 0; i < LD; ++i) {
+        int r, kc16, vc16;
+        piece(i, ln, r, kc16, vc16);
         const int pd = (w * LD + i) * 1024;
-        const int key = min(k0 + prow[i], T_ - 1);
-        glds16(kbase + (long)key * rs + pkc[i] * 8, kb + pd);
-        glds16(vbase + (long)key * rs + pvc[i] * 8, kb + TILE_B + pd);
+        const int key = min(k0 + r, T_ - 1);
+        glds16(kbase + (long)key * rs + kc16 * 8, kb + pd);
+        glds16(vbase + (long)key * rs + vc16 * 8, kb + TILE_B + pd);
       }
     }
   };
-
   auto ring_wait = [&](int t) {
     if constexpr (NBUF == 3) {
       if (t + 2 < ntiles) wait_vm<NPW>(); else wait_vm0();
@@ -348,23 +353,31 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd_mfma_k(const T* __restrict_
   using IcN = std::integral_constant<int, NKT>;
   using Yes = std::true_type;
   using No = std::false_type;
-  for (; t < nact; ++t) {
+  // Interior tiles (no masked key: below the causal diagonal, inside the sequence) form a
+  // prefix of the wave's tiles; they run in a loop of their own with the one unmasked body, so
+  // the O accumulators never meet the edge variants' registers on the hot path (a shared loop
+  // made hipcc copy them between variants every tile).
+  const int n_int = wq_hi >= T_ ? 0 : min(min(nact, T_ / FWD_BK), causal ? (wq_lo + 1) / FWD_BK : nact);
+  for (; t < n_int; ++t) {
     flush_mask();  // keep bits of tile t - 1
+    if (t + NBUF - 1 < ntiles) issue(t + NBUF - 1, buf == 0 ? NBUF - 1 : buf - 1);
+    kw_t = t;
+    const char* kb = smem + buf * 2 * TILE_B;
+    body(IcN{}, No{}, t * FWD_BK, kb, kb + TILE_B);
+    ring_wait(t);  // the DMA of tile t+1 has landed (asm-issued, so drained by hand)
+    buf = buf == NBUF - 1 ? 0 : buf + 1;
+  }
+  // causal diagonal / sequence tail tiles
+  for (; t < nact; ++t) {
+    flush_mask();
     if (t + NBUF - 1 < ntiles) issue(t + NBUF - 1, buf == 0 ? NBUF - 1 : buf - 1);
     const int k0 = t * FWD_BK;
     kw_t = t;
     const char* kb = smem + buf * 2 * TILE_B;
-    const char* vb = kb + TILE_B;
-    // wave-uniform: causal diagonal / sequence tail tiles need masking
-    const bool edge = (causal && k0 + FWD_BK - 1 > wq_lo) || k0 + FWD_BK > T_ || wq_hi >= T_;
-    if (!edge) {
-      body(IcN{}, No{}, k0, kb, vb);
-    } else {
-      const int kvis = min(causal ? wq_hi : T_ - 1, T_ - 1) - k0;  // >= 0 for an active tile
-      if (NKT == 1 || kvis >= 32) body(IcN{}, Yes{}, k0, kb, vb);
-      else body(Ic1{}, Yes{}, k0, kb, vb);
-    }
-    ring_wait(t);  // the DMA of tile t+1 has landed (asm-issued, so drained by hand)
+    const int kvis = min(causal ? wq_hi : T_ - 1, T_ - 1) - k0;  // >= 0 for an active tile
+    if (NKT == 1 || kvis >= 32) body(IcN{}, Yes{}, k0, kb, kb + TILE_B);
+    else body(Ic1{}, Yes{}, k0, kb, kb + TILE_B);
+    ring_wait(t);
     buf = buf == NBUF - 1 ? 0 : buf + 1;
   }
   flush_mask();
