@@ -94,6 +94,8 @@ def build_parser() -> argparse.ArgumentParser:
     x.add_argument("--device", choices=["auto", "cpu", "cuda"], default="auto")
     x.add_argument("--synthetic_data", action="store_true",
                    help="generate Gutenberg-/Alpaca-shaped data into --data_dir if it is empty")
+    x.add_argument("--synthetic_mb", type=float, default=0.5,
+                   help="size of the generated Gutenberg-shaped corpus (MB of text)")
     x.add_argument("--sample_tokens", type=int, default=200)
     x.add_argument("--resume", type=str, default=None,
                    help="model_pg_*.pth to resume from (+ its .state.pt written by --save_resume_state)")
@@ -153,7 +155,7 @@ def _prepare_data(args, cfg, rank):
         if args.finetune:
             make_alpaca_json(os.path.join(args.data_dir, "instruction-data-alpaca.json"), 1000)
         else:
-            make_gutenberg_corpus(args.data_dir, n_files=1, mb_per_file=0.5)
+            make_gutenberg_corpus(args.data_dir, n_files=1, mb_per_file=getattr(args, "synthetic_mb", 0.5))
     return files
 
 
