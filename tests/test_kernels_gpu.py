@@ -293,6 +293,13 @@ def test_flash_attention_gqa_fused_heads(p, hd):
     test_flash_attention(torch.bfloat16, 128, 128, 16, 8, hd, p, True)
 
 
+@pytest.mark.parametrize("hd", [64, 128])
+def test_flash_attention_keep_mask_fused_gqa(hd):
+    """The keep-mask path of the fused-GQA-heads dK/dV kernel (the workgroup sweeps its kv
+    head's query heads, each with its own mask rows)."""
+    test_flash_attention_keep_mask(hd, 128, 128, 16, 8, True)
+
+
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("B,H,G,hd,L,Tmax", [(2, 8, 2, 128, 37, 64), (1, 4, 4, 64, 1, 16), (3, 32, 8, 128, 1000, 1024)])
 def test_attn_decode(dt, B, H, G, hd, L, Tmax):
