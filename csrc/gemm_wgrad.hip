@@ -39,6 +39,8 @@
 //   1  next slot's fragments read under the current slot's MFMAs
 //   2  as 1, LDS-DMA issued by waves 0-3 only (see Geo::LOADERS) — default: 1.02-1.13x variant 1
 //      (Llama-3-8B gate/up 1.33 -> 1.40 PF, LM head 1.18 -> 1.34 PF)
+//   3  as 2 on v_mfma_f32_32x32x16 (acc[4][2] of 32 x 32, own LDS swizzle) — correct, but 3-10 %
+//      slower than 2 on every benchmark shape (profiles/r2_kernel_experiments.md); kept for A/B
 // Measured and dropped (tools/bench_wgrad.py, profiles/r1_wgrad_kernel.md): 4 waves of 128 x 128
 // (one wave per SIMD) -25 %; LDS-DMA pieces interleaved between MFMA groups instead of one burst
 // after the barrier -5 %.
@@ -54,6 +56,7 @@ namespace {
 typedef short s16x8 __attribute__((ext_vector_type(8)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
@@ -64,10 +67,18 @@ template <> struct Mfma<bf16_t> {
     return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c,
                                                    0, 0, 0);
   }
+  static __device__ __forceinline__ f32x16 run(s16x8 a, s16x8 b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c,
+                                                   0, 0, 0);
+  }
 };
 template <> struct Mfma<f16_t> {
   static __device__ __forceinline__ f32x4 run(s16x8 a, s16x8 b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c,
+                                                  0, 0, 0);
+  }
+  static __device__ __forceinline__ f32x16 run(s16x8 a, s16x8 b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c,
                                                   0, 0, 0);
   }
 };
@@ -90,13 +101,19 @@ template <int VAR> struct Geo {
   // Variant 2: only waves 0-3 (one per SIMD) issue the slot's LDS-DMA, so each SIMD's other
   // wave (4-7) goes straight from the barrier to its MFMAs and keeps the matrix pipe busy while
   // its partner spends ~60 issue cycles per piece; variants 0/1 split the pieces over all 8.
-  static constexpr int LOADERS = VAR == 2 ? 4 : 8;
+  static constexpr int LOADERS = VAR >= 2 ? 4 : 8;
   static constexpr int DJ = (SLOTB / 1024) / LOADERS;  // LDS-DMA pieces per operand per slot per loader
   static constexpr int PER_STAGE = 2 * DJ;             // vmcnt units one staged slot adds (loaders)
   static constexpr bool PREFETCH = VAR >= 1;           // next slot's fragments under this slot's MFMAs
+  // Variant 3: v_mfma_f32_32x32x16 (acc[4][2] of 32 x 32) — half the MFMA instructions and half
+  // the operand-register reads per FLOP of 16x16x32; same fragment count per k-step.
+  static constexpr bool M32 = VAR == 3;
 };
 
 __device__ __forceinline__ int swz(int r) { return 2 * ((r & 3) | (((r >> 3) & 1) << 2)); }
+// 32x32 fragments: a 32-lane half reads 4 k-rows x 64 B (two 16-column blocks), so XOR the
+// 4-chunk block index by (r & 3) — the 4 rows land on 4 distinct 64-B bank groups
+__device__ __forceinline__ int swz32(int r) { return 4 * (r & 3); }
 
 __device__ __forceinline__ s16x8 frag(const char* p) {
   const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p));
@@ -145,7 +162,7 @@ __global__ __launch_bounds__(Geo<VAR>::THREADS) void wgrad_gemm_k(const T* __res
   uint32_t voffA[DJ], voffB[DJ];
 #pragma unroll
   for (int j = 0; j < DJ; ++j) {
-    const int r = (wave * DJ + j) * 2 + (lane >> 5), c = (lane & 31) ^ swz(r);
+    const int r = (wave * DJ + j) * 2 + (lane >> 5), c = (lane & 31) ^ (G::M32 ? swz32(r) : swz(r));
     voffB[j] = (uint32_t)((r * ldb + 8 * c) * (long)sizeof(T));
     if constexpr (AK) {  // piece = 16 m-rows x 64 B; lane -> row l/4, physical chunk l%4
       const int ra = (wave * DJ + j) * 16 + (lane >> 2), ca = (lane & 3) ^ fA((ra >> 2) & 3);
@@ -181,6 +198,13 @@ __global__ __launch_bounds__(Geo<VAR>::THREADS) void wgrad_gemm_k(const T* __res
   for (int i = 0; i < 8; ++i)
     aoff[i] = AK ? (wm * 128 + 16 * i + (lane & 15)) * 64 + (((lane >> 4) ^ fA((lane & 15) >> 2)) << 4)
                  : rowb + (wm * 16 + ((2 * i) ^ f)) * 16;
+  if constexpr (G::M32) {
+    // lane (g, q, p): k-rows 8(g>>1) + q (+4) of k-half i>>2, columns 16(g&1) + 4p.. of 32-wide
+    // m tile i&3 (a[i]) / n tile j&1 of k-half j>>1 (b[j]) — the 32x32x16 operand layout
+    const int rb32 = (8 * (g >> 1) + qq) * ROWB + (p & 1) * 8 + (p >> 1) * 16 + 2 * (g & 1) * 16;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) aoff[i] = rb32 + (i >> 2) * 16 * ROWB + (wm * 16 + 4 * ((i & 3) ^ qq)) * 16;
+  }
   // A fragment: 8 k-values of one m row (row read) or of one m column (two transposed reads)
   auto fragA = [&](const char* p) -> s16x8 {
     if constexpr (AK) return *(const __attribute__((address_space(3))) s16x8*)(p);
@@ -188,12 +212,19 @@ __global__ __launch_bounds__(Geo<VAR>::THREADS) void wgrad_gemm_k(const T* __res
   };
 #pragma unroll
   for (int j = 0; j < FN; ++j) boff[j] = B_BASE + rowb + ((wn * 2 * FN + 2 * j) ^ f) * 16;
+  if constexpr (G::M32) {
+    const int rb32 = (8 * (g >> 1) + qq) * ROWB + (p & 1) * 8 + (p >> 1) * 16 + 2 * (g & 1) * 16;
+#pragma unroll
+    for (int j = 0; j < FN; ++j) boff[j] = B_BASE + rb32 + (j >> 1) * 16 * ROWB + ((wn * 8 + 4 * (j & 1)) ^ (4 * qq)) * 16;
+  }
 
-  f32x4 acc[8][FN];
+  using Acc = std::conditional_t<G::M32, f32x16, f32x4>;
+  constexpr int AI = G::M32 ? 4 : 8, AJ = G::M32 ? 2 : FN;
+  Acc acc[AI][AJ];
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+  for (int i = 0; i < AI; ++i)
 #pragma unroll
-    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < AJ; ++j) acc[i][j] = Acc{};
 
   if constexpr (G::PREFETCH) {
     // Fragments of slot kt+1 are read into the second register set WHILE slot kt's MFMAs
@@ -227,8 +258,13 @@ __global__ __launch_bounds__(Geo<VAR>::THREADS) void wgrad_gemm_k(const T* __res
       for (int i = 0; i < 8; ++i) {
         if constexpr (!LAST) Gn.a[i] = fragA(nxt + aoff[i]);
         __builtin_amdgcn_s_setprio(1);
+        if constexpr (G::M32) {
 #pragma unroll
-        for (int j = 0; j < FN; ++j) acc[i][j] = Mfma<T>::run(F.a[i], F.b[j], acc[i][j]);
+          for (int j = 0; j < 2; ++j) acc[i & 3][j] = Mfma<T>::run(F.a[i], F.b[(i >> 2) * 2 + j], acc[i & 3][j]);
+        } else {
+#pragma unroll
+          for (int j = 0; j < FN; ++j) acc[i][j] = Mfma<T>::run(F.a[i], F.b[j], acc[i][j]);
+        }
         __builtin_amdgcn_s_setprio(0);
       }
     };
@@ -257,7 +293,7 @@ __global__ __launch_bounds__(Geo<VAR>::THREADS) void wgrad_gemm_k(const T* __res
     it(W1{}, Nn{}, Nn{}, kt + 1, F1, F0);
     it(W0{}, Nn{}, Nn{}, kt + 2, F0, F1);
     it(W0{}, Nn{}, Y{}, kt + 3, F1, F0);
-  } else {
+  } else if constexpr (!G::M32) {
   stage(0, 0);
   stage(1, 1);
   stage(2, 2);
@@ -311,15 +347,27 @@ __global__ __launch_bounds__(Geo<VAR>::THREADS) void wgrad_gemm_k(const T* __res
 #pragma unroll
     for (int pass = 0; pass < 2; ++pass) {
       if (wm == pass) {
+        if constexpr (G::M32) {  // 32x32 layout: row 8(e>>2) + 4(l>>5) + (e&3), column l&31
 #pragma unroll
-        for (int i = 0; i < 8; ++i)
+          for (int i = 0; i < 4; ++i)
 #pragma unroll
-          for (int e = 0; e < 4; ++e)
+            for (int e = 0; e < 16; ++e)
 #pragma unroll
-            for (int j = 0; j < FN; ++j) {
-              const int lr = 16 * i + 4 * (lane >> 4) + e, col = wn * 16 * FN + 16 * j + (lane & 15);
-              *(float*)(smem + lr * RB + ((((col >> 2) ^ (lr & 7)) << 4) | ((col & 3) << 2))) = acc[i][j][e];
-            }
+              for (int j = 0; j < 2; ++j) {
+                const int lr = 32 * i + 8 * (e >> 2) + 4 * (lane >> 5) + (e & 3), col = wn * 64 + 32 * j + (lane & 31);
+                *(float*)(smem + lr * RB + ((((col >> 2) ^ (lr & 7)) << 4) | ((col & 3) << 2))) = acc[i][j][e];
+              }
+        } else {
+#pragma unroll
+          for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+#pragma unroll
+              for (int j = 0; j < FN; ++j) {
+                const int lr = 16 * i + 4 * (lane >> 4) + e, col = wn * 16 * FN + 16 * j + (lane & 15);
+                *(float*)(smem + lr * RB + ((((col >> 2) ^ (lr & 7)) << 4) | ((col & 3) << 2))) = acc[i][j][e];
+              }
+        }
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
@@ -356,6 +404,19 @@ __global__ __launch_bounds__(Geo<VAR>::THREADS) void wgrad_gemm_k(const T* __res
   }
   // (unaligned output: element stores; the accumulate test is hoisted out of the element loops —
   //  a per-element select makes hipcc branch around every load and wait for each separately)
+  if constexpr (G::M32) {
+    OT* c = cbase + (wm * 128 + 4 * (lane >> 5)) * ldc + wn * 64 + (lane & 31);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int e = 0; e < 16; ++e)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          OT* o = c + (long)(32 * i + 8 * (e >> 2) + (e & 3)) * ldc + 32 * j;
+          *o = from_f<OT>((accumulate ? to_f(*o) : 0.f) + acc[i][j][e]);
+        }
+    return;
+  } else {
   OT* c = cbase + (wm * 128 + 4 * (lane >> 4)) * ldc + wn * 16 * FN + (lane & 15);
   if (accumulate) {
 #pragma unroll
@@ -374,6 +435,7 @@ __global__ __launch_bounds__(Geo<VAR>::THREADS) void wgrad_gemm_k(const T* __res
       for (int e = 0; e < 4; ++e)
 #pragma unroll
         for (int j = 0; j < FN; ++j) c[(long)(16 * i + e) * ldc + 16 * j] = from_f<OT>(acc[i][j][e]);
+  }
   }
 }
 
@@ -403,6 +465,7 @@ void launch(const void* a, long lda, const void* b, long ldb, void* c, long ldc,
   switch (variant()) {
     case 0: launch_v<T, OT, 0>(a, lda, b, ldb, c, ldc, c_split, M, N, K, S, accumulate, s); break;
     case 2: launch_v<T, OT, 2>(a, lda, b, ldb, c, ldc, c_split, M, N, K, S, accumulate, s); break;
+    case 3: launch_v<T, OT, 3>(a, lda, b, ldb, c, ldc, c_split, M, N, K, S, accumulate, s); break;
     default: launch_v<T, OT, 1>(a, lda, b, ldb, c, ldc, c_split, M, N, K, S, accumulate, s); break;
   }
 }
