@@ -99,6 +99,9 @@ def parse(argv=None):
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
                     help="cpu: tiny config on gloo (distributed plumbing check, not a measurement)")
     ap.add_argument("--pg_timeout_min", type=float, default=20.0)
+    ap.add_argument("--force_comm", action="store_true",
+                    help="world 1: run the engines' N>1 collective path (RCCL copies) instead of the "
+                         "world-1 shortcut (BLLM_FORCE_COMM=1) — a one-GPU rehearsal of the multi-GPU path")
     ap.add_argument("--tunableop", default=None,
                     help="PyTorch TunableOp results CSV (every hipBLASLt + rocBLAS solution timed per GEMM "
                          "shape), e.g. configs/tunableop_llama3_8b_b40_mi355x.csv: +0.6 %% on the headline "
@@ -201,6 +204,8 @@ def main(argv=None):
     from building_llm_from_scratch_amd.parallel.mixed_precision import get_policy
     from building_llm_from_scratch_amd.train.optim import FusedAdamW
 
+    if a.force_comm:
+        os.environ["BLLM_FORCE_COMM"] = "1"
     dist, dev, world, rank = init_dist(a)
     cuda = dev.type == "cuda"
     if cuda:
@@ -316,7 +321,8 @@ def main(argv=None):
                 "seq_len": T if a.data != "alpaca" else f"variable (mean {T_eff:.0f}, max {cfg.context_length})",
                 "parallelism": f"{a.parallel}{world}",
                 "engine": type(engine).__name__ + (" (world 1: no-shard)" if getattr(engine, "no_shard", False)
-                                                   else ""),
+                                                   else (" (world 1: forced collective path)"
+                                                         if world == 1 and a.force_comm else "")),
                 "actv_ckpt": a.actv_ckpt,
                 "ckpt_blocks": f"{n_ckpt}/{cfg.n_layers} recomputed"
                 + (f" (checkpoint_sequential segments={a.ckpt_segments})" if a.ckpt_segments

@@ -11,6 +11,8 @@
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from ..models.base import LocalEngine
@@ -27,6 +29,14 @@ def nccl_pg_options():
         return opts
     except (AttributeError, RuntimeError):  # torch built without NCCL/RCCL
         return None
+
+
+def force_comm() -> bool:
+    """``BLLM_FORCE_COMM=1``: engines run their collective path even at world size 1 (every
+    all-gather / reduce-scatter / all-reduce issued on RCCL's stream, shards freed and re-gathered)
+    instead of the world-1 shortcut — the N>1 code path rehearsed on a single GPU, where RCCL
+    cannot put two ranks (tests/test_engines_gpu.py, bench.py --force_comm)."""
+    return os.environ.get("BLLM_FORCE_COMM", "0") not in ("", "0")
 
 
 def setup_engine(model, kind: str = "local", device=None, reduce_dtype=None, bucket_mb: float = 256.0,

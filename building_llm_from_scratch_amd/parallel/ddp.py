@@ -33,7 +33,8 @@ class DDPEngine(LocalEngine):
         self.arena = Arena(model, device, dtype, self.world_size, bucket_mb * 2 ** 20)
         self.reduce_dtype = reduce_dtype if reduce_dtype not in (None, dtype) else None
         # a single rank has nothing to average with: no broadcast, no all-reduce (same hooks)
-        self.no_comm = self.world_size == 1
+        from . import force_comm
+        self.no_comm = self.world_size == 1 and not force_comm()
         if broadcast and not self.no_comm:
             self._broadcast_params()
         self.grad_prescale = 1.0 / self.world_size

@@ -24,7 +24,8 @@ bf16 collectives — reference datautils/mixed_precision.py:24-28); master weigh
 World size 1: like torch FSDP, which clamps FULL_SHARD to NO_SHARD when there is a single
 rank (torch/distributed/fsdp/_init_utils.py:426-437), the shard IS the full flat: nothing is
 freed, gathered or reduce-scattered (a world-1 collective is a device copy of every unit per
-pass).  It is the same engine class, hooks and optimizer slots as at N>1.
+pass).  It is the same engine class, hooks and optimizer slots as at N>1.  ``BLLM_FORCE_COMM=1`` keeps
+the sharded path at world 1 (RCCL copies) to rehearse it on one GPU.
 """
 from __future__ import annotations
 
@@ -66,7 +67,8 @@ class FSDPEngine(LocalEngine):
         self.prefetch = max(1, int(prefetch))
         self.grad_prescale = 1.0 / self.world_size
         self.is_cuda = self.device.type == "cuda"
-        self.no_shard = self.world_size == 1
+        from . import force_comm
+        self.no_shard = self.world_size == 1 and not force_comm()
         dtype = next(model.parameters()).dtype
         self.reduce_dtype = reduce_dtype if reduce_dtype not in (None, dtype) else None
         model.flatten(device=device, dtype=dtype, pad_to=self.world_size * ALIGN)

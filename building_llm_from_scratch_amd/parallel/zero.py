@@ -33,7 +33,8 @@ class ZeroEngine(LocalEngine):
         dtype = next(model.parameters()).dtype
         self.reduce_dtype = reduce_dtype if reduce_dtype not in (None, dtype) else None
         self.arena = Arena(model, device, dtype, self.world_size, bucket_mb * 2 ** 20)
-        self.no_comm = self.world_size == 1      # one rank: its shard is the whole bucket
+        from . import force_comm
+        self.no_comm = self.world_size == 1 and not force_comm()  # one rank: its shard is the whole bucket
         if not self.no_comm:
             dist.broadcast(self.arena.param, src=0, group=pg)
             for u in model.units:

@@ -208,3 +208,12 @@ def test_fsdp_full_ckpt_and_zero2_mode():
         sd = torch.load(out, weights_only=True)["sd"]
     for k in ref_sd:
         assert torch.allclose(sd[k].float(), ref_sd[k].float(), atol=1e-4, rtol=1e-4), k
+
+
+@pytest.mark.parametrize("kind", ["ddp", "zero1", "fsdp"])
+def test_world1_forced_comm_path(kind, monkeypatch):
+    """BLLM_FORCE_COMM=1: the world-1 engines take their N>1 collective path (shards freed and
+    re-gathered, reduce-scatter into grad shards) and still match single-process training."""
+    monkeypatch.setenv("BLLM_FORCE_COMM", "1")
+    ref_sd, ref_losses = _reference("llama", False)
+    _check(_spawn(1, kind, "llama", False, ckpt="full"), ref_sd, ref_losses)
