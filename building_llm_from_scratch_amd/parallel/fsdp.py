@@ -161,9 +161,8 @@ class FSDPEngine(LocalEngine):
     def post_forward(self, unit):
         last = unit.index == len(self.units) - 1
         training = torch.is_grad_enabled() and self.model.training
-        if not training:
-            if not last or True:
-                self._reshard(unit)
+        if not training:  # eval / sampling: nothing is kept for a backward
+            self._reshard(unit)
             return
         if self.reshard_after_forward and not last:
             self._reshard(unit)

@@ -770,8 +770,8 @@ static bool fuse_gqa_heads(int B, int T_, int H, int G) {
 // dQ variant: 0 = 32-key tiles, 3-slot ring, 2 workgroups per CU; 1 = 64-key tiles, 1 per CU
 // dK/dV staging: 1 = one dual-use LDS image per Q / dO tile and a 4-slot ring (DUAL kernels),
 // 0 = separate row and transposed images, 2-slot ring.  Unset: dual at hd 128 (Llama-3-8B
-// B=24 backward 1.143 -> 1.100 ms), separate images at hd 64 (Llama-3.2-1B 0.548 vs 0.568 ms);
-// BLLM_ATTN_KV_DUAL overrides.
+// B=24 backward 1.143 -> 1.100 ms) and at hd 64 with a dropout keep mask, else separate images
+// (Llama-3.2-1B 0.548 vs 0.568 ms); BLLM_ATTN_KV_DUAL overrides.
 static int kv_dual_from_env() {
   const char* e = getenv("BLLM_ATTN_KV_DUAL");
   return e ? atoi(e) : -1;
@@ -850,13 +850,17 @@ void attn_bwd_mfma(DType dt, const void* qkv, const void* o, const float* lse, c
   (void)dq_acc;
   static const int kv_variant = kv_variant_from_env();
   static const int q_variant = q_variant_from_env();
-  static const int kv_dual_env = kv_dual_from_env();
-  const bool kv_dual = kv_dual_env >= 0 ? kv_dual_env != 0 : hd == 128;
-  static const int kv_vlds_env = kv_vlds_from_env();
-  const bool kv_vlds = kv_vlds_env >= 0 ? kv_vlds_env > 0 : hd == 128;
   const int nkb = (T_ + BWD_BKV - 1) / BWD_BKV;
   // kv variant 2 (GQA, large grids): the dK/dV workgroup sweeps the H/G heads of its kv head
   const bool fuseg = fuse_gqa_heads(B, T_, H, G);
+  // dual images: hd 128, and hd 64 with the forward's keep mask (GPT-2 774M B=24 dK/dV+dQ
+  // 0.430 -> 0.420 ms; without dropout or with fused GQA heads they lose: 0.367 -> 0.376,
+  // Llama-3.2-1B 0.575 -> 0.602 ms — profiles/r2_attn_hd64_dual.md)
+  static const int kv_dual_env = kv_dual_from_env();
+  const bool kv_dual = kv_dual_env >= 0 ? kv_dual_env != 0
+                                        : (hd == 128 || (p > 0.f && keep_mask != nullptr && !fuseg));
+  static const int kv_vlds_env = kv_vlds_from_env();
+  const bool kv_vlds = kv_vlds_env >= 0 ? kv_vlds_env > 0 : hd == 128;
   dim3 grid_kv(nkb * (fuseg ? G : H) * B), grid_q(((T_ + DQ_BQ - 1) / DQ_BQ) * H * B);
   const bool drop = p > 0.f;
   const BwdArgs a{qkv, o, dout, lse, delta, dkv_part, dqkv, T_, H, G, B, causal, drop_threshold16(p),
