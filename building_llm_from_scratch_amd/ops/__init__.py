@@ -26,7 +26,7 @@ __all__ = [
     "sq_norm_multi", "adamw_step_", "attn_decode", "bias_grad_", "ext_available", "load_ext", "attention_backend",
     "lora_down", "lora_up_", "lora_wgrad", "lora_pack_t", "lora_kernel_ok", "sum_partials_",
     "wgrad_gemm_", "wgrad_gemm_ok", "wgrad_gemm_enabled", "wgrad_gemm_preferred", "wgrad_splits",
-    "gemm_nn_", "gemm_nn_ok", "dgrad_gemm_enabled", "transpose2d", "dgrad_wt_enabled", "attn_keep_mask",
+    "gemm_nn_", "gemm_nt_", "gemm_nn_ok", "dgrad_gemm_enabled", "transpose2d", "dgrad_wt_enabled", "attn_keep_mask",
 ]
 
 rope_tables = ref.rope_tables
@@ -310,6 +310,19 @@ def gemm_nn_(a, b, c, accumulate: bool = False):
         _k().gemm_nn_(a, b, c, bool(accumulate))
         return c
     r = a.float() @ b.float()
+    if accumulate:
+        r += c.float()
+    c.copy_(r)
+    return c
+
+
+def gemm_nt_(a, b, c, accumulate: bool = False):
+    """c (+)= a @ b^T with a [M, K], b [N, K] (both K-contiguous, a Linear's forward y = x W^T),
+    fp32 accumulation on the MFMA kernel of csrc/gemm_wgrad.hip (shape rules of gemm_nn_ok)."""
+    if _hip(a):
+        _k().gemm_nt_(a, b, c, bool(accumulate))
+        return c
+    r = a.float() @ b.float().t()
     if accumulate:
         r += c.float()
     c.copy_(r)

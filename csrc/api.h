@@ -155,6 +155,10 @@ void wgrad_gemm(DType dt, DType odt, const void* a, long lda, const void* b, lon
 bool gemm_nn_supported(int M, int N, int K);
 void gemm_nn(DType dt, DType odt, const void* a, long lda, const void* b, long ldb, void* c, long ldc, int M, int N,
              int K, bool accumulate, hipStream_t s);
+// same kernel, both operands K-contiguous: C[M, N] (+)= A[M, K] B[N, K]^T (forward y = x W^T);
+// shape rules of gemm_nn_supported
+void gemm_nt(DType dt, DType odt, const void* a, long lda, const void* b, long ldb, void* c, long ldc, int M, int N,
+             int K, bool accumulate, hipStream_t s);
 
 // optim.hip
 void adamw_step(DType pdt, DType gdt, void* param, float* master, const void* grad, float* m, float* v, long n,

@@ -307,6 +307,27 @@ void gemm_nn_(const Tensor& a, const Tensor& b, Tensor& c, bool accumulate) {
                 (int)M, (int)N, (int)K, accumulate, stream());
 }
 
+// c[M, N] (+)= a[M, K] . b[N, K]^T on the MFMA kernel (both operands K-contiguous)
+void gemm_nt_(const Tensor& a, const Tensor& b, Tensor& c, bool accumulate) {
+  TORCH_CHECK(a.is_cuda() && b.is_cuda() && c.is_cuda(), "gemm_nt: GPU tensors");
+  c10::DeviceGuard g(a.device());
+  TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && c.dim() == 2, "gemm_nt: 2-D operands");
+  const int64_t M = a.size(0), K = a.size(1), N = b.size(0);
+  TORCH_CHECK(b.size(1) == K && c.size(0) == M && c.size(1) == N, "gemm_nt: shapes");
+  TORCH_CHECK(a.scalar_type() == b.scalar_type() &&
+                  (a.scalar_type() == at::kBFloat16 || a.scalar_type() == at::kHalf), "gemm_nt: bf16/fp16 operands");
+  TORCH_CHECK(c.scalar_type() == a.scalar_type() || c.scalar_type() == at::kFloat, "gemm_nt: output dtype");
+  TORCH_CHECK(a.stride(1) == 1 && b.stride(1) == 1 && c.stride(1) == 1, "gemm_nt: unit column strides");
+  TORCH_CHECK(a.stride(0) % 8 == 0 && b.stride(0) % 8 == 0, "gemm_nt: rows must be 16-B aligned");
+  TORCH_CHECK((reinterpret_cast<uintptr_t>(a.data_ptr()) | reinterpret_cast<uintptr_t>(b.data_ptr())) % 16 == 0,
+              "gemm_nt: operands must be 16-B aligned");
+  TORCH_CHECK(a.stride(0) < (int64_t(1) << 26) && b.stride(0) < (int64_t(1) << 26), "gemm_nt: row stride too large");
+  TORCH_CHECK(M < (int64_t(1) << 31) && N < (int64_t(1) << 31) && K < (int64_t(1) << 31));
+  TORCH_CHECK(bllm::gemm_nn_supported((int)M, (int)N, (int)K), "gemm_nt: unsupported shape ", M, "x", N, "x", K);
+  bllm::gemm_nt(dt_of(a), dt_of(c), a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0), c.data_ptr(), c.stride(0),
+                (int)M, (int)N, (int)K, accumulate, stream());
+}
+
 // qkv [B, (H+2G)*hd] (one decode token per row); kc / vc [B, G, Tmax, hd] valid below *pos;
 // appends the token's k / v at *pos and attends over pos + 1 keys -> out [B, H*hd]
 Tensor attn_decode_append(const Tensor& qkv, Tensor& kc, Tensor& vc, const Tensor& pos, int64_t H, int64_t G) {
@@ -808,6 +829,7 @@ TORCH_LIBRARY(bllm, m) {
   m.def("sum_partials_(Tensor part, Tensor(a!) out, bool accumulate) -> ()");
   m.def("wgrad_gemm_(Tensor a, Tensor b, Tensor(a!) c, bool accumulate, int splits) -> ()");
   m.def("gemm_nn_(Tensor a, Tensor b, Tensor(a!) c, bool accumulate) -> ()");
+  m.def("gemm_nt_(Tensor a, Tensor b, Tensor(a!) c, bool accumulate) -> ()");
   m.def("attn_decode(Tensor q, Tensor kcache, Tensor vcache, int L) -> Tensor");
   m.def("attn_decode_append(Tensor qkv, Tensor(a!) kcache, Tensor(b!) vcache, Tensor pos, int H, int G) -> Tensor");
   m.def("rope_dev_(Tensor(a!) qkv, Tensor cos, Tensor sin, int H, int G, int hd, Tensor pos) -> ()");
@@ -846,6 +868,7 @@ TORCH_LIBRARY_IMPL(bllm, CUDA, m) {
   m.impl("sum_partials_", &sum_partials_);
   m.impl("wgrad_gemm_", &wgrad_gemm_);
   m.impl("gemm_nn_", &gemm_nn_);
+  m.impl("gemm_nt_", &gemm_nt_);
   m.impl("bias_grad_", &bias_grad_);
   m.impl("flash_attn_bwd", &flash_attn_bwd);
   m.impl("ce_fwd", &ce_fwd);

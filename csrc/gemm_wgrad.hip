@@ -130,7 +130,7 @@ template <int N> __device__ __forceinline__ void vm_wait() { asm volatile("s_wai
 //             covers 16 distinct bank quads), fragments read with ds_read_b128.
 __device__ __forceinline__ int fA(int q) { return (0x78 >> (2 * q)) & 3; }
 
-template <typename T, typename OT, int VAR, bool AK = false>
+template <typename T, typename OT, int VAR, bool AK = false, bool BKC = false>
 __global__ __launch_bounds__(Geo<VAR>::THREADS) void wgrad_gemm_k(const T* __restrict__ A, long lda,
                                                                   const T* __restrict__ B, long ldb,
                                                                   OT* __restrict__ C, long ldc, long c_split,
@@ -163,7 +163,12 @@ __global__ __launch_bounds__(Geo<VAR>::THREADS) void wgrad_gemm_k(const T* __res
 #pragma unroll
   for (int j = 0; j < DJ; ++j) {
     const int r = (wave * DJ + j) * 2 + (lane >> 5), c = (lane & 31) ^ (G::M32 ? swz32(r) : swz(r));
-    voffB[j] = (uint32_t)((r * ldb + 8 * c) * (long)sizeof(T));
+    if constexpr (BKC) {  // B [N, K] K-contiguous: staged like a K-contiguous A
+      const int rb = (wave * DJ + j) * 16 + (lane >> 2), cb = (lane & 3) ^ fA((rb >> 2) & 3);
+      voffB[j] = (uint32_t)((rb * ldb + 8 * cb) * (long)sizeof(T));
+    } else {
+      voffB[j] = (uint32_t)((r * ldb + 8 * c) * (long)sizeof(T));
+    }
     if constexpr (AK) {  // piece = 16 m-rows x 64 B; lane -> row l/4, physical chunk l%4
       const int ra = (wave * DJ + j) * 16 + (lane >> 2), ca = (lane & 3) ^ fA((ra >> 2) & 3);
       voffA[j] = (uint32_t)((ra * lda + 8 * ca) * (long)sizeof(T));
@@ -173,7 +178,7 @@ __global__ __launch_bounds__(Geo<VAR>::THREADS) void wgrad_gemm_k(const T* __res
   }
   const uint32_t lds0 = lds_u32(smem);
   const T* Abase = AK ? A + m0 * lda + (long)c_lo * KCH : A + (long)c_lo * KCH * lda + m0;
-  const T* Bbase = B + (long)c_lo * KCH * ldb + n0;
+  const T* Bbase = BKC ? B + n0 * ldb + (long)c_lo * KCH : B + (long)c_lo * KCH * ldb + n0;
   // piece q of a stage: q even = A piece q/2, q odd = B piece q/2 (issue order A0 B0 A1 B1 ..)
   auto piece = [&](const void* a, const void* b, int q, int slot) {
     const int j = q >> 1;
@@ -183,7 +188,7 @@ __global__ __launch_bounds__(Geo<VAR>::THREADS) void wgrad_gemm_k(const T* __res
   auto stage = [&](int kt, int slot) {
     if (G::LOADERS < G::NW && wave >= G::LOADERS) return;  // wave-uniform (readfirstlane'd)
     const void* a = sgpr_ptr(Abase + (AK ? (long)kt * BK : (long)kt * BK * lda));
-    const void* b = sgpr_ptr(Bbase + (long)kt * BK * ldb);
+    const void* b = sgpr_ptr(Bbase + (BKC ? (long)kt * BK : (long)kt * BK * ldb));
 #pragma unroll
     for (int q = 0; q < PS; ++q) piece(a, b, q, slot);
   };
@@ -211,7 +216,14 @@ __global__ __launch_bounds__(Geo<VAR>::THREADS) void wgrad_gemm_k(const T* __res
     else return frag(p);
   };
 #pragma unroll
-  for (int j = 0; j < FN; ++j) boff[j] = B_BASE + rowb + ((wn * 2 * FN + 2 * j) ^ f) * 16;
+  for (int j = 0; j < FN; ++j)
+    boff[j] = BKC ? B_BASE + (wn * 16 * FN + 16 * j + (lane & 15)) * 64 + (((lane >> 4) ^ fA((lane & 15) >> 2)) << 4)
+                  : B_BASE + rowb + ((wn * 2 * FN + 2 * j) ^ f) * 16;
+  // B fragment: 8 k-values of one n column (two transposed reads) or of one n row (BKC)
+  auto fragB = [&](const char* p) -> s16x8 {
+    if constexpr (BKC) return *(const __attribute__((address_space(3))) s16x8*)(p);
+    else return frag(p);
+  };
   if constexpr (G::M32) {
     const int rb32 = (8 * (g >> 1) + qq) * ROWB + (p & 1) * 8 + (p >> 1) * 16 + 2 * (g & 1) * 16;
 #pragma unroll
@@ -234,7 +246,7 @@ __global__ __launch_bounds__(Geo<VAR>::THREADS) void wgrad_gemm_k(const T* __res
     auto load = [&](Frags& F, int slot) {
       const char* base = smem + slot * SLOTB;
 #pragma unroll
-      for (int j = 0; j < FN; ++j) F.b[j] = frag(base + boff[j]);
+      for (int j = 0; j < FN; ++j) F.b[j] = fragB(base + boff[j]);
 #pragma unroll
       for (int i = 0; i < 8; ++i) F.a[i] = fragA(base + aoff[i]);
     };
@@ -252,7 +264,7 @@ __global__ __launch_bounds__(Geo<VAR>::THREADS) void wgrad_gemm_k(const T* __res
         asm volatile("" ::: "memory");
         if constexpr (STAGE) stage(kt + 4, kt & (NSLOT - 1));
 #pragma unroll
-        for (int j = 0; j < FN; ++j) Gn.b[j] = frag(nxt + boff[j]);
+        for (int j = 0; j < FN; ++j) Gn.b[j] = fragB(nxt + boff[j]);
       }
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
@@ -310,7 +322,7 @@ __global__ __launch_bounds__(Geo<VAR>::THREADS) void wgrad_gemm_k(const T* __res
     const char* base = smem + slot * SLOTB;
     s16x8 bf[FN];
 #pragma unroll
-    for (int j = 0; j < FN; ++j) bf[j] = frag(base + boff[j]);
+    for (int j = 0; j < FN; ++j) bf[j] = fragB(base + boff[j]);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const s16x8 af = fragA(base + aoff[i]);
@@ -439,16 +451,16 @@ __global__ __launch_bounds__(Geo<VAR>::THREADS) void wgrad_gemm_k(const T* __res
   }
 }
 
-template <typename T, typename OT, int VAR, bool AK = false>
+template <typename T, typename OT, int VAR, bool AK = false, bool BKC = false>
 void launch_v(const void* a, long lda, const void* b, long ldb, void* c, long ldc, long c_split, int M, int N, int K,
               int S, bool accumulate, hipStream_t s) {
-  static const bool attr = hipFuncSetAttribute((const void*)wgrad_gemm_k<T, OT, VAR, AK>,
+  static const bool attr = hipFuncSetAttribute((const void*)wgrad_gemm_k<T, OT, VAR, AK, BKC>,
                                                hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES) == hipSuccess;
   (void)attr;
   const dim3 grid((M / BM) * (N / BN), S);
   const bool wide = reinterpret_cast<uintptr_t>(c) % 16 == 0 && (ldc * (long)sizeof(OT)) % 16 == 0 &&
                     (c_split * (long)sizeof(OT)) % 16 == 0;
-  hipLaunchKernelGGL((wgrad_gemm_k<T, OT, VAR, AK>), grid, dim3(Geo<VAR>::THREADS), LDS_BYTES, s, (const T*)a, lda,
+  hipLaunchKernelGGL((wgrad_gemm_k<T, OT, VAR, AK, BKC>), grid, dim3(Geo<VAR>::THREADS), LDS_BYTES, s, (const T*)a, lda,
                      (const T*)b, ldb, (OT*)c, ldc, c_split, M, N, K, (int)accumulate, (int)wide);
 }
 
@@ -479,6 +491,15 @@ void gemm_nn(DType dt, DType odt, const void* a, long lda, const void* b, long l
   BLLM_DISPATCH(odt, OT, {
     if (dt == DType::BF16) launch_v<bf16_t, OT, DEFAULT_VARIANT, true>(a, lda, b, ldb, c, ldc, 0, M, N, K, 1, accumulate, s);
     else launch_v<f16_t, OT, DEFAULT_VARIANT, true>(a, lda, b, ldb, c, ldc, 0, M, N, K, 1, accumulate, s);
+  });
+}
+
+// both operands K-contiguous: C[M, N] (+)= A[M, K] B[N, K]^T (a Linear's forward y = x W^T)
+void gemm_nt(DType dt, DType odt, const void* a, long lda, const void* b, long ldb, void* c, long ldc, int M, int N,
+             int K, bool accumulate, hipStream_t s) {
+  BLLM_DISPATCH(odt, OT, {
+    if (dt == DType::BF16) launch_v<bf16_t, OT, DEFAULT_VARIANT, true, true>(a, lda, b, ldb, c, ldc, 0, M, N, K, 1, accumulate, s);
+    else launch_v<f16_t, OT, DEFAULT_VARIANT, true, true>(a, lda, b, ldb, c, ldc, 0, M, N, K, 1, accumulate, s);
   });
 }
 

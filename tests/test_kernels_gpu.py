@@ -490,6 +490,24 @@ def test_wgrad_gemm_unaligned_output(accumulate):
 @pytest.mark.parametrize("odt", [None, torch.float32])
 @pytest.mark.parametrize("M,K,N", [(256, 128, 256), (512, 384, 768), (768, 1024, 512)])
 @pytest.mark.parametrize("accumulate", [False, True])
+def test_gemm_nt(dt, odt, M, K, N, accumulate):
+    """Both-operands-K-contiguous variant (c = a . b^T, the forward layout) vs an fp32 matmul,
+    strided rows."""
+    a_full = torch.randn(M, K + 64, device=DEV).to(dt)
+    a = a_full[:, 32:32 + K]
+    b_full = torch.randn(N, K + 32, device=DEV).to(dt)
+    b = b_full[:, :K]
+    c = torch.randn(M, N, device=DEV).to(odt or dt)
+    expect = a.float() @ b.float().t() + (c.float() if accumulate else 0)
+    ops.gemm_nt_(a, b, c, accumulate)
+    err = (c.float() - expect).abs().max().item()
+    assert err <= (8e-3 if (odt or dt) != torch.float32 else 1e-4) * expect.abs().max().item(), err
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("odt", [None, torch.float32])
+@pytest.mark.parametrize("M,K,N", [(256, 128, 256), (512, 384, 768), (768, 1024, 512)])
+@pytest.mark.parametrize("accumulate", [False, True])
 def test_gemm_nn(dt, odt, M, K, N, accumulate):
     """K-contiguous-A variant of the MFMA GEMM (dX = dY W) vs an fp32 matmul, strided A rows."""
     a_full = torch.randn(M, K + 64, device=DEV).to(dt)

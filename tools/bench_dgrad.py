@@ -42,6 +42,9 @@ def main():
             r = {"model": model, "gemm": name, "layout": "fwd" if a.forward else "dx",
                  "k_n": [out_f, in_f], "tokens": Nt}
             times = {"hipblaslt_us": [], "hipblaslt_wt_us": [], "mfma_us": []}
+            if a.forward:
+                times["mfma_nt_us"] = []
+                d3 = torch.empty_like(d0)
             # forward: the model's hipBLASLt call is x @ W^T on the [out, in] weight (= Wt.t());
             # the kernel needs B row-major [K, N] = W here
             lt_main, lt_alt = (Wt.t(), W) if a.forward else (W, Wt.t())
@@ -49,16 +52,22 @@ def main():
                 times["hipblaslt_us"].append(timeit(lambda: torch.mm(dy, lt_main, out=d0), a.iters))
                 times["hipblaslt_wt_us"].append(timeit(lambda: torch.mm(dy, lt_alt, out=d2), a.iters))
                 times["mfma_us"].append(timeit(lambda: ops.gemm_nn_(dy, W, d1, False), a.iters))
+                if a.forward:  # both operands K-contiguous: x [N, in] . Wlin[out, in]^T
+                    times["mfma_nt_us"].append(timeit(lambda: ops.gemm_nt_(dy, Wt, d3, False), a.iters))
             for k, ts in times.items():
                 r[k] = sorted(ts)[len(ts) // 2]
             torch.cuda.synchronize()
             r["max_rel_err_vs_hipblaslt"] = round(((d1.float() - d0.float()).abs().max() / d0.float().abs().max()).item(), 5)
+            if a.forward:
+                r["nt_max_rel_err"] = round(((d3.float() - d0.float()).abs().max() / d0.float().abs().max()).item(), 5)
             for k in list(r):
                 if k.endswith("_us"):
                     r[k.replace("_us", "_tflops")] = round(fl / r[k] / 1e6, 1)
                     r[k] = round(r[k], 1)
             print(json.dumps(r), flush=True)
             del dy, W, Wt, d0, d1, d2
+            if a.forward:
+                del d3
             torch.cuda.empty_cache()
 
 
