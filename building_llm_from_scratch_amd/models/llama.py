@@ -303,13 +303,82 @@ class HeadComputeMixin:
             if gW is not None:
                 _weight_grad(dl, hc, gW, accumulate=s0 > 0)
             del logits, dl
-        return total[0] / nvalid, (x2d, ns, dh, gW, "fused")
+        return total[0] / nvalid, (x2d, ns, dh, gW, [], "fused")
+
+    def _fused_lora_ok(self) -> bool:
+        hd = self.head
+        return (hd.has_lora and len(hd.specs) == 1 and hd.b_params is None
+                and not hd.unit.trainable(hd.W_params[0])
+                and os.environ.get("BLLM_LORA_HEAD_FUSED", "1") != "0")
+
+    def _waug(self, W, Bm):
+        """[W | B^T] ([V, d + r]) in a buffer kept across steps; both parts re-copied per call
+        (FSDP may re-materialise W, the optimizer moves B): ~0.2 ms for the Llama-3.2-1B head."""
+        V, d = W.shape
+        r = Bm.shape[0]
+        buf = getattr(self, "_waug_buf", None)
+        if buf is None or buf.shape != (V, d + r) or buf.dtype != W.dtype or buf.device != W.device:
+            buf = self._waug_buf = torch.empty(V, d + r, dtype=W.dtype, device=W.device)
+        buf[:, :d].copy_(W)
+        buf[:, d:].copy_(Bm.t())
+        return buf
+
+    def _fused_lora_loss(self, x2d, h, ns, targets, nvalid):
+        """LoRA head (the reference's replace_linear_with_lora also wraps the output head; its
+        base weight is frozen) on the same chunked head + CE, with the rank-r path folded into
+        the head GEMMs by augmenting K (t = h A, s = alpha / r):
+            logits         = [h | s t] . [W | B^T]^T
+            [dh_W | dl B^T] = dl . [W | B^T]
+        one GEMM each per chunk instead of a separate s t B pass over the [N, V] logits plus a
+        beta = 1 GEMM, and a separate dl B^T pass over dlogits (Llama-3.2-1B Alpaca: ~2 ms of
+        a 75 ms step)."""
+        hd, u = self.head, self.head.unit
+        spec = hd.specs[0]
+        A, Bm, sc = u.data(spec.lora_A), u.data(spec.lora_B), float(spec.scaling)   # [d, r], [r, V]
+        W = hd.W()
+        N, d = h.shape
+        V, r = W.shape[0], A.shape[1]
+        Wa = self._waug(W, Bm)
+        t = torch.mm(h, A)                                                  # [N, r]
+        ha = torch.empty(N, d + r, dtype=h.dtype, device=h.device)
+        ha[:, :d].copy_(h)
+        ha[:, d:].copy_(t * sc)
+        rows = max(MIN_CHUNK_ROWS, LOGIT_CHUNK_BYTES // (V * h.element_size()) // MIN_CHUNK_ROWS * MIN_CHUNK_ROWS)
+        Wd = Wa
+        if _dgrad_wt_ok(ha[:rows], Wa):
+            Wd = ops.transpose2d(Wa).t()
+        dha = torch.empty_like(ha)
+        # (grad views only exist in backward: FSDP allocates the full gradient in pre_backward)
+        gB = torch.zeros(r, V, dtype=torch.float32, device=h.device) if u.trainable(spec.lora_B) else None
+        scale = (1.0 / nvalid).reshape(1)
+        total = torch.zeros(1, dtype=torch.float32, device=h.device)
+        for s0 in range(0, N, rows):
+            hc, tc = ha[s0:s0 + rows], targets[s0:s0 + rows]
+            logits = torch.mm(hc, Wa.t())
+            lrow, lse = ops.ce_fwd(logits, tc, self.ignore_index)
+            total += lrow.sum()
+            dl = ops.ce_bwd_(logits, tc, lse, scale, self.ignore_index)   # in place
+            torch.mm(dl, Wd, out=dha[s0:s0 + rows])
+            if gB is not None:                                            # dB = s t^T dl
+                gB += torch.mm(t[s0:s0 + rows].t(), dl).float().mul_(sc)
+            del logits, dl
+        ub = dha[:, d:]                                                   # dl B^T
+        dh = torch.addmm(dha[:, :d], ub, A.t(), alpha=sc)                 # + s (dl B^T) A^T
+        lora = []
+        if gB is not None:
+            lora.append((spec.lora_B, gB))
+        if u.trainable(spec.lora_A):                                      # dA = s h^T (dl B^T)
+            lora.append((spec.lora_A, torch.mm(h.t(), ub).float().mul_(sc)))
+        del dha, ha
+        return total[0] / nvalid, (x2d, ns, dh, None, lora, "fused")
 
     def forward_loss(self, x, targets, save):
         x2d = x.reshape(-1, x.shape[-1])
         h, ns = self._norm_fwd(x2d)
-        if save and self._fused_ok(h):
+        if save and (self._fused_ok(h) or self._fused_lora_ok()):
             nvalid = (targets != self.ignore_index).sum().to(torch.float32).clamp_(min=1.0)
+            if not self._fused_ok(h):
+                return self._fused_lora_loss(x2d, h, ns, targets, nvalid)
             return self._fused_loss(x2d, h, ns, targets, nvalid)
         logits, xa = self.head.forward(h)
         rows, lse = ops.ce_fwd(logits, targets, self.ignore_index)
@@ -323,7 +392,7 @@ class HeadComputeMixin:
 
     def backward_loss(self, dloss, saved):
         if saved[-1] == "fused":
-            x2d, ns, dh, gW, _ = saved
+            x2d, ns, dh, gW, lora, _ = saved
             dls = dloss.float().reshape(1)
             dh.mul_(dls)
             if gW is not None:
@@ -332,6 +401,12 @@ class HeadComputeMixin:
                     g.add_(gW * dls)
                 else:
                     torch.mul(gW, dls, out=g)
+            for p, gp in lora:  # LoRA head: dA / dB taken for dloss = 1 in forward
+                g = self.head.unit.grad(p)
+                if self.rctx.accumulate:
+                    g.add_(gp * dls)
+                else:
+                    g.copy_(gp * dls)
             dx = self._norm_bwd(dh, (x2d,) + ns)
             return dx.view(self.rctx.B, self.rctx.T, -1)
         x2d, h, ns, xa, logits, lse, targets, nvalid = saved

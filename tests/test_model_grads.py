@@ -117,6 +117,43 @@ def test_grouped_lora_path_grads(family, monkeypatch, ckpt):
 
 
 @pytest.mark.parametrize("family", ["llama", "gpt2"])
+def test_fused_chunked_lora_head(family, monkeypatch):
+    """LoRA head (frozen base) on the chunked head + CE with the rank-r path folded into the
+    head GEMMs ([h | s t] . [W | B^T]^T): several chunks, ignore_index targets, non-unit dloss,
+    vs the eager oracle."""
+    from building_llm_from_scratch_amd.models import llama
+    monkeypatch.setattr(llama, "MIN_CHUNK_ROWS", 8)
+    monkeypatch.setattr(llama, "LOGIT_CHUNK_BYTES", 8 * 97 * 4)
+    torch.manual_seed(0)
+    cfg = _small_llama() if family == "llama" else _small_gpt2()
+    m = build_model(cfg)
+    for p in m.parameters():
+        p.requires_grad = False
+    replace_linear_with_lora(m, rank=4, alpha=8)
+    for mod in m.modules():
+        if hasattr(mod, "B") and isinstance(mod.B, torch.nn.Parameter):
+            torch.nn.init.normal_(mod.B, std=0.05)
+    m.flatten()
+    head = m.computes[-1]
+    assert head._fused_lora_ok()
+    idx = torch.randint(0, cfg.vocab_size, (3, 13))
+    tgt = torch.randint(0, cfg.vocab_size, (3, 13))
+    tgt[1, :5] = -100
+    if family == "llama":
+        cos, sin = ops.rope_tables(cfg.head_dim, cfg.context_length, cfg.rope_base, cfg.rope_freq)
+        fn = lambda sd: llama_loss(sd, cfg, idx, tgt, cos, sin, lora=2.0)  # noqa: E731
+    else:
+        fn = lambda sd: gpt2_loss(sd, cfg, idx, tgt, lora=2.0)  # noqa: E731
+    _compare(m, fn, idx, tgt)
+    (m(idx, tgt) * 4.0).backward()
+    g4 = {n: p.grad.clone() for n, p in m.named_parameters() if p.grad is not None}
+    m(idx, tgt).backward()
+    g1 = {n: p.grad.clone() for n, p in m.named_parameters() if p.grad is not None}
+    for n in g1:
+        assert torch.allclose(g4[n], 4.0 * g1[n], rtol=1e-5, atol=1e-6), n
+
+
+@pytest.mark.parametrize("family", ["llama", "gpt2"])
 def test_fused_chunked_head_ce(family, monkeypatch):
     """Head + CE fused chunk by chunk (logits never materialised whole): several chunks, a
     chunk boundary inside the sequence, ignore_index targets, and a non-unit dloss (fp16 loss
