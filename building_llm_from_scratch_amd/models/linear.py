@@ -18,6 +18,7 @@ a multiple of 64 such as single-token decode) use per-member hipBLASLt GEMMs.
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 from typing import List, Optional, Sequence
 
@@ -191,6 +192,32 @@ class FusedLinear:
             return True
         return ops.lora_kernel_ok(x, self.lora_r, [x.shape[1]] + self.lora_len + self.lora_c0)
 
+    def _kaug_ok(self, x: torch.Tensor, residual, b) -> bool:
+        """K-augmented LoRA (see forward) for wide frozen groups whose output dwarfs the input
+        (gate/up: out = 8 d): copying x into [x | s t] costs less than the s t B write plus the
+        beta = 1 read of y it replaces.  BLLM_LORA_KAUG=0 turns it off."""
+        return (residual is None and b is None and self.out_total >= 4 * x.shape[1]
+                and not self.unit.trainable(self.W_params[0])
+                and os.environ.get("BLLM_LORA_KAUG", "1") != "0")
+
+    def _waug(self, W: torch.Tensor, K: int) -> torch.Tensor:
+        """[W | Bd^T] [out_total, K + R]: member m's B_m^T in rows c0_m.., columns K + off_m...
+        Kept across calls: the frozen W part is re-copied only when W's storage or version
+        changed (FSDP re-gather, a state-dict load); the B block (trained) every call."""
+        u = self.unit
+        key = (W.data_ptr(), W._version, W.shape, W.dtype)
+        cached = getattr(self, "_wa_cache", None)
+        if cached is not None and cached[0] == key:
+            Wa = cached[1]
+        else:
+            Wa = torch.empty(W.shape[0], K + self.lora_R, dtype=W.dtype, device=W.device)
+            Wa[:, :K].copy_(W)
+            self._wa_cache = (key, Wa)
+        Wa[:, K:].zero_()
+        for s, c0, n, off, r in zip(self.lora_specs, self.lora_c0, self.lora_len, self.lora_off, self.lora_r):
+            Wa[c0:c0 + n, K + off:K + off + r].copy_(u.data(s.lora_B).t())
+        return Wa
+
     # views are re-fetched every call: FSDP may have re-materialised the storage
     def W(self):
         return self.unit.fused_data(self.W_params)
@@ -204,6 +231,18 @@ class FusedLinear:
         b = self.b()
         if residual is not None:
             assert b is None
+        if self.has_lora and self._grouped_lora(x) and self._kaug_ok(x, residual, b):
+            # K-augmented: y = [x | s t] . [W | Bd^T]^T, one GEMM (no s t B pass over y, no
+            # beta = 1 re-read); backward gets dy Bd = dy B^T from the dX GEMM the same way
+            u = self.unit
+            K = x.shape[1]
+            P = ops.lora_pack_t([u.data(s.lora_A) for s in self.lora_specs])          # [R, K]
+            t = ops.lora_down(x, [P], [0], [K], [0], self.lora_R)                     # x A_cat
+            xa = torch.empty(x.shape[0], K + self.lora_R, dtype=x.dtype, device=x.device)
+            xa[:, :K].copy_(x)
+            xa[:, K:].copy_(t * self.lora_scale)
+            Wa = self._waug(W, K)
+            return torch.mm(xa, Wa.t()), ("kaug", t, P, Wa)
         if self.has_lora and self._grouped_lora(x):
             # y = (residual | bias) + s t B, written by lora_up, then the base GEMM accumulates
             # onto it (beta = 1): the rank-r update costs no read-modify-write pass of y
@@ -259,6 +298,8 @@ class FusedLinear:
             gb = u.fused_grad(self.b_params)
             if gb is not None:
                 ops.bias_grad_(dy, gb, accumulate)
+        if self.has_lora and isinstance(xa, tuple) and xa[0] == "kaug":
+            return self._kaug_lora_backward(dy, x, xa[1], xa[2], xa[3], need_dx, dx_acc, accumulate)
         if self.has_lora and isinstance(xa, tuple) and xa[0] == "grouped":
             return self._grouped_lora_backward(dy, x, xa[1], xa[2], need_dx, dx_acc, accumulate)
         dx = None
@@ -286,6 +327,29 @@ class FusedLinear:
                         torch.addmm(gA, x.t(), dyB, beta=0, alpha=s.scaling, out=gA)
                 if need_dx:
                     dx.addmm_(dyB, A.t(), alpha=s.scaling)
+        return dx
+
+    def _kaug_lora_backward(self, dy, x, t, P, Wa, need_dx, dx_acc, accumulate):
+        u_ = self.unit
+        sc = self.lora_scale
+        K = x.shape[1]
+        gB = [(u_.grad(s.lora_B), c0, off) for s, c0, off in zip(self.lora_specs, self.lora_c0, self.lora_off)]
+        gB = [g for g in gB if g[0] is not None]
+        if gB:
+            ops.lora_wgrad(t, dy, [g for g, _, _ in gB], [o for _, _, o in gB], [c for _, c, _ in gB], sc,
+                           accumulate)
+        dxa = _input_grad(dy, Wa)                                  # [dy W | dy Bd] = [dx_W | dy B^T]
+        ub = dxa[:, K:]
+        gA = [(u_.grad(s.lora_A), off) for s, off in zip(self.lora_specs, self.lora_off)]
+        gA = [g for g in gA if g[0] is not None]
+        if gA:
+            ops.lora_wgrad(ub, x, [g.t() for g, _ in gA], [o for _, o in gA], [0] * len(gA), sc, accumulate)
+        if not need_dx:
+            return None
+        dx = torch.empty(x.shape, dtype=x.dtype, device=x.device)
+        ops.lora_up_(dx, ub, [P], [0], [0], sc, base=dxa[:, :K])  # dx_W + s (dy B^T) A_cat^T
+        if dx_acc is not None:
+            dx += dx_acc
         return dx
 
     def _grouped_lora_backward(self, dy, x, t, P, need_dx, dx_acc, accumulate):

@@ -116,6 +116,33 @@ def test_grouped_lora_path_grads(family, monkeypatch, ckpt):
     test_lora_grads(family, ckpt)
 
 
+@pytest.mark.parametrize("ckpt", ["none", "full"])
+def test_kaug_grouped_lora_grads(ckpt, monkeypatch):
+    """K-augmented grouped LoRA (gate/up: out >= 4 in): y = [x | s t] . [W | Bd^T]^T and the
+    dX GEMM's extra columns as dy B^T, vs the eager oracle."""
+    from building_llm_from_scratch_amd.models import linear
+    monkeypatch.setattr(linear, "FORCE_GROUPED_LORA", True)
+    calls = []
+    orig = linear.FusedLinear._kaug_lora_backward
+    monkeypatch.setattr(linear.FusedLinear, "_kaug_lora_backward",
+                        lambda self, *a, **k: (calls.append(1), orig(self, *a, **k))[1])
+    torch.manual_seed(0)
+    cfg = _small_llama().replace(hidden_dim=128)                 # gate/up out 256 = 4 x 64
+    m = build_model(cfg, use_actv_ckpt=ckpt)
+    for p in m.parameters():
+        p.requires_grad = False
+    replace_linear_with_lora(m, rank=16, alpha=8)
+    for mod in m.modules():
+        if hasattr(mod, "B") and isinstance(mod.B, torch.nn.Parameter):
+            torch.nn.init.normal_(mod.B, std=0.05)
+    m.flatten()
+    idx = torch.randint(0, cfg.vocab_size, (2, 16))
+    tgt = torch.randint(0, cfg.vocab_size, (2, 16))
+    cos, sin = ops.rope_tables(cfg.head_dim, cfg.context_length, cfg.rope_base, cfg.rope_freq)
+    _compare(m, lambda sd: llama_loss(sd, cfg, idx, tgt, cos, sin, lora=0.5), idx, tgt)
+    assert len(calls) == cfg.n_layers
+
+
 @pytest.mark.parametrize("family", ["llama", "gpt2"])
 def test_fused_chunked_lora_head(family, monkeypatch):
     """LoRA head (frozen base) on the chunked head + CE with the rank-r path folded into the
