@@ -329,6 +329,12 @@ class FusedLinear:
                     dx.addmm_(dyB, A.t(), alpha=s.scaling)
         return dx
 
+    def input_grad(self, dy: torch.Tensor) -> torch.Tensor:
+        """dx = dy W alone (no LoRA, no parameter grads): lets a caller run the dX GEMM before the
+        dW GEMM whose input it is still producing (``backward(..., need_dx=False)`` then)."""
+        assert not self.has_lora
+        return _input_grad(dy, self.W())
+
     def _kaug_lora_backward(self, dy, x, t, P, Wa, need_dx, dx_acc, accumulate):
         u_ = self.unit
         sc = self.lora_scale

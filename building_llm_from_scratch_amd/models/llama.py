@@ -160,15 +160,21 @@ class LlamaBlockCompute(UnitCompute):
         x2, xa_o = self.o.forward(o, residual=x2d)
         h2, r2 = ops.rmsnorm_fwd(x2, u.data(b.norm2.weight), eps)
         gu, xa_gu = self.gu.forward(h2)
-        act = ops.swiglu_fwd(gu)
-        if recompute:
-            x3, xa_dn = None, self.down.lora_state(act)
+        if recompute and not self.down.has_lora:
+            # backward rebuilds act inside the SwiGLU backward kernel (swiglu_bwd_act)
+            act, x3, xa_dn = None, None, None
         else:
-            x3, xa_dn = self.down.forward(act, residual=x2)
+            act = ops.swiglu_fwd(gu)
+            if recompute:
+                x3, xa_dn = None, self.down.lora_state(act)
+            else:
+                x3, xa_dn = self.down.forward(act, residual=x2)
         saved = None
         if save:
-            saved = dict(x=x2d, r1=r1, qkv=qkv, o=o, lse=lse, x2=x2, r2=r2, gu=gu, act=act,
+            saved = dict(x=x2d, r1=r1, qkv=qkv, o=o, lse=lse, x2=x2, r2=r2, gu=gu,
                          xa=(xa_qkv, xa_o, xa_gu, xa_dn))
+            if act is not None:
+                saved["act"] = act
             if rc.block_mode(self.index) == "none" or recompute:  # the recompute's norm outputs live one block
                 saved.update(h1=h1, h2=h2)
         return (x3.view(B, T, d) if x3 is not None else None), saved
@@ -214,11 +220,19 @@ class LlamaBlockCompute(UnitCompute):
         dy2 = dy.reshape(N, d)
         w1, w2 = u.data(b.norm1.weight), u.data(b.norm2.weight)
         # ---- MLP
-        act = s["act"] if "act" in s else ops.swiglu_fwd(s["gu"])
-        d_act = self.down.backward(dy2, act, xa_dn, accumulate=acc)
-        del act
-        d_gu = ops.swiglu_bwd(s["gu"], d_act)
-        del d_act
+        if "act" in s or self.down.has_lora:
+            act = s["act"] if "act" in s else ops.swiglu_fwd(s["gu"])
+            d_act = self.down.backward(dy2, act, xa_dn, accumulate=acc)
+            del act
+            d_gu = ops.swiglu_bwd(s["gu"], d_act)
+            del d_act
+        else:
+            # recompute without act: dX GEMM first, then one SwiGLU backward pass that also
+            # rebuilds act in place of d_act, then the down projection's dW from it
+            act = self.down.input_grad(dy2)
+            d_gu = ops.swiglu_bwd_act(s["gu"], act)
+            self.down.backward(dy2, act, None, need_dx=False, accumulate=acc)
+            del act
         h2 = s["h2"] if "h2" in s else ops.rmsnorm_fwd(s["x2"], w2, eps)[0]
         dh2 = self.gu.backward(d_gu, h2, xa_gu, accumulate=acc)
         del d_gu, h2
@@ -226,9 +240,9 @@ class LlamaBlockCompute(UnitCompute):
         del dh2
         # ---- attention
         d_o = self.o.backward(dx2, s["o"], xa_o, accumulate=acc)
-        dqkv = ops.flash_attn_bwd(s["qkv"], s["o"], s["lse"], d_o, B, T, H, G, hd, causal=True)
+        dqkv = ops.flash_attn_bwd(s["qkv"], s["o"], s["lse"], d_o, B, T, H, G, hd, causal=True,
+                                  rope=(cos, sin))  # inverse RoPE fused into the kernels' epilogues
         del d_o
-        ops.rope_(dqkv, cos, sin, T, H, G, hd, inverse=True)
         h1 = s["h1"] if "h1" in s else ops.rmsnorm_fwd(s["x"], w1, eps)[0]
         dh1 = self.qkv.backward(dqkv, h1, xa_qkv, accumulate=acc)
         del dqkv, h1

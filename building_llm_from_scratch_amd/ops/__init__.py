@@ -21,7 +21,7 @@ from ._ext import ext_available, kernel_debug, load_ext
 
 __all__ = [
     "rmsnorm_fwd", "rmsnorm_bwd", "layernorm_fwd", "layernorm_bwd", "dropout_add", "dropout_bwd",
-    "rope_", "rope_tables", "flash_attn_fwd", "flash_attn_bwd", "swiglu_fwd", "swiglu_bwd",
+    "rope_", "rope_tables", "flash_attn_fwd", "flash_attn_bwd", "swiglu_fwd", "swiglu_bwd", "swiglu_bwd_act",
     "gelu_fwd", "gelu_bwd", "ce_fwd", "ce_bwd_", "embedding_fwd", "embedding_bwd",
     "sq_norm_multi", "adamw_step_", "attn_decode", "bias_grad_", "ext_available", "load_ext", "attention_backend",
     "lora_down", "lora_up_", "lora_wgrad", "lora_pack_t", "lora_kernel_ok", "sum_partials_",
@@ -351,14 +351,20 @@ def attn_decode(q, kcache, vcache, L: int):
 
 
 def flash_attn_bwd(qkv, o, lse, do, B, T, H, G, hd, causal=True, dropout_p=0.0, seed=0, offset=0,
-                   keep_mask=None):
+                   keep_mask=None, rope=None):
     """``keep_mask``: the buffer the matching forward filled (``attn_keep_mask``), or None to
-    regenerate the dropout bits from the counter hash (identical result)."""
+    regenerate the dropout bits from the counter hash (identical result).  ``rope``: the
+    (cos, sin) tables the forward rotated q/k with; the returned dq/dk are then already
+    un-rotated (``rope_(..., inverse=True)`` fused into the MFMA kernels' epilogues)."""
     if qkv.device.type == "cuda" and qkv.dtype in (torch.bfloat16, torch.float16, torch.float32):
         load_ext(required=True)
+        rc, rs = rope if rope is not None else (None, None)
         return _k().flash_attn_bwd(qkv, o, lse, do, B, T, H, G, hd, causal, float(dropout_p),
-                                   int(seed), int(offset), keep_mask)
-    return ref.flash_attn_bwd(qkv, o, lse, do, B, T, H, G, hd, causal, dropout_p, seed, offset)
+                                   int(seed), int(offset), keep_mask, rc, rs)
+    dqkv = ref.flash_attn_bwd(qkv, o, lse, do, B, T, H, G, hd, causal, dropout_p, seed, offset)
+    if rope is not None:
+        ref.rope_(dqkv, rope[0], rope[1], T, H, G, hd, inverse=True)
+    return dqkv
 
 
 # --------------------------------------------------------------------------- activations
@@ -372,6 +378,16 @@ def swiglu_bwd(gu, dact):
     if _hip(gu):
         return _k().swiglu_bwd(gu, dact)
     return ref.swiglu_bwd(gu, dact)
+
+
+def swiglu_bwd_act(gu, dact):
+    """``swiglu_bwd`` that also overwrites ``dact`` in place with act = silu(g) * u (what
+    ``swiglu_fwd`` returns): the checkpoint recompute skips its SwiGLU forward pass."""
+    if _hip(gu):
+        return _k().swiglu_bwd_act(gu, dact)
+    dgu = ref.swiglu_bwd(gu, dact)
+    dact.copy_(ref.swiglu_fwd(gu))
+    return dgu
 
 
 def gelu_fwd(f):

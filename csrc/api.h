@@ -25,7 +25,9 @@ void col_reduce(const float* part, DType odt, void* out, int P, int d, bool accu
 // out[C, R] = in[R, C]^T, 16-bit elements, R % 8 == 0 and C % 8 == 0
 void transpose16(const void* in, void* out, long R, long C, hipStream_t s);
 void swiglu_fwd(DType dt, const void* gu, void* act, long N, int F, hipStream_t s);
-void swiglu_bwd(DType dt, const void* gu, const void* dact, void* dgu, long N, int F, hipStream_t s);
+// act (nullable, may alias dact): also write silu(g) * u there -- the activation-checkpoint
+// recompute then needs no separate SwiGLU forward pass for the down projection's dW
+void swiglu_bwd(DType dt, const void* gu, const void* dact, void* dgu, void* act, long N, int F, hipStream_t s);
 void gelu_fwd(DType dt, const void* f, void* g, long n, hipStream_t s);
 void gelu_bwd(DType dt, const void* f, const void* dg, void* df, long n, hipStream_t s);
 void dropout_add(DType dt, const void* x, const void* a, void* out, long n, float p, uint64_t seed, uint64_t offset,
@@ -44,7 +46,7 @@ void attn_fwd(DType dt, const void* qkv, void* o, float* lse, int B, int T, int 
               float p, uint64_t seed, uint64_t offset, uint32_t* keep_mask, hipStream_t s);
 void attn_bwd(DType dt, const void* qkv, const void* o, const float* lse, const void* dout, void* dqkv, float* delta,
               float* dq_acc, float* dkv_part, int B, int T, int H, int G, int hd, bool causal, float p, uint64_t seed,
-              uint64_t offset, const uint32_t* keep_mask, hipStream_t s);
+              uint64_t offset, const uint32_t* keep_mask, const float* rcos, const float* rsin, hipStream_t s);
 bool attn_mfma_head_dim(int hd);
 void attn_fwd_naive(DType dt, const void* qkv, void* o, float* lse, int B, int T, int H, int G, int hd, bool causal,
                     float p, uint64_t seed, uint64_t offset, hipStream_t s);

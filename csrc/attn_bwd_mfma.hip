@@ -132,6 +132,42 @@ template <int HD, bool DUAL = false, bool MASK = false> constexpr int dkdv_buf_b
 // K + V fragments (64) + dK/dV accumulators (128) + S/dP (32) leave too little of the 256 VGPRs
 // two waves per SIMD allow, and hipcc spilled the fragments to scratch, reloading them every
 // step behind an s_waitcnt vmcnt(0) that also drained the Q/dO DMA ring.
+// Inverse RoPE in a backward epilogue (rotate_half form, reference common_components.py:6-35):
+// the lane holds elements d..d+3 (d = dc + 8 gq + 4 hh) of the first half in lo and the same
+// elements of the second half (d + HD/2) in hi, so each rotation pair is lane-local:
+//   g1' = g1 c + g2 s,  g2' = g2 c - g1 s   (c, s = cos/sin [T, HD/2] fp32 at position pos).
+// Replaces a separate rope pass over dQ / dK (read + write of [N, (H + G) hd]).  ``row`` is the
+// head's first element.
+template <typename T, int HD>
+__device__ __forceinline__ void rope_bwd_store(const f32x16& lo, const f32x16& hi, float scale, int hh, int pos,
+                                               int dc, const float* __restrict__ rcos,
+                                               const float* __restrict__ rsin, T* row) {
+  constexpr int HALF = HD / 2;
+  const float* cp = rcos + (long)pos * HALF + dc + 4 * hh;
+  const float* sp = rsin + (long)pos * HALF + dc + 4 * hh;
+#pragma unroll
+  for (int gq = 0; gq < 4; ++gq) {
+    const float4 c = *reinterpret_cast<const float4*>(cp + 8 * gq);
+    const float4 sn = *reinterpret_cast<const float4*>(sp + 8 * gq);
+    const float cc[4] = {c.x, c.y, c.z, c.w}, ss[4] = {sn.x, sn.y, sn.z, sn.w};
+    float o1[4], o2[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float g1 = lo[4 * gq + j] * scale, g2 = hi[4 * gq + j] * scale;
+      o1[j] = g1 * cc[j] + g2 * ss[j];
+      o2[j] = g2 * cc[j] - g1 * ss[j];
+    }
+    const int d0 = dc + 8 * gq + 4 * hh;
+    uint2 v1, v2;
+    v1.x = pk2<T>(o1[0], o1[1]);
+    v1.y = pk2<T>(o1[2], o1[3]);
+    v2.x = pk2<T>(o2[0], o2[1]);
+    v2.y = pk2<T>(o2[2], o2[3]);
+    *reinterpret_cast<uint2*>(row + d0) = v1;
+    *reinterpret_cast<uint2*>(row + d0 + HALF) = v2;
+  }
+}
+
 template <typename T, int HD, bool DROP, int NBUF, int OCC, bool FUSEG = false, bool DUAL = false, bool MASK = false,
           bool VLDS = false>
 __global__ __launch_bounds__(256, OCC) void attn_bwd_mfma_k(const T* __restrict__ qkv, const T* __restrict__ dout,
@@ -140,7 +176,9 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_mfma_k(const T* __restrict_
                                                             float* __restrict__ dkv_part, int T_, int H, int G, int B_,
                                                             bool causal, uint32_t thr, float inv_keep,
                                                             uint64_t seed, uint64_t doff,
-                                                            const uint32_t* __restrict__ kmask) {
+                                                            const uint32_t* __restrict__ kmask,
+                                                            const float* __restrict__ rcos,
+                                                            const float* __restrict__ rsin) {
   typedef typename MFb<T>::v8 v8;
   constexpr int KK = HD / 16, DT = HD / 32, CH = HD / 8, ROWB = HD * 2;
   constexpr int IMG = BWD_BQ * ROWB;            // bytes of one [32][HD] image
@@ -424,17 +462,29 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_mfma_k(const T* __restrict_
   if (mykey < T_ && (FUSEG || H == G)) {
     T* pk = dqkv + ((long)b * T_ + mykey) * rs + (long)(H + g) * HD;
     T* pv = dqkv + ((long)b * T_ + mykey) * rs + (long)(H + G + g) * HD;
+    if (rcos) {  // the backward of the forward's RoPE on K, applied to dK before it is stored
+#pragma unroll
+      for (int dt = 0; dt < DT / 2; ++dt) rope_bwd_store<T, HD>(dk[dt], dk[dt + DT / 2], scale, hh, mykey, dt * 32, rcos, rsin, pk);
+    } else {
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+        for (int gq = 0; gq < 4; ++gq) {
+          const int d0 = dt * 32 + 8 * gq + 4 * hh;
+          uint2 a;
+          a.x = pk2<T>(dk[dt][4 * gq] * scale, dk[dt][4 * gq + 1] * scale);
+          a.y = pk2<T>(dk[dt][4 * gq + 2] * scale, dk[dt][4 * gq + 3] * scale);
+          *reinterpret_cast<uint2*>(pk + d0) = a;
+        }
+    }
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt)
 #pragma unroll
       for (int gq = 0; gq < 4; ++gq) {
         const int d0 = dt * 32 + 8 * gq + 4 * hh;
-        uint2 a, bb;
-        a.x = pk2<T>(dk[dt][4 * gq] * scale, dk[dt][4 * gq + 1] * scale);
-        a.y = pk2<T>(dk[dt][4 * gq + 2] * scale, dk[dt][4 * gq + 3] * scale);
+        uint2 bb;
         bb.x = pk2<T>(dv[dt][4 * gq], dv[dt][4 * gq + 1]);
         bb.y = pk2<T>(dv[dt][4 * gq + 2], dv[dt][4 * gq + 3]);
-        *reinterpret_cast<uint2*>(pk + d0) = a;
         *reinterpret_cast<uint2*>(pv + d0) = bb;
       }
   } else if (mykey < T_) {
@@ -472,7 +522,9 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_dq_k(const T* __restrict__ 
                                                         float* __restrict__ delta, T* __restrict__ dqkv,
                                                         int T_, int H, int G, int B_, bool causal, uint32_t thr,
                                                         float inv_keep, uint64_t seed, uint64_t doff,
-                                                        const uint32_t* __restrict__ kmask) {
+                                                        const uint32_t* __restrict__ kmask,
+                                                        const float* __restrict__ rcos,
+                                                        const float* __restrict__ rsin) {
   typedef typename MFb<T>::v8 v8;
   constexpr int KK = HD / 16, DT = HD / 32, CH = HD / 8, ROWB = HD * 2;
   constexpr int IMG = DQ_BK * ROWB;             // bytes of one [BK][HD] image
@@ -712,6 +764,11 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_dq_k(const T* __restrict__ 
   }
   if (qi < T_) {
     T* row = dqkv + ((long)b * T_ + qi) * rs + (long)h * HD;
+    if (rcos) {  // the backward of the forward's RoPE on Q, applied to dQ before it is stored
+#pragma unroll
+      for (int dt = 0; dt < DT / 2; ++dt) rope_bwd_store<T, HD>(dq[dt], dq[dt + DT / 2], scale, hh, qi, dt * 32, rcos, rsin, row);
+      return;
+    }
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt)
 #pragma unroll
@@ -726,10 +783,14 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_dq_k(const T* __restrict__ 
 }
 
 // GQA: dqkv[:, k/v part] = bf16(sum over the H/G query heads of each kv group)
+// With rcos: the inverse RoPE on dK as well (the thread of the first-half chunk d also sums the
+// chunk d + HD/2 and writes both; second-half threads of K have nothing to do).
 template <typename T>
 __global__ __launch_bounds__(256) void attn_bwd_kv_reduce_k(const float* __restrict__ dkv_part, T* __restrict__ dqkv,
-                                                            long BT, int H, int G, int HD) {
-  const int rep = H / G;
+                                                            long BT, int H, int G, int HD, int T_,
+                                                            const float* __restrict__ rcos,
+                                                            const float* __restrict__ rsin) {
+  const int rep = H / G, half = HD / 2;
   const long rs = (long)(H + 2 * G) * HD;
   const long per_row = 2L * G * HD / 4;
   const long total = BT * per_row;
@@ -738,15 +799,31 @@ __global__ __launch_bounds__(256) void attn_bwd_kv_reduce_k(const float* __restr
     const int kvcol = (int)(i - row * per_row) * 4;  // in [0, 2*G*HD)
     const int which = kvcol / (G * HD);
     const int gg = (kvcol % (G * HD)) / HD, d = kvcol % HD;
+    const bool rot = rcos && which == 0;
+    if (rot && d >= half) continue;
     const float* src = dkv_part + (long)which * BT * H * HD + row * H * HD;
-    float v[4] = {0.f, 0.f, 0.f, 0.f};
+    float v[4] = {0.f, 0.f, 0.f, 0.f}, w[4] = {0.f, 0.f, 0.f, 0.f};
     for (int r = 0; r < rep; ++r) {
       const float4 x = *reinterpret_cast<const float4*>(src + (long)(gg * rep + r) * HD + d);
       v[0] += x.x; v[1] += x.y; v[2] += x.z; v[3] += x.w;
+      if (rot) {
+        const float4 y = *reinterpret_cast<const float4*>(src + (long)(gg * rep + r) * HD + d + half);
+        w[0] += y.x; w[1] += y.y; w[2] += y.z; w[3] += y.w;
+      }
     }
     T* dst = dqkv + row * rs + (long)H * HD + kvcol;
+    if (rot) {
+      const int pos = (int)(row % T_);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) dst[j] = from_f<T>(v[j]);
+      for (int j = 0; j < 4; ++j) {
+        const float c = rcos[(long)pos * half + d + j], sn = rsin[(long)pos * half + d + j];
+        dst[j] = from_f<T>(v[j] * c + w[j] * sn);
+        dst[j + half] = from_f<T>(w[j] * c - v[j] * sn);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) dst[j] = from_f<T>(v[j]);
+    }
   }
 }
 
@@ -803,13 +880,14 @@ struct BwdArgs {
   float ik;
   uint64_t seed, offset;
   const uint32_t* kmask;
+  const float *rcos, *rsin;
   hipStream_t s;
 };
 template <typename TT, int HDD, bool DROP, int BK, int NB, int OC, bool MASK>
 static void launch_dq1(const BwdArgs& a, dim3 grid) {
   constexpr int lds = NB * dq_buf_bytes<HDD, BK, MASK>();
   hipLaunchKernelGGL((attn_bwd_dq_k<TT, HDD, DROP, BK, NB, OC, MASK>), grid, dim3(256), lds, a.s, (const TT*)a.qkv, (const TT*)a.o, (const TT*)a.dout, a.lse, a.delta, (TT*)a.dqkv, a.T_, a.H,
-                     a.G, a.B, a.causal, a.thr, a.ik, a.seed, a.offset, a.kmask);
+                     a.G, a.B, a.causal, a.thr, a.ik, a.seed, a.offset, a.kmask, a.rcos, a.rsin);
 }
 template <typename TT, int HDD, int BK, int NB, int OC>
 static void launch_dq(const BwdArgs& a, bool drop, dim3 grid) {
@@ -821,7 +899,8 @@ template <typename TT, int HDD, bool DROP, int NB, int OC, bool FG, bool DU, boo
 static void launch_kv1(const BwdArgs& a, dim3 grid) {
   constexpr int lds = NB * dkdv_buf_bytes<HDD, DU, MASK>() + (VL ? BWD_BKV * HDD * 2 : 0);
   hipLaunchKernelGGL((attn_bwd_mfma_k<TT, HDD, DROP, NB, OC, FG, DU, MASK, VL>), grid, dim3(256), lds, a.s, (const TT*)a.qkv, (const TT*)a.dout, a.lse, a.delta,
-                     (TT*)a.dqkv, a.dkv_part, a.T_, a.H, a.G, a.B, a.causal, a.thr, a.ik, a.seed, a.offset, a.kmask);
+                     (TT*)a.dqkv, a.dkv_part, a.T_, a.H, a.G, a.B, a.causal, a.thr, a.ik, a.seed, a.offset, a.kmask,
+                     a.rcos, a.rsin);
 }
 template <typename TT, int HDD, int NB, int OC, bool FG, bool DU, bool VL = false>
 static void launch_kv(const BwdArgs& a, bool drop, dim3 grid) {
@@ -846,7 +925,8 @@ static void launch_bwd(const BwdArgs& a, bool drop, int q_variant, int kv_varian
 
 void attn_bwd_mfma(DType dt, const void* qkv, const void* o, const float* lse, const void* dout, void* dqkv,
                    float* delta, float* dq_acc, float* dkv_part, int B, int T_, int H, int G, int hd, bool causal,
-                   float p, uint64_t seed, uint64_t offset, const uint32_t* keep_mask, hipStream_t s) {
+                   float p, uint64_t seed, uint64_t offset, const uint32_t* keep_mask, const float* rcos,
+                   const float* rsin, hipStream_t s) {
   (void)dq_acc;
   static const int kv_variant = kv_variant_from_env();
   static const int q_variant = q_variant_from_env();
@@ -864,7 +944,7 @@ void attn_bwd_mfma(DType dt, const void* qkv, const void* o, const float* lse, c
   dim3 grid_kv(nkb * (fuseg ? G : H) * B), grid_q(((T_ + DQ_BQ - 1) / DQ_BQ) * H * B);
   const bool drop = p > 0.f;
   const BwdArgs a{qkv, o, dout, lse, delta, dkv_part, dqkv, T_, H, G, B, causal, drop_threshold16(p),
-                  drop_inv_keep(p), seed, offset, drop ? keep_mask : nullptr, s};
+                  drop_inv_keep(p), seed, offset, drop ? keep_mask : nullptr, rcos, rsin, s};
   if (dt == DType::BF16) {
     if (hd == 128) launch_bwd<bf16_t, 128>(a, drop, q_variant, kv_variant, fuseg, kv_dual, kv_vlds, grid_q, grid_kv);
     else launch_bwd<bf16_t, 64>(a, drop, q_variant, kv_variant, fuseg, kv_dual, kv_vlds, grid_q, grid_kv);
@@ -877,7 +957,8 @@ void attn_bwd_mfma(DType dt, const void* qkv, const void* o, const float* lse, c
     const long groups = BT * 2L * G * hd / 4;
     const int fg = (int)((groups + 255) / 256 < 4096 ? (groups + 255) / 256 : 4096);
     BLLM_DISPATCH(dt, TT, {
-      hipLaunchKernelGGL(attn_bwd_kv_reduce_k<TT>, dim3(fg), dim3(256), 0, s, dkv_part, (TT*)dqkv, BT, H, G, hd);
+      hipLaunchKernelGGL(attn_bwd_kv_reduce_k<TT>, dim3(fg), dim3(256), 0, s, dkv_part, (TT*)dqkv, BT, H, G, hd, T_,
+                         rcos, rsin);
     });
   }
 }

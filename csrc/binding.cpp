@@ -188,7 +188,18 @@ Tensor swiglu_bwd(const Tensor& gu, const Tensor& dact) {
   const int64_t N = gu.size(0), F = gu.size(1) / 2;
   TORCH_CHECK(dact.size(0) == N && dact.size(1) == F && dact.scalar_type() == gu.scalar_type());
   auto dgu = at::empty_like(gu);
-  bllm::swiglu_bwd(dt_of(gu), gu.data_ptr(), dact.data_ptr(), dgu.data_ptr(), N, F, stream());
+  bllm::swiglu_bwd(dt_of(gu), gu.data_ptr(), dact.data_ptr(), dgu.data_ptr(), nullptr, N, F, stream());
+  return dgu;
+}
+
+// dgu as swiglu_bwd, and dact is overwritten in place by act = silu(g) * u
+Tensor swiglu_bwd_act(const Tensor& gu, Tensor& dact) {
+  check_gpu(gu, "gu"); check_gpu(dact, "dact");
+  c10::DeviceGuard g(gu.device());
+  const int64_t N = gu.size(0), F = gu.size(1) / 2;
+  TORCH_CHECK(dact.size(0) == N && dact.size(1) == F && dact.scalar_type() == gu.scalar_type());
+  auto dgu = at::empty_like(gu);
+  bllm::swiglu_bwd(dt_of(gu), gu.data_ptr(), dact.data_ptr(), dgu.data_ptr(), dact.data_ptr(), N, F, stream());
   return dgu;
 }
 
@@ -394,9 +405,18 @@ std::tuple<Tensor, Tensor> flash_attn_fwd(const Tensor& qkv, int64_t B, int64_t 
   return {o, lse};
 }
 
+// fp32 [>= T, hd/2] RoPE table for the inverse rotation fused into the attention backward
+static const float* rope_ptr(const optional<Tensor>& t, const Tensor& qkv, int64_t T, int64_t hd) {
+  if (!t.has_value() || !t->defined()) return nullptr;
+  TORCH_CHECK(t->device() == qkv.device() && t->scalar_type() == at::kFloat && t->is_contiguous() && t->dim() == 2 &&
+              t->size(0) >= T && t->size(1) == hd / 2, "flash_attn_bwd: rope table must be fp32 [>= T, hd/2] on the qkv device");
+  return t->data_ptr<float>();
+}
+
 Tensor flash_attn_bwd(const Tensor& qkv, const Tensor& o, const Tensor& lse, const Tensor& dout, int64_t B,
                       int64_t T, int64_t H, int64_t G, int64_t hd, bool causal, double p, int64_t seed,
-                      int64_t offset, const optional<Tensor>& keep_mask) {
+                      int64_t offset, const optional<Tensor>& keep_mask, const optional<Tensor>& rope_cos,
+                      const optional<Tensor>& rope_sin) {
   check_gpu(qkv, "qkv"); check_gpu(o, "o"); check_gpu(lse, "lse"); check_gpu(dout, "dout");
   c10::DeviceGuard g(qkv.device());
   TORCH_CHECK(qkv.scalar_type() == at::kBFloat16 || qkv.scalar_type() == at::kHalf ||
@@ -413,7 +433,8 @@ Tensor flash_attn_bwd(const Tensor& qkv, const Tensor& o, const Tensor& lse, con
   auto dkv_part = (mfma && bllm::attn_bwd_kv_partials((int)B, (int)T, (int)H, (int)G)) ? at::empty({2, B * T, H, hd}, qkv.options().dtype(at::kFloat)) : Tensor();
   bllm::attn_bwd(dt_of(qkv), qkv.data_ptr(), o.data_ptr(), lse.data_ptr<float>(), dout.data_ptr(), dqkv.data_ptr(),
                  delta.data_ptr<float>(), nullptr, dkv_part.defined() ? dkv_part.data_ptr<float>() : nullptr, (int)B, (int)T, (int)H, (int)G, (int)hd, causal,
-                 (float)p, (uint64_t)seed, (uint64_t)offset, keep_mask_ptr(keep_mask, qkv, B, T, H, hd, p), stream());
+                 (float)p, (uint64_t)seed, (uint64_t)offset, keep_mask_ptr(keep_mask, qkv, B, T, H, hd, p),
+                 rope_ptr(rope_cos, qkv, T, hd), rope_ptr(rope_sin, qkv, T, hd), stream());
   return dqkv;
 }
 
@@ -822,6 +843,7 @@ TORCH_LIBRARY(bllm, m) {
   m.def("linear_residual(Tensor x, Tensor W, Tensor C) -> Tensor");
   m.def("swiglu_fwd(Tensor gu) -> Tensor");
   m.def("swiglu_bwd(Tensor gu, Tensor dact) -> Tensor");
+  m.def("swiglu_bwd_act(Tensor gu, Tensor(a!) dact) -> Tensor");
   m.def("gelu_fwd(Tensor f) -> Tensor");
   m.def("gelu_bwd(Tensor f, Tensor dg) -> Tensor");
   m.def("rope_(Tensor(a!) qkv, Tensor cos, Tensor sin, int T, int H, int G, int hd, bool inverse, int pos_offset) -> ()");
@@ -834,7 +856,7 @@ TORCH_LIBRARY(bllm, m) {
   m.def("attn_decode_append(Tensor qkv, Tensor(a!) kcache, Tensor(b!) vcache, Tensor pos, int H, int G) -> Tensor");
   m.def("rope_dev_(Tensor(a!) qkv, Tensor cos, Tensor sin, int H, int G, int hd, Tensor pos) -> ()");
   m.def("flash_attn_fwd(Tensor qkv, int B, int T, int H, int G, int hd, bool causal, float p, int seed, int offset, Tensor(a!)? keep_mask=None) -> (Tensor, Tensor)");
-  m.def("flash_attn_bwd(Tensor qkv, Tensor o, Tensor lse, Tensor dout, int B, int T, int H, int G, int hd, bool causal, float p, int seed, int offset, Tensor? keep_mask=None) -> Tensor");
+  m.def("flash_attn_bwd(Tensor qkv, Tensor o, Tensor lse, Tensor dout, int B, int T, int H, int G, int hd, bool causal, float p, int seed, int offset, Tensor? keep_mask=None, Tensor? rope_cos=None, Tensor? rope_sin=None) -> Tensor");
   m.def("ce_fwd(Tensor logits, Tensor targets, int ignore_index) -> (Tensor, Tensor)");
   m.def("ce_bwd_(Tensor(a!) logits, Tensor targets, Tensor lse, Tensor scale, int ignore_index) -> ()");
   m.def("embedding_fwd(Tensor idx, Tensor wte, Tensor? wpe, int T, float p, int seed, int offset) -> Tensor");
@@ -858,6 +880,7 @@ TORCH_LIBRARY_IMPL(bllm, CUDA, m) {
   m.impl("linear_residual", &linear_residual);
   m.impl("swiglu_fwd", &swiglu_fwd);
   m.impl("swiglu_bwd", &swiglu_bwd);
+  m.impl("swiglu_bwd_act", &swiglu_bwd_act);
   m.impl("gelu_fwd", &gelu_fwd);
   m.impl("gelu_bwd", &gelu_bwd);
   m.impl("rope_", &rope_);

@@ -44,24 +44,26 @@ __global__ __launch_bounds__(256) void swiglu_fwd_k(const T* __restrict__ gu, T*
 }
 
 template <typename T, int VEC>
-__global__ __launch_bounds__(256) void swiglu_bwd_k(const T* __restrict__ gu, const T* __restrict__ dact,
-                                                    T* __restrict__ dgu, long N, int F) {
+__global__ __launch_bounds__(256) void swiglu_bwd_k(const T* __restrict__ gu, const T* dact,
+                                                    T* __restrict__ dgu, T* act, long N, int F) {
   const int fv = F / VEC;
   const long total = N * fv;
   for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
     const long r = i / fv;
     const int c = (int)(i - r * fv) * VEC;
     VecN<T, VEC> g = ldv<T, VEC>(gu + r * 2 * F + c), u = ldv<T, VEC>(gu + r * 2 * F + F + c), d = ldv<T, VEC>(dact + r * F + c);
-    VecN<T, VEC> dg, du;
+    VecN<T, VEC> dg, du, o;
 #pragma unroll
     for (int j = 0; j < VEC; ++j) {
       const float a = to_f(g.v[j]), b = to_f(u.v[j]), dd = to_f(d.v[j]);
       const float sg = 1.f / (1.f + __expf(-a));
       dg.v[j] = from_f<T>(dd * b * sg * (1.f + a * (1.f - sg)));
       du.v[j] = from_f<T>(dd * a * sg);
+      o.v[j] = from_f<T>(a / (1.f + __expf(-a)) * b);  // bitwise as swiglu_fwd
     }
     stv<T, VEC>(dgu + r * 2 * F + c, dg);
     stv<T, VEC>(dgu + r * 2 * F + F + c, du);
+    if (act) stv<T, VEC>(act + r * F + c, o);
   }
 }
 
@@ -101,8 +103,8 @@ __global__ __launch_bounds__(256) void swiglu_fwd_rows_k(const T* __restrict__ g
 }
 
 template <typename T, int VEC, int U>
-__global__ __launch_bounds__(256) void swiglu_bwd_rows_k(const T* __restrict__ gu, const T* __restrict__ dact,
-                                                         T* __restrict__ dgu, int F) {
+__global__ __launch_bounds__(256) void swiglu_bwd_rows_k(const T* __restrict__ gu, const T* dact,
+                                                         T* __restrict__ dgu, T* act, int F) {
   const int fv = F / VEC;
   const long row = blockIdx.x;
   const T* g0 = gu + row * 2 * F;
@@ -110,6 +112,7 @@ __global__ __launch_bounds__(256) void swiglu_bwd_rows_k(const T* __restrict__ g
   const T* d0 = dact + row * F;
   T* dg0 = dgu + row * 2 * F;
   T* du0 = dg0 + F;
+  T* a0 = act ? act + row * F : nullptr;
   for (int base = threadIdx.x; base < fv; base += 256 * U) {
     VecN<T, VEC> g[U], u[U], d[U];
 #pragma unroll
@@ -125,16 +128,18 @@ __global__ __launch_bounds__(256) void swiglu_bwd_rows_k(const T* __restrict__ g
     for (int k = 0; k < U; ++k) {
       const int c = base + k * 256;
       if (c < fv) {
-        VecN<T, VEC> dg, du;
+        VecN<T, VEC> dg, du, o;
 #pragma unroll
         for (int j = 0; j < VEC; ++j) {
           const float a = to_f(g[k].v[j]), b = to_f(u[k].v[j]), dd = to_f(d[k].v[j]);
           const float sg = 1.f / (1.f + __expf(-a));
           dg.v[j] = from_f<T>(dd * b * sg * (1.f + a * (1.f - sg)));
           du.v[j] = from_f<T>(dd * a * sg);
+          o.v[j] = from_f<T>(a / (1.f + __expf(-a)) * b);  // bitwise as swiglu_fwd
         }
         stv<T, VEC>(dg0 + c * VEC, dg);
         stv<T, VEC>(du0 + c * VEC, du);
+        if (a0) stv<T, VEC>(a0 + c * VEC, o);
       }
     }
   }
@@ -341,15 +346,15 @@ void swiglu_fwd(DType dt, const void* gu, void* act, long N, int F, hipStream_t 
     });
   });
 }
-void swiglu_bwd(DType dt, const void* gu, const void* dact, void* dgu, long N, int F, hipStream_t s) {
+void swiglu_bwd(DType dt, const void* gu, const void* dact, void* dgu, void* act, long N, int F, hipStream_t s) {
   BLLM_DISPATCH(dt, T, {
     EW_VEC(T, F % (16 / sizeof(T)) == 0, {
       if (swiglu_rows() && F / VEC >= 512 && N <= 0x7fffffffL) {
         hipLaunchKernelGGL((swiglu_bwd_rows_k<T, VEC, 4>), dim3((unsigned)N), dim3(256), 0, s, (const T*)gu,
-                           (const T*)dact, (T*)dgu, F);
+                           (const T*)dact, (T*)dgu, (T*)act, F);
       } else {
         hipLaunchKernelGGL((swiglu_bwd_k<T, VEC>), dim3(ew_grid(N * F / VEC)), dim3(256), 0, s, (const T*)gu,
-                           (const T*)dact, (T*)dgu, N, F);
+                           (const T*)dact, (T*)dgu, (T*)act, N, F);
       }
     });
   });

@@ -82,7 +82,12 @@ def test_swiglu_gelu(dt, F):
     da = torch.randn(33, F, device=DEV).to(dt)
     _close(ops.swiglu_fwd(gu), ref.swiglu_fwd(gu.cpu().float()), dt, name="swiglu")
     _close(ops.swiglu_bwd(gu, da), ref.swiglu_bwd(gu.cpu().float(), da.cpu().float()), dt, 2, name="swiglu_bwd")
-    f = torch.randn(33, F, device=DEV).to(dt)
+    # fused variant: same dgu, and act written in place of dact
+    da2 = da.clone()
+    dgu2 = ops.swiglu_bwd_act(gu, da2)
+    assert torch.equal(dgu2, ops.swiglu_bwd(gu, da))
+    assert torch.equal(da2, ops.swiglu_fwd(gu))
+    f =torch.randn(33, F, device=DEV).to(dt)
     _close(ops.gelu_fwd(f), ref.gelu_fwd(f.cpu().float()), dt, name="gelu")
     _close(ops.gelu_bwd(f, da), ref.gelu_bwd(f.cpu().float(), da.cpu().float()), dt, name="gelu_bwd")
 
@@ -300,8 +305,30 @@ def test_flash_attention_keep_mask_fused_gqa(hd):
     test_flash_attention_keep_mask(hd, 128, 128, 16, 8, True)
 
 
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16, torch.float32])
+@pytest.mark.parametrize("B,T,H,G,hd", [(2, 200, 4, 4, 128),     # MHA: dK written by the dK/dV kernel
+                                         (1, 300, 8, 2, 128),     # GQA: fp32 partials + reduce kernel
+                                         (128, 128, 16, 8, 128),  # GQA heads fused in one workgroup
+                                         (2, 130, 4, 2, 64), (128, 128, 16, 8, 64)])
+def test_flash_attention_bwd_fused_rope(dt, B, T, H, G, hd):
+    """``flash_attn_bwd(..., rope=(cos, sin))`` un-rotates dQ / dK in the kernels' epilogues:
+    equal (to rounding) to the backward followed by the separate inverse ``rope_`` pass, and to
+    the fp32 oracle of that composition."""
+    cos, sin = ops.rope_tables(hd, 512, 500000.0, device=DEV)
+    qkv = torch.randn(B * T, (H + 2 * G) * hd, device=DEV).to(dt)
+    do = torch.randn(B * T, H * hd, device=DEV).to(dt)
+    o, lse = ops.flash_attn_fwd(qkv, B, T, H, G, hd, True)
+    fused = ops.flash_attn_bwd(qkv, o, lse, do, B, T, H, G, hd, True, rope=(cos, sin))
+    sep = ops.flash_attn_bwd(qkv, o, lse, do, B, T, H, G, hd, True)
+    ops.rope_(sep, cos, sin, T, H, G, hd, inverse=True)
+    _close(fused, sep.float().cpu(), dt, 2, name="fused vs separate")
+    want = ref.flash_attn_bwd(qkv.float(), o.float(), lse, do.float(), B, T, H, G, hd, True)
+    ref.rope_(want, cos, sin, T, H, G, hd, inverse=True)
+    _close(fused, want.cpu(), dt, 4, name="fused vs oracle")
+
+
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
-@pytest.mark.parametrize("B,H,G,hd,L,Tmax", [(2, 8, 2, 128, 37, 64), (1, 4, 4, 64, 1, 16), (3, 32, 8, 128, 1000, 1024)])
+@pytest.mark.parametrize("B,H,G,hd,L,Tmax",[(2, 8, 2, 128, 37, 64), (1, 4, 4, 64, 1, 16), (3, 32, 8, 128, 1000, 1024)])
 def test_attn_decode(dt, B, H, G, hd, L, Tmax):
     q = torch.randn(B, H, hd, device=DEV).to(dt)
     kc = torch.randn(B, G, Tmax, hd, device=DEV).to(dt)
