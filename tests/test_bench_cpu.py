@@ -1,4 +1,4 @@
-"""bench.py's distributed branch, executed: torchrun at world 2 and 4 on gloo (``--device cpu``
+"""bench.py's distributed branch, executed: torchrun at world 2, 4 (and 8 for FSDP) on gloo (``--device cpu``
 tiny config) for every engine and preset, checking the driver's JSON-line contract.  On the GPU
 node the same code path runs with RCCL; only the backend and the model size differ."""
 import json
@@ -47,6 +47,11 @@ def test_bench_torchrun_gloo(n, parallel):
     assert out["config"]["parallelism"] == f"{parallel}{n}"
     assert out["config"]["global_batch"] == 2 * n
     assert out["config"]["actv_ckpt"] == "full"
+
+
+def test_bench_torchrun_gloo_world8_fsdp():
+    """The driver's largest scaling point (8 ranks, FSDP full-shard + full checkpointing)."""
+    test_bench_torchrun_gloo(8, "fsdp")
 
 
 def test_bench_world1_uses_fsdp_engine():
