@@ -16,6 +16,8 @@ in-kernel dropout[HIP MFMA] -> out-proj GEMM (+bias) -> dropout+residual[HIP] ->
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn as nn
 
@@ -106,6 +108,19 @@ def _ln_bwd(unit, norm, dy, x, mean, rstd, dx_acc, acc):
     dx, _, _ = ops.layernorm_bwd(dy, x, unit.data(norm.weight), mean, rstd, dx_acc, unit.grad(norm.weight),
                                  unit.grad(norm.bias), acc)
     return dx
+
+
+# BLLM_FUSED_BIAS=0: bias gradients by the separate column-sum pass (A/B)
+FUSED_BIAS = os.environ.get("BLLM_FUSED_BIAS", "1") != "0"
+
+
+def _drop_bwd_bias(lin, dy, p, seed, offset, acc):
+    """dropout backward of ``dy`` with ``lin``'s bias gradient summed in the same pass (when it
+    has a trainable bias and dropout is on); returns (d, bias_done)."""
+    gb = lin.bias_grad_buf() if FUSED_BIAS else None
+    if gb is not None and p > 0.0:
+        return ops.dropout_bwd_bias(dy, p, seed, offset, gb, acc), True
+    return ops.dropout_bwd(dy, p, seed, offset), False
 
 
 class GPTBlockCompute(UnitCompute):
@@ -207,19 +222,24 @@ class GPTBlockCompute(UnitCompute):
         xa_qkv, xa_o, xa_fc, xa_pr = s["xa"]
         dy2 = dy.reshape(N, d)
         # ---- MLP branch: x3 = x2 + drop(proj(gelu(fc(ln2(x2)))))
-        dm = ops.dropout_bwd(dy2, p, rc.seed, offs[2])
+        # the bias-gradient column sums ride along in the dropout / GELU backward passes
+        dm, pr_b = _drop_bwd_bias(self.proj, dy2, p, rc.seed, offs[2], acc)
         g = s["g"] if "g" in s else ops.gelu_fwd(s["f"])
-        dg = self.proj.backward(dm, g, xa_pr, accumulate=acc)
+        dg = self.proj.backward(dm, g, xa_pr, accumulate=acc, bias_done=pr_b)
         del dm, g
-        df = ops.gelu_bwd(s["f"], dg)
+        gb = self.fc.bias_grad_buf() if FUSED_BIAS else None
+        if gb is not None:
+            df = ops.gelu_bwd_bias(s["f"], dg, gb, acc)
+        else:
+            df = ops.gelu_bwd(s["f"], dg)
         del dg
         h2 = s["h2"] if "h2" in s else self._ln(s["x2"], b.norm2)[0]
-        dh2 = self.fc.backward(df, h2, xa_fc, accumulate=acc)
+        dh2 = self.fc.backward(df, h2, xa_fc, accumulate=acc, bias_done=gb is not None)
         del df, h2
         dx2 = _ln_bwd(u, b.norm2, dh2, s["x2"], s["m2"], s["r2"], dy2, acc)
         # ---- attention branch: x2 = x + drop(out_proj(attn(ln1(x))))
-        da = ops.dropout_bwd(dx2, p, rc.seed, offs[1])
-        d_o = self.o.backward(da, s["o"], xa_o, accumulate=acc)
+        da, o_b = _drop_bwd_bias(self.o, dx2, p, rc.seed, offs[1], acc)
+        d_o = self.o.backward(da, s["o"], xa_o, accumulate=acc, bias_done=o_b)
         del da
         dqkv = ops.flash_attn_bwd(s["qkv"], s["o"], s["lse"], d_o, B, T, H, H, hd, True, p, rc.seed, offs[0],
                                   keep_mask=s.get("km"))

@@ -287,14 +287,19 @@ class FusedLinear:
         return [torch.mm(x, u.data(s.lora_A)) if s.lora_A is not None else None for s in self.specs]
 
     # ------------------------------------------------------------------ bwd
+    def bias_grad_buf(self) -> Optional[torch.Tensor]:
+        """The flat gradient view of the fused bias (None: no bias or frozen); a caller that fills
+        it itself passes ``bias_done=True`` to ``backward``."""
+        return self.unit.fused_grad(self.b_params) if self.b_params is not None else None
+
     def backward(self, dy: torch.Tensor, x: torch.Tensor, xa, need_dx: bool = True,
-                 accumulate: bool = False, dx_acc: Optional[torch.Tensor] = None):
+                 accumulate: bool = False, dx_acc: Optional[torch.Tensor] = None, bias_done: bool = False):
         """Returns dx (plus ``dx_acc`` if given) and writes parameter grads into the flat."""
         u = self.unit
         gW = u.fused_grad(self.W_params)
         if gW is not None:
             _weight_grad(dy, x, gW, accumulate)
-        if self.b_params is not None:
+        if self.b_params is not None and not bias_done:
             gb = u.fused_grad(self.b_params)
             if gb is not None:
                 ops.bias_grad_(dy, gb, accumulate)

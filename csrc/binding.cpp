@@ -257,6 +257,28 @@ void bias_grad_(const Tensor& dy, Tensor& db, bool accumulate) {
                   stream());
 }
 
+// fused elementwise backward + bias grad: op 0 = dropout backward of src (p, seed, offset),
+// op 1 = exact-GELU backward (src = dg, aux = f); returns the elementwise result, db (+)= its column sums
+Tensor bwd_bias_grad_(const Tensor& src, const optional<Tensor>& aux, Tensor& db, bool accumulate, int64_t op,
+                      double p, int64_t seed, int64_t offset) {
+  check_gpu(src, "src"); check_gpu(db, "db");
+  c10::DeviceGuard g(src.device());
+  TORCH_CHECK(src.dim() == 2 && src.is_contiguous() && db.dim() == 1 && db.size(0) == src.size(1), "bwd_bias_grad: shapes");
+  TORCH_CHECK(op == 0 || op == 1, "bwd_bias_grad: op");
+  const int N = (int)src.size(0), F = (int)src.size(1);
+  TORCH_CHECK(F % (16 / (int)src.element_size()) == 0, "bwd_bias_grad: F must be a multiple of 16 bytes");
+  if (op == 1) {
+    TORCH_CHECK(aux.has_value() && aux->sizes() == src.sizes() && aux->is_contiguous() &&
+                aux->scalar_type() == src.scalar_type() && aux->device() == src.device(), "bwd_bias_grad: gelu input");
+  }
+  auto out = at::empty_like(src);
+  auto part = at::empty({bllm::colsum_bands(N, F), F}, src.options().dtype(at::kFloat));
+  bllm::bwd_bias_grad(dt_of(src), dt_of(db), (int)op, src.data_ptr(), op == 1 ? aux->data_ptr() : nullptr,
+                      out.data_ptr(), part.data_ptr<float>(), db.data_ptr(), N, F, accumulate, (float)p,
+                      (uint64_t)seed, (uint64_t)offset, stream());
+  return out;
+}
+
 // out (+)= part.sum(0): part [S, ...] any float dtype, out contiguous with part[0]'s numel
 void sum_partials_(const Tensor& part, Tensor& out, bool accumulate) {
   check_gpu(part, "part"); check_gpu(out, "out");
@@ -839,6 +861,7 @@ TORCH_LIBRARY(bllm, m) {
   m.def("layernorm_bwd(Tensor dy, Tensor x, Tensor w, Tensor mean, Tensor rstd, Tensor? dx_acc, Tensor(a!)? dw_out, Tensor(b!)? db_out, bool accumulate) -> (Tensor, Tensor, Tensor)");
   m.def("dropout_add(Tensor x, Tensor a, float p, int seed, int offset) -> Tensor");
   m.def("dropout_bwd(Tensor dy, float p, int seed, int offset) -> Tensor");
+  m.def("bwd_bias_grad_(Tensor src, Tensor? aux, Tensor(a!) db, bool accumulate, int op, float p, int seed, int offset) -> Tensor");
   m.def("transpose2d(Tensor a) -> Tensor");
   m.def("linear_residual(Tensor x, Tensor W, Tensor C) -> Tensor");
   m.def("swiglu_fwd(Tensor gu) -> Tensor");
@@ -876,6 +899,7 @@ TORCH_LIBRARY_IMPL(bllm, CUDA, m) {
   m.impl("layernorm_bwd", &layernorm_bwd);
   m.impl("dropout_add", &dropout_add);
   m.impl("dropout_bwd", &dropout_bwd);
+  m.impl("bwd_bias_grad_", &bwd_bias_grad_);
   m.impl("transpose2d", &transpose2d);
   m.impl("linear_residual", &linear_residual);
   m.impl("swiglu_fwd", &swiglu_fwd);

@@ -314,6 +314,93 @@ int colsum_bands(int N, int F) {
   return N >= 16 * cap ? cap : (N + 15) / 16;
 }
 
+// Elementwise backward + bias-gradient column sums in one pass (GPT-2: the dropout backward in
+// front of the out_proj / c_proj bias grads, the GELU backward in front of the c_fc bias grad,
+// reference GPT2.py:58-62 + nn.Linear bias).  Same band split, per-lane row order and fp32
+// partials as colsum_partial_k over the rounded outputs, so db is bitwise the separate path's;
+// the separate colsum pass's re-read of the [N, F] gradient is gone.
+//   OP 0: out = dropout_bwd(src)  (keep bits by the counter hash at element index r * F + c)
+//   OP 1: out = src * gelu'(aux)   (exact erf GELU)
+template <typename T, int OP>
+__global__ __launch_bounds__(256) void bwd_colsum_k(const T* __restrict__ src, const T* __restrict__ aux,
+                                                    T* __restrict__ out, float* __restrict__ part, int N, int F,
+                                                    int rows_per, uint64_t seed, uint64_t offset, uint32_t thr,
+                                                    float inv_keep) {
+  constexpr int VEC = 16 / sizeof(T);
+  const int cv = blockIdx.x * 256 + threadIdx.x;
+  if (cv * VEC >= F) return;
+  const int r0 = blockIdx.y * rows_per, r1 = min(N, r0 + rows_per);
+  float acc[VEC];
+#pragma unroll
+  for (int j = 0; j < VEC; ++j) acc[j] = 0.f;
+  auto row = [&](int r, const Vec16<T>& v, const Vec16<T>& a) {
+    const long e = (long)r * F + cv * VEC;
+    Vec16<T> o;
+    if constexpr (OP == 0) {
+      uint32_t bits[VEC];
+      drop_bits_run<VEC>(seed, offset + (uint64_t)e, bits);
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) o.v[j] = from_f<T>(bits[j] >= thr ? to_f(v.v[j]) * inv_keep : 0.f);
+    } else {
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) {
+        const float x = to_f(a.v[j]);
+        const float cdf = 0.5f * (1.f + erff(x * 0.70710678118654752f));
+        const float pdf = __expf(-0.5f * x * x) * 0.39894228040143268f;
+        o.v[j] = from_f<T>(to_f(v.v[j]) * (cdf + x * pdf));
+      }
+    }
+    st16(out + e, o);
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) {
+      // opaque copy: for fp32 (from_f = identity) the compiler would otherwise fuse the output
+      // product into the column sum (one FMA), skipping the rounding the stored output had --
+      // the sums must match colsum_partial_k over the stored values bitwise
+      float ov = to_f(o.v[j]);
+      asm volatile("" : "+v"(ov));
+      acc[j] += ov;
+    }
+  };
+  int r = r0;
+  for (; r + 4 <= r1; r += 4) {  // 4 independent row loads (x2 with the GELU input) in flight per lane
+    Vec16<T> v[4], a[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      v[k] = ld16(src + (long)(r + k) * F + cv * VEC);
+      if constexpr (OP == 1) a[k] = ld16(aux + (long)(r + k) * F + cv * VEC);
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) row(r + k, v[k], a[k]);
+  }
+  for (; r < r1; ++r) {
+    Vec16<T> v = ld16(src + (long)r * F + cv * VEC), a;
+    if constexpr (OP == 1) a = ld16(aux + (long)r * F + cv * VEC);
+    row(r, v, a);
+  }
+  float* o = part + (long)blockIdx.y * F + cv * VEC;
+#pragma unroll
+  for (int j = 0; j < VEC; ++j) o[j] = acc[j];
+}
+
+void bwd_bias_grad(DType dt, DType odt, int op, const void* src, const void* aux, void* out, float* part, void* db,
+                   int N, int F, bool accumulate, float p, uint64_t seed, uint64_t offset, hipStream_t s) {
+  const int P = colsum_bands(N, F);
+  const int rows_per = (N + P - 1) / P;
+  const uint32_t thr = drop_threshold16(p);
+  const float inv_keep = drop_inv_keep(p);
+  BLLM_DISPATCH(dt, T, {
+    constexpr int VEC = 16 / sizeof(T);
+    dim3 grid((F / VEC + 255) / 256, P);
+    if (op == 0)
+      hipLaunchKernelGGL((bwd_colsum_k<T, 0>), grid, dim3(256), 0, s, (const T*)src, (const T*)aux, (T*)out, part, N, F,
+                         rows_per, seed, offset, thr, inv_keep);
+    else
+      hipLaunchKernelGGL((bwd_colsum_k<T, 1>), grid, dim3(256), 0, s, (const T*)src, (const T*)aux, (T*)out, part, N, F,
+                         rows_per, seed, offset, thr, inv_keep);
+  });
+  col_reduce(part, odt, db, P, F, accumulate, s);
+}
+
 // dy [N, F] (F % (16/sizeof(T)) == 0), out [F] in dtype odt (written, or added when accumulate)
 void bias_grad(DType dt, DType odt, const void* dy, float* part, void* out, int N, int F, bool accumulate,
                hipStream_t s) {

@@ -87,7 +87,7 @@ def test_swiglu_gelu(dt, F):
     dgu2 = ops.swiglu_bwd_act(gu, da2)
     assert torch.equal(dgu2, ops.swiglu_bwd(gu, da))
     assert torch.equal(da2, ops.swiglu_fwd(gu))
-    f =torch.randn(33, F, device=DEV).to(dt)
+    f = torch.randn(33, F, device=DEV).to(dt)
     _close(ops.gelu_fwd(f), ref.gelu_fwd(f.cpu().float()), dt, name="gelu")
     _close(ops.gelu_bwd(f, da), ref.gelu_bwd(f.cpu().float(), da.cpu().float()), dt, name="gelu_bwd")
 
@@ -347,6 +347,27 @@ def test_bias_grad(dt, N, F, acc):
     ref0 = dy.float().sum(0) + (db.float() if acc else 0)
     ops.bias_grad_(dy, db, acc)
     _close(db, ref0.cpu(), dt, 4, name="bias_grad")
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+@pytest.mark.parametrize("N,F", [(24576, 1280), (24576, 5120), (1000, 768), (37, 64)])
+@pytest.mark.parametrize("acc", [False, True])
+def test_bwd_bias_grad_fused(dt, N, F, acc):
+    """dropout / GELU backward with the bias column sums in the same pass: outputs and db
+    bitwise equal to the separate kernels (same bands, same per-lane row order)."""
+    dy = torch.randn(N, F, device=DEV).to(dt)
+    f = torch.randn(N, F, device=DEV).to(dt)
+    db0 = torch.randn(F, device=DEV).to(dt)
+    for name, fused, sep in (
+            ("dropout", lambda db: ops.dropout_bwd_bias(dy, 0.1, 1234, 77, db, acc),
+             lambda: ops.dropout_bwd(dy, 0.1, 1234, 77)),
+            ("gelu", lambda db: ops.gelu_bwd_bias(f, dy, db, acc), lambda: ops.gelu_bwd(f, dy))):
+        db1, db2 = db0.clone(), db0.clone()
+        out1 = fused(db1)
+        out2 = sep()
+        ops.bias_grad_(out2, db2, acc)
+        assert torch.equal(out1, out2), name
+        assert torch.equal(db1, db2), name
 
 
 # ------------------------------------------------------------------ LoRA (csrc/lora.hip)
