@@ -112,6 +112,8 @@ def _ln_bwd(unit, norm, dy, x, mean, rstd, dx_acc, acc):
 
 # BLLM_FUSED_BIAS=0: bias gradients by the separate column-sum pass (A/B)
 FUSED_BIAS = os.environ.get("BLLM_FUSED_BIAS", "1") != "0"
+# BLLM_RECOMPUTE_FUSED=0: the checkpoint recompute runs its GELU forward as a separate pass (A/B)
+RECOMPUTE_FUSED = os.environ.get("BLLM_RECOMPUTE_FUSED", "1") != "0"
 
 
 def _drop_bwd_bias(lin, dy, p, seed, offset, acc):
@@ -197,18 +199,24 @@ class GPTBlockCompute(UnitCompute):
         del a
         h2, m2, r2 = self._ln(x2, b.norm2)
         f, xa_fc = self.fc.forward(h2)
-        g = ops.gelu_fwd(f)
-        if recompute:
+        if recompute and not self.proj.has_lora and RECOMPUTE_FUSED:
+            # backward rebuilds g inside the GELU backward pass (ops.gelu_bwd_act)
+            g, x3, xa_pr = None, None, None
+        elif recompute:
+            g = ops.gelu_fwd(f)
             x3, xa_pr = None, self.proj.lora_state(g)
         else:
+            g = ops.gelu_fwd(f)
             m, xa_pr = self.proj.forward(g)
             x3 = ops.dropout_add(x2, m, p, rc.seed, offs[2])
         if not save:
             # full-recompute mode: _BlockFn keeps ``offs`` as the replay token so the
             # recomputed forward regenerates identical dropout masks
             return x3.view(B, T, d), offs
-        saved = dict(x=x2d, m1=m1, r1=r1, qkv=qkv, o=o, lse=lse, km=km, x2=x2, m2=m2, r2=r2, f=f, g=g,
+        saved = dict(x=x2d, m1=m1, r1=r1, qkv=qkv, o=o, lse=lse, km=km, x2=x2, m2=m2, r2=r2, f=f,
                      p=p, offs=offs, xa=(xa_qkv, xa_o, xa_fc, xa_pr))
+        if g is not None:
+            saved["g"] = g
         if rc.block_mode(self.index) == "none" or recompute:  # the recompute's norm outputs live one block
             saved.update(h1=h1, h2=h2)
         return (x3.view(B, T, d) if x3 is not None else None), saved
@@ -224,14 +232,22 @@ class GPTBlockCompute(UnitCompute):
         # ---- MLP branch: x3 = x2 + drop(proj(gelu(fc(ln2(x2)))))
         # the bias-gradient column sums ride along in the dropout / GELU backward passes
         dm, pr_b = _drop_bwd_bias(self.proj, dy2, p, rc.seed, offs[2], acc)
-        g = s["g"] if "g" in s else ops.gelu_fwd(s["f"])
-        dg = self.proj.backward(dm, g, xa_pr, accumulate=acc, bias_done=pr_b)
-        del dm, g
         gb = self.fc.bias_grad_buf() if FUSED_BIAS else None
-        if gb is not None:
-            df = ops.gelu_bwd_bias(s["f"], dg, gb, acc)
+        if "g" in s or self.proj.has_lora:
+            g = s["g"] if "g" in s else ops.gelu_fwd(s["f"])
+            dg = self.proj.backward(dm, g, xa_pr, accumulate=acc, bias_done=pr_b)
+            del dm, g
+            if gb is not None:
+                df = ops.gelu_bwd_bias(s["f"], dg, gb, acc)
+            else:
+                df = ops.gelu_bwd(s["f"], dg)
         else:
-            df = ops.gelu_bwd(s["f"], dg)
+            # recompute without g: c_proj dX first, then one GELU backward pass that also
+            # rebuilds g in place of dg (and sums the c_fc bias grad), then c_proj's dW from g
+            dg = self.proj.input_grad(dm)
+            df = ops.gelu_bwd_act(s["f"], dg, gb, acc)
+            self.proj.backward(dm, dg, None, need_dx=False, accumulate=acc, bias_done=pr_b)
+            del dm
         del dg
         h2 = s["h2"] if "h2" in s else self._ln(s["x2"], b.norm2)[0]
         dh2 = self.fc.backward(df, h2, xa_fc, accumulate=acc, bias_done=gb is not None)

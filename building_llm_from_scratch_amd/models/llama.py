@@ -160,7 +160,7 @@ class LlamaBlockCompute(UnitCompute):
         x2, xa_o = self.o.forward(o, residual=x2d)
         h2, r2 = ops.rmsnorm_fwd(x2, u.data(b.norm2.weight), eps)
         gu, xa_gu = self.gu.forward(h2)
-        if recompute and not self.down.has_lora:
+        if recompute and not self.down.has_lora and RECOMPUTE_FUSED:
             # backward rebuilds act inside the SwiGLU backward kernel (swiglu_bwd_act)
             act, x3, xa_dn = None, None, None
         else:
@@ -249,6 +249,9 @@ class LlamaBlockCompute(UnitCompute):
         dx, _ = ops.rmsnorm_bwd(dh1, s["x"], w1, s["r1"], dx2, u.grad(b.norm1.weight), acc)
         return dx.view(B, T, d)
 
+
+# BLLM_RECOMPUTE_FUSED=0: the checkpoint recompute runs its SwiGLU forward as a separate pass (A/B)
+RECOMPUTE_FUSED = os.environ.get("BLLM_RECOMPUTE_FUSED", "1") != "0"
 
 # logits chunk budget of the fused head + CE (bytes of one [rows, V] chunk)
 LOGIT_CHUNK_BYTES = int(os.environ.get("BLLM_LOGIT_CHUNK_MB", "2048")) * 2 ** 20

@@ -22,7 +22,7 @@ from ._ext import ext_available, kernel_debug, load_ext
 __all__ = [
     "rmsnorm_fwd", "rmsnorm_bwd", "layernorm_fwd", "layernorm_bwd", "dropout_add", "dropout_bwd",
     "rope_", "rope_tables", "flash_attn_fwd", "flash_attn_bwd", "swiglu_fwd", "swiglu_bwd", "swiglu_bwd_act",
-    "gelu_fwd", "gelu_bwd", "gelu_bwd_bias", "dropout_bwd_bias", "ce_fwd", "ce_bwd_", "embedding_fwd", "embedding_bwd",
+    "gelu_fwd", "gelu_bwd", "gelu_bwd_bias", "gelu_bwd_act", "dropout_bwd_bias", "ce_fwd", "ce_bwd_", "embedding_fwd", "embedding_bwd",
     "sq_norm_multi", "adamw_step_", "attn_decode", "bias_grad_", "ext_available", "load_ext", "attention_backend",
     "lora_down", "lora_up_", "lora_wgrad", "lora_pack_t", "lora_kernel_ok", "sum_partials_",
     "wgrad_gemm_", "wgrad_gemm_ok", "wgrad_gemm_enabled", "wgrad_gemm_preferred", "wgrad_splits",
@@ -130,10 +130,10 @@ def _bwd_bias_ok(t: torch.Tensor) -> bool:
 
 
 def dropout_bwd_bias(dy, p: float, seed: int, offset: int, db, accumulate: bool = False):
-    """``dropout_bwd(dy)`` and db (+)= its column sums, in one pass over dy (bitwise equal to
-    ``bias_grad_`` of the separate result)."""
+    """``dropout_bwd(dy)`` and db (+)= its column sums, in one pass over dy (the output bitwise
+    ``dropout_bwd``'s; the sums as ``bias_grad_`` of it, same bands and order)."""
     if p > 0.0 and _bwd_bias_ok(dy):
-        return _k().bwd_bias_grad_(dy, None, db, bool(accumulate), 0, float(p), int(seed), int(offset))
+        return _k().bwd_bias_grad_(dy, None, db, bool(accumulate), 0, float(p), int(seed), int(offset), False)
     d = dropout_bwd(dy, p, seed, offset)
     bias_grad_(d, db, accumulate)
     return d
@@ -142,9 +142,22 @@ def dropout_bwd_bias(dy, p: float, seed: int, offset: int, db, accumulate: bool 
 def gelu_bwd_bias(f, dg, db, accumulate: bool = False):
     """``gelu_bwd(f, dg)`` and db (+)= its column sums, in one pass."""
     if _bwd_bias_ok(dg) and f.is_contiguous():
-        return _k().bwd_bias_grad_(dg, f, db, bool(accumulate), 1, 0.0, 0, 0)
+        return _k().bwd_bias_grad_(dg, f, db, bool(accumulate), 1, 0.0, 0, 0, False)
     d = gelu_bwd(f, dg)
     bias_grad_(d, db, accumulate)
+    return d
+
+
+def gelu_bwd_act(f, dg, db=None, accumulate: bool = False):
+    """``gelu_bwd(f, dg)`` (returned; db (+)= its column sums if given) and ``dg`` overwritten in
+    place with g = gelu(f), bitwise ``gelu_fwd(f)``: the activation-checkpoint recompute of a
+    GPT-2 block then runs no GELU forward for the c_proj weight gradient."""
+    if _bwd_bias_ok(dg) and f.is_contiguous():
+        return _k().bwd_bias_grad_(dg, f, db, bool(accumulate), 1, 0.0, 0, 0, True)
+    d = gelu_bwd(f, dg)
+    if db is not None:
+        bias_grad_(d, db, accumulate)
+    dg.copy_(gelu_fwd(f))
     return d
 
 

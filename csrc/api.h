@@ -71,8 +71,9 @@ void attn_delta(DType dt, const void* o, const void* dout, float* delta, int B, 
 // elementwise.hip — bias gradient (column sums), part must hold colsum_bands(N, F) * F floats
 int colsum_bands(int N, int F);
 // op 0: out = dropout_bwd(src), op 1: out = src * gelu'(aux); db (+)= out.sum(0) from the same pass
+// (part == nullptr: no sums); op 1 with act: also act = gelu(aux) (may alias src)
 void bwd_bias_grad(DType dt, DType odt, int op, const void* src, const void* aux, void* out, float* part, void* db,
-                   int N, int F, bool accumulate, float p, uint64_t seed, uint64_t offset, hipStream_t s);
+                   int N, int F, bool accumulate, float p, uint64_t seed, uint64_t offset, void* act, hipStream_t s);
 void bias_grad(DType dt, DType odt, const void* dy, float* part, void* out, int N, int F, bool accumulate,
                hipStream_t s);
 

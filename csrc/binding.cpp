@@ -259,11 +259,18 @@ void bias_grad_(const Tensor& dy, Tensor& db, bool accumulate) {
 
 // fused elementwise backward + bias grad: op 0 = dropout backward of src (p, seed, offset),
 // op 1 = exact-GELU backward (src = dg, aux = f); returns the elementwise result, db (+)= its column sums
-Tensor bwd_bias_grad_(const Tensor& src, const optional<Tensor>& aux, Tensor& db, bool accumulate, int64_t op,
-                      double p, int64_t seed, int64_t offset) {
-  check_gpu(src, "src"); check_gpu(db, "db");
+// db None: no bias sums; act_inplace (op 1): src is overwritten with gelu(aux)
+Tensor bwd_bias_grad_(Tensor& src, const optional<Tensor>& aux, const optional<Tensor>& db_, bool accumulate,
+                      int64_t op, double p, int64_t seed, int64_t offset, bool act_inplace) {
+  check_gpu(src, "src");
   c10::DeviceGuard g(src.device());
-  TORCH_CHECK(src.dim() == 2 && src.is_contiguous() && db.dim() == 1 && db.size(0) == src.size(1), "bwd_bias_grad: shapes");
+  const bool has_db = db_.has_value() && db_->defined();
+  TORCH_CHECK(src.dim() == 2 && src.is_contiguous(), "bwd_bias_grad: src");
+  if (has_db) {
+    check_gpu(*db_, "db");
+    TORCH_CHECK(db_->dim() == 1 && db_->size(0) == src.size(1), "bwd_bias_grad: db shape");
+  }
+  TORCH_CHECK(!act_inplace || op == 1, "bwd_bias_grad: act only with the GELU backward");
   TORCH_CHECK(op == 0 || op == 1, "bwd_bias_grad: op");
   const int N = (int)src.size(0), F = (int)src.size(1);
   TORCH_CHECK(F % (16 / (int)src.element_size()) == 0, "bwd_bias_grad: F must be a multiple of 16 bytes");
@@ -272,10 +279,12 @@ Tensor bwd_bias_grad_(const Tensor& src, const optional<Tensor>& aux, Tensor& db
                 aux->scalar_type() == src.scalar_type() && aux->device() == src.device(), "bwd_bias_grad: gelu input");
   }
   auto out = at::empty_like(src);
-  auto part = at::empty({bllm::colsum_bands(N, F), F}, src.options().dtype(at::kFloat));
-  bllm::bwd_bias_grad(dt_of(src), dt_of(db), (int)op, src.data_ptr(), op == 1 ? aux->data_ptr() : nullptr,
-                      out.data_ptr(), part.data_ptr<float>(), db.data_ptr(), N, F, accumulate, (float)p,
-                      (uint64_t)seed, (uint64_t)offset, stream());
+  Tensor part;
+  if (has_db) part = at::empty({bllm::colsum_bands(N, F), F}, src.options().dtype(at::kFloat));
+  bllm::bwd_bias_grad(dt_of(src), has_db ? dt_of(*db_) : dt_of(src), (int)op, src.data_ptr(),
+                      op == 1 ? aux->data_ptr() : nullptr, out.data_ptr(), has_db ? part.data_ptr<float>() : nullptr,
+                      has_db ? db_->data_ptr() : nullptr, N, F, accumulate, (float)p, (uint64_t)seed,
+                      (uint64_t)offset, act_inplace ? src.data_ptr() : nullptr, stream());
   return out;
 }
 
@@ -861,7 +870,7 @@ TORCH_LIBRARY(bllm, m) {
   m.def("layernorm_bwd(Tensor dy, Tensor x, Tensor w, Tensor mean, Tensor rstd, Tensor? dx_acc, Tensor(a!)? dw_out, Tensor(b!)? db_out, bool accumulate) -> (Tensor, Tensor, Tensor)");
   m.def("dropout_add(Tensor x, Tensor a, float p, int seed, int offset) -> Tensor");
   m.def("dropout_bwd(Tensor dy, float p, int seed, int offset) -> Tensor");
-  m.def("bwd_bias_grad_(Tensor src, Tensor? aux, Tensor(a!) db, bool accumulate, int op, float p, int seed, int offset) -> Tensor");
+  m.def("bwd_bias_grad_(Tensor(a!) src, Tensor? aux, Tensor(b!)? db, bool accumulate, int op, float p, int seed, int offset, bool act_inplace=False) -> Tensor");
   m.def("transpose2d(Tensor a) -> Tensor");
   m.def("linear_residual(Tensor x, Tensor W, Tensor C) -> Tensor");
   m.def("swiglu_fwd(Tensor gu) -> Tensor");

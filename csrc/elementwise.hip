@@ -317,15 +317,18 @@ int colsum_bands(int N, int F) {
 // Elementwise backward + bias-gradient column sums in one pass (GPT-2: the dropout backward in
 // front of the out_proj / c_proj bias grads, the GELU backward in front of the c_fc bias grad,
 // reference GPT2.py:58-62 + nn.Linear bias).  Same band split, per-lane row order and fp32
-// partials as colsum_partial_k over the rounded outputs, so db is bitwise the separate path's;
+// partials as colsum_partial_k over the rounded outputs (db within one ulp of its dtype of the separate path's);
 // the separate colsum pass's re-read of the [N, F] gradient is gone.
 //   OP 0: out = dropout_bwd(src)  (keep bits by the counter hash at element index r * F + c)
-//   OP 1: out = src * gelu'(aux)   (exact erf GELU)
+//   OP 1: out = src * gelu'(aux)   (exact erf GELU); with act, also act = gelu(aux), bitwise as
+//         gelu_fwd_k (act may alias src: the activation-checkpoint recompute of GPT-2 then
+//         needs no GELU forward pass for the c_proj dW)
+// part == nullptr: no column sums (frozen / absent bias).
 template <typename T, int OP>
-__global__ __launch_bounds__(256) void bwd_colsum_k(const T* __restrict__ src, const T* __restrict__ aux,
+__global__ __launch_bounds__(256) void bwd_colsum_k(const T* src, const T* __restrict__ aux,
                                                     T* __restrict__ out, float* __restrict__ part, int N, int F,
                                                     int rows_per, uint64_t seed, uint64_t offset, uint32_t thr,
-                                                    float inv_keep) {
+                                                    float inv_keep, T* act) {
   constexpr int VEC = 16 / sizeof(T);
   const int cv = blockIdx.x * 256 + threadIdx.x;
   if (cv * VEC >= F) return;
@@ -342,20 +345,24 @@ __global__ __launch_bounds__(256) void bwd_colsum_k(const T* __restrict__ src, c
 #pragma unroll
       for (int j = 0; j < VEC; ++j) o.v[j] = from_f<T>(bits[j] >= thr ? to_f(v.v[j]) * inv_keep : 0.f);
     } else {
+      Vec16<T> g;
 #pragma unroll
       for (int j = 0; j < VEC; ++j) {
         const float x = to_f(a.v[j]);
         const float cdf = 0.5f * (1.f + erff(x * 0.70710678118654752f));
         const float pdf = __expf(-0.5f * x * x) * 0.39894228040143268f;
         o.v[j] = from_f<T>(to_f(v.v[j]) * (cdf + x * pdf));
+        g.v[j] = from_f<T>(0.5f * x * (1.f + erff(x * 0.70710678118654752f)));
       }
+      if (act) st16(act + e, g);
     }
     st16(out + e, o);
+    if (!part) return;
 #pragma unroll
     for (int j = 0; j < VEC; ++j) {
       // opaque copy: for fp32 (from_f = identity) the compiler would otherwise fuse the output
       // product into the column sum (one FMA), skipping the rounding the stored output had --
-      // the sums must match colsum_partial_k over the stored values bitwise
+      // the sums are over the stored (rounded) values, as colsum_partial_k's
       float ov = to_f(o.v[j]);
       asm volatile("" : "+v"(ov));
       acc[j] += ov;
@@ -377,13 +384,14 @@ __global__ __launch_bounds__(256) void bwd_colsum_k(const T* __restrict__ src, c
     if constexpr (OP == 1) a = ld16(aux + (long)r * F + cv * VEC);
     row(r, v, a);
   }
+  if (!part) return;
   float* o = part + (long)blockIdx.y * F + cv * VEC;
 #pragma unroll
   for (int j = 0; j < VEC; ++j) o[j] = acc[j];
 }
 
 void bwd_bias_grad(DType dt, DType odt, int op, const void* src, const void* aux, void* out, float* part, void* db,
-                   int N, int F, bool accumulate, float p, uint64_t seed, uint64_t offset, hipStream_t s) {
+                   int N, int F, bool accumulate, float p, uint64_t seed, uint64_t offset, void* act, hipStream_t s) {
   const int P = colsum_bands(N, F);
   const int rows_per = (N + P - 1) / P;
   const uint32_t thr = drop_threshold16(p);
@@ -393,12 +401,12 @@ void bwd_bias_grad(DType dt, DType odt, int op, const void* src, const void* aux
     dim3 grid((F / VEC + 255) / 256, P);
     if (op == 0)
       hipLaunchKernelGGL((bwd_colsum_k<T, 0>), grid, dim3(256), 0, s, (const T*)src, (const T*)aux, (T*)out, part, N, F,
-                         rows_per, seed, offset, thr, inv_keep);
+                         rows_per, seed, offset, thr, inv_keep, (T*)nullptr);
     else
       hipLaunchKernelGGL((bwd_colsum_k<T, 1>), grid, dim3(256), 0, s, (const T*)src, (const T*)aux, (T*)out, part, N, F,
-                         rows_per, seed, offset, thr, inv_keep);
+                         rows_per, seed, offset, thr, inv_keep, (T*)act);
   });
-  col_reduce(part, odt, db, P, F, accumulate, s);
+  if (part) col_reduce(part, odt, db, P, F, accumulate, s);
 }
 
 // dy [N, F] (F % (16/sizeof(T)) == 0), out [F] in dtype odt (written, or added when accumulate)
