@@ -12,6 +12,12 @@ if HERE not in sys.path:
 
 os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
 os.environ.setdefault("GLOO_SOCKET_IFNAME", "lo")
+if os.environ.get("PYTEST_XDIST_WORKER"):
+    # under pytest -n K every worker would otherwise run K x cpu_count intra-op threads next to
+    # the gloo multi-process tests' ranks; the tiny CPU models gain nothing from more than two
+    os.environ.setdefault("OMP_NUM_THREADS", "2")
+    import torch
+    torch.set_num_threads(int(os.environ["OMP_NUM_THREADS"]))
 
 
 def pytest_configure(config):
