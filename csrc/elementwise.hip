@@ -19,6 +19,16 @@ static bool swiglu_rows() {
   return v;
 }
 
+// BLLM_SWIGLU_U=2|4|8: 16-B load groups in flight per lane in the row-per-workgroup SwiGLU kernels (A/B)
+static int swiglu_u() {
+  static const int v = [] {
+    const char* e = getenv("BLLM_SWIGLU_U");
+    const int u = e ? atoi(e) : 4;
+    return (u == 2 || u == 8) ? u : 4;
+  }();
+  return v;
+}
+
 static inline int ew_grid(long nvec) {
   long g = (nvec + 255) / 256;
   return (int)(g < 2048 ? (g > 0 ? g : 1) : 2048);
@@ -432,8 +442,16 @@ void swiglu_fwd(DType dt, const void* gu, void* act, long N, int F, hipStream_t 
   BLLM_DISPATCH(dt, T, {
     EW_VEC(T, F % (16 / sizeof(T)) == 0, {
       if (swiglu_rows() && F / VEC >= 512 && N <= 0x7fffffffL) {
-        hipLaunchKernelGGL((swiglu_fwd_rows_k<T, VEC, 4>), dim3((unsigned)N), dim3(256), 0, s, (const T*)gu,
-                           (T*)act, F);
+        const int u = swiglu_u();
+        if (u == 2)
+          hipLaunchKernelGGL((swiglu_fwd_rows_k<T, VEC, 2>), dim3((unsigned)N), dim3(256), 0, s, (const T*)gu,
+                             (T*)act, F);
+        else if (u == 8)
+          hipLaunchKernelGGL((swiglu_fwd_rows_k<T, VEC, 8>), dim3((unsigned)N), dim3(256), 0, s, (const T*)gu,
+                             (T*)act, F);
+        else
+          hipLaunchKernelGGL((swiglu_fwd_rows_k<T, VEC, 4>), dim3((unsigned)N), dim3(256), 0, s, (const T*)gu,
+                             (T*)act, F);
       } else {
         hipLaunchKernelGGL((swiglu_fwd_k<T, VEC>), dim3(ew_grid(N * F / VEC)), dim3(256), 0, s, (const T*)gu,
                            (T*)act, N, F);
@@ -445,8 +463,16 @@ void swiglu_bwd(DType dt, const void* gu, const void* dact, void* dgu, void* act
   BLLM_DISPATCH(dt, T, {
     EW_VEC(T, F % (16 / sizeof(T)) == 0, {
       if (swiglu_rows() && F / VEC >= 512 && N <= 0x7fffffffL) {
-        hipLaunchKernelGGL((swiglu_bwd_rows_k<T, VEC, 4>), dim3((unsigned)N), dim3(256), 0, s, (const T*)gu,
-                           (const T*)dact, (T*)dgu, (T*)act, F);
+        const int u = swiglu_u();
+        if (u == 2)
+          hipLaunchKernelGGL((swiglu_bwd_rows_k<T, VEC, 2>), dim3((unsigned)N), dim3(256), 0, s, (const T*)gu,
+                             (const T*)dact, (T*)dgu, (T*)act, F);
+        else if (u == 8)
+          hipLaunchKernelGGL((swiglu_bwd_rows_k<T, VEC, 8>), dim3((unsigned)N), dim3(256), 0, s, (const T*)gu,
+                             (const T*)dact, (T*)dgu, (T*)act, F);
+        else
+          hipLaunchKernelGGL((swiglu_bwd_rows_k<T, VEC, 4>), dim3((unsigned)N), dim3(256), 0, s, (const T*)gu,
+                             (const T*)dact, (T*)dgu, (T*)act, F);
       } else {
         hipLaunchKernelGGL((swiglu_bwd_k<T, VEC>), dim3(ew_grid(N * F / VEC)), dim3(256), 0, s, (const T*)gu,
                            (const T*)dact, (T*)dgu, (T*)act, N, F);

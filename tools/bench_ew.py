@@ -43,10 +43,11 @@ def main():
     g5 = torch.randn(N, 5120, device=dev).to(dt)     # GPT2-774M fc1 bias grad
     db1 = torch.zeros(1280, device=dev, dtype=dt)
     db5 = torch.zeros(5120, device=dev, dtype=dt)
-    res = {"env": {k: os.environ.get(k) for k in ("BLLM_SWIGLU_ROWS", "BLLM_NORM_BWD_WG")}}
+    res = {"env": {k: os.environ.get(k) for k in ("BLLM_SWIGLU_ROWS", "BLLM_NORM_BWD_WG", "BLLM_SWIGLU_U")}}
     for name, fn, nbytes in (
         ("swiglu_fwd", lambda: ops.swiglu_fwd(gu), 3 * N * F * 2),
         ("swiglu_bwd", lambda: ops.swiglu_bwd(gu, da), 5 * N * F * 2),
+        ("swiglu_bwd_act", lambda: ops.swiglu_bwd_act(gu, da), 6 * N * F * 2),
         ("rmsnorm_fwd", lambda: ops.rmsnorm_fwd(x, w, 1e-5), 2 * N * d * 2),
         ("rmsnorm_bwd", lambda: ops.rmsnorm_bwd(dy, x, w, rstd, acc, dw, True), 4 * N * d * 2),
         ("bias_grad_1280", lambda: ops.bias_grad_(g1, db1, True), N * 1280 * 2),
