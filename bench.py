@@ -2,27 +2,39 @@
 """Headline benchmark (BASELINE.json): whole-node training tokens/s, Llama-3-8B bf16 FSDP
 full-shard + activation checkpointing, at 1/2/4/8 MI355X.
 
-    python bench.py --gpus N --steps K --warmup W
+    python bench.py --gpus N --steps K --warmup W          # N > 1: bench.py spawns N ranks itself
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+
+Launch: under torchrun (RANK / WORLD_SIZE in the environment) each process is one rank.  Without
+it, ``--gpus N > 1`` starts N worker processes itself with torch.multiprocessing spawn, as the
+reference's ``mp.spawn(main, nprocs=torch.cuda.device_count())`` (main.py:185-191) — before
+anything in the parent touches the GPU (only ``torch.cuda.device_count()``, which does not
+initialise HIP, and no exec); rank 0 prints the one JSON line.
 
 Every run — N=1 included — initialises a process group (RCCL; gloo with ``--device cpu``) and
 trains through the SAME ``FSDPEngine`` (parallel/fsdp.py).  At N=1 that engine behaves like
 torch FSDP at world size 1, which clamps FULL_SHARD to NO_SHARD (torch/distributed/fsdp/
 _init_utils.py:426-437): the single rank's shard is the whole flat, so no collective runs.
 
-One step = forward, fused CE, backward (with full activation-checkpoint recompute: only each
-block's input is saved, every block's forward is re-run in backward — the reference's
-``checkpoint_sequential(segments=n_layers)``, Llama3.py:198-199), global-norm clip 1.0 (one
-scalar all-reduce) and AdamW(wd 0.1) with fp32 master weights on this rank's shard, on
+One step = forward, fused CE, backward (with activation checkpointing), global-norm clip 1.0
+(one scalar all-reduce) and AdamW(wd 0.1) with fp32 master weights on this rank's shard, on
 random-init weights of the full architecture and synthetic token ids.  W untimed warm-up
 steps, then exactly K timed steps bracketed by barrier + device sync; the slowest rank's time
-is reported.  Weak scaling: the per-GPU micro-batch is fixed, total tokens grow with N.
+is reported (every rank's time and peak memory are in the JSON).  Weak scaling: the per-GPU
+micro-batch is fixed, total tokens grow with N.
+
+Activation checkpointing (headline default ``--actv_ckpt auto``): the granularity is chosen per
+N from the 288 GB budget by train/memplan.py — every block ``selective`` (norm outputs and the
+SwiGLU activation recomputed inside passes the backward runs anyway), plus the fewest fully
+recomputed blocks that keep the predicted per-rank peak under ``--ckpt_budget_gib`` (250); the
+first warm-up step measures the real peak and re-plans if it is over.  FSDP sharding at N > 1
+frees the fp32 master / moments, so the plan can only get lighter with N.  ``--actv_ckpt
+full`` is the reference's ``--use_actv_ckpt`` exactly (``checkpoint_sequential(segments=
+n_layers)``, Llama3.py:198-199: 31 of 32 blocks re-run in backward); the JSON states which.
 
 Micro-batch: the reference's ``--batch_size`` default 4 (args.py:53) was sized for a 16 GB T4;
 one MI355X holds 288 GB, so each rank runs 40 x 1024 tokens (``--batch_size 4`` reproduces the
-reference default).  With full checkpointing only block inputs are kept, so memory barely grows
-with B (same box, profiles/r2_bsweep.md): B=24 21.93k tok/s at 130.6 GiB, B=32 22.26k at 134.2,
-B=40 22.40k at 137.8 -- larger GEMM row counts and fewer LM-head chunk tails per token.
+reference default).
 
 ``mfu`` counts model FLOPs only (6·N_nonemb + 12·L·d·T per token, no recompute); ``hfu`` adds
 what the hardware also executes under full checkpointing: each block's forward re-run minus its
@@ -59,7 +71,7 @@ METRIC = "tokens/sec (whole node) Llama-3-8B bf16 FSDP at 1/2/4/8 MI355X"
 PEAK_BF16 = 2.5e15
 
 PRESETS = {
-    "llama3_8b_fsdp": dict(model="llama3", num_params="8B", parallel="fsdp", actv_ckpt="full", batch_size=40,
+    "llama3_8b_fsdp": dict(model="llama3", num_params="8B", parallel="fsdp", actv_ckpt="auto", batch_size=40,
                            data="pretrain", mixed_precision=None, lora_rank=0),
     "gpt2_774m_ddp": dict(model="GPT2", num_params="774M", parallel="ddp", actv_ckpt="none", batch_size=24,
                           data="pretrain", mixed_precision=None, lora_rank=0),
@@ -81,11 +93,14 @@ def parse(argv=None):
     ap.add_argument("--num_params", default=None)
     ap.add_argument("--batch_size", type=int, default=None, help="micro-batch per GPU (reference CLI default: 4)")
     ap.add_argument("--seq_len", type=int, default=1024)
-    ap.add_argument("--actv_ckpt", default=None, choices=["none", "selective", "full"],
-                    help="full = reference checkpoint_sequential semantics (headline); selective recomputes norms")
+    ap.add_argument("--actv_ckpt", default=None, choices=["none", "selective", "full", "auto"],
+                    help="auto = granularity from the HBM budget (headline); full = reference "
+                         "checkpoint_sequential semantics; selective recomputes norms + SwiGLU/GELU act")
     ap.add_argument("--ckpt_segments", type=int, default=None,
                     help="full mode: checkpoint_sequential segments (default n_layers = the reference's "
                          "--use_actv_ckpt; fewer segments recompute fewer blocks)")
+    ap.add_argument("--ckpt_budget_gib", type=float, default=None,
+                    help="auto mode: per-rank peak-memory ceiling (default 250 GiB, capped at device - 18 GiB)")
     ap.add_argument("--parallel", default=None, choices=["fsdp", "ddp", "zero1"])
     ap.add_argument("--mixed_precision", default=None, choices=["bf16", "fp16", "bf16_hybrid", "fp32"])
     ap.add_argument("--lora_rank", type=int, default=None)
@@ -122,7 +137,8 @@ def init_dist(a):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    assert world == a.gpus, f"--gpus {a.gpus} but WORLD_SIZE={world} (launch with torchrun for N>1)"
+    if world != a.gpus:
+        raise SystemExit(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={world}")
     if a.device == "cuda":
         torch.cuda.set_device(local)
         dev = torch.device("cuda", local)
@@ -188,6 +204,37 @@ def alpaca_loader(a, cfg, rank, world):
     return forever()
 
 
+def _free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _spawn_worker(local_rank: int, argv, world: int, port: int):
+    """One rank of a self-launched run (the parent did not touch the GPU)."""
+    os.environ.update(RANK=str(local_rank), LOCAL_RANK=str(local_rank), WORLD_SIZE=str(world),
+                      LOCAL_WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                      BLLM_BENCH_LAUNCHER="spawn")
+    main(argv)
+
+
+def launch(argv=None):
+    """Entry point: run in-process (N = 1, or one rank under torchrun) or spawn N ranks."""
+    a = parse(argv)
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        import torch
+        import torch.multiprocessing as mp
+        if a.device == "cuda":
+            n = torch.cuda.device_count()   # counts devices without initialising HIP in this process
+            if n < a.gpus:
+                raise SystemExit(f"bench.py: --gpus {a.gpus} but only {n} GPU(s) visible")
+        mp.start_processes(_spawn_worker, args=(argv, a.gpus, _free_port()), nprocs=a.gpus, join=True,
+                           start_method="spawn")
+        return
+    main(argv)
+
+
 def main(argv=None):
     a = parse(argv)
     if a.tunableop:  # must be set before the first GEMM; TunableOp reads <name><device ordinal>.csv
@@ -214,10 +261,19 @@ def main(argv=None):
 
     cfg = build_config(a, dev)
     torch.manual_seed(123)
-    model = build_model(cfg, use_actv_ckpt=a.actv_ckpt, device=dev)
+    plan = None
+    ckpt_mode = "selective" if a.actv_ckpt == "auto" else a.actv_ckpt
+    model = build_model(cfg, use_actv_ckpt=ckpt_mode, device=dev)
     if a.ckpt_segments:
         model.set_actv_ckpt(a.actv_ckpt, a.ckpt_segments)
-    n_ckpt = sum(model.rctx.block_mode(i) == "full" for i in range(cfg.n_layers))
+    B, T = a.batch_size, a.seq_len
+    if a.actv_ckpt == "auto":
+        from building_llm_from_scratch_amd.train import memplan
+        total = torch.cuda.get_device_properties(dev).total_memory if cuda else None
+        budget = a.ckpt_budget_gib * memplan.GIB if a.ckpt_budget_gib else None
+        plan = memplan.plan_ckpt(cfg, B, T, world=world, engine=a.parallel, budget=budget, device_total=total,
+                                 elt=torch.empty((), dtype=cfg.dtype).element_size(), prefetch=a.fsdp_prefetch)
+        model.set_block_modes(plan.modes)
     if a.lora_rank:
         for p in model.parameters():
             p.requires_grad = False
@@ -226,7 +282,6 @@ def main(argv=None):
     engine = setup_engine(model, a.parallel, device=dev, reduce_dtype=reduce,
                           reshard_after_forward=bool(a.reshard_after_forward), prefetch=a.fsdp_prefetch)
     opt = FusedAdamW(model, lr=3e-4, weight_decay=0.1, engine=engine, overlap=a.overlap_optimizer)
-    B, T = a.batch_size, a.seq_len
 
     if a.data == "alpaca":
         batches = alpaca_loader(a, cfg, rank, world)
@@ -256,8 +311,21 @@ def main(argv=None):
         tokens += x.numel()
         return loss
 
+    probe_peak = None
     for i in range(a.warmup):
         loss = step(i)
+        if i == 0 and plan is not None and cuda:
+            # memory probe: the first step's measured peak (max over ranks) checks the plan
+            sync()
+            pk = torch.tensor([float(torch.cuda.max_memory_allocated(dev))], device=dev)
+            dist.all_reduce(pk, op=dist.ReduceOp.MAX)
+            probe_peak = pk.item()
+            new = memplan.replan_after_probe(plan, cfg, B, T, probe_peak,
+                                             elt=torch.empty((), dtype=cfg.dtype).element_size())
+            if new is not plan:
+                plan = new
+                model.set_block_modes(plan.modes)
+                torch.cuda.reset_peak_memory_stats(dev)
     sync()
     dist.barrier()
     sync()
@@ -269,14 +337,17 @@ def main(argv=None):
     dist.barrier()
     sync()
     elapsed = time.perf_counter() - t0
-    red = torch.tensor([elapsed, float(tokens)], device=dev, dtype=torch.float64)
-    el = red[:1].clone()
-    dist.all_reduce(el, op=dist.ReduceOp.MAX)
-    tok = red[1:].clone()
-    dist.all_reduce(tok, op=dist.ReduceOp.SUM)
-    elapsed, total_tokens = el.item(), tok.item()
+    peak = float(torch.cuda.max_memory_allocated(dev)) if cuda else 0.0
+    # every rank's (time, tokens, peak): rank 0 reports the max time, the token sum and the spread
+    mine = torch.tensor([elapsed, float(tokens), peak], device=dev, dtype=torch.float64)
+    allr = [torch.zeros_like(mine) for _ in range(world)]
+    dist.all_gather(allr, mine)
+    per_rank = torch.stack(allr).cpu().tolist()
+    elapsed = max(r[0] for r in per_rank)
+    total_tokens = sum(r[1] for r in per_rank)
     tps = total_tokens / elapsed
     ms = 1000 * elapsed / a.steps
+    n_ckpt = sum(model.rctx.block_mode(i) == "full" for i in range(cfg.n_layers))
     T_eff = total_tokens / (world * a.steps * B)           # mean padded length (alpaca); == T otherwise
     flops_tok = cfg.train_flops_per_token(int(round(T_eff)))
     if a.lora_rank:  # frozen base: no weight-gradient GEMMs (2 of the 6 N FLOPs per param)
@@ -298,6 +369,17 @@ def main(argv=None):
             + (f" LoRA r={a.lora_rank} Alpaca finetune" if a.lora_rank else "")
             + (f" mixed_precision={a.mixed_precision}" if a.mixed_precision else "")
             + (" [cpu plumbing, tiny config]" if not cuda else ""))
+        summ = model.ckpt_summary()
+        if a.actv_ckpt == "auto":
+            ckpt_desc = (f"{summ['full']}/{cfg.n_layers} fully recomputed, {summ['selective']} selective "
+                         "(auto: memory planner)")
+        elif a.actv_ckpt == "full":
+            ckpt_desc = f"{n_ckpt}/{cfg.n_layers} recomputed" + (
+                f" (checkpoint_sequential segments={a.ckpt_segments})" if a.ckpt_segments
+                else " (checkpoint_sequential segments=n_layers, as the reference)")
+        else:
+            ckpt_desc = f"{n_ckpt}/{cfg.n_layers} recomputed ({a.actv_ckpt})"
+        gib = lambda v: round(v / 2 ** 30, 1)  # noqa: E731
         out = {
             "metric": metric,
             "value": round(tps, 1),
@@ -324,19 +406,26 @@ def main(argv=None):
                                                    else (" (world 1: forced collective path)"
                                                          if world == 1 and a.force_comm else "")),
                 "actv_ckpt": a.actv_ckpt,
-                "ckpt_blocks": f"{n_ckpt}/{cfg.n_layers} recomputed"
-                + (f" (checkpoint_sequential segments={a.ckpt_segments})" if a.ckpt_segments
-                   else (" (checkpoint_sequential segments=n_layers, as the reference)"
-                         if a.actv_ckpt == "full" else "")),
+                "ckpt_blocks": ckpt_desc,
                 "mixed_precision": a.mixed_precision,
                 "lora": {"rank": a.lora_rank, "alpha": a.lora_alpha} if a.lora_rank else None,
                 "optimizer": "AdamW fp32 master, wd 0.1, clip 1.0",
             },
             "mfu": round(mfu, 4),
             "hfu": round(mfu * recompute, 4),
-            "peak_mem_gib": round(torch.cuda.max_memory_allocated(dev) / 2**30, 1) if cuda else None,
+            "peak_mem_gib": gib(max(r[2] for r in per_rank)) if cuda else None,
             "final_loss": round(float(loss.item()), 4),
+            "rccl_world": dist.get_world_size(),
+            "backend": dist.get_backend(),
+            "launcher": os.environ.get("BLLM_BENCH_LAUNCHER", "torchrun" if "TORCHELASTIC_RUN_ID" in os.environ
+                                       else ("env" if world > 1 else "single")),
+            "per_rank": {"ms_per_step_min": round(1000 * min(r[0] for r in per_rank) / a.steps, 2),
+                         "ms_per_step_max": round(ms, 2),
+                         "ms_per_step": [round(1000 * r[0] / a.steps, 2) for r in per_rank],
+                         "peak_mem_gib": [gib(r[2]) for r in per_rank] if cuda else None},
         }
+        if plan is not None:
+            out["ckpt_plan"] = dict(plan.summary(), probe_peak_gib=gib(probe_peak) if probe_peak else None)
         if prof is not None:
             out["profile_ms"] = prof
         print(json.dumps(out), flush=True)
@@ -366,4 +455,4 @@ def profile_phases(model, opt, next_batch, dev, n=3):
 
 
 if __name__ == "__main__":
-    main()
+    launch(sys.argv[1:])

@@ -8,8 +8,10 @@ hand (models/gpt2.py, models/llama.py) on top of the HIP kernels and hipBLASLt G
 gives exact control over:
 
   * what each block saves for backward (``actv_ckpt``: ``none`` | ``selective`` — recompute
-    only the norm outputs, the cheapest memory-bound ops; everything a GEMM or the attention
-    kernel produced is kept, which 288 GB of HBM affords | ``full`` — save the block input
+    only the norm outputs and the SwiGLU / GELU activation, the cheapest memory-bound ops (the
+    activation is rebuilt inside the activation-backward pass, in place of its gradient, so it
+    costs no extra pass); everything a GEMM or the attention kernel produced is kept, which
+    288 GB of HBM affords | ``full`` — save the block input
     only, the reference's ``checkpoint_sequential(blocks, segments=n_layers)`` semantics
     (Llama3.py:199, GPT2.py:116): every block of the first ``segments - 1`` segments is
     recomputed in backward, the last segment runs without checkpointing.  ``ckpt_segments``
@@ -73,6 +75,9 @@ class RunCtx:
         self.cfg = cfg
         self.actv_ckpt = actv_ckpt
         self.ckpt_segments = None      # full mode: checkpoint_sequential segments (None = n_layers)
+        # explicit per-block modes (the memory planner's choice, train/memplan.py); overrides
+        # actv_ckpt / ckpt_segments when set
+        self.block_modes: Optional[List[str]] = None
         self.training = True
         self.engine = LocalEngine()
         self.accumulate = False        # micro-batch gradient accumulation: add into grads
@@ -90,6 +95,8 @@ class RunCtx:
         """Checkpoint mode of block ``i``.  ``full`` follows torch's checkpoint_sequential:
         segment size n // s, the first s - 1 segments checkpointed, the rest (the last segment
         plus the remainder) run plainly -- with s = n_layers only the last block is not."""
+        if self.block_modes is not None:
+            return self.block_modes[i]
         if self.actv_ckpt != "full":
             return self.actv_ckpt
         n = self.cfg.n_layers
@@ -291,7 +298,22 @@ class BaseLM(nn.Module):
         assert mode in ("none", "selective", "full")
         self._rctx.actv_ckpt = mode
         self._rctx.ckpt_segments = segments
+        self._rctx.block_modes = None
         self.use_actv_ckpt = mode != "none"
+
+    def set_block_modes(self, modes: List[str]):
+        """Per-block checkpoint modes (``none`` | ``selective`` | ``full`` for each block), e.g.
+        the memory planner's choice (train/memplan.py): the first k blocks fully recomputed, the
+        rest selective."""
+        assert len(modes) == self.cfg.n_layers and all(m in ("none", "selective", "full") for m in modes)
+        self._rctx.block_modes = list(modes)
+        self._rctx.actv_ckpt = "full" if "full" in modes else ("selective" if "selective" in modes else "none")
+        self.use_actv_ckpt = any(m != "none" for m in modes)
+
+    def ckpt_summary(self) -> dict:
+        """How many blocks run in each checkpoint mode."""
+        modes = [self._rctx.block_mode(i) for i in range(self.cfg.n_layers)]
+        return {m: modes.count(m) for m in ("full", "selective", "none")}
 
     def set_engine(self, engine):
         self._rctx.engine = engine

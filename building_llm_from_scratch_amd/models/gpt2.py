@@ -215,9 +215,11 @@ class GPTBlockCompute(UnitCompute):
             return x3.view(B, T, d), offs
         saved = dict(x=x2d, m1=m1, r1=r1, qkv=qkv, o=o, lse=lse, km=km, x2=x2, m2=m2, r2=r2, f=f,
                      p=p, offs=offs, xa=(xa_qkv, xa_o, xa_fc, xa_pr))
-        if g is not None:
+        keep = rc.block_mode(self.index) == "none" or recompute  # the recompute's outputs live one block
+        # selective: g is rebuilt by the GELU backward (gelu_bwd_act), h1/h2 by the LayerNorm
+        if g is not None and (keep or self.proj.has_lora or not RECOMPUTE_FUSED):
             saved["g"] = g
-        if rc.block_mode(self.index) == "none" or recompute:  # the recompute's norm outputs live one block
+        if keep:
             saved.update(h1=h1, h2=h2)
         return (x3.view(B, T, d) if x3 is not None else None), saved
 

@@ -173,9 +173,11 @@ class LlamaBlockCompute(UnitCompute):
         if save:
             saved = dict(x=x2d, r1=r1, qkv=qkv, o=o, lse=lse, x2=x2, r2=r2, gu=gu,
                          xa=(xa_qkv, xa_o, xa_gu, xa_dn))
-            if act is not None:
+            keep = rc.block_mode(self.index) == "none" or recompute  # the recompute's outputs live one block
+            # selective: act is rebuilt by the SwiGLU backward (swiglu_bwd_act), h1/h2 by rmsnorm
+            if act is not None and (keep or self.down.has_lora or not RECOMPUTE_FUSED):
                 saved["act"] = act
-            if rc.block_mode(self.index) == "none" or recompute:  # the recompute's norm outputs live one block
+            if keep:
                 saved.update(h1=h1, h2=h2)
         return (x3.view(B, T, d) if x3 is not None else None), saved
 

@@ -1,6 +1,8 @@
-"""bench.py's distributed branch, executed: torchrun at world 2, 4 (and 8 for FSDP) on gloo (``--device cpu``
-tiny config) for every engine and preset, checking the driver's JSON-line contract.  On the GPU
-node the same code path runs with RCCL; only the backend and the model size differ."""
+"""bench.py's distributed branch, executed on gloo (``--device cpu`` tiny config) for every engine
+and preset, checking the driver's JSON-line contract: under torchrun at world 2 and 4, and
+self-launched (``python bench.py --gpus N``, no torchrun: bench.py spawns the N ranks itself) at
+world 2, 4 and 8.  On the GPU node the same code path runs with RCCL; only the backend and the
+model size differ."""
 import json
 import os
 import subprocess
@@ -19,9 +21,11 @@ def _port():
         return s.getsockname()[1]
 
 
-def _run(n, extra, timeout=600):
+def _run(n, extra, timeout=600, spawn=False):
     env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", OMP_NUM_THREADS="1")
-    if n == 1:
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    if n == 1 or spawn:
         cmd = [sys.executable, BENCH]
     else:
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
@@ -36,6 +40,10 @@ def _run(n, extra, timeout=600):
               "scaling", "vs_baseline", "dtype", "data", "config"):
         assert k in out, k
     assert out["n_gpus"] == n and out["steps"] == 2 and out["warmup"] == 1 and out["value"] > 0
+    assert out["rccl_world"] == n                # the process group really had N ranks
+    assert len(out["per_rank"]["ms_per_step"]) == n
+    assert out["per_rank"]["ms_per_step_max"] == out["ms_per_step"]
+    assert out["launcher"] == ("spawn" if spawn and n > 1 else ("single" if n == 1 else "torchrun"))
     assert "INVALID" in out["config"]["model"]  # a CPU run can never pass for a measurement
     return out
 
@@ -46,7 +54,30 @@ def test_bench_torchrun_gloo(n, parallel):
     out = _run(n, ["--parallel", parallel])
     assert out["config"]["parallelism"] == f"{parallel}{n}"
     assert out["config"]["global_batch"] == 2 * n
-    assert out["config"]["actv_ckpt"] == "full"
+    assert out["config"]["actv_ckpt"] == "auto"
+    assert out["ckpt_plan"]["full"] + out["ckpt_plan"]["selective"] == 2   # checkpointing stays on
+
+
+@pytest.mark.parametrize("n", [2, 4, 8])
+@pytest.mark.parametrize("parallel", ["fsdp", "ddp", "zero1"])
+def test_bench_self_spawn(n, parallel):
+    """``python bench.py --gpus N`` without torchrun: bench.py starts the N ranks itself."""
+    out = _run(n, ["--parallel", parallel], spawn=True)
+    assert out["config"]["parallelism"] == f"{parallel}{n}"
+    assert out["config"]["global_batch"] == 2 * n
+
+
+@pytest.mark.parametrize("n", [2, 4, 8])
+@pytest.mark.parametrize("preset", ["llama32_1b_lora_alpaca", "llama2_7b_fsdp_mp", "gpt2_774m_ddp"])
+def test_bench_self_spawn_presets(preset, n):
+    out = _run(n, ["--preset", preset], spawn=True)
+    assert out["config"]["parallelism"].endswith(str(n))
+
+
+def test_bench_reference_ckpt():
+    """``--actv_ckpt full`` is the reference's checkpoint_sequential(segments=n_layers)."""
+    out = _run(1, ["--actv_ckpt", "full"])
+    assert out["config"]["ckpt_blocks"].startswith("1/2 recomputed")
 
 
 def test_bench_torchrun_gloo_world8_fsdp():
