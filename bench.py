@@ -106,7 +106,8 @@ def parse(argv=None):
     ap.add_argument("--lora_rank", type=int, default=None)
     ap.add_argument("--lora_alpha", type=int, default=32)
     ap.add_argument("--reshard_after_forward", type=int, default=1)
-    ap.add_argument("--fsdp_prefetch", type=int, default=1, help="FSDP units all-gathered ahead")
+    ap.add_argument("--fsdp_prefetch", type=int, default=0,
+                    help="FSDP units all-gathered ahead (0 = auto: gather time over xGMI vs unit compute)")
     ap.add_argument("--layers", type=int, default=None, help="(debug only) override n_layers; invalidates the metric")
     ap.add_argument("--profile", action="store_true", help="print a per-phase timing breakdown to stderr")
     ap.add_argument("--overlap_optimizer", action="store_true",
@@ -272,7 +273,7 @@ def main(argv=None):
         total = torch.cuda.get_device_properties(dev).total_memory if cuda else None
         budget = a.ckpt_budget_gib * memplan.GIB if a.ckpt_budget_gib else None
         plan = memplan.plan_ckpt(cfg, B, T, world=world, engine=a.parallel, budget=budget, device_total=total,
-                                 elt=torch.empty((), dtype=cfg.dtype).element_size(), prefetch=a.fsdp_prefetch)
+                                 elt=torch.empty((), dtype=cfg.dtype).element_size(), prefetch=max(1, a.fsdp_prefetch or 2))
         model.set_block_modes(plan.modes)
     if a.lora_rank:
         for p in model.parameters():
@@ -424,6 +425,8 @@ def main(argv=None):
                          "ms_per_step": [round(1000 * r[0] / a.steps, 2) for r in per_rank],
                          "peak_mem_gib": [gib(r[2]) for r in per_rank] if cuda else None},
         }
+        if getattr(engine, "prefetch", None) is not None and not getattr(engine, "no_shard", True):
+            out["config"]["fsdp_prefetch"] = engine.prefetch
         if plan is not None:
             out["ckpt_plan"] = dict(plan.summary(), probe_peak_gib=gib(probe_peak) if probe_peak else None)
         if prof is not None:

@@ -94,7 +94,7 @@ def build_model(config, rank, device, args):
         logger.info(f"Mixed precision: {pol}")
     engine = setup_engine(model, engine_kind(args), device=device, reduce_dtype=reduce,
                           reshard_after_forward=not getattr(args, "no_reshard_after_forward", False),
-                          prefetch=getattr(args, "fsdp_prefetch", 1),
+                          prefetch=getattr(args, "fsdp_prefetch", 0),
                           bucket_mb=getattr(args, "bucket_mb", 256.0))
     if rank == 0:
         misc.print_memory_usage()

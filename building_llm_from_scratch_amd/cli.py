@@ -107,7 +107,8 @@ def build_parser() -> argparse.ArgumentParser:
     x.add_argument("--pg_timeout_min", type=float, default=30.0,
                    help="collective timeout (minutes): a wedged RCCL/gloo collective raises instead of hanging")
     x.add_argument("--bucket_mb", type=float, default=256.0, help="DDP all-reduce bucket size")
-    x.add_argument("--fsdp_prefetch", type=int, default=1, help="FSDP: units all-gathered ahead of the computing one")
+    x.add_argument("--fsdp_prefetch", type=int, default=0,
+                   help="FSDP: units all-gathered ahead of the computing one (0 = auto from gather vs compute time)")
     x.add_argument("--no_reshard_after_forward", action="store_true",
                    help="FSDP: keep gathered params from forward to backward (ZeRO-2 style)")
     x.add_argument("--no_plot", action="store_true")

@@ -95,12 +95,6 @@ def format_input(entry: dict) -> str:
     return instruction_text + input_text
 
 
-def format_input_phi(entry: dict) -> str:
-    instruction_text = f"<|user|>\n{entry['instruction']}"
-    input_text = f"\n{entry['input']}" if entry.get("input") else ""
-    return instruction_text + input_text
-
-
 class InstructionDataset(Dataset):
     def __init__(self, data: Sequence[dict], tokenizer):
         self.data = data
@@ -114,19 +108,6 @@ class InstructionDataset(Dataset):
 
     def __getitem__(self, index):
         return self.instruction_lengths[index], self.encoded_texts[index]
-
-    def __len__(self):
-        return len(self.data)
-
-
-class InstructionDatasetPhi(Dataset):
-    def __init__(self, data: Sequence[dict], tokenizer):
-        self.data = data
-        self.encoded_texts = [tokenizer.encode(format_input_phi(e) + f"\n<|assistant|>:\n{e['output']}")
-                              for e in data]
-
-    def __getitem__(self, index):
-        return self.encoded_texts[index]
 
     def __len__(self):
         return len(self.data)

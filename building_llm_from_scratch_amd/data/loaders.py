@@ -2,8 +2,9 @@
 dataloader_instruction_finetune.py:53-134).
 
 Semantics kept: raw text split by characters ``train_ratio`` / rest; train loader shuffled
-with ``drop_last=True``, val loader in order; multi-GPU uses a ``DistributedSampler`` (which
-shuffles, seed 0, pads by repetition) with ``set_epoch`` called by the trainer.
+with ``drop_last=True``, val loader in order on one process; multi-GPU uses a
+``DistributedSampler`` for both (which shuffles, seed 0, pads by repetition) with ``set_epoch``
+called by the trainer.
 Differences: the instruction pad id defaults to the model's eos id (SURVEY §2.8 defect 7),
 ``get_total_steps_epoch`` reuses cached tokenisation (``cache_dir``: a memory-mapped uint32
 token stream per text, written once), worker processes are used under DistributedSampler too,
@@ -31,9 +32,12 @@ def _make_loader(owner, ds, shuffle, drop_last, num_workers, generator):
     if num_workers > 0:
         workers["prefetch_factor"] = 4
     if owner.run_type == "multi_gpu" and _is_dist():
-        # DistributedSampler(shuffle=True, seed=0) + set_epoch: identical order on resume
+        # DistributedSampler(shuffle=True, seed=0) + set_epoch: identical order on resume.  The
+        # validation loader shuffles too, as the reference's DistributedSampler(dataset) default
+        # does (datautils/dataloader.py:50, dataloader_instruction_finetune.py:94): eval_iter
+        # batches then come from a seeded random subset, not the leading one
         return DataLoader(ds, batch_size=owner.batch_size, pin_memory=owner.pin_memory, shuffle=False,
-                          drop_last=drop_last, sampler=DistributedSampler(ds, shuffle=shuffle),
+                          drop_last=drop_last, sampler=DistributedSampler(ds, shuffle=True),
                           collate_fn=owner.collate_func, **workers)
     return DataLoader(ds, batch_size=owner.batch_size, pin_memory=owner.pin_memory, shuffle=shuffle,
                       drop_last=drop_last, collate_fn=owner.collate_func,

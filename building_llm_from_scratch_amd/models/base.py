@@ -81,6 +81,10 @@ class RunCtx:
         self.training = True
         self.engine = LocalEngine()
         self.accumulate = False        # micro-batch gradient accumulation: add into grads
+        # expected dloss of the next backward (the fp16 loss scale): the fused head + CE takes the
+        # logit gradient during the forward at this scale and divides it out in backward
+        self.loss_scale = 1.0
+        self.grad_forward = False      # whether the current model forward builds a backward
         self.seed = 1234
         self._offset = 0
         self.rope = None               # (cos, sin) fp32 [T, hd/2] on device
@@ -384,6 +388,7 @@ class BaseLM(nn.Module):
         rc.B, rc.T = B, T
         idx = in_idx.to(self._anchor.device, non_blocking=True)
         grad = torch.is_grad_enabled()
+        rc.grad_forward = grad          # engines read this: inside autograd.Function.forward grad is off
         emb, blocks, head = comps[0], comps[1:-1], comps[-1]
         eng = rc.engine
         wait = rc.wait_param_ready if rc.param_ready else (lambda i: None)

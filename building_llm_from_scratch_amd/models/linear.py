@@ -195,9 +195,13 @@ class FusedLinear:
     def _kaug_ok(self, x: torch.Tensor, residual, b) -> bool:
         """K-augmented LoRA (see forward) for wide frozen groups whose output dwarfs the input
         (gate/up: out = 8 d): copying x into [x | s t] costs less than the s t B write plus the
-        beta = 1 read of y it replaces.  BLLM_LORA_KAUG=0 turns it off."""
+        beta = 1 read of y it replaces.  BLLM_LORA_KAUG=0 turns it off.  Not under a sharding
+        FSDP engine: the persistent [W | Bd^T] copy would keep a full unsharded frozen weight
+        per rank (Llama-3-8B gate/up: ~7.5 GB regardless of world size) and would be rebuilt
+        after every re-gather."""
         return (residual is None and b is None and self.out_total >= 4 * x.shape[1]
                 and not self.unit.trainable(self.W_params[0])
+                and not self.unit.state.get("sharded", False)
                 and os.environ.get("BLLM_LORA_KAUG", "1") != "0")
 
     def _waug(self, W: torch.Tensor, K: int) -> torch.Tensor:

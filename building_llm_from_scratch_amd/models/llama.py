@@ -267,8 +267,11 @@ class HeadComputeMixin:
     both head gradient GEMMs run chunk by chunk over the tokens, so the [N, V] logits never exist
     at once (Llama-3-8B, 24k tokens: 6.3 GB of bf16 logits -> 2 GiB chunks, 3 of them; 6 chunks
     of 1 GiB measured +5 ms / step, profiles/r2_llama3_8b_fsdp_full_v3.md).  The loss
-    gradient is taken for dloss = 1 and scaled by the real dloss in backward (dh and dW, one
-    pass each) -- exact for any dloss, including fp16 loss scaling."""
+    gradient is taken for dloss = ``rctx.loss_scale`` (1, or the fp16 loss scale the trainer
+    announces before the forward) and rescaled by dloss / loss_scale in backward (dh and dW, one
+    pass each; exactly 1 when the announced scale is the dloss that arrives).  Taking it at the
+    loss scale matters in fp16: softmax tails p / nvalid below fp16's smallest subnormal would
+    round to 0 before any later scaling could lift them."""
 
     ignore_index = -100
 
@@ -310,7 +313,7 @@ class HeadComputeMixin:
         Wd = W
         if _dgrad_wt_ok(h[:rows], W):   # one K-contiguous copy of W for every chunk's dX GEMM
             Wd = ops.transpose2d(W).t()
-        scale = (1.0 / nvalid).reshape(1)
+        scale = (self.rctx.loss_scale / nvalid).reshape(1)
         total = torch.zeros(1, dtype=torch.float32, device=h.device)
         for s0 in range(0, N, rows):
             hc, tc = h[s0:s0 + rows], targets[s0:s0 + rows]
@@ -322,7 +325,7 @@ class HeadComputeMixin:
             if gW is not None:
                 _weight_grad(dl, hc, gW, accumulate=s0 > 0)
             del logits, dl
-        return total[0] / nvalid, (x2d, ns, dh, gW, [], "fused")
+        return total[0] / nvalid, (x2d, ns, dh, gW, [], self.rctx.loss_scale, "fused")
 
     def _fused_lora_ok(self) -> bool:
         hd = self.head
@@ -369,7 +372,7 @@ class HeadComputeMixin:
         dha = torch.empty_like(ha)
         # (grad views only exist in backward: FSDP allocates the full gradient in pre_backward)
         gB = torch.zeros(r, V, dtype=torch.float32, device=h.device) if u.trainable(spec.lora_B) else None
-        scale = (1.0 / nvalid).reshape(1)
+        scale = (self.rctx.loss_scale / nvalid).reshape(1)
         total = torch.zeros(1, dtype=torch.float32, device=h.device)
         for s0 in range(0, N, rows):
             hc, tc = ha[s0:s0 + rows], targets[s0:s0 + rows]
@@ -389,7 +392,7 @@ class HeadComputeMixin:
         if u.trainable(spec.lora_A):                                      # dA = s h^T (dl B^T)
             lora.append((spec.lora_A, torch.mm(h.t(), ub).float().mul_(sc)))
         del dha, ha
-        return total[0] / nvalid, (x2d, ns, dh, None, lora, "fused")
+        return total[0] / nvalid, (x2d, ns, dh, None, lora, self.rctx.loss_scale, "fused")
 
     def forward_loss(self, x, targets, save):
         x2d = x.reshape(-1, x.shape[-1])
@@ -411,8 +414,8 @@ class HeadComputeMixin:
 
     def backward_loss(self, dloss, saved):
         if saved[-1] == "fused":
-            x2d, ns, dh, gW, lora, _ = saved
-            dls = dloss.float().reshape(1)
+            x2d, ns, dh, gW, lora, ls, _ = saved
+            dls = dloss.float().reshape(1) / ls
             dh.mul_(dls)
             if gW is not None:
                 g = self.head.unit.fused_grad(self.head.W_params)

@@ -40,7 +40,7 @@ def force_comm() -> bool:
 
 
 def setup_engine(model, kind: str = "local", device=None, reduce_dtype=None, bucket_mb: float = 256.0,
-                 reshard_after_forward: bool = True, process_group=None, prefetch: int = 1):
+                 reshard_after_forward: bool = True, process_group=None, prefetch: int = 0):
     """Flatten ``model`` onto ``device`` and attach the requested engine; returns it."""
     device = torch.device(device) if device is not None else model.device
     if kind in ("local", "single", "single_gpu"):

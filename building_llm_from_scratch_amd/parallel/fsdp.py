@@ -63,8 +63,12 @@ class FSDPEngine(LocalEngine):
         self.reshard_after_forward = reshard_after_forward
         # units gathered ahead of the one computing (forward: i+1..i+prefetch, backward:
         # i-1..i-prefetch); each extra unit costs one gathered unit of memory (Llama-3-8B block:
-        # 436 MB bf16) and buys slack when a gather is slower than one unit's compute
-        self.prefetch = max(1, int(prefetch))
+        # 436 MB bf16) and buys slack when a gather is slower than one unit's compute.
+        # prefetch 0 / None = auto: sized per batch shape from the block's gather time over xGMI
+        # vs its forward compute (parallel/commplan.py:fsdp_prefetch_depth)
+        self.prefetch_auto = prefetch in (0, None, "auto")
+        self.prefetch = 1 if self.prefetch_auto else max(1, int(prefetch))
+        self._prefetch_tokens = None
         self.grad_prescale = 1.0 / self.world_size
         self.is_cuda = self.device.type == "cuda"
         from . import force_comm
@@ -97,6 +101,7 @@ class FSDPEngine(LocalEngine):
                 st["bufs"].append(fb)
             st["gathered"] = self.no_shard
             st["gather_work"] = None
+            st["sharded"] = not self.no_shard   # read by FusedLinear._kaug_ok (no persistent W copies)
         self._rs_works: List = []
         self._in_backward = False
         model.set_engine(self)
@@ -152,15 +157,32 @@ class FSDPEngine(LocalEngine):
             _free(fb.data)
         st["gathered"] = False
 
+    def _size_prefetch(self):
+        rc = self.model.rctx
+        tokens = rc.B * rc.T
+        if tokens == self._prefetch_tokens:
+            return
+        from .commplan import fsdp_prefetch_depth
+        self._prefetch_tokens = tokens
+        blocks = [u for u in self.units if u.name.startswith(("trf_blocks", "blocks"))] or self.units
+        big = max(blocks, key=lambda u: sum(fb.numel for fb in u.state["bufs"]))
+        numel = sum(fb.numel for fb in big.state["bufs"])
+        nbytes = sum(fb.numel * fb.data.element_size() for fb in big.state["bufs"])
+        self.prefetch = fsdp_prefetch_depth(nbytes, numel, tokens, self.world_size)
+
     # ------------------------------------------------------------------ hooks
     def pre_forward(self, unit):
+        if self.prefetch_auto and unit.index == 0:
+            self._size_prefetch()
         self._wait_gather(unit)
         for nxt in range(unit.index + 1, min(unit.index + 1 + self.prefetch, len(self.units))):
             self._issue_gather(self.units[nxt], async_op=True)
 
     def post_forward(self, unit):
         last = unit.index == len(self.units) - 1
-        training = torch.is_grad_enabled() and self.model.training
+        # (torch.is_grad_enabled() is False inside the units' autograd.Function.forward: the
+        # model forward records whether it builds a backward)
+        training = self.model.rctx.grad_forward and self.model.training
         if not training:  # eval / sampling: nothing is kept for a backward
             self._reshard(unit)
             return

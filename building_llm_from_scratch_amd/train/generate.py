@@ -63,7 +63,10 @@ class DecodeGraph:
                 model.forward_cached_dev(self.idx, cache, self.pos)
         cur.wait_stream(side)
         self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph):
+        # thread_local: the sample print runs mid-epoch while DataLoader worker / pin-memory
+        # threads may make allocator or event calls; in "global" mode those would invalidate
+        # (or be rejected during) this capture
+        with torch.cuda.graph(self.graph, capture_error_mode="thread_local"):
             self.logits = model.forward_cached_dev(self.idx, cache, self.pos)
 
     def step(self, idx_next: torch.Tensor, pos: int) -> torch.Tensor:

@@ -161,6 +161,11 @@ class Trainer:
         for g in self.optimizer.param_groups:
             g["lr"] = lr
         self.track_lrs.append(lr)
+        rc = getattr(self.model, "rctx", None)
+        if rc is not None and self.loss_scaler is not None:
+            # the fused head takes the logit gradient inside its forward: tell it the dloss that
+            # backward will bring, so fp16 softmax tails are scaled before they are rounded
+            rc.loss_scale = float(self.loss_scaler.scale)
         loss = self.calc_loss_batch(input_batch, target_batch)
         if self.loss_scaler is not None:
             (loss * self.loss_scaler.scale).backward()

@@ -59,3 +59,16 @@ def test_cli_llama32_lora_finetune_gpu(tmp_path):
           "--sample_tokens", "2"], tmp_path)
     sd = torch.load(out / "model_pg_final.pth", weights_only=True)
     assert "trf_blocks.0.att.W_query.lora.A" in sd
+
+
+def test_cli_sample_mid_epoch_with_workers_gpu(tmp_path):
+    """The sample print's HIP-graph decode is captured mid-epoch while DataLoader workers and
+    the pin-memory thread are alive (num_workers 2, pin_memory on the GPU): the capture runs in
+    thread_local mode so their allocator / event calls cannot invalidate it."""
+    out = tmp_path / "ckpt"
+    r = _run(["--model", "GPT2", "--num_params", "124M", "--debug", "--data_dir", str(tmp_path / "data"),
+              "--synthetic_data", "--output_dir", str(out), "--n_epochs", "1", "--max_steps", "6", "--eval_freq", "3",
+              "--save_ckpt_freq", "100", "--print_sample_iter", "2", "--batch_size", "2", "--data_type", "bf16",
+              "--num_workers", "2", "--sample_tokens", "8", "--no_plot"], tmp_path)
+    text = r.stdout + r.stderr
+    assert text.count("Generated Sample:") >= 3, text[-3000:]   # start-up sample + mid-epoch samples

@@ -1,8 +1,16 @@
-"""HIP kernels vs the plain-PyTorch fp32 reference (ops/reference.py).  GPU only."""
+"""HIP kernels vs the plain-PyTorch fp32 reference (ops/reference.py).  GPU only.
+
+Closeness (tests/numerics.py): the error is measured in units of what rounding the exact fp32
+oracle to the kernel's output dtype costs, globally and per |ref|-magnitude decile, so an error
+confined to small elements (a GQA partial, a masked-tile edge) is not hidden by the large ones;
+``k`` is the allowance per kernel class (<= 5 for bf16 / fp16: test_numerics_check.py shows a 1 %
+perturbation of the smallest 10 % of elements exceeds it).  Per-row statistics (log-sum-exp,
+CE rows, rstd) and the optimizer state are checked elementwise (``check_elem``)."""
 import math
 
 import pytest
 import torch
+from numerics import check_close, check_elem
 
 from building_llm_from_scratch_amd import ops
 from building_llm_from_scratch_amd.ops import reference as ref
@@ -10,14 +18,25 @@ from building_llm_from_scratch_amd.ops import reference as ref
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
 DTYPES = [torch.bfloat16, torch.float16, torch.float32]
-TOL = {torch.bfloat16: 2e-2, torch.float16: 2e-3, torch.float32: 1e-5}
+# allowance per kernel class, in rounding units: the former max-normalised scale factor -> k
+K_OF = {0.5: 1.5, 1: 2.0, 2: 3.0, 4: 5.0}
+K_MAX = 5.0
 
 
 def _close(a, b, dt, scale=1.0, name=""):
-    a, b = a.float().cpu(), b.float().cpu()
-    err = (a - b).abs().max().item()
-    ref_mag = b.abs().max().item() + 1e-6
-    assert err <= TOL[dt] * max(ref_mag, 1.0) * scale, f"{name}: max err {err} (ref mag {ref_mag})"
+    k = K_OF[scale]
+    assert k <= K_MAX
+    check_close(a, b, dt, k=k, name=name)
+
+
+def _ulps(a, b, dt, n=1.0, name=""):
+    """Two GPU results that should agree to n ulps of dt (same arithmetic, different order)."""
+    u = {torch.bfloat16: 2.0 ** -7, torch.float16: 2.0 ** -10, torch.float32: 2.0 ** -22}[dt]
+    b = b.float()
+    check_elem(a.float(), b, rtol=n * u, atol=n * u * b.abs().max().item() * 1e-3, name=name)
+
+
+LSE_TOL = dict(rtol=1e-5, atol=2e-5)      # fp32 log-sum-exp of bf16 / fp16 / fp32 scores
 
 
 @pytest.fixture(autouse=True)
@@ -37,7 +56,7 @@ def test_rmsnorm(dt, d):
     y, r = ops.rmsnorm_fwd(x, w, 1e-5)
     y0, r0 = ref.rmsnorm_fwd(x.cpu().float(), w.cpu().float(), 1e-5)
     _close(y, y0, dt, name="y")
-    _close(r, r0, torch.float32, 10, name="rstd")
+    check_elem(r, r0, rtol=2e-5, atol=0, name="rstd")
     dx, dw = ops.rmsnorm_bwd(dy, x, w, r, acc)
     dx0, dw0 = ref.rmsnorm_bwd(dy.cpu().float(), x.cpu().float(), w.cpu().float(), r0, acc.cpu().float())
     _close(dx, dx0, dt, 2, name="dx")
@@ -115,7 +134,7 @@ def test_rope(dt, hd, H, G):
     q1 = ops.rope_(qkv.clone(), cos, sin, T, H, G, hd)
     _close(q1, q0, dt, name="rope")
     back = ops.rope_(q1.clone(), cos, sin, T, H, G, hd, inverse=True)
-    _close(back, qkv, dt, 2, name="rope inverse")
+    _close(back, qkv.float(), dt, 2, name="rope inverse")
 
 
 @pytest.mark.parametrize("dt", DTYPES)
@@ -127,8 +146,8 @@ def test_cross_entropy(dt, V):
     tgt[3] = -100
     l, lse = ops.ce_fwd(logits, tgt)
     l0, lse0 = ref.ce_fwd(logits.cpu().float(), tgt.cpu())
-    _close(l, l0, torch.float32, 100, name="loss")
-    _close(lse, lse0, torch.float32, 100, name="lse")
+    check_elem(l, l0, **LSE_TOL, name="loss")
+    check_elem(lse, lse0, **LSE_TOL, name="lse")
     scale = torch.tensor([0.5], device=DEV)
     g = ops.ce_bwd_(logits.clone(), tgt, lse, scale)
     g0 = ref.ce_bwd_(logits.cpu().float().clone(), tgt.cpu(), lse0, scale.cpu())
@@ -171,10 +190,10 @@ def test_adamw_and_norm(pdt):
     refs = [t.cpu().clone() if t is not None else None for t in (param, master, g, m, v)]
     ops.adamw_step_(param, master, g, m, v, grad_scale=scale, **args)
     ref.adamw_step_(refs[0], refs[1], refs[2], refs[3], refs[4], grad_scale=scale.cpu(), **args)
-    _close(m, refs[3], torch.float32, 10, name="m")
-    _close(v, refs[4], torch.float32, 10, name="v")
+    check_elem(m, refs[3], rtol=1e-6, atol=1e-7, name="m")
+    check_elem(v, refs[4], rtol=1e-6, atol=1e-9, name="v")
     if master is not None:
-        _close(master, refs[1], torch.float32, 10, name="master")
+        check_elem(master, refs[1], rtol=1e-6, atol=1e-7, name="master")
     _close(param, refs[0], pdt, name="param")
     ts = [torch.randn(1000, device=DEV).to(pdt), torch.randn(37, device=DEV), torch.randn(100003, device=DEV).to(pdt)]
     sq = ops.sq_norm_multi(ts)
@@ -194,7 +213,7 @@ def test_flash_attention(dt, B, T, H, G, hd, p, causal):
     o, lse = ops.flash_attn_fwd(qkv, B, T, H, G, hd, causal, p, 99, 12345)
     o0, lse0 = ref.flash_attn_fwd(qkv.cpu().float(), B, T, H, G, hd, causal, p, 99, 12345)
     _close(o, o0, dt, 2, name="o")
-    _close(lse, lse0, torch.float32, 1000, name="lse")
+    check_elem(lse, lse0, **LSE_TOL, name="lse")
     dqkv = ops.flash_attn_bwd(qkv, o, lse, do, B, T, H, G, hd, causal, p, 99, 12345)
     dqkv0 = ref.flash_attn_bwd(qkv.cpu().float(), o0, lse0, do.cpu().float(), B, T, H, G, hd, causal, p, 99,
                                12345)
@@ -249,7 +268,7 @@ def test_flash_attention_deferred_rescale(dt, hd, step):
     o, lse = ops.flash_attn_fwd(qkv, B, T, H, G, hd, True, 0.0, 1, 0)
     o0, lse0 = ref.flash_attn_fwd(qkv.float(), B, T, H, G, hd, True, 0.0, 1, 0)
     _close(o, o0, dt, 2, name="o")
-    _close(lse, lse0, torch.float32, 1000, name="lse")
+    check_elem(lse, lse0, **LSE_TOL, name="lse")
     dqkv = ops.flash_attn_bwd(qkv, o, lse, do, B, T, H, G, hd, True, 0.0, 1, 0)
     dqkv0 = ref.flash_attn_bwd(qkv.float(), o0, lse0, do.float(), B, T, H, G, hd, True, 0.0, 1, 0)
     _close(dqkv, dqkv0, dt, 4, name="dqkv")
@@ -284,7 +303,7 @@ def test_flash_attention_long_context(T, H, G, hd, p):
     o, lse = ops.flash_attn_fwd(qkv, B, T, H, G, hd, True, p, 7, 4242)
     o0, lse0 = ref.flash_attn_fwd(qkv.float(), B, T, H, G, hd, True, p, 7, 4242)
     _close(o, o0, torch.bfloat16, 2, name="o")
-    _close(lse, lse0, torch.float32, 1000, name="lse")
+    check_elem(lse, lse0, **LSE_TOL, name="lse")
     dqkv = ops.flash_attn_bwd(qkv, o, lse, do, B, T, H, G, hd, True, p, 7, 4242)
     del o0
     dqkv0 = ref.flash_attn_bwd(qkv.float(), o.float(), lse0, do.float(), B, T, H, G, hd, True, p, 7, 4242)
@@ -321,10 +340,10 @@ def test_flash_attention_bwd_fused_rope(dt, B, T, H, G, hd):
     fused = ops.flash_attn_bwd(qkv, o, lse, do, B, T, H, G, hd, True, rope=(cos, sin))
     sep = ops.flash_attn_bwd(qkv, o, lse, do, B, T, H, G, hd, True)
     ops.rope_(sep, cos, sin, T, H, G, hd, inverse=True)
-    _close(fused, sep.float().cpu(), dt, 2, name="fused vs separate")
     want = ref.flash_attn_bwd(qkv.float(), o.float(), lse, do.float(), B, T, H, G, hd, True)
     ref.rope_(want, cos, sin, T, H, G, hd, inverse=True)
     _close(fused, want.cpu(), dt, 4, name="fused vs oracle")
+    _close(sep, want.cpu(), dt, 4, name="separate vs oracle")
 
 
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
@@ -368,7 +387,7 @@ def test_bwd_bias_grad_fused(dt, N, F, acc):
         out2 = sep()
         ops.bias_grad_(out2, db2, acc)
         assert torch.equal(out1, out2), name
-        _close(db1, db2, dt, 0.5, name=name + " db")  # one ulp of db's dtype
+        _ulps(db1, db2, dt, 1, name=name + " db")  # one ulp of db's dtype
     # GELU backward that also rebuilds g = gelu(f) in place of dg (GPT-2 checkpoint recompute),
     # with and without the bias sums
     for with_db in (True, False):
@@ -380,7 +399,7 @@ def test_bwd_bias_grad_fused(dt, N, F, acc):
         if with_db:
             db4 = db0.clone()
             ops.bias_grad_(out3, db4, acc)
-            _close(db3, db4, dt, 0.5, name="gelu act db")
+            _ulps(db3, db4, dt, 1, name="gelu act db")
 
 
 # ------------------------------------------------------------------ LoRA (csrc/lora.hip)
@@ -513,9 +532,7 @@ def test_wgrad_gemm(dt, odt, K, M, N, S, accumulate, variant, monkeypatch):
     assert ops.wgrad_gemm_ok(a, b, c)
     expect = a.float().t() @ b.float() + (c.float() if accumulate else 0)
     ops.wgrad_gemm_(a, b, c, accumulate, S)
-    err = (c.float() - expect).abs().max().item()
-    mag = expect.abs().max().item()
-    assert err <= (8e-3 if odt == torch.bfloat16 else 1e-4) * mag, (err, mag)
+    check_close(c, expect, odt if odt == torch.float32 else dt, k=3.0, name="wgrad")
 
 
 def test_wgrad_gemm_in_weight_grad_path():
@@ -542,8 +559,7 @@ def test_wgrad_gemm_unaligned_output(accumulate):
     before = c_full.clone()
     expect = a.float().t() @ b.float() + (c.float() if accumulate else 0)
     ops.wgrad_gemm_(a, b, c, accumulate, 1)
-    err = (c.float() - expect).abs().max().item()
-    assert err <= 8e-3 * expect.abs().max().item(), err
+    check_close(c, expect, torch.bfloat16, k=3.0, name="wgrad unaligned")
     assert torch.equal(c_full[:, 0], before[:, 0]) and torch.equal(c_full[:, 1 + N:], before[:, 1 + N:])
 
 
@@ -561,8 +577,7 @@ def test_gemm_nt(dt, odt, M, K, N, accumulate):
     c = torch.randn(M, N, device=DEV).to(odt or dt)
     expect = a.float() @ b.float().t() + (c.float() if accumulate else 0)
     ops.gemm_nt_(a, b, c, accumulate)
-    err = (c.float() - expect).abs().max().item()
-    assert err <= (8e-3 if (odt or dt) != torch.float32 else 1e-4) * expect.abs().max().item(), err
+    check_close(c, expect, odt or dt, k=3.0, name="gemm_nt")
 
 
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
@@ -578,9 +593,7 @@ def test_gemm_nn(dt, odt, M, K, N, accumulate):
     assert ops.gemm_nn_ok(a, b, c)
     expect = a.float() @ b.float() + (c.float() if accumulate else 0)
     ops.gemm_nn_(a, b, c, accumulate)
-    err = (c.float() - expect).abs().max().item()
-    mag = expect.abs().max().item()
-    assert err <= (8e-3 if c.dtype != torch.float32 else 1e-4) * mag, (err, mag)
+    check_close(c, expect, c.dtype, k=3.0, name="gemm_nn")
 
 
 def test_dgrad_in_linear_backward(monkeypatch):
