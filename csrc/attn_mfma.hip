@@ -14,8 +14,12 @@
 // (element j of lane half h = key 16s + 8(j>>2) + 4h + (j&3)); the V^T operand is read
 // with the matching key permutation: two transposed reads of 4 keys each.
 //
-// Workgroup = 4 waves = 128 queries of one (batch, head); K/V tiles of 64 keys, register
-// DMA (global_load_lds) of tile t+1 under the MFMAs of tile t, double-buffered LDS.  GQA reads kv head h / (H/G)
+// Workgroup = 4 waves; each wave owns QB 32-query blocks (QB = 1: 128 queries per workgroup;
+// QB = 2: 256): every K fragment and V^T fragment read from LDS feeds QB MFMAs, so QB = 2 halves
+// the LDS read bytes, the DMA landing waits and the barriers per FLOP (at QB = 1 the K + V
+// reads of a tile, 32 KiB per wave at hd 128, match the MFMA time of the tile).  K/V tiles of
+// 64 keys, register DMA (global_load_lds) of tile t+1 under the MFMAs of tile t,
+// double-buffered LDS.  GQA reads kv head h / (H/G)
 // directly; causal tiles above the diagonal are skipped; q-blocks are launched
 // heaviest-first.  LDS images are XOR-swizzled: K in 16-B chunks (conflict-free
 // ds_read_b128 row reads), V in 64-B chunks (conflict-free transposed reads).
@@ -50,7 +54,7 @@ template <> struct MF<f16_t> {
 
 constexpr float kLog2e = 1.4426950408889634f;
 constexpr float kRescaleThr = 8.f;  // deferred online-softmax rescale threshold (log2 units)
-constexpr int FWD_BQ = 128;  // queries per workgroup
+constexpr int FWD_BQ = 128;  // queries per workgroup per q-block of each wave (x QB)
 // keys per tile (FWD_BK), LDS ring depth and workgroups per CU are template parameters
 
 // ---- swizzled LDS images (byte offsets) -------------------------------------------------
@@ -80,7 +84,7 @@ template <typename T> __device__ __forceinline__ uint32_t pack2(float a, float b
 // per-lane offsets, 2x(LD) saddr DMA issues with precomputed per-lane source offsets, and
 // ~130 VALU of online softmax (scale folded into the exp2 FMA; the O rescale is skipped when
 // no lane's running max moved, which is the common case after the first tiles).
-template <typename T, int HD, bool DROP, int FWD_BK, int NBUF, int OCC>
+template <typename T, int HD, bool DROP, int FWD_BK, int NBUF, int OCC, int QB>
 __global__ __launch_bounds__(256, OCC) void attn_fwd_mfma_k(const T* __restrict__ qkv, T* __restrict__ out,
                                                           float* __restrict__ lse, int T_, int H, int G, int B_,
                                                           bool causal, uint32_t thr, float inv_keep, uint64_t seed,
@@ -94,12 +98,15 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd_mfma_k(const T* __restrict_
   constexpr int LD = FWD_BK * CH / 256;     // 1-KiB pieces per wave per tile (K and V each)
   constexpr int NPW = 2 * LD;
   constexpr int NKT = FWD_BK / 32;          // 32-key MFMA tiles per step
+  constexpr int WQ = 32 * QB;               // queries per wave
+  constexpr int BQ = FWD_BQ * QB;           // queries per workgroup
   static_assert(NBUF == 2 || NBUF == 3, "ring depth");
+  static_assert(QB == 1 || QB == 2, "q-blocks per wave");
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   // heaviest (latest, for causal) q-blocks first over the whole grid; the q-blocks of one
   // (b, h) share lin % 8 (one XCD / L2 for their common K/V stream)
-  const int nqb = (T_ + FWD_BQ - 1) / FWD_BQ;
+  const int nqb = (T_ + BQ - 1) / BQ;
   const int lin = blockIdx.x, nbh = H * B_;
   const int qbi = lin / nbh, bh = lin - qbi * nbh;
   const int qb = causal ? nqb - 1 - qbi : qbi;
@@ -112,9 +119,11 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd_mfma_k(const T* __restrict_
   const T* qbase = qkv + (long)b * T_ * rs + (long)h * HD;
   const T* kbase = qkv + (long)b * T_ * rs + (long)(H + g) * HD;
   const T* vbase = qkv + (long)b * T_ * rs + (long)(H + G + g) * HD;
-  const int q0 = qb * FWD_BQ;
-  const int wq_lo = q0 + w * 32, wq_hi = wq_lo + 31;  // this wave's query range
-  const int qi = wq_lo + l32;                          // this lane's query
+  const int q0 = qb * BQ;
+  const int wq_lo = q0 + w * WQ, wq_hi = wq_lo + WQ - 1;  // this wave's query range
+  int qi[QB];                                             // this lane's query in each q-block
+#pragma unroll
+  for (int u = 0; u < QB; ++u) qi[u] = wq_lo + 32 * u + l32;
   const float c = rsqrtf((float)HD) * kLog2e;
   DropSlab ds;
   uint64_t dslab = 0;
@@ -126,19 +135,27 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd_mfma_k(const T* __restrict_
   }
 
   // ---- Q fragments (B operand): Q[qi][16kk + 8hh + 0..7]
-  v8 qf[KK];
+  v8 qf[QB][KK];
 #pragma unroll
-  for (int kk = 0; kk < KK; ++kk) {
-    if (qi < T_) qf[kk] = *reinterpret_cast<const v8*>(qbase + (long)qi * rs + kk * 16 + hh * 8);
-    else qf[kk] = v8{};
-  }
+  for (int u = 0; u < QB; ++u)
 #pragma unroll
-  for (int kk = 0; kk < KK; ++kk) asm volatile("" ::"v"(qf[kk]));  // retire before the loop
+    for (int kk = 0; kk < KK; ++kk) {
+      if (qi[u] < T_) qf[u][kk] = *reinterpret_cast<const v8*>(qbase + (long)qi[u] * rs + kk * 16 + hh * 8);
+      else qf[u][kk] = v8{};
+    }
+#pragma unroll
+  for (int u = 0; u < QB; ++u)
+#pragma unroll
+    for (int kk = 0; kk < KK; ++kk) asm volatile("" ::"v"(qf[u][kk]));  // retire before the loop
 
-  f32x16 o[DT];
+  f32x16 o[QB][DT];
 #pragma unroll
-  for (int i = 0; i < DT; ++i) o[i] = f32x16{};
-  float m = -1e30f, l = 0.f;
+  for (int u = 0; u < QB; ++u)
+#pragma unroll
+    for (int i = 0; i < DT; ++i) o[u][i] = f32x16{};
+  float m[QB], l[QB];
+#pragma unroll
+  for (int u = 0; u < QB; ++u) m[u] = -1e30f, l[u] = 0.f;
 
   // ---- loop-invariant per-lane offsets
   int koff[KK];
@@ -162,9 +179,9 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd_mfma_k(const T* __restrict_
   };
   const uint32_t smem_u = lds_u32(smem);
 
-  const int kend = causal ? min(T_, q0 + FWD_BQ) : T_;
+  const int kend = causal ? min(T_, q0 + BQ) : T_;
   const int ntiles = (kend + FWD_BK - 1) / FWD_BK;
-  const int nact = wq_lo >= T_ ? 0 : (causal ? min(ntiles, wq_hi / FWD_BK + 1) : ntiles);
+  const int nact = wq_lo >= T_ ? 0 : (causal ? min(ntiles, min(wq_hi, T_ - 1) / FWD_BK + 1) : ntiles);
 
   // K/V tiles land in LDS by direct DMA (1 KiB per wave instruction, lane-linear destination);
   // the XOR swizzle is applied to the per-lane SOURCE offset, so the linear DMA image IS the
@@ -220,16 +237,20 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd_mfma_k(const T* __restrict_
   // dropout keep-mask words of the last computed tile (kmask != nullptr): stored at the top of
   // the next iteration, BEFORE that iteration's DMA issue -- vector memory completes in order,
   // so the ring's counted waits are not lengthened by the stores
-  uint32_t kw_pend[NKT];
+  uint32_t kw_pend[QB][NKT];
   int kw_n = 0, kw_t = 0;
   const long kw_row = (long)((T_ + 31) / 32) * T_;  // words per (b, h)
   auto flush_mask = [&]() {
     if constexpr (DROP) {
-      if (kmask != nullptr && hh == 0 && qi < T_) {
-        uint32_t* mrow = kmask + (long)(b * H + h) * kw_row + qi;
+      if (kmask != nullptr && hh == 0) {
 #pragma unroll
-        for (int kt = 0; kt < NKT; ++kt)
-          if (kt < kw_n) mrow[(long)(kw_t * NKT + kt) * T_] = kw_pend[kt];
+        for (int u = 0; u < QB; ++u) {
+          if (qi[u] >= T_) continue;
+          uint32_t* mrow = kmask + (long)(b * H + h) * kw_row + qi[u];
+#pragma unroll
+          for (int kt = 0; kt < NKT; ++kt)
+            if (kt < kw_n) mrow[(long)(kw_t * NKT + kt) * T_] = kw_pend[u][kt];
+        }
       }
       kw_n = 0;
     }
@@ -240,104 +261,112 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd_mfma_k(const T* __restrict_
   auto body = [&](auto nv_c, auto edge_c, int k0, const char* kb, const char* vb) {
     constexpr int NV = decltype(nv_c)::value;
     constexpr bool EDGE = decltype(edge_c)::value;
-    // ---- S^T = K Q^T for the visible 32-key sub-tiles
-    f32x16 s[NV];
-    {
+    // ---- S^T = K Q^T for the visible 32-key sub-tiles; each K fragment feeds QB MFMAs
+    f32x16 s[QB][NV];
 #pragma unroll
-      for (int kt = 0; kt < NV; ++kt) {
-        s[kt] = f32x16{};
+    for (int kt = 0; kt < NV; ++kt) {
 #pragma unroll
-        for (int kk = 0; kk < KK; ++kk)
-          s[kt] = MF<T>::mma(*reinterpret_cast<const v8*>(kb + kt * 32 * ROWB + koff[kk]), qf[kk], s[kt]);
+      for (int u = 0; u < QB; ++u) s[u][kt] = f32x16{};
+#pragma unroll
+      for (int kk = 0; kk < KK; ++kk) {
+        const v8 kf = *reinterpret_cast<const v8*>(kb + kt * 32 * ROWB + koff[kk]);
+#pragma unroll
+        for (int u = 0; u < QB; ++u) s[u][kt] = MF<T>::mma(kf, qf[u][kk], s[u][kt]);
       }
     }
-    // ---- mask: key k0 + 4hh + off is visible iff off <= lim (one compare + select each)
-    if constexpr (EDGE) {
-      const int lim = (causal ? min(qi, T_ - 1) : T_ - 1) - (k0 + 4 * hh);
+#pragma unroll
+    for (int u = 0; u < QB; ++u) {
+      // ---- mask: key k0 + 4hh + off is visible iff off <= lim (one compare + select each)
+      if constexpr (EDGE) {
+        const int lim = (causal ? min(qi[u], T_ - 1) : T_ - 1) - (k0 + 4 * hh);
+#pragma unroll
+        for (int kt = 0; kt < NV; ++kt)
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            if (kt * 32 + (r & 3) + 8 * (r >> 2) > lim) s[u][kt][r] = -INFINITY;
+      }
+      // ---- online softmax
+      float mx = -INFINITY;
 #pragma unroll
       for (int kt = 0; kt < NV; ++kt)
 #pragma unroll
-        for (int r = 0; r < 16; ++r)
-          if (kt * 32 + (r & 3) + 8 * (r >> 2) > lim) s[kt][r] = -INFINITY;
-    }
-    // ---- online softmax
-    float mx = -INFINITY;
-#pragma unroll
-    for (int kt = 0; kt < NV; ++kt)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s[kt][r]);
-    {  // other half's max: one v_permlane32_swap (no LDS round trip / lgkmcnt wait)
-      const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
-      mx = fmaxf(mx, fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]))) * c;
-    }
-    // deferred rescale: only when some lane's max grew by more than kRescaleThr (log2 units);
-    // until then P is exponentiated against the stale max and stays below 2^kRescaleThr
-    // (fp32 O / l accumulators; bf16 P keeps its relative precision), and the epilogue's
-    // lse = m + log2(l) is exact for whatever m the sums were taken against
-    if (__builtin_amdgcn_ballot_w64(mx > m + kRescaleThr)) {
-      const float mn = fmaxf(m, mx);
-      const float alpha = __builtin_amdgcn_exp2f(m - mn);
-      l *= alpha;
-#pragma unroll
-      for (int i = 0; i < DT; ++i) o[i] *= alpha;
-      m = mn;
-    }
-    float ls = 0.f;
-#pragma unroll
-    for (int kt = 0; kt < NV; ++kt)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float p = __builtin_amdgcn_exp2f(fmaf(s[kt][r], c, -m));
-        ls += p;
-        s[kt][r] = p;
+        for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s[u][kt][r]);
+      {  // other half's max: one v_permlane32_swap (no LDS round trip / lgkmcnt wait)
+        const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
+        mx = fmaxf(mx, fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]))) * c;
       }
-    l += ls;
-    if constexpr (DROP) {
-      // keys (r, r+1) with r even are adjacent: one hash serves both when the row base is even.
-      // The keep bits also go to the backward's mask (bit (r&3) + 8(r>>2) + 4hh of the word of
-      // this query and 32-key sub-tile; the two lane halves' bits are merged by one swap).
-      const uint64_t rowbase = dslab + (uint64_t)qi * T_;
+      // deferred rescale: only when some lane's max grew by more than kRescaleThr (log2 units);
+      // until then P is exponentiated against the stale max and stays below 2^kRescaleThr
+      // (fp32 O / l accumulators; bf16 P keeps its relative precision), and the epilogue's
+      // lse = m + log2(l) is exact for whatever m the sums were taken against
+      if (__builtin_amdgcn_ballot_w64(mx > m[u] + kRescaleThr)) {
+        const float mn = fmaxf(m[u], mx);
+        const float alpha = __builtin_amdgcn_exp2f(m[u] - mn);
+        l[u] *= alpha;
 #pragma unroll
-      for (int kt = 0; kt < NV; ++kt) {
-        uint32_t kbits = 0;
-        if (dpair) {
+        for (int i = 0; i < DT; ++i) o[u][i] *= alpha;
+        m[u] = mn;
+      }
+      float ls = 0.f;
 #pragma unroll
-          for (int r = 0; r < 16; r += 2) {
-            const int key = k0 + kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
-            const uint32_t hv = ds.pair_hash((rowbase + key) >> 1);
-            const bool k0b = (hv & 0xFFFFu) >= thr, k1b = (hv >> 16) >= thr;
-            s[kt][r] = k0b ? s[kt][r] * inv_keep : 0.f;
-            s[kt][r + 1] = k1b ? s[kt][r + 1] * inv_keep : 0.f;
-            kbits |= ((uint32_t)k0b << ((r & 3) + 8 * (r >> 2))) | ((uint32_t)k1b << (((r + 1) & 3) + 8 * (r >> 2)));
+      for (int kt = 0; kt < NV; ++kt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float pv = __builtin_amdgcn_exp2f(fmaf(s[u][kt][r], c, -m[u]));
+          ls += pv;
+          s[u][kt][r] = pv;
+        }
+      l[u] += ls;
+      if constexpr (DROP) {
+        // keys (r, r+1) with r even are adjacent: one hash serves both when the row base is even.
+        // The keep bits also go to the backward's mask (bit (r&3) + 8(r>>2) + 4hh of the word of
+        // this query and 32-key sub-tile; the two lane halves' bits are merged by one swap).
+        const uint64_t rowbase = dslab + (uint64_t)qi[u] * T_;
+#pragma unroll
+        for (int kt = 0; kt < NV; ++kt) {
+          uint32_t kbits = 0;
+          if (dpair) {
+#pragma unroll
+            for (int r = 0; r < 16; r += 2) {
+              const int key = k0 + kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+              const uint32_t hv = ds.pair_hash((rowbase + key) >> 1);
+              const bool k0b = (hv & 0xFFFFu) >= thr, k1b = (hv >> 16) >= thr;
+              s[u][kt][r] = k0b ? s[u][kt][r] * inv_keep : 0.f;
+              s[u][kt][r + 1] = k1b ? s[u][kt][r + 1] * inv_keep : 0.f;
+              kbits |= ((uint32_t)k0b << ((r & 3) + 8 * (r >> 2))) |
+                       ((uint32_t)k1b << (((r + 1) & 3) + 8 * (r >> 2)));
+            }
+          } else {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const int key = k0 + kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+              const bool kb_ = ds.bits16(rowbase + key) >= thr;
+              s[u][kt][r] = kb_ ? s[u][kt][r] * inv_keep : 0.f;
+              kbits |= (uint32_t)kb_ << ((r & 3) + 8 * (r >> 2));
+            }
           }
-        } else {
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int key = k0 + kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
-            const bool kb = ds.bits16(rowbase + key) >= thr;
-            s[kt][r] = kb ? s[kt][r] * inv_keep : 0.f;
-            kbits |= (uint32_t)kb << ((r & 3) + 8 * (r >> 2));
+          if (kmask != nullptr) {
+            const uint32_t mine = kbits << (4 * hh);
+            const auto sw = __builtin_amdgcn_permlane32_swap(mine, mine, false, false);
+            kw_pend[u][kt] = mine | sw[0] | sw[1];
           }
         }
-        if (kmask != nullptr) {
-          const uint32_t mine = kbits << (4 * hh);
-          const auto sw = __builtin_amdgcn_permlane32_swap(mine, mine, false, false);
-          kw_pend[kt] = mine | sw[0] | sw[1];
-        }
+        kw_n = NV;
       }
-      kw_n = NV;
     }
     // ---- O^T += V^T P^T: P fragments packed from the accumulators, V^T by transposed reads
+    //      (each V^T fragment feeds QB MFMAs)
 #pragma unroll
     for (int kt = 0; kt < NV; ++kt)
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) {
-        v8 pf;
-        {
-          uint32_t u[4];
+        v8 pf[QB];
 #pragma unroll
-          for (int j = 0; j < 4; ++j) u[j] = pack2<T>(s[kt][8 * s2 + 2 * j], s[kt][8 * s2 + 2 * j + 1]);
-          __builtin_memcpy(&pf, u, 16);
+        for (int u = 0; u < QB; ++u) {
+          uint32_t uu[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) uu[j] = pack2<T>(s[u][kt][8 * s2 + 2 * j], s[u][kt][8 * s2 + 2 * j + 1]);
+          __builtin_memcpy(&pf[u], uu, 16);
         }
 #pragma unroll
         for (int dt = 0; dt < DT; ++dt) {
@@ -345,7 +374,8 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd_mfma_k(const T* __restrict_
           const s16x4 r1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(vb + off));
           const s16x4 r2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(vb + off + 8 * ROWB));
           const v8 va = __builtin_bit_cast(v8, __builtin_shufflevector(r1, r2, 0, 1, 2, 3, 4, 5, 6, 7));
-          o[dt] = MF<T>::mma(va, pf, o[dt]);
+#pragma unroll
+          for (int u = 0; u < QB; ++u) o[u][dt] = MF<T>::mma(va, pf[u], o[u][dt]);
         }
       }
   };
@@ -353,10 +383,10 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd_mfma_k(const T* __restrict_
   using IcN = std::integral_constant<int, NKT>;
   using Yes = std::true_type;
   using No = std::false_type;
-  // Interior tiles (no masked key: below the causal diagonal, inside the sequence) form a
-  // prefix of the wave's tiles; they run in a loop of their own with the one unmasked body, so
-  // the O accumulators never meet the edge variants' registers on the hot path (a shared loop
-  // made hipcc copy them between variants every tile).
+  // Interior tiles (no masked key for any of the wave's queries: below the causal diagonal,
+  // inside the sequence) form a prefix of the wave's tiles; they run in a loop of their own with
+  // the one unmasked body, so the O accumulators never meet the edge variants' registers on the
+  // hot path (a shared loop made hipcc copy them between variants every tile).
   const int n_int = wq_hi >= T_ ? 0 : min(min(nact, T_ / FWD_BK), causal ? (wq_lo + 1) / FWD_BK : nact);
   for (; t < n_int; ++t) {
     flush_mask();  // keep bits of tile t - 1
@@ -388,29 +418,34 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd_mfma_k(const T* __restrict_
   }
 
   // ---- epilogue: combine the two halves' partial sums, normalise, store O and LSE
-  l += __shfl_xor(l, 32, 64);
-  if (qi < T_) {
-    const float inv = l > 0.f ? 1.f / l : 0.f;
-    T* orow = out + ((long)b * T_ + qi) * (long)H * HD + (long)h * HD;
 #pragma unroll
-    for (int dt = 0; dt < DT; ++dt)
+  for (int u = 0; u < QB; ++u) {
+    const float lt = l[u] + __shfl_xor(l[u], 32, 64);
+    if (qi[u] < T_) {
+      const float inv = lt > 0.f ? 1.f / lt : 0.f;
+      T* orow = out + ((long)b * T_ + qi[u]) * (long)H * HD + (long)h * HD;
 #pragma unroll
-      for (int gq = 0; gq < 4; ++gq) {
-        const int d0 = dt * 32 + 8 * gq + 4 * hh;
-        uint2 v;
-        v.x = pack2<T>(o[dt][4 * gq + 0] * inv, o[dt][4 * gq + 1] * inv);
-        v.y = pack2<T>(o[dt][4 * gq + 2] * inv, o[dt][4 * gq + 3] * inv);
-        *reinterpret_cast<uint2*>(orow + d0) = v;
-      }
-    if (hh == 0) lse[((long)b * H + h) * T_ + qi] = m + log2f(l);
+      for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+        for (int gq = 0; gq < 4; ++gq) {
+          const int d0 = dt * 32 + 8 * gq + 4 * hh;
+          uint2 v;
+          v.x = pack2<T>(o[u][dt][4 * gq + 0] * inv, o[u][dt][4 * gq + 1] * inv);
+          v.y = pack2<T>(o[u][dt][4 * gq + 2] * inv, o[u][dt][4 * gq + 3] * inv);
+          *reinterpret_cast<uint2*>(orow + d0) = v;
+        }
+      if (hh == 0) lse[((long)b * H + h) * T_ + qi[u]] = m[u] + log2f(lt);
+    }
   }
 }
 
 bool attn_mfma_head_dim(int hd) { return hd == 64 || hd == 128; }
 
 // forward variant (BLLM_ATTN_FWD_VARIANT, for A/B measurement): 0 = 64-key tiles, 2-slot ring,
-// 2 WGs/CU (measured best: equal at hd 128, +7% at hd 64); 1 = 32-key tiles, 3-slot ring;
-// 2 = 32-key tiles, 2-slot ring (up to 3 WGs/CU)
+// 2 WGs/CU, one 32-query block per wave (round-2 default); 1 = 32-key tiles, 3-slot ring;
+// 2 = 32-key tiles, 2-slot ring (up to 3 WGs/CU); 4 = two 32-query blocks per wave (QB = 2),
+// 64-key tiles (hd 64), 32-key tiles at hd 128 (register budget of 2 waves per SIMD);
+// 5 = QB = 2 with 64-key tiles and one workgroup per CU at hd 128
 static int fwd_variant_from_env() {
   const char* e = getenv("BLLM_ATTN_FWD_VARIANT");
   return e ? atoi(e) : 0;
@@ -420,23 +455,25 @@ void attn_fwd_mfma(DType dt, const void* qkv, void* o, float* lse, int B, int T_
                    float p, uint64_t seed, uint64_t offset, uint32_t* keep_mask, hipStream_t s) {
   const uint32_t thr = drop_threshold16(p);
   const float ik = drop_inv_keep(p);
-  static const int fwd_variant = fwd_variant_from_env();
-  dim3 grid(((T_ + FWD_BQ - 1) / FWD_BQ) * H * B), block(256);
-#define LAUNCH_V(TT, HDD, BK, NB, OC)                                                                     \
+  const int fwd_variant = fwd_variant_from_env();
+#define LAUNCH_V(TT, HDD, BK, NB, OC, QBB)                                                                \
   do {                                                                                                        \
     const int lds = NB * 2 * BK * HDD * 2;                                                                    \
+    const dim3 grid(((T_ + FWD_BQ * QBB - 1) / (FWD_BQ * QBB)) * H * B), block(256);                          \
     if (p > 0.f)                                                                                              \
-      hipLaunchKernelGGL((attn_fwd_mfma_k<TT, HDD, true, BK, NB, OC>), grid, block, lds, s,               \
+      hipLaunchKernelGGL((attn_fwd_mfma_k<TT, HDD, true, BK, NB, OC, QBB>), grid, block, lds, s,          \
                          (const TT*)qkv, (TT*)o, lse, T_, H, G, B, causal, thr, ik, seed, offset, keep_mask); \
     else                                                                                                      \
-      hipLaunchKernelGGL((attn_fwd_mfma_k<TT, HDD, false, BK, NB, OC>), grid, block, lds, s,              \
+      hipLaunchKernelGGL((attn_fwd_mfma_k<TT, HDD, false, BK, NB, OC, QBB>), grid, block, lds, s,         \
                          (const TT*)qkv, (TT*)o, lse, T_, H, G, B, causal, thr, ik, seed, offset, nullptr); \
   } while (0)
 #define LAUNCH(TT, HDD)                                                                                       \
   do {                                                                                                        \
-    if (fwd_variant == 1) LAUNCH_V(TT, HDD, 32, 3, 2);                                                        \
-    else if (fwd_variant == 2) LAUNCH_V(TT, HDD, 32, 2, 3);                                                   \
-    else LAUNCH_V(TT, HDD, 64, 2, 2);                                                                         \
+    if (fwd_variant == 1) LAUNCH_V(TT, HDD, 32, 3, 2, 1);                                                     \
+    else if (fwd_variant == 2) LAUNCH_V(TT, HDD, 32, 2, 3, 1);                                                \
+    else if (fwd_variant == 4) LAUNCH_V(TT, HDD, 32, 3, 2, 2);                                                \
+    else if (fwd_variant == 5) LAUNCH_V(TT, HDD, 64, 2, (HDD == 64 ? 2 : 1), 2);                             \
+    else LAUNCH_V(TT, HDD, 64, 2, 2, 1);                                                                      \
   } while (0)
   if (dt == DType::BF16) {
     if (hd == 128) LAUNCH(bf16_t, 128); else LAUNCH(bf16_t, 64);

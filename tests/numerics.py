@@ -49,8 +49,9 @@ def _eps(r: torch.Tensor, dt: torch.dtype) -> float:
 
 def close_ratio(out: torch.Tensor, ref: torch.Tensor, dt: torch.dtype, bands: int = 10) -> float:
     """Worst condition of check_close in units of k (<= k passes)."""
-    a = out.detach().double().cpu().flatten()
-    r = ref.detach().double().cpu().flatten()
+    dev = out.device if out.is_cuda else ref.device      # evaluate on the GPU when there is one
+    a = out.detach().to(dev, torch.float64).flatten()
+    r = ref.detach().to(dev, torch.float64).flatten()
     assert a.numel() == r.numel(), (a.shape, r.shape)
     if not torch.isfinite(a).all():
         return math.inf

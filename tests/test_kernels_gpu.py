@@ -33,7 +33,9 @@ def _ulps(a, b, dt, n=1.0, name=""):
     """Two GPU results that should agree to n ulps of dt (same arithmetic, different order)."""
     u = {torch.bfloat16: 2.0 ** -7, torch.float16: 2.0 ** -10, torch.float32: 2.0 ** -22}[dt]
     b = b.float()
-    check_elem(a.float(), b, rtol=n * u, atol=n * u * b.abs().max().item() * 1e-3, name=name)
+    # atol: n ulps of the vector's RMS (a column sum that cancels to ~0 differs by the fp32
+    # summation order, not by a fraction of its own tiny magnitude)
+    check_elem(a.float(), b, rtol=n * u, atol=n * u * b.pow(2).mean().sqrt().item(), name=name)
 
 
 LSE_TOL = dict(rtol=1e-5, atol=2e-5)      # fp32 log-sum-exp of bf16 / fp16 / fp32 scores
@@ -191,7 +193,7 @@ def test_adamw_and_norm(pdt):
     ops.adamw_step_(param, master, g, m, v, grad_scale=scale, **args)
     ref.adamw_step_(refs[0], refs[1], refs[2], refs[3], refs[4], grad_scale=scale.cpu(), **args)
     check_elem(m, refs[3], rtol=1e-6, atol=1e-7, name="m")
-    check_elem(v, refs[4], rtol=1e-6, atol=1e-9, name="v")
+    check_elem(v, refs[4], rtol=1e-5, atol=1e-9, name="v")
     if master is not None:
         check_elem(master, refs[1], rtol=1e-6, atol=1e-7, name="master")
     _close(param, refs[0], pdt, name="param")
@@ -532,7 +534,7 @@ def test_wgrad_gemm(dt, odt, K, M, N, S, accumulate, variant, monkeypatch):
     assert ops.wgrad_gemm_ok(a, b, c)
     expect = a.float().t() @ b.float() + (c.float() if accumulate else 0)
     ops.wgrad_gemm_(a, b, c, accumulate, S)
-    check_close(c, expect, odt if odt == torch.float32 else dt, k=3.0, name="wgrad")
+    check_close(c, expect, odt, k=3.0, name="wgrad")
 
 
 def test_wgrad_gemm_in_weight_grad_path():

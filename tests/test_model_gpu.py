@@ -186,3 +186,39 @@ def test_training_is_bitwise_deterministic(name):
         finals.append({k: v.float().cpu() for k, v in m.state_dict().items()})
     for k in finals[0]:
         assert torch.equal(finals[0][k], finals[1][k]), k
+
+
+@pytest.mark.parametrize("name", ["gpt2", "llama_hd64"])
+def test_fp16_fused_head_under_loss_scaling(name, monkeypatch):
+    """fp16 + dynamic loss scaling (the Trainer's fp16 path, loss scale 2^16): the fused chunked
+    head + CE takes the logit gradient inside its forward at the announced loss scale, so softmax
+    tails p / nvalid below fp16's subnormal range are not flushed before scaling.  Its gradients
+    must match the unfused head (full fp16 logits, CE backward at dloss = scale) and the fp32
+    CPU oracle."""
+    from building_llm_from_scratch_amd.models import llama as L
+    ops.load_ext(required=True)
+    cfg = _cfgs()[name].replace(vocab_size=32000)
+    S = 65536.0
+    torch.manual_seed(0)
+    ref = build_model(cfg.replace(dtype=torch.float32))
+    idx = torch.randint(0, cfg.vocab_size, (2, 257))
+    lr = ref(idx[:, :-1], idx[:, 1:])
+    lr.backward()
+    named = dict(ref.named_parameters())
+    head = "output_head.weight" if name == "gpt2" else "out_head.weight"
+    grads = {}
+    for fused in (True, False):
+        if not fused:
+            monkeypatch.setattr(L.HeadComputeMixin, "_fused_ok", lambda self, h: False)
+        m = build_model(cfg.replace(dtype=torch.float16), device="cuda")
+        m.load_state_dict(ref.state_dict())
+        m.rctx.loss_scale = S
+        loss = m(idx[:, :-1].cuda(), idx[:, 1:].cuda())
+        (loss * S).backward()
+        grads[fused] = {k: p.grad.float() / S for k, p in m.named_parameters()}
+        assert abs(loss.item() - lr.item()) < 1e-2 * lr.item()
+    for k in (head, "tok_emb.weight"):
+        e_fused = _rel(grads[True][k], named[k].grad)
+        e_unfused = _rel(grads[False][k], named[k].grad)
+        assert e_fused < 1e-2, (k, e_fused)
+        assert e_fused <= 1.5 * e_unfused + 1e-3, (k, e_fused, e_unfused)

@@ -35,14 +35,16 @@ def recipes(p):
     extra = pre + bs + ck + p.get("args", "")
     steps = int(p.get("steps", 10))
     return {
-        "tests": [("gpu_tests", 1500, f"{PY} -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread "
+        "tests": [("gpu_tests", 900, f"{PY} -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread "
                    "-p no:cacheprovider " + p.get("tests", ""))],
         "smoke": [("smoke", 300, f"{PY} -u -c 'import __graft_entry__ as g; g.smoke()'")],
         "bench": [("bench", 600, _bench(extra, steps))],
         "presets": [(f"preset_{n}", 500, _bench(f"--preset {n} " + p.get("args", ""), steps))
                     for n in ("llama3_8b_fsdp", "gpt2_774m_ddp", "llama32_1b_lora_alpaca", "llama2_7b_fsdp_mp")],
         "prof": [("prof", 600, f"rocprofv3 --kernel-trace --stats -d gpurun_out/{p['tag']}/rocprof -o run -- "
-                  + _bench(extra, int(p.get("steps", 3)), 2))],
+                  + _bench(extra, int(p.get("steps", 3)), 2)),
+                 ("breakdown", 120, f"{PY} tools/step_breakdown.py \"$(find gpurun_out/{p['tag']}/rocprof -name "
+                  f"'*.db' -print -quit)\" --marker {p.get('marker', 'emb_fwd')}")],
         "cmd": [("cmd", int(p.get("timeout", 600)), p.get("cmd", "true"))],
     }
 
