@@ -193,7 +193,7 @@ def test_adamw_and_norm(pdt):
     ops.adamw_step_(param, master, g, m, v, grad_scale=scale, **args)
     ref.adamw_step_(refs[0], refs[1], refs[2], refs[3], refs[4], grad_scale=scale.cpu(), **args)
     check_elem(m, refs[3], rtol=1e-6, atol=1e-7, name="m")
-    check_elem(v, refs[4], rtol=1e-5, atol=1e-9, name="v")
+    check_elem(v, refs[4], rtol=5e-5, atol=1e-9, name="v")  # v + (1-b2)(g^2 - v) form: ~1e-5 rel
     if master is not None:
         check_elem(master, refs[1], rtol=1e-6, atol=1e-7, name="master")
     _close(param, refs[0], pdt, name="param")
