@@ -118,6 +118,9 @@ def parse(argv=None):
     ap.add_argument("--force_comm", action="store_true",
                     help="world 1: run the engines' N>1 collective path (RCCL copies) instead of the "
                          "world-1 shortcut (BLLM_FORCE_COMM=1) — a one-GPU rehearsal of the multi-GPU path")
+    ap.add_argument("--tunableop_tune", default=None,
+                    help="tune every hipBLASLt/rocBLAS GEMM shape this run meets with PyTorch TunableOp and write "
+                         "the results CSV here (a tuning run, not a measurement)")
     ap.add_argument("--tunableop", default=None,
                     help="PyTorch TunableOp results CSV (every hipBLASLt + rocBLAS solution timed per GEMM "
                          "shape), e.g. configs/tunableop_llama3_8b_b40_mi355x.csv: +0.6 %% on the headline "
@@ -238,6 +241,9 @@ def launch(argv=None):
 
 def main(argv=None):
     a = parse(argv)
+    if a.tunableop_tune:
+        os.environ.update(PYTORCH_TUNABLEOP_ENABLED="1", PYTORCH_TUNABLEOP_TUNING="1",
+                          PYTORCH_TUNABLEOP_FILENAME=os.path.abspath(a.tunableop_tune).replace(".csv", "%d.csv"))
     if a.tunableop:  # must be set before the first GEMM; TunableOp reads <name><device ordinal>.csv
         import tempfile
         d = tempfile.mkdtemp(prefix="bllm_tunableop_")
@@ -432,6 +438,8 @@ def main(argv=None):
         if prof is not None:
             out["profile_ms"] = prof
         print(json.dumps(out), flush=True)
+    if a.tunableop_tune and cuda:
+        torch.cuda.tunable.write_file()
     dist.destroy_process_group()
 
 

@@ -333,3 +333,33 @@ def test_generate_cached_eos_stop_matches_reference(check_every, rows, monkeypat
         got = G.generate_cached(m, idx, 40, 24, eos_id=eos)
         assert torch.equal(ref, got), (eos, ref.shape, got.shape)
     assert free.shape[1] == 43
+
+
+def test_multi_gpu_loaders_use_shuffling_distributed_sampler():
+    """Under multi_gpu both loaders take DistributedSampler(dataset) with its default shuffle,
+    as the reference (datautils/dataloader.py:50, dataloader_instruction_finetune.py:94): the
+    validation batches that calc_loss_loader evaluates come from a seeded random subset."""
+    import torch.distributed as dist
+    from torch.utils.data.distributed import DistributedSampler
+
+    from building_llm_from_scratch_amd.data.loaders import DataloaderIF, DataloaderPT
+    from building_llm_from_scratch_amd.data.tokenizer import ByteTokenizer
+    port = _free_port()
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+    try:
+        tok = ByteTokenizer({"<|endoftext|>": 256})
+        pt = DataloaderPT(tok, batch_size=2, max_length=8, stride=8, run_type="multi_gpu", cache_dir=None)
+        train, val = pt.create_dataloaders("hello world, " * 200)
+        recs = [{"instruction": f"say {i}", "input": "", "output": f"{i}"} for i in range(50)]
+        tr2, va2 = DataloaderIF(tok, batch_size=2, max_length=64, run_type="multi_gpu").create_dataloaders(recs)
+        for dl in (train, val, tr2, va2):
+            assert isinstance(dl.sampler, DistributedSampler) and dl.sampler.shuffle
+    finally:
+        dist.destroy_process_group()
+
+
+def _free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]

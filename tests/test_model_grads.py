@@ -207,6 +207,39 @@ def test_fused_chunked_head_ce(family, monkeypatch):
     g1 = {n: p.grad.clone() for n, p in m.named_parameters() if p.grad is not None}
     for n in g1:
         assert torch.allclose(g4[n], 4.0 * g1[n], rtol=1e-5, atol=1e-6), n
+    # announced loss scale (the Trainer's fp16 path): the logit gradient is taken at dloss = S in
+    # the forward and divided by S in backward; S = the arriving dloss gives the same gradients
+    m.rctx.loss_scale = 1024.0
+    (m(idx, tgt) * 1024.0).backward()
+    gs = {n: p.grad.clone() / 1024.0 for n, p in m.named_parameters() if p.grad is not None}
+    m.rctx.loss_scale = 1.0
+    for n in g1:
+        assert torch.allclose(gs[n], g1[n], rtol=1e-5, atol=1e-7), n
+
+
+def test_selective_rebuilds_activation_and_norms():
+    """``selective`` keeps neither the norm outputs nor the SwiGLU / GELU activation (the
+    backward rebuilds them); ``none`` keeps both.  Gradients are covered by test_llama_grads."""
+    from building_llm_from_scratch_amd.models.base import _BlockFn
+    seen = {}
+    orig = _BlockFn.forward
+
+    def spy(ctx, x, comp):
+        y = orig(ctx, x, comp)
+        seen[comp.rctx.block_mode(comp.index)] = set(ctx.saved)
+        return y
+    for family, cfg in (("llama", _small_llama()), ("gpt2", _small_gpt2())):
+        for mode in ("none", "selective"):
+            m = build_model(cfg, use_actv_ckpt=mode)
+            idx = torch.randint(0, cfg.vocab_size, (2, 16))
+            _BlockFn.forward = staticmethod(spy)
+            try:
+                m(idx, idx)
+            finally:
+                _BlockFn.forward = staticmethod(orig)
+            act = "act" if family == "llama" else "g"
+            keys = seen[mode]
+            assert ({"h1", "h2", act} <= keys) == (mode == "none"), (family, mode, keys)
 
 
 def _torch_ckpt_blocks(n, segments):
