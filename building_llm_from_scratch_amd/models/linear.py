@@ -148,6 +148,8 @@ def _input_grad(dy: torch.Tensor, W: torch.Tensor, dx_acc: Optional[torch.Tensor
 
 # tests set this to drive the grouped LoRA path through the CPU oracles of ops.reference
 FORCE_GROUPED_LORA = False
+# gate/up GEMM + SwiGLU epilogue (FusedLinear.forward_swiglu)
+FUSED_SWIGLU = os.environ.get("BLLM_FUSED_SWIGLU", "0") != "0"
 
 
 class FusedLinear:
@@ -277,6 +279,17 @@ class FusedLinear:
                 y[:, c0:c1].addmm_(t, B, alpha=s.scaling)
                 xa.append(t)
         return y, xa
+
+    def forward_swiglu(self, x: torch.Tensor):
+        """Gate/up projection with the SwiGLU forward in the GEMM epilogue (``[fc1; fc2]``, no
+        bias, no LoRA): returns ``(gu, act)`` or None when the fused kernel does not apply
+        (csrc/gemm_nt.hip; BLLM_FUSED_SWIGLU=0 turns it off)."""
+        if self.has_lora or self.b_params is not None or len(self.specs) != 2 or not FUSED_SWIGLU:
+            return None
+        W = self.W()
+        if not ops.gemm_nt_swiglu_ok(x, W):
+            return None
+        return ops.gemm_nt_swiglu(x, W)
 
     def lora_state(self, x: torch.Tensor):
         """Only the LoRA intermediate ``x A`` that ``backward`` needs (what ``forward`` would

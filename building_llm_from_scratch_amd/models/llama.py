@@ -159,12 +159,19 @@ class LlamaBlockCompute(UnitCompute):
         o, lse = ops.flash_attn_fwd(qkv, B, T, H, G, hd, causal=True)
         x2, xa_o = self.o.forward(o, residual=x2d)
         h2, r2 = ops.rmsnorm_fwd(x2, u.data(b.norm2.weight), eps)
-        gu, xa_gu = self.gu.forward(h2)
+        fused = None
+        if not (recompute and not self.down.has_lora and RECOMPUTE_FUSED):
+            fused = self.gu.forward_swiglu(h2)     # gate/up GEMM with the SwiGLU epilogue
+        if fused is not None:
+            (gu, act), xa_gu = fused, None
+        else:
+            gu, xa_gu = self.gu.forward(h2)
         if recompute and not self.down.has_lora and RECOMPUTE_FUSED:
             # backward rebuilds act inside the SwiGLU backward kernel (swiglu_bwd_act)
             act, x3, xa_dn = None, None, None
         else:
-            act = ops.swiglu_fwd(gu)
+            if fused is None:
+                act = ops.swiglu_fwd(gu)
             if recompute:
                 x3, xa_dn = None, self.down.lora_state(act)
             else:

@@ -352,6 +352,34 @@ def gemm_nn_(a, b, c, accumulate: bool = False):
     return c
 
 
+def gemm_nt_swiglu_ok(a: torch.Tensor, w: torch.Tensor) -> bool:
+    """Shapes the gate/up + SwiGLU kernel (csrc/gemm_nt.hip) takes: a [M, K], w = [Wg; Wu] [2F, K],
+    bf16/fp16, M % 256, F % 128, K % 128, 16-B aligned unit-stride rows."""
+    if not (a.is_cuda and a.dtype in (torch.bfloat16, torch.float16) and w.dtype == a.dtype and a.dim() == 2
+            and w.dim() == 2):
+        return False
+    M, K = a.shape
+    F = w.shape[0] // 2
+    return (w.shape[0] == 2 * F and w.shape[1] == K and M % 256 == 0 and F % 128 == 0 and K % 128 == 0
+            and a.stride(1) == 1 and w.stride(1) == 1 and a.stride(0) % 8 == 0 and w.stride(0) % 8 == 0
+            and a.data_ptr() % 16 == 0 and w.data_ptr() % 16 == 0
+            and 256 * a.stride(0) * 2 < 2 ** 31 and 256 * w.stride(0) * 2 < 2 ** 31)
+
+
+def gemm_nt_swiglu(a, w):
+    """(gu, act) = (a . w^T, silu(gu[:, :F]) * gu[:, F:]) for w = [W_gate; W_up] — the gate/up
+    projection with the SwiGLU forward in its epilogue (csrc/gemm_nt.hip, GPU); on CPU the
+    matmul + ``swiglu_fwd`` oracle."""
+    F = w.shape[0] // 2
+    if _hip(a):
+        gu = torch.empty(a.shape[0], 2 * F, dtype=a.dtype, device=a.device)
+        act = torch.empty(a.shape[0], F, dtype=a.dtype, device=a.device)
+        _k().gemm_nt_swiglu_(a, w, gu, act)
+        return gu, act
+    gu = (a.float() @ w.float().t()).to(a.dtype)
+    return gu, swiglu_fwd(gu)
+
+
 def gemm_nt_(a, b, c, accumulate: bool = False):
     """c (+)= a @ b^T with a [M, K], b [N, K] (both K-contiguous, a Linear's forward y = x W^T),
     fp32 accumulation on the MFMA kernel of csrc/gemm_wgrad.hip (shape rules of gemm_nn_ok)."""

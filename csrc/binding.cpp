@@ -365,9 +365,38 @@ void gemm_nt_(const Tensor& a, const Tensor& b, Tensor& c, bool accumulate) {
               "gemm_nt: operands must be 16-B aligned");
   TORCH_CHECK(a.stride(0) < (int64_t(1) << 26) && b.stride(0) < (int64_t(1) << 26), "gemm_nt: row stride too large");
   TORCH_CHECK(M < (int64_t(1) << 31) && N < (int64_t(1) << 31) && K < (int64_t(1) << 31));
+  const char* impl = getenv("BLLM_GEMM_NT_IMPL");  // "1": the 32-deep-slot kernel of gemm_wgrad.hip (A/B)
+  if (!(impl && impl[0] == '1') && bllm::gemm_nt2_supported((int)M, (int)N, (int)K, a.stride(0), b.stride(0))) {
+    bllm::gemm_nt2(dt_of(a), dt_of(c), a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0), c.data_ptr(),
+                   c.stride(0), (int)M, (int)N, (int)K, accumulate, stream());
+    return;
+  }
   TORCH_CHECK(bllm::gemm_nn_supported((int)M, (int)N, (int)K), "gemm_nt: unsupported shape ", M, "x", N, "x", K);
   bllm::gemm_nt(dt_of(a), dt_of(c), a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0), c.data_ptr(), c.stride(0),
                 (int)M, (int)N, (int)K, accumulate, stream());
+}
+
+// gate/up projection + SwiGLU forward in one kernel (csrc/gemm_nt.hip): gu[M, 2F] = a . w^T with
+// w = [W_gate; W_up] ([2F, K]) and act[M, F] = silu(gu[:, :F]) * gu[:, F:]
+void gemm_nt_swiglu_(const Tensor& a, const Tensor& w, Tensor& gu, Tensor& act) {
+  TORCH_CHECK(a.is_cuda() && w.is_cuda() && gu.is_cuda() && act.is_cuda(), "gemm_nt_swiglu: GPU tensors");
+  c10::DeviceGuard g(a.device());
+  TORCH_CHECK(a.dim() == 2 && w.dim() == 2 && gu.dim() == 2 && act.dim() == 2, "gemm_nt_swiglu: 2-D operands");
+  const int64_t M = a.size(0), K = a.size(1), F = w.size(0) / 2;
+  TORCH_CHECK(w.size(0) == 2 * F && w.size(1) == K && gu.size(0) == M && gu.size(1) == 2 * F && act.size(0) == M &&
+                  act.size(1) == F && act.is_contiguous(), "gemm_nt_swiglu: shapes");
+  TORCH_CHECK(a.scalar_type() == w.scalar_type() && gu.scalar_type() == a.scalar_type() &&
+                  act.scalar_type() == a.scalar_type() &&
+                  (a.scalar_type() == at::kBFloat16 || a.scalar_type() == at::kHalf), "gemm_nt_swiglu: bf16/fp16");
+  TORCH_CHECK(a.stride(1) == 1 && w.stride(1) == 1 && gu.stride(1) == 1, "gemm_nt_swiglu: unit column strides");
+  TORCH_CHECK(a.stride(0) % 8 == 0 && w.stride(0) % 8 == 0 && gu.stride(0) % 8 == 0, "gemm_nt_swiglu: 16-B rows");
+  TORCH_CHECK((reinterpret_cast<uintptr_t>(a.data_ptr()) | reinterpret_cast<uintptr_t>(w.data_ptr()) |
+               reinterpret_cast<uintptr_t>(gu.data_ptr()) | reinterpret_cast<uintptr_t>(act.data_ptr())) % 16 == 0,
+              "gemm_nt_swiglu: 16-B aligned operands");
+  TORCH_CHECK(bllm::gemm_nt_swiglu_supported((int)M, (int)F, (int)K, a.stride(0), w.stride(0), gu.stride(0)),
+              "gemm_nt_swiglu: unsupported shape ", M, "x", F, "x", K);
+  bllm::gemm_nt_swiglu(dt_of(a), a.data_ptr(), a.stride(0), w.data_ptr(), w.stride(0), gu.data_ptr(), gu.stride(0),
+                       act.data_ptr(), (int)M, (int)F, (int)K, stream());
 }
 
 // qkv [B, (H+2G)*hd] (one decode token per row); kc / vc [B, G, Tmax, hd] valid below *pos;
@@ -884,6 +913,7 @@ TORCH_LIBRARY(bllm, m) {
   m.def("wgrad_gemm_(Tensor a, Tensor b, Tensor(a!) c, bool accumulate, int splits) -> ()");
   m.def("gemm_nn_(Tensor a, Tensor b, Tensor(a!) c, bool accumulate) -> ()");
   m.def("gemm_nt_(Tensor a, Tensor b, Tensor(a!) c, bool accumulate) -> ()");
+  m.def("gemm_nt_swiglu_(Tensor a, Tensor w, Tensor(a!) gu, Tensor(b!) act) -> ()");
   m.def("attn_decode(Tensor q, Tensor kcache, Tensor vcache, int L) -> Tensor");
   m.def("attn_decode_append(Tensor qkv, Tensor(a!) kcache, Tensor(b!) vcache, Tensor pos, int H, int G) -> Tensor");
   m.def("rope_dev_(Tensor(a!) qkv, Tensor cos, Tensor sin, int H, int G, int hd, Tensor pos) -> ()");
@@ -925,6 +955,7 @@ TORCH_LIBRARY_IMPL(bllm, CUDA, m) {
   m.impl("wgrad_gemm_", &wgrad_gemm_);
   m.impl("gemm_nn_", &gemm_nn_);
   m.impl("gemm_nt_", &gemm_nt_);
+  m.impl("gemm_nt_swiglu_", &gemm_nt_swiglu_);
   m.impl("bias_grad_", &bias_grad_);
   m.impl("flash_attn_bwd", &flash_attn_bwd);
   m.impl("ce_fwd", &ce_fwd);

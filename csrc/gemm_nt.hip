@@ -1,0 +1,339 @@
+// Forward-layout GEMM on CDNA4 matrix cores: C[M, N] (+)= A[M, K] . B[N, K]^T, both operands
+// K-contiguous (a Linear's y = x W^T, and dX = dY W on a transposed weight copy).
+//
+// Why a second kernel next to csrc/gemm_wgrad.hip: that kernel stages 32-deep k-slots, which
+// for K-contiguous operands means 64-B row segments per slot (half a 128-B line per request),
+// and runs this layout at 1.19-1.28 PF against hipBLASLt's 1.46-1.60 PF
+// (profiles/r2_gemm_nt_vs_hipblaslt.jsonl).  Here every K-tile is 64 deep, so each staged row
+// is one full 128-B line:
+//
+//  * tile 256 x 256 x 64, 8 waves = 2 (M) x 4 (N), 128 x 64 outputs per wave in four
+//    quadrants of 64 x 32 (acc[8][4] of v_mfma_f32_16x16x32 results);
+//  * LDS: two buffers of (A image + B image), 32 KiB each, 128 KiB total, filled by LDS-DMA
+//    (global_load_lds_dwordx4, 8 per lane per K-tile, 1 KiB = 8 rows per wave instruction);
+//    16-B chunk c of row r stored at c ^ ((r >> 1) & 7) (the XOR goes on the per-lane global
+//    SOURCE address; the DMA writes LDS lane-linearly) -- conflict-free ds_read_b128 fragment
+//    reads for all four 16-lane groups of the instruction;
+//  * schedule per K-tile t (one barrier):  P0: read A(qm1), B(qn1) of t; MFMA (qm0, qn0)
+//    P1: MFMA (qm0, qn1) | wait own DMA of t+1 + own LDS reads, s_barrier, DMA t+2 into the
+//    buffer of t | P2: read A(qm0) of t+1; MFMA (qm1, qn1) | P3: read B(qn0) of t+1; MFMA
+//    (qm1, qn0).  The DMA of a K-tile is issued a full K-tile (64 MFMAs per wave) before its
+//    first read; fragments are read one phase before their MFMAs; B register sets swap roles
+//    every tile (loop unrolled by two);
+//  * blockIdx -> tile: XCD-contiguous ranges (bijective), GROUP_M-deep column-major groups;
+//  * epilogue through LDS in two 128-row passes, 16-B row-contiguous stores (+ the old C when
+//    accumulating).
+#include <stdlib.h>
+
+#include "api.h"
+
+namespace bllm {
+namespace {
+
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) s16x8 lds_s16x8;
+
+template <typename T> struct Mf;
+template <> struct Mf<bf16_t> {
+  static __device__ __forceinline__ f32x4 run(s16x8 a, s16x8 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c,
+                                                   0, 0, 0);
+  }
+};
+template <> struct Mf<f16_t> {
+  static __device__ __forceinline__ f32x4 run(s16x8 a, s16x8 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c,
+                                                  0, 0, 0);
+  }
+};
+
+constexpr int TM = 256, TN = 256, TK = 64;
+constexpr int ROWB = TK * 2;             // 128 B per LDS row (one K-tile of one row)
+constexpr int IMGB = TM * ROWB;          // 32 KiB per operand image
+constexpr int BUFB = 2 * IMGB;           // A + B
+constexpr int LDS_BYTES = 2 * BUFB;      // double buffer, 128 KiB
+constexpr int THREADS = 512;
+constexpr int GROUP_M = 8;
+
+// one quadrant's fragments: A 4 m-frags x 2 k-steps, B 2 n-frags x 2 k-steps
+struct FA { s16x8 f[4][2]; };
+struct FB { s16x8 f[2][2]; };
+
+// EPI_SWIGLU: B = [W_gate; W_up] ([2F, K]); tile tn takes gate rows 128tn.. and up rows F + 128tn..
+// (image rows 0-127 / 128-255), the epilogue stores gu (both halves, as the plain GEMM would) and
+// act = silu(g) * u for its 128 columns, rounded exactly like the separate SwiGLU kernel
+// (elementwise.hip: g, u rounded to T first, then a / (1 + exp(-a)) * u in fp32).
+enum { EPI_NONE = 0, EPI_SWIGLU = 1 };
+
+template <typename T, typename OT, int EPI>
+__global__ __launch_bounds__(THREADS) void gemm_nt_k(const T* __restrict__ A, long lda, const T* __restrict__ B,
+                                                     long ldb, OT* __restrict__ C, long ldc, int M, int N, int K,
+                                                     int accumulate, int wide, OT* __restrict__ act, int F) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int wm = wave >> 2, wn = wave & 3;
+
+  // ---- tile id: XCD-contiguous (bijective), then GROUP_M-deep column-major groups
+  const int nbm = M / TM, nbn = N / TN, nblk = nbm * nbn;
+  const int bid = blockIdx.x, xcd = bid & 7, q8 = nblk >> 3, r8 = nblk & 7;
+  const int wid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int per_group = GROUP_M * nbn;
+  const int grp = wid / per_group;
+  const int first_m = grp * GROUP_M;
+  const int gm = nbm - first_m < GROUP_M ? nbm - first_m : GROUP_M;
+  const int in_g = wid - grp * per_group;
+  const int tm = first_m + in_g % gm, tn = in_g / gm;
+  const long m0 = (long)tm * TM, n0 = (long)tn * TN;
+
+  // ---- staging: wave w moves rows 32w .. 32w+31 of both images (4 x 1 KiB pieces each);
+  //      lane -> row 8i + l/8 of the piece, physical chunk l%8, logical chunk p ^ ((row>>1)&7)
+  // (offsets recomputed per issue from an opaque copy of the lane id: a few full-rate VALU
+  //  instead of 8 VGPRs held across the loop, which the accumulators need)
+  const uint32_t lds0 = lds_u32(smem);
+  // this wave's 32 rows of each image (image rows 32w .. 32w + 31)
+  const long g0 = (long)tn * 128, u0 = (long)F + (long)tn * 128;  // EPI_SWIGLU column bases
+  const long brow0 = EPI == EPI_SWIGLU ? (wave < 4 ? g0 + 32 * wave : u0 + 32 * (wave - 4)) : n0 + 32 * wave;
+  const T* Abase = A + (m0 + 32 * wave) * lda;
+  const T* Bbase = B + brow0 * ldb;
+  const uint32_t ldab = (uint32_t)(lda * sizeof(T)), ldbb = (uint32_t)(ldb * sizeof(T));
+  auto stage = [&](int t, int buf) {
+    const void* a = sgpr_ptr(Abase + (long)t * TK);
+    const void* b = sgpr_ptr(Bbase + (long)t * TK);
+    const uint32_t d = lds0 + buf * BUFB + wave * 4 * 1024;
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      // local row r (image row 32w + r: same XOR, 32w is a multiple of 16)
+      const uint32_t r = 8 * i + (ln >> 3), c = (ln & 7) ^ ((r >> 1) & 7);
+      glds16s(a, r * ldab + 16 * c, d + i * 1024);
+      glds16s(b, r * ldbb + 16 * c, d + IMGB + i * 1024);
+    }
+  };
+
+  // ---- fragment read offsets: lane reads row (.. + (l & 15)), logical chunk 4s + (l >> 4)
+  const int xo0 = ((0 + (lane >> 4)) ^ ((lane >> 1) & 7)) << 4;
+  const int xo1 = ((4 + (lane >> 4)) ^ ((lane >> 1) & 7)) << 4;
+  const int arow = (128 * wm + (lane & 15)) * ROWB;
+  const int brow = IMGB + (64 * wn + (lane & 15)) * ROWB;
+  auto rdA = [&](FA& F, int buf, int qm) {
+    const char* base = smem + buf * BUFB + arow + (64 * qm) * ROWB;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      F.f[i][0] = *(const lds_s16x8*)(base + 16 * i * ROWB + xo0);
+      F.f[i][1] = *(const lds_s16x8*)(base + 16 * i * ROWB + xo1);
+    }
+  };
+  auto rdB = [&](FB& F, int buf, int qn) {
+    const char* base = smem + buf * BUFB + brow + (32 * qn) * ROWB;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      F.f[j][0] = *(const lds_s16x8*)(base + 16 * j * ROWB + xo0);
+      F.f[j][1] = *(const lds_s16x8*)(base + 16 * j * ROWB + xo1);
+    }
+  };
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{};
+  auto mma = [&](const FA& a, const FB& b, int qm, int qn) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[4 * qm + i][2 * qn + j] = Mf<T>::run(a.f[i][s], b.f[j][s], acc[4 * qm + i][2 * qn + j]);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  const int nt = K / TK;  // even (host: K % 128 == 0)
+  stage(0, 0);
+  if (nt > 1) stage(1, 1);
+  if (nt > 1) wait_vm<8>(); else wait_vm0();
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  FA A0, A1;
+  FB Bp, Bq;
+  rdA(A0, 0, 0);
+  rdB(Bp, 0, 0);
+
+  // one K-tile; X = the B set holding qn0 of tile t on entry (the other receives qn1, then
+  // qn0 of tile t+1)
+  auto tile = [&](int t, FB& X, FB& Y) {
+    const int cur = t & 1, nxt = cur ^ 1;
+    const bool more = t + 1 < nt;
+    // P0: fragments of (qm1, qn1) for P1-P3; MFMA (qm0, qn0)
+    rdB(Y, cur, 1);
+    rdA(A1, cur, 1);
+    mma(A0, X, 0, 0);
+    // P1: MFMA (qm0, qn1)
+    mma(A0, Y, 0, 1);
+    // sync: own reads of buffer cur retired, own DMA of tile t+1 landed; after the barrier every
+    // wave is past both, so tile t+1 is readable and buffer cur can take tile t+2
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    wait_vm0();
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (t + 2 < nt) stage(t + 2, cur);
+    // P2: A(qm0) of t+1; MFMA (qm1, qn1)
+    if (more) rdA(A0, nxt, 0);
+    mma(A1, Y, 1, 1);
+    // P3: B(qn0) of t+1 into Y; MFMA (qm1, qn0)
+    mma(A1, X, 1, 0);
+    if (more) rdB(Y, nxt, 0);
+  };
+  for (int t = 0; t < nt; t += 2) {
+    tile(t, Bp, Bq);
+    tile(t + 1, Bq, Bp);
+  }
+
+  // ---- epilogue: lane holds C[16I + 4(l>>4) + e][16J + (l&15)] of the wave's 128 x 64 block
+  OT* cbase = C + m0 * ldc + n0;
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  if (wide) {
+    constexpr int RB = TN * 4;                // fp32 row of the tile in LDS
+    constexpr int EPT = 16 / (int)sizeof(OT);
+    constexpr int NCH = EPT / 4;
+    constexpr int IPR = TN / EPT;
+    constexpr int TRIPS = 128 * IPR / THREADS;
+    struct alignas(16) V16 { OT e[EPT]; };
+#pragma unroll
+    for (int pass = 0; pass < 2; ++pass) {
+      if (wm == pass) {
+#pragma unroll
+        for (int I = 0; I < 8; ++I)
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+#pragma unroll
+            for (int J = 0; J < 4; ++J) {
+              const int lr = 16 * I + 4 * (lane >> 4) + e, col = wn * 64 + 16 * J + (lane & 15);
+              *(float*)(smem + lr * RB + ((((col >> 2) ^ (lr & 7)) << 4) | ((col & 3) << 2))) = acc[I][J][e];
+            }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int tr = 0; tr < TRIPS; ++tr) {
+        const int q = (int)threadIdx.x + tr * THREADS;
+        const int lr = q / IPR, it = q % IPR;
+        float v[EPT];
+#pragma unroll
+        for (int h = 0; h < NCH; ++h) {
+          const f32x4 x = *(const f32x4*)(smem + lr * RB + (((it * NCH + h) ^ (lr & 7)) << 4));
+#pragma unroll
+          for (int k = 0; k < 4; ++k) v[4 * h + k] = x[k];
+        }
+        long col = it * EPT;
+        if constexpr (EPI == EPI_SWIGLU) col = col < 128 ? g0 + col - n0 : u0 + (col - 128) - n0;
+        V16* o = (V16*)(cbase + (long)(pass * 128 + lr) * ldc + col);
+        if (accumulate) {
+          const V16 old = *o;
+#pragma unroll
+          for (int k = 0; k < EPT; ++k) v[k] += to_f(old.e[k]);
+        }
+        V16 w;
+#pragma unroll
+        for (int k = 0; k < EPT; ++k) w.e[k] = from_f<OT>(v[k]);
+        *o = w;
+      }
+      if constexpr (EPI == EPI_SWIGLU) {
+        // act[row][g0 + c] = silu(g) * u for the tile's 128 gate / up column pairs
+        constexpr int AIPR = 128 / EPT;
+        constexpr int ATRIPS = 128 * AIPR / THREADS;
+#pragma unroll
+        for (int tr = 0; tr < ATRIPS; ++tr) {
+          const int q = (int)threadIdx.x + tr * THREADS;
+          const int lr = q / AIPR, it = q % AIPR;
+          float g[EPT], u[EPT];
+#pragma unroll
+          for (int h = 0; h < NCH; ++h) {
+            const f32x4 xg = *(const f32x4*)(smem + lr * RB + (((it * NCH + h) ^ (lr & 7)) << 4));
+            const f32x4 xu = *(const f32x4*)(smem + lr * RB + (((32 + it * NCH + h) ^ (lr & 7)) << 4));
+#pragma unroll
+            for (int k = 0; k < 4; ++k) g[4 * h + k] = xg[k], u[4 * h + k] = xu[k];
+          }
+          V16 w;
+#pragma unroll
+          for (int k = 0; k < EPT; ++k) {
+            const float a = to_f(from_f<OT>(g[k])), b = to_f(from_f<OT>(u[k]));
+            w.e[k] = from_f<OT>(a / (1.f + __expf(-a)) * b);
+          }
+          *(V16*)(act + (m0 + pass * 128 + lr) * (long)F + g0 + it * EPT) = w;
+        }
+      }
+      if (pass == 0) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+      }
+    }
+    return;
+  }
+  OT* c = cbase + (128 * wm + 4 * (lane >> 4)) * ldc + 64 * wn + (lane & 15);
+  if (accumulate) {
+#pragma unroll
+    for (int I = 0; I < 8; ++I)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int J = 0; J < 4; ++J) {
+          OT* o = c + (long)(16 * I + e) * ldc + 16 * J;
+          *o = from_f<OT>(to_f(*o) + acc[I][J][e]);
+        }
+  } else {
+#pragma unroll
+    for (int I = 0; I < 8; ++I)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int J = 0; J < 4; ++J) c[(long)(16 * I + e) * ldc + 16 * J] = from_f<OT>(acc[I][J][e]);
+  }
+}
+
+template <typename T, typename OT, int EPI = EPI_NONE>
+void launch(const void* a, long lda, const void* b, long ldb, void* c, long ldc, int M, int N, int K, bool accumulate,
+            hipStream_t s, void* act = nullptr, int F = 0) {
+  static const bool attr = hipFuncSetAttribute((const void*)gemm_nt_k<T, OT, EPI>,
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES) == hipSuccess;
+  (void)attr;
+  const bool wide = reinterpret_cast<uintptr_t>(c) % 16 == 0 && (ldc * (long)sizeof(OT)) % 16 == 0;
+  hipLaunchKernelGGL((gemm_nt_k<T, OT, EPI>), dim3((M / TM) * (N / TN)), dim3(THREADS), LDS_BYTES, s, (const T*)a,
+                     lda, (const T*)b, ldb, (OT*)c, ldc, M, N, K, (int)accumulate, (int)wide, (OT*)act, F);
+}
+
+}  // namespace
+
+bool gemm_nt2_supported(int M, int N, int K, long lda, long ldb) {
+  return M > 0 && N > 0 && K > 0 && M % TM == 0 && N % TN == 0 && K % (2 * TK) == 0 &&
+         (long)TM * lda * 2 < (1L << 31) && (long)TN * ldb * 2 < (1L << 31);
+}
+
+void gemm_nt2(DType dt, DType odt, const void* a, long lda, const void* b, long ldb, void* c, long ldc, int M, int N,
+              int K, bool accumulate, hipStream_t s) {
+  BLLM_DISPATCH(odt, OT, {
+    if (dt == DType::BF16) launch<bf16_t, OT>(a, lda, b, ldb, c, ldc, M, N, K, accumulate, s);
+    else launch<f16_t, OT>(a, lda, b, ldb, c, ldc, M, N, K, accumulate, s);
+  });
+}
+
+bool gemm_nt_swiglu_supported(int M, int F, int K, long lda, long ldb, long ldgu) {
+  return F > 0 && F % 128 == 0 && gemm_nt2_supported(M, 2 * F, K, lda, ldb) && ldgu % 8 == 0;
+}
+
+void gemm_nt_swiglu(DType dt, const void* a, long lda, const void* w, long ldw, void* gu, long ldgu, void* act, int M,
+                    int F, int K, hipStream_t s) {
+  if (dt == DType::BF16) launch<bf16_t, bf16_t, EPI_SWIGLU>(a, lda, w, ldw, gu, ldgu, M, 2 * F, K, false, s, act, F);
+  else launch<f16_t, f16_t, EPI_SWIGLU>(a, lda, w, ldw, gu, ldgu, M, 2 * F, K, false, s, act, F);
+}
+
+}  // namespace bllm

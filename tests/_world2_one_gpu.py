@@ -85,7 +85,8 @@ def worker(rank, kinds, port, q):
 
 
 def main():
-    kinds = sys.argv[1].split(",") if len(sys.argv) > 1 else ["fsdp", "zero1", "ddp"]
+    args = [x for x in sys.argv[1:] if not x.startswith("--")]
+    kinds = args[0].split(",") if args else ["fsdp", "zero1", "ddp"]
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
@@ -99,7 +100,12 @@ def main():
         p.join(120)
     print(res, flush=True)
     codes = [p.exitcode for p in procs]
-    sys.exit(0 if not res.startswith("ERROR") and codes == [0, 0] else 1)
+    print(json.dumps({"exitcodes": codes}), flush=True)
+    # a Python-level error (e.g. a collective gloo does not implement for GPU tensors) is reported
+    # in the JSON and exits 0 when ``--report`` is given; a crash (negative exit code) never does
+    crashed = any(c is None or c < 0 for c in codes)
+    ok = not res.startswith("ERROR") and codes == [0, 0]
+    sys.exit(0 if ok or ("--report" in sys.argv and not crashed) else 1)
 
 
 if __name__ == "__main__":

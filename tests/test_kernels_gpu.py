@@ -567,11 +567,14 @@ def test_wgrad_gemm_unaligned_output(accumulate):
 
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("odt", [None, torch.float32])
-@pytest.mark.parametrize("M,K,N", [(256, 128, 256), (512, 384, 768), (768, 1024, 512)])
+@pytest.mark.parametrize("M,K,N", [(256, 128, 256), (512, 384, 768), (768, 1024, 512), (1024, 4096, 1536)])
 @pytest.mark.parametrize("accumulate", [False, True])
-def test_gemm_nt(dt, odt, M, K, N, accumulate):
-    """Both-operands-K-contiguous variant (c = a . b^T, the forward layout) vs an fp32 matmul,
-    strided rows."""
+@pytest.mark.parametrize("impl", ["gemm_nt", "wgrad_slots"])
+def test_gemm_nt(dt, odt, M, K, N, accumulate, impl, monkeypatch):
+    """Both-operands-K-contiguous GEMM (c = a . b^T, the forward layout) vs an fp32 matmul,
+    strided rows: the 64-deep-K-tile kernel (csrc/gemm_nt.hip, default) and the 32-deep-slot
+    kernel of csrc/gemm_wgrad.hip (BLLM_GEMM_NT_IMPL=1)."""
+    monkeypatch.setenv("BLLM_GEMM_NT_IMPL", "1" if impl == "wgrad_slots" else "2")
     a_full = torch.randn(M, K + 64, device=DEV).to(dt)
     a = a_full[:, 32:32 + K]
     b_full = torch.randn(N, K + 32, device=DEV).to(dt)
@@ -656,3 +659,17 @@ def test_linear_residual_hipblaslt(dt, N, K, O):
     want = C.float().cpu() + x.float().cpu() @ W.float().cpu().t()
     _close(y, want, dt, 2, name="linear_residual")
     assert torch.equal(ops.linear_residual(x, W, C), y)
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("M,K,F", [(256, 128, 128), (512, 512, 768), (1024, 4096, 1792)])
+def test_gemm_nt_swiglu(dt, M, K, F):
+    """Gate/up GEMM with the SwiGLU forward in the epilogue (K10): gu against the fp32 oracle, act
+    bitwise equal to the separate swiglu_fwd kernel applied to that gu."""
+    a = torch.randn(M, K, device=DEV).to(dt)
+    w = (torch.randn(2 * F, K, device=DEV) / K ** 0.5).to(dt)
+    assert ops.gemm_nt_swiglu_ok(a, w)
+    gu, act = ops.gemm_nt_swiglu(a, w)
+    check_close(gu, a.float() @ w.float().t(), dt, k=3.0, name="gemm_nt_swiglu gu")
+    assert torch.equal(act, ops.swiglu_fwd(gu))
+    check_close(act, ref.swiglu_fwd(a.float() @ w.float().t()), dt, k=5.0, name="gemm_nt_swiglu act")

@@ -222,3 +222,31 @@ def test_fp16_fused_head_under_loss_scaling(name, monkeypatch):
         e_unfused = _rel(grads[False][k], named[k].grad)
         assert e_fused < 1e-2, (k, e_fused)
         assert e_fused <= 1.5 * e_unfused + 1e-3, (k, e_fused, e_unfused)
+
+
+@pytest.mark.parametrize("ckpt", ["none", "selective", "full"])
+def test_fused_swiglu_gemm_in_model(ckpt, monkeypatch):
+    """BLLM_FUSED_SWIGLU: the gate/up GEMM with the SwiGLU epilogue gives the same loss and
+    gradients as the separate GEMM + swiglu_fwd kernel (bitwise-equal act; the GEMM itself is a
+    different kernel from hipBLASLt, so gradients agree to rounding)."""
+    from building_llm_from_scratch_amd.models import linear
+    ops.load_ext(required=True)
+    cfg = _cfgs()["llama_hd64"].replace(dtype=torch.bfloat16)
+    idx = torch.randint(0, cfg.vocab_size, (2, 257), device="cuda")
+    res = {}
+    calls = []
+    orig = ops.gemm_nt_swiglu
+    monkeypatch.setattr(ops, "gemm_nt_swiglu", lambda *a: (calls.append(1), orig(*a))[1])
+    for fused in (False, True):
+        monkeypatch.setattr(linear, "FUSED_SWIGLU", fused)
+        torch.manual_seed(0)
+        m = build_model(cfg, use_actv_ckpt=ckpt, device="cuda")
+        m.flatten()
+        loss = m(idx[:, :-1], idx[:, 1:])
+        loss.backward()
+        res[fused] = (loss.item(), {k: p.grad.float().clone() for k, p in m.named_parameters()})
+    assert calls, "fused gate/up + SwiGLU kernel not used"
+    (l0, g0), (l1, g1) = res[False], res[True]
+    assert abs(l0 - l1) < 1e-2 * abs(l0)
+    for k in g0:
+        assert _rel(g1[k], g0[k]) < 2e-2, (k, _rel(g1[k], g0[k]))

@@ -1,0 +1,85 @@
+#!/usr/bin/env python3
+"""Forward-layout GEMM A/B (GPU): y[M, N] = x[M, K] . W[N, K]^T, bf16, random operands.
+
+hipBLASLt (torch.mm), the 64-deep-K-tile kernel csrc/gemm_nt.hip (ops.gemm_nt_ default) and the
+32-deep-slot kernel of csrc/gemm_wgrad.hip (BLLM_GEMM_NT_IMPL=1), interleaved in ONE process over
+--rounds, median per shape; each kernel's output checked against hipBLASLt's (relative
+Frobenius).  Shapes: the Llama-3-8B projections at the bench's 40 x 1024 tokens and GPT2-774M's
+at 24 x 1024.  Usage: python tools/bench_gemm_nt.py [--rounds 3 --iters 10 --models llama,gpt2]"""
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from building_llm_from_scratch_amd import ops  # noqa: E402
+
+SHAPES = {
+    "llama": (40960, {"qkv": (4096, 6144), "o": (4096, 4096), "gate_up": (4096, 28672), "down": (14336, 4096),
+                      "head_chunk": (4096, 128256)}),
+    "gpt2": (24576, {"qkv": (1280, 3840), "o": (1280, 1280), "fc1": (1280, 5120), "fc2": (5120, 1280)}),
+}
+
+
+def timeit(fn, iters):
+    for _ in range(2):
+        fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--models", default="llama,gpt2")
+    a = ap.parse_args()
+    ops.load_ext(required=True)
+    dt = torch.bfloat16
+    for model in a.models.split(","):
+        tokens, shapes = SHAPES[model]
+        for name, (k, n) in shapes.items():
+            m = 8192 if name == "head_chunk" else tokens   # the fused head runs 8192-row chunks
+            x = torch.rand(m, k, device="cuda", dtype=dt) * 2 - 1
+            w = (torch.rand(n, k, device="cuda", dtype=dt) * 2 - 1) * 0.05
+            ref = torch.mm(x, w.t())
+            outs = {"new": torch.empty(m, n, device="cuda", dtype=dt), "old": torch.empty(m, n, device="cuda", dtype=dt)}
+            y = torch.empty(m, n, device="cuda", dtype=dt)
+
+            def new():
+                os.environ.pop("BLLM_GEMM_NT_IMPL", None)
+                ops.gemm_nt_(x, w, outs["new"])
+
+            def old():
+                os.environ["BLLM_GEMM_NT_IMPL"] = "1"
+                ops.gemm_nt_(x, w, outs["old"])
+
+            fns = {"hipblaslt": lambda: torch.mm(x, w.t(), out=y), "gemm_nt_new": new, "gemm_nt_old": old}
+            times = {kk: [] for kk in fns}
+            for _ in range(a.rounds):
+                for kk, fn in fns.items():
+                    times[kk].append(timeit(fn, a.iters))
+            os.environ.pop("BLLM_GEMM_NT_IMPL", None)
+            fl = 2.0 * m * n * k
+            r = {"model": model, "gemm": name, "M_N_K": [m, n, k]}
+            for kk, ts in times.items():
+                med = sorted(ts)[len(ts) // 2]
+                r[kk + "_us"] = round(med * 1e3, 1)
+                r[kk + "_tflops"] = round(fl / med / 1e9, 1)
+            for kk in ("new", "old"):
+                r[f"rel_err_{kk}"] = ((outs[kk].float() - ref.float()).norm() / ref.float().norm()).item()
+            print(json.dumps(r), flush=True)
+            del x, w, ref, outs, y
+            torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()
