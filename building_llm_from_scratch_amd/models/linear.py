@@ -120,6 +120,21 @@ def _dgrad_wt_ok(dy: torch.Tensor, W: torch.Tensor) -> bool:
             and dy.shape[0] >= DGRAD_WT_MIN_TOKENS)
 
 
+# BLLM_GEMM_NT=1: the forward-layout GEMMs (y = x W^T, dX on the transposed weight copy, the fused
+# head's logits and dh) run on csrc/gemm_nt.hip instead of hipBLASLt (A/B switch)
+GEMM_NT = os.environ.get("BLLM_GEMM_NT", "0") != "0"
+
+
+def mm_nt(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """a @ b^T for b stored [N, K] (both operands K-contiguous)."""
+    if GEMM_NT and ops.gemm_nt_ok(a, b, out):
+        if out is None:
+            out = torch.empty(a.shape[0], b.shape[0], dtype=a.dtype, device=a.device)
+        ops.gemm_nt_(a, b, out, False)
+        return out
+    return torch.mm(a, b.t(), out=out) if out is not None else torch.mm(a, b.t())
+
+
 def _input_grad(dy: torch.Tensor, W: torch.Tensor, dx_acc: Optional[torch.Tensor] = None,
                 out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """dx = dy @ W (+ dx_acc) [+ written into / added to ``out``].  GPU shapes the MFMA kernel
@@ -128,7 +143,10 @@ def _input_grad(dy: torch.Tensor, W: torch.Tensor, dx_acc: Optional[torch.Tensor
     if not nn_kernel and _dgrad_wt_ok(dy, W):
         # W^T scratch copy (HBM-bound, ~0.2 ms per Llama-3-8B layer) buys the K-contiguous
         # hipBLASLt layout for the GEMM (~1 ms per layer at 24k tokens)
-        W = ops.transpose2d(W).t()
+        Wt = ops.transpose2d(W)
+        if out is None and dx_acc is None and GEMM_NT and ops.gemm_nt_ok(dy, Wt):
+            return mm_nt(dy, Wt)
+        W = Wt.t()
     if out is not None:  # out += dy @ W
         if nn_kernel:
             ops.gemm_nn_(dy, W, out, True)
@@ -265,7 +283,7 @@ class FusedLinear:
         elif b is not None:
             y = torch.addmm(b, x, W.t())
         else:
-            y = torch.mm(x, W.t())
+            y = mm_nt(x, W)
         xa = None
         if self.has_lora:
             xa = []

@@ -24,7 +24,7 @@ import torch.nn as nn
 
 from .. import ops
 from .base import BaseLM, UnitCompute, cached_attention
-from .linear import FusedLinear, _dgrad_wt_ok, _weight_grad
+from .linear import FusedLinear, _dgrad_wt_ok, _weight_grad, mm_nt
 
 
 # ---------------------------------------------------------------------------
@@ -324,11 +324,14 @@ class HeadComputeMixin:
         total = torch.zeros(1, dtype=torch.float32, device=h.device)
         for s0 in range(0, N, rows):
             hc, tc = h[s0:s0 + rows], targets[s0:s0 + rows]
-            logits = torch.mm(hc, W.t())
+            logits = mm_nt(hc, W)
             lrow, lse = ops.ce_fwd(logits, tc, self.ignore_index)
             total += lrow.sum()
             dl = ops.ce_bwd_(logits, tc, lse, scale, self.ignore_index)   # in place
-            torch.mm(dl, Wd, out=dh[s0:s0 + rows])
+            if Wd is not W:
+                mm_nt(dl, Wd.t(), out=dh[s0:s0 + rows])                   # dh = dl . W (W^T copy)
+            else:
+                torch.mm(dl, Wd, out=dh[s0:s0 + rows])
             if gW is not None:
                 _weight_grad(dl, hc, gW, accumulate=s0 > 0)
             del logits, dl

@@ -352,6 +352,20 @@ def gemm_nn_(a, b, c, accumulate: bool = False):
     return c
 
 
+def gemm_nt_ok(a: torch.Tensor, b: torch.Tensor, c: Optional[torch.Tensor] = None) -> bool:
+    """Shapes the 64-deep-K-tile kernel (csrc/gemm_nt.hip) takes for c [M, N] = a [M, K] b [N, K]^T:
+    bf16/fp16, M, N multiples of 256, K of 128, 16-B aligned unit-stride rows."""
+    if not (a.is_cuda and a.dtype in (torch.bfloat16, torch.float16) and b.dtype == a.dtype and a.dim() == 2
+            and b.dim() == 2):
+        return False
+    M, K = a.shape
+    N = b.shape[0]
+    return (b.shape[1] == K and M % 256 == 0 and N % 256 == 0 and K % 128 == 0 and a.stride(1) == 1
+            and b.stride(1) == 1 and a.stride(0) % 8 == 0 and b.stride(0) % 8 == 0 and a.data_ptr() % 16 == 0
+            and b.data_ptr() % 16 == 0 and 256 * a.stride(0) * 2 < 2 ** 31 and 256 * b.stride(0) * 2 < 2 ** 31
+            and (c is None or (c.stride(1) == 1 and c.stride(0) % 8 == 0 and c.data_ptr() % 16 == 0)))
+
+
 def gemm_nt_swiglu_ok(a: torch.Tensor, w: torch.Tensor) -> bool:
     """Shapes the gate/up + SwiGLU kernel (csrc/gemm_nt.hip) takes: a [M, K], w = [Wg; Wu] [2F, K],
     bf16/fp16, M % 256, F % 128, K % 128, 16-B aligned unit-stride rows."""
