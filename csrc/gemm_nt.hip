@@ -68,6 +68,116 @@ struct FB { s16x8 f[2][2]; };
 // (elementwise.hip: g, u rounded to T first, then a / (1 + exp(-a)) * u in fp32).
 enum { EPI_NONE = 0, EPI_SWIGLU = 1 };
 
+// ---- epilogue: lane holds C[16I + 4(l>>4) + e][16J + (l&15)] of its wave's 128 x 64 block
+template <typename T, typename OT, int EPI>
+__device__ __forceinline__ void epilogue(f32x4 (&acc)[8][4], char* smem, int wm, int wn, int lane, OT* C, long ldc,
+                                         long m0, long n0, long g0, long u0, int accumulate, int wide, OT* act,
+                                         int F) {
+  OT* cbase = C + m0 * ldc + n0;
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  if (wide) {
+    constexpr int RB = TN * 4;                // fp32 row of the tile in LDS
+    constexpr int EPT = 16 / (int)sizeof(OT);
+    constexpr int NCH = EPT / 4;
+    constexpr int IPR = TN / EPT;
+    constexpr int TRIPS = 128 * IPR / THREADS;
+    struct alignas(16) V16 { OT e[EPT]; };
+#pragma unroll
+    for (int pass = 0; pass < 2; ++pass) {
+      if (wm == pass) {
+#pragma unroll
+        for (int I = 0; I < 8; ++I)
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+#pragma unroll
+            for (int J = 0; J < 4; ++J) {
+              const int lr = 16 * I + 4 * (lane >> 4) + e, col = wn * 64 + 16 * J + (lane & 15);
+              *(float*)(smem + lr * RB + ((((col >> 2) ^ (lr & 7)) << 4) | ((col & 3) << 2))) = acc[I][J][e];
+            }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int tr = 0; tr < TRIPS; ++tr) {
+        const int q = (int)threadIdx.x + tr * THREADS;
+        const int lr = q / IPR, it = q % IPR;
+        float v[EPT];
+#pragma unroll
+        for (int h = 0; h < NCH; ++h) {
+          const f32x4 x = *(const f32x4*)(smem + lr * RB + (((it * NCH + h) ^ (lr & 7)) << 4));
+#pragma unroll
+          for (int k = 0; k < 4; ++k) v[4 * h + k] = x[k];
+        }
+        long col = it * EPT;
+        if constexpr (EPI == EPI_SWIGLU) col = col < 128 ? g0 + col - n0 : u0 + (col - 128) - n0;
+        V16* o = (V16*)(cbase + (long)(pass * 128 + lr) * ldc + col);
+        if (accumulate) {
+          const V16 old = *o;
+#pragma unroll
+          for (int k = 0; k < EPT; ++k) v[k] += to_f(old.e[k]);
+        }
+        V16 w;
+#pragma unroll
+        for (int k = 0; k < EPT; ++k) w.e[k] = from_f<OT>(v[k]);
+        *o = w;
+      }
+      if constexpr (EPI == EPI_SWIGLU) {
+        // act[row][g0 + c] = silu(g) * u for the tile's 128 gate / up column pairs
+        constexpr int AIPR = 128 / EPT;
+        constexpr int ATRIPS = 128 * AIPR / THREADS;
+#pragma unroll
+        for (int tr = 0; tr < ATRIPS; ++tr) {
+          const int q = (int)threadIdx.x + tr * THREADS;
+          const int lr = q / AIPR, it = q % AIPR;
+          float g[EPT], u[EPT];
+#pragma unroll
+          for (int h = 0; h < NCH; ++h) {
+            const f32x4 xg = *(const f32x4*)(smem + lr * RB + (((it * NCH + h) ^ (lr & 7)) << 4));
+            const f32x4 xu = *(const f32x4*)(smem + lr * RB + (((32 + it * NCH + h) ^ (lr & 7)) << 4));
+#pragma unroll
+            for (int k = 0; k < 4; ++k) g[4 * h + k] = xg[k], u[4 * h + k] = xu[k];
+          }
+          V16 w;
+#pragma unroll
+          for (int k = 0; k < EPT; ++k) {
+            const float a = to_f(from_f<OT>(g[k])), b = to_f(from_f<OT>(u[k]));
+            w.e[k] = from_f<OT>(a / (1.f + __expf(-a)) * b);
+          }
+          *(V16*)(act + (m0 + pass * 128 + lr) * (long)F + g0 + it * EPT) = w;
+        }
+      }
+      if (pass == 0) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+      }
+    }
+    return;
+  }
+  OT* c = cbase + (128 * wm + 4 * (lane >> 4)) * ldc + 64 * wn + (lane & 15);
+  if (accumulate) {
+#pragma unroll
+    for (int I = 0; I < 8; ++I)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int J = 0; J < 4; ++J) {
+          OT* o = c + (long)(16 * I + e) * ldc + 16 * J;
+          *o = from_f<OT>(to_f(*o) + acc[I][J][e]);
+        }
+  } else {
+#pragma unroll
+    for (int I = 0; I < 8; ++I)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int J = 0; J < 4; ++J) c[(long)(16 * I + e) * ldc + 16 * J] = from_f<OT>(acc[I][J][e]);
+  }
+}
+
 template <typename T, typename OT, int EPI>
 __global__ __launch_bounds__(THREADS) void gemm_nt_k(const T* __restrict__ A, long lda, const T* __restrict__ B,
                                                      long ldb, OT* __restrict__ C, long ldc, int M, int N, int K,
@@ -194,121 +304,202 @@ __global__ __launch_bounds__(THREADS) void gemm_nt_k(const T* __restrict__ A, lo
     tile(t + 1, Bq, Bp);
   }
 
-  // ---- epilogue: lane holds C[16I + 4(l>>4) + e][16J + (l&15)] of the wave's 128 x 64 block
-  OT* cbase = C + m0 * ldc + n0;
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  epilogue<T, OT, EPI>(acc, smem, wm, wn, lane, C, ldc, m0, n0, g0, u0, accumulate, wide, act, F);
+}
+
+// ---- ping-pong schedule (BLLM_GEMM_NT_SCHED=1): same tile, waves, LDS images and epilogue;
+// the two wave rows (wm = 0: waves 0-3, wm = 1: waves 4-7, one of each per SIMD) run one
+// barrier apart, so on every SIMD one wave is in its 16-MFMA block while the other issues its
+// fragment reads and LDS-DMA and waits.  Per K-tile, four phases, one C quadrant each:
+//   phase 1 (qm0, qn0): read A(qm0) + B(qn0)   phase 2 (qm0, qn1): read B(qn1)
+//   phase 3 (qm1, qn1): read A(qm1)            phase 4 (qm1, qn0): no reads (B(qn0) kept)
+// and each phase = [reads] [2 LDS-DMA of one staged quarter] vmcnt(8) barrier lgkmcnt(0)
+// [16 MFMA] barrier.  Staging is by quarter (16 KiB: the A rows of one qm, or the B rows of one
+// qn, over the whole tile), in the order the phases consume them, each into the buffer of its
+// K-tile's parity: quarter sequence 4t + {0: A qm0, 1: B qn0, 2: B qn1, 3: A qm1}; quarter s is
+// issued in the phase 4 phases before the one whose reads retire it, i.e. with 4 quarters
+// (8 DMA per wave) in flight behind it: every phase waits vmcnt(8) (fewer in the tail).
+// RAW: a quarter is read only in a phase after the barrier that follows every wave's wait for
+// it (the stagger moves the other row's wait one barrier EARLIER, never later).  WAR: a slot is
+// refilled >= 2 phases after its last read, whose lgkmcnt(0) precedes an intervening barrier.
+template <typename T, typename OT, int EPI>
+__global__ __launch_bounds__(THREADS) void gemm_nt_pp_k(const T* __restrict__ A, long lda, const T* __restrict__ B,
+                                                        long ldb, OT* __restrict__ C, long ldc, int M, int N, int K,
+                                                        int accumulate, int wide, OT* __restrict__ act, int F) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int wm = wave >> 2, wn = wave & 3;
+
+  const int nbm = M / TM, nbn = N / TN, nblk = nbm * nbn;
+  const int bid = blockIdx.x, xcd = bid & 7, q8 = nblk >> 3, r8 = nblk & 7;
+  const int wid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int per_group = GROUP_M * nbn;
+  const int grp = wid / per_group;
+  const int first_m = grp * GROUP_M;
+  const int gm = nbm - first_m < GROUP_M ? nbm - first_m : GROUP_M;
+  const int in_g = wid - grp * per_group;
+  const int tm = first_m + in_g % gm, tn = in_g / gm;
+  const long m0 = (long)tm * TM, n0 = (long)tn * TN;
+  const long g0 = (long)tn * 128, u0 = (long)F + (long)tn * 128;
+
+  const uint32_t lds0 = lds_u32(smem);
+  const uint32_t ldab = (uint32_t)(lda * sizeof(T)), ldbb = (uint32_t)(ldb * sizeof(T));
+  const int nt = K / TK;
+  // quarter k of K-tile t: this wave moves 8-row groups 2w, 2w+1 of the quarter's 128 rows
+  auto stageq = [&](int t, int k) {
+    const int buf = t & 1;
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int g = 2 * wave + j;
+      const void* src;
+      uint32_t ld, dst;
+      int r0;
+      if (k == 0 || k == 3) {  // A rows 128 (g>>3) + 64 qm + 8 (g&7) ..
+        r0 = 128 * (g >> 3) + 64 * (k == 3) + 8 * (g & 7);
+        src = sgpr_ptr(A + (m0 + r0) * lda + (long)t * TK);
+        ld = ldab;
+        dst = lds0 + buf * BUFB + r0 * ROWB;
+      } else {                 // B rows 64 (g>>2) + 32 qn + 8 (g&3) ..
+        r0 = 64 * (g >> 2) + 32 * (k == 2) + 8 * (g & 3);
+        const long br = EPI == EPI_SWIGLU ? (r0 < 128 ? g0 + r0 : u0 + (r0 - 128)) : n0 + r0;
+        src = sgpr_ptr(B + br * ldb + (long)t * TK);
+        ld = ldbb;
+        dst = lds0 + buf * BUFB + IMGB + r0 * ROWB;
+      }
+      // image row r0 + l/8, physical chunk l%8 holds logical chunk p ^ ((row >> 1) & 7)
+      const uint32_t r = (uint32_t)(ln >> 3), c = (ln & 7) ^ (((r0 + r) >> 1) & 7);
+      glds16s(src, r * ld + 16 * c, dst);
+    }
+  };
+
+  const int xo0 = ((0 + (lane >> 4)) ^ ((lane >> 1) & 7)) << 4;
+  const int xo1 = ((4 + (lane >> 4)) ^ ((lane >> 1) & 7)) << 4;
+  const int arow = (128 * wm + (lane & 15)) * ROWB;
+  const int brow = IMGB + (64 * wn + (lane & 15)) * ROWB;
+  auto rdA = [&](FA& Fr, int buf, int qm) {
+    const char* base = smem + buf * BUFB + arow + (64 * qm) * ROWB;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      Fr.f[i][0] = *(const lds_s16x8*)(base + 16 * i * ROWB + xo0);
+      Fr.f[i][1] = *(const lds_s16x8*)(base + 16 * i * ROWB + xo1);
+    }
+  };
+  auto rdB = [&](FB& Fr, int buf, int qn) {
+    const char* base = smem + buf * BUFB + brow + (32 * qn) * ROWB;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      Fr.f[j][0] = *(const lds_s16x8*)(base + 16 * j * ROWB + xo0);
+      Fr.f[j][1] = *(const lds_s16x8*)(base + 16 * j * ROWB + xo1);
+    }
+  };
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{};
+
+  // the quarter with sequence s (4t + k) is issued iff t < nt; when phase p of tile t waits, the
+  // newest issued quarter is min(iss, 4 nt - 1) and the one it must retire is req
+  auto wait_for = [&](int iss, int req) {
+    const int last = 4 * nt - 1;
+    const int n = 2 * ((iss < last ? iss : last) - req);
+    if (n >= 8) wait_vm<8>();
+    else if (n == 6) wait_vm<6>();
+    else if (n == 4) wait_vm<4>();
+    else if (n == 2) wait_vm<2>();
+    else wait_vm0();
+  };
+  auto sync_mma = [&](const FA& a, const FB& b, int qm, int qn) {
+    __builtin_amdgcn_s_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[4 * qm + i][2 * qn + j] = Mf<T>::run(a.f[i][s], b.f[j][s], acc[4 * qm + i][2 * qn + j]);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+
+  // prologue: quarters 0..5 (tile 0 and A qm0 / B qn0 of tile 1), retire quarters 0, 1
+  stageq(0, 0);
+  stageq(0, 1);
+  stageq(0, 2);
+  stageq(0, 3);
+  if (nt > 1) {
+    stageq(1, 0);
+    stageq(1, 1);
+  }
+  wait_for(5, 1);
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
-  if (wide) {
-    constexpr int RB = TN * 4;                // fp32 row of the tile in LDS
-    constexpr int EPT = 16 / (int)sizeof(OT);
-    constexpr int NCH = EPT / 4;
-    constexpr int IPR = TN / EPT;
-    constexpr int TRIPS = 128 * IPR / THREADS;
-    struct alignas(16) V16 { OT e[EPT]; };
-#pragma unroll
-    for (int pass = 0; pass < 2; ++pass) {
-      if (wm == pass) {
-#pragma unroll
-        for (int I = 0; I < 8; ++I)
-#pragma unroll
-          for (int e = 0; e < 4; ++e)
-#pragma unroll
-            for (int J = 0; J < 4; ++J) {
-              const int lr = 16 * I + 4 * (lane >> 4) + e, col = wn * 64 + 16 * J + (lane & 15);
-              *(float*)(smem + lr * RB + ((((col >> 2) ^ (lr & 7)) << 4) | ((col & 3) << 2))) = acc[I][J][e];
-            }
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-#pragma unroll
-      for (int tr = 0; tr < TRIPS; ++tr) {
-        const int q = (int)threadIdx.x + tr * THREADS;
-        const int lr = q / IPR, it = q % IPR;
-        float v[EPT];
-#pragma unroll
-        for (int h = 0; h < NCH; ++h) {
-          const f32x4 x = *(const f32x4*)(smem + lr * RB + (((it * NCH + h) ^ (lr & 7)) << 4));
-#pragma unroll
-          for (int k = 0; k < 4; ++k) v[4 * h + k] = x[k];
-        }
-        long col = it * EPT;
-        if constexpr (EPI == EPI_SWIGLU) col = col < 128 ? g0 + col - n0 : u0 + (col - 128) - n0;
-        V16* o = (V16*)(cbase + (long)(pass * 128 + lr) * ldc + col);
-        if (accumulate) {
-          const V16 old = *o;
-#pragma unroll
-          for (int k = 0; k < EPT; ++k) v[k] += to_f(old.e[k]);
-        }
-        V16 w;
-#pragma unroll
-        for (int k = 0; k < EPT; ++k) w.e[k] = from_f<OT>(v[k]);
-        *o = w;
-      }
-      if constexpr (EPI == EPI_SWIGLU) {
-        // act[row][g0 + c] = silu(g) * u for the tile's 128 gate / up column pairs
-        constexpr int AIPR = 128 / EPT;
-        constexpr int ATRIPS = 128 * AIPR / THREADS;
-#pragma unroll
-        for (int tr = 0; tr < ATRIPS; ++tr) {
-          const int q = (int)threadIdx.x + tr * THREADS;
-          const int lr = q / AIPR, it = q % AIPR;
-          float g[EPT], u[EPT];
-#pragma unroll
-          for (int h = 0; h < NCH; ++h) {
-            const f32x4 xg = *(const f32x4*)(smem + lr * RB + (((it * NCH + h) ^ (lr & 7)) << 4));
-            const f32x4 xu = *(const f32x4*)(smem + lr * RB + (((32 + it * NCH + h) ^ (lr & 7)) << 4));
-#pragma unroll
-            for (int k = 0; k < 4; ++k) g[4 * h + k] = xg[k], u[4 * h + k] = xu[k];
-          }
-          V16 w;
-#pragma unroll
-          for (int k = 0; k < EPT; ++k) {
-            const float a = to_f(from_f<OT>(g[k])), b = to_f(from_f<OT>(u[k]));
-            w.e[k] = from_f<OT>(a / (1.f + __expf(-a)) * b);
-          }
-          *(V16*)(act + (m0 + pass * 128 + lr) * (long)F + g0 + it * EPT) = w;
-        }
-      }
-      if (pass == 0) {
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-      }
-    }
-    return;
+  if (wm == 1) {  // the stagger: row 1 runs one barrier behind row 0
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
   }
-  OT* c = cbase + (128 * wm + 4 * (lane >> 4)) * ldc + 64 * wn + (lane & 15);
-  if (accumulate) {
-#pragma unroll
-    for (int I = 0; I < 8; ++I)
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-#pragma unroll
-        for (int J = 0; J < 4; ++J) {
-          OT* o = c + (long)(16 * I + e) * ldc + 16 * J;
-          *o = from_f<OT>(to_f(*o) + acc[I][J][e]);
-        }
-  } else {
-#pragma unroll
-    for (int I = 0; I < 8; ++I)
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-#pragma unroll
-        for (int J = 0; J < 4; ++J) c[(long)(16 * I + e) * ldc + 16 * J] = from_f<OT>(acc[I][J][e]);
+  FA a;
+  FB b0, b1;
+  for (int t = 0; t < nt; ++t) {
+    const int cur = t & 1;
+    // phase 1: (qm0, qn0); stage B qn1 of t+1; retire B qn1 of t (read in phase 2)
+    rdA(a, cur, 0);
+    rdB(b0, cur, 0);
+    if (t + 1 < nt) stageq(t + 1, 2);
+    wait_for(4 * (t + 1) + 2, 4 * t + 2);
+    sync_mma(a, b0, 0, 0);
+    // phase 2: (qm0, qn1); stage A qm1 of t+1
+    rdB(b1, cur, 1);
+    if (t + 1 < nt) stageq(t + 1, 3);
+    wait_for(4 * (t + 1) + 3, 4 * t + 3);
+    sync_mma(a, b1, 0, 1);
+    // phase 3: (qm1, qn1); stage A qm0 of t+2
+    rdA(a, cur, 1);
+    if (t + 2 < nt) stageq(t + 2, 0);
+    wait_for(4 * (t + 2), 4 * (t + 1));
+    sync_mma(a, b1, 1, 1);
+    // phase 4: (qm1, qn0), no reads; stage B qn0 of t+2
+    if (t + 2 < nt) stageq(t + 2, 1);
+    wait_for(4 * (t + 2) + 1, 4 * (t + 1) + 1);
+    sync_mma(a, b0, 1, 0);
   }
+  if (wm == 0) {  // balance the stagger
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  }
+  epilogue<T, OT, EPI>(acc, smem, wm, wn, lane, C, ldc, m0, n0, g0, u0, accumulate, wide, act, F);
+}
+
+// BLLM_GEMM_NT_SCHED (read per launch, so one process can A/B): 0 = one barrier per K-tile
+// (gemm_nt_k), 1 = ping-pong wave rows (gemm_nt_pp_k)
+inline int nt_sched() {
+  const char* e = getenv("BLLM_GEMM_NT_SCHED");
+  return e ? atoi(e) : 0;
 }
 
 template <typename T, typename OT, int EPI = EPI_NONE>
 void launch(const void* a, long lda, const void* b, long ldb, void* c, long ldc, int M, int N, int K, bool accumulate,
             hipStream_t s, void* act = nullptr, int F = 0) {
   static const bool attr = hipFuncSetAttribute((const void*)gemm_nt_k<T, OT, EPI>,
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES) == hipSuccess &&
+                           hipFuncSetAttribute((const void*)gemm_nt_pp_k<T, OT, EPI>,
                                                hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES) == hipSuccess;
   (void)attr;
   const bool wide = reinterpret_cast<uintptr_t>(c) % 16 == 0 && (ldc * (long)sizeof(OT)) % 16 == 0;
-  hipLaunchKernelGGL((gemm_nt_k<T, OT, EPI>), dim3((M / TM) * (N / TN)), dim3(THREADS), LDS_BYTES, s, (const T*)a,
-                     lda, (const T*)b, ldb, (OT*)c, ldc, M, N, K, (int)accumulate, (int)wide, (OT*)act, F);
+  if (nt_sched() == 1)
+    hipLaunchKernelGGL((gemm_nt_pp_k<T, OT, EPI>), dim3((M / TM) * (N / TN)), dim3(THREADS), LDS_BYTES, s,
+                       (const T*)a, lda, (const T*)b, ldb, (OT*)c, ldc, M, N, K, (int)accumulate, (int)wide, (OT*)act, F);
+  else
+    hipLaunchKernelGGL((gemm_nt_k<T, OT, EPI>), dim3((M / TM) * (N / TN)), dim3(THREADS), LDS_BYTES, s, (const T*)a,
+                       lda, (const T*)b, ldb, (OT*)c, ldc, M, N, K, (int)accumulate, (int)wide, (OT*)act, F);
 }
 
 }  // namespace

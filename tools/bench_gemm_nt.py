@@ -1,8 +1,9 @@
 #!/usr/bin/env python3
 """Forward-layout GEMM A/B (GPU): y[M, N] = x[M, K] . W[N, K]^T, bf16, random operands.
 
-hipBLASLt (torch.mm), the 64-deep-K-tile kernel csrc/gemm_nt.hip (ops.gemm_nt_ default) and the
-32-deep-slot kernel of csrc/gemm_wgrad.hip (BLLM_GEMM_NT_IMPL=1), interleaved in ONE process over
+hipBLASLt (torch.mm), the 64-deep-K-tile kernel csrc/gemm_nt.hip (ops.gemm_nt_ default), its
+ping-pong schedule (BLLM_GEMM_NT_SCHED=1) and the 32-deep-slot kernel of csrc/gemm_wgrad.hip
+(BLLM_GEMM_NT_IMPL=1), interleaved in ONE process over
 --rounds, median per shape; each kernel's output checked against hipBLASLt's (relative
 Frobenius).  Shapes: the Llama-3-8B projections at the bench's 40 x 1024 tokens and GPT2-774M's
 at 24 x 1024.  Usage: python tools/bench_gemm_nt.py [--rounds 3 --iters 10 --models llama,gpt2]"""
@@ -51,18 +52,25 @@ def main():
             x = torch.rand(m, k, device="cuda", dtype=dt) * 2 - 1
             w = (torch.rand(n, k, device="cuda", dtype=dt) * 2 - 1) * 0.05
             ref = torch.mm(x, w.t())
-            outs = {"new": torch.empty(m, n, device="cuda", dtype=dt), "old": torch.empty(m, n, device="cuda", dtype=dt)}
+            outs = {k_: torch.empty(m, n, device="cuda", dtype=dt) for k_ in ("new", "pp", "old")}
             y = torch.empty(m, n, device="cuda", dtype=dt)
 
             def new():
                 os.environ.pop("BLLM_GEMM_NT_IMPL", None)
+                os.environ["BLLM_GEMM_NT_SCHED"] = "0"
                 ops.gemm_nt_(x, w, outs["new"])
+
+            def pp():
+                os.environ.pop("BLLM_GEMM_NT_IMPL", None)
+                os.environ["BLLM_GEMM_NT_SCHED"] = "1"
+                ops.gemm_nt_(x, w, outs["pp"])
 
             def old():
                 os.environ["BLLM_GEMM_NT_IMPL"] = "1"
                 ops.gemm_nt_(x, w, outs["old"])
 
-            fns = {"hipblaslt": lambda: torch.mm(x, w.t(), out=y), "gemm_nt_new": new, "gemm_nt_old": old}
+            fns = {"hipblaslt": lambda: torch.mm(x, w.t(), out=y), "gemm_nt_new": new, "gemm_nt_pp": pp,
+                   "gemm_nt_old": old}
             times = {kk: [] for kk in fns}
             for _ in range(a.rounds):
                 for kk, fn in fns.items():
@@ -74,7 +82,7 @@ def main():
                 med = sorted(ts)[len(ts) // 2]
                 r[kk + "_us"] = round(med * 1e3, 1)
                 r[kk + "_tflops"] = round(fl / med / 1e9, 1)
-            for kk in ("new", "old"):
+            for kk in ("new", "pp", "old"):
                 r[f"rel_err_{kk}"] = ((outs[kk].float() - ref.float()).norm() / ref.float().norm()).item()
             print(json.dumps(r), flush=True)
             del x, w, ref, outs, y
