@@ -120,17 +120,60 @@ def _dgrad_wt_ok(dy: torch.Tensor, W: torch.Tensor) -> bool:
             and dy.shape[0] >= DGRAD_WT_MIN_TOKENS)
 
 
-# BLLM_GEMM_NT=1: the forward-layout GEMMs (y = x W^T, dX on the transposed weight copy, the fused
-# head's logits and dh) run on csrc/gemm_nt.hip instead of hipBLASLt (A/B switch)
-GEMM_NT = os.environ.get("BLLM_GEMM_NT", "0") != "0"
+# The forward-layout GEMMs (y = x W^T, dX on the transposed weight copy, the fused head's logits
+# and dh).  BLLM_GEMM_NT: 0 = hipBLASLt; 1 = csrc/gemm_nt.hip wherever its shape rules hold
+# (schedule from BLLM_GEMM_NT_SCHED); auto = per shape, whichever of hipBLASLt and the two
+# gemm_nt schedules timed fastest on this device (measured once per shape and process, like
+# TunableOp; never inside a graph capture)
+GEMM_NT_MODE = os.environ.get("BLLM_GEMM_NT", "0")
+GEMM_NT = GEMM_NT_MODE not in ("0", "")
+_NT_PICK: dict = {}
+
+
+def _time_nt(a, b, out) -> int:
+    """-1 (hipBLASLt) or the gemm_nt schedule that ran this shape fastest (median of 3 x 3)."""
+    c = torch.empty(a.shape[0], b.shape[0], dtype=out.dtype if out is not None else a.dtype, device=a.device)
+    arms = {-1: lambda: torch.mm(a, b.t(), out=c) if c.dtype == a.dtype else c.copy_(torch.mm(a, b.t())),
+            0: lambda: ops.gemm_nt_(a, b, c, False, 0), 1: lambda: ops.gemm_nt_(a, b, c, False, 1)}
+    times = {k: [] for k in arms}
+    for fn in arms.values():
+        fn()
+    for _ in range(3):
+        for k, fn in arms.items():
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            for _ in range(3):
+                fn()
+            e.record()
+            e.synchronize()
+            times[k].append(s.elapsed_time(e))
+    med = {k: sorted(v)[1] for k, v in times.items()}
+    return min(med, key=med.get)
+
+
+def nt_choice(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None) -> int:
+    """-1 = hipBLASLt, else the gemm_nt schedule mm_nt uses for this call."""
+    if not GEMM_NT or not ops.gemm_nt_ok(a, b, out):
+        return -1
+    if GEMM_NT_MODE != "auto":
+        return int(os.environ.get("BLLM_GEMM_NT_SCHED", "0") or 0)
+    key = (tuple(a.shape), a.stride(0), tuple(b.shape), b.stride(0), a.dtype,
+           None if out is None else (out.dtype, out.stride(0)), a.device)
+    pick = _NT_PICK.get(key)
+    if pick is None:
+        if torch.cuda.is_current_stream_capturing():
+            return -1
+        pick = _NT_PICK[key] = _time_nt(a, b, out)
+    return pick
 
 
 def mm_nt(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """a @ b^T for b stored [N, K] (both operands K-contiguous)."""
-    if GEMM_NT and ops.gemm_nt_ok(a, b, out):
+    sched = nt_choice(a, b, out)
+    if sched >= 0:
         if out is None:
             out = torch.empty(a.shape[0], b.shape[0], dtype=a.dtype, device=a.device)
-        ops.gemm_nt_(a, b, out, False)
+        ops.gemm_nt_(a, b, out, False, sched)
         return out
     return torch.mm(a, b.t(), out=out) if out is not None else torch.mm(a, b.t())
 

@@ -350,7 +350,7 @@ void gemm_nn_(const Tensor& a, const Tensor& b, Tensor& c, bool accumulate) {
 }
 
 // c[M, N] (+)= a[M, K] . b[N, K]^T on the MFMA kernel (both operands K-contiguous)
-void gemm_nt_(const Tensor& a, const Tensor& b, Tensor& c, bool accumulate) {
+void gemm_nt_(const Tensor& a, const Tensor& b, Tensor& c, bool accumulate, int64_t sched) {
   TORCH_CHECK(a.is_cuda() && b.is_cuda() && c.is_cuda(), "gemm_nt: GPU tensors");
   c10::DeviceGuard g(a.device());
   TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && c.dim() == 2, "gemm_nt: 2-D operands");
@@ -368,7 +368,7 @@ void gemm_nt_(const Tensor& a, const Tensor& b, Tensor& c, bool accumulate) {
   const char* impl = getenv("BLLM_GEMM_NT_IMPL");  // "1": the 32-deep-slot kernel of gemm_wgrad.hip (A/B)
   if (!(impl && impl[0] == '1') && bllm::gemm_nt2_supported((int)M, (int)N, (int)K, a.stride(0), b.stride(0))) {
     bllm::gemm_nt2(dt_of(a), dt_of(c), a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0), c.data_ptr(),
-                   c.stride(0), (int)M, (int)N, (int)K, accumulate, stream());
+                   c.stride(0), (int)M, (int)N, (int)K, accumulate, stream(), (int)sched);
     return;
   }
   TORCH_CHECK(bllm::gemm_nn_supported((int)M, (int)N, (int)K), "gemm_nt: unsupported shape ", M, "x", N, "x", K);
@@ -912,7 +912,7 @@ TORCH_LIBRARY(bllm, m) {
   m.def("sum_partials_(Tensor part, Tensor(a!) out, bool accumulate) -> ()");
   m.def("wgrad_gemm_(Tensor a, Tensor b, Tensor(a!) c, bool accumulate, int splits) -> ()");
   m.def("gemm_nn_(Tensor a, Tensor b, Tensor(a!) c, bool accumulate) -> ()");
-  m.def("gemm_nt_(Tensor a, Tensor b, Tensor(a!) c, bool accumulate) -> ()");
+  m.def("gemm_nt_(Tensor a, Tensor b, Tensor(a!) c, bool accumulate, int sched=-1) -> ()");
   m.def("gemm_nt_swiglu_(Tensor a, Tensor w, Tensor(a!) gu, Tensor(b!) act) -> ()");
   m.def("attn_decode(Tensor q, Tensor kcache, Tensor vcache, int L) -> Tensor");
   m.def("attn_decode_append(Tensor qkv, Tensor(a!) kcache, Tensor(b!) vcache, Tensor pos, int H, int G) -> Tensor");

@@ -487,14 +487,14 @@ inline int nt_sched() {
 
 template <typename T, typename OT, int EPI = EPI_NONE>
 void launch(const void* a, long lda, const void* b, long ldb, void* c, long ldc, int M, int N, int K, bool accumulate,
-            hipStream_t s, void* act = nullptr, int F = 0) {
+            hipStream_t s, void* act = nullptr, int F = 0, int sched = -1) {
   static const bool attr = hipFuncSetAttribute((const void*)gemm_nt_k<T, OT, EPI>,
                                                hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES) == hipSuccess &&
                            hipFuncSetAttribute((const void*)gemm_nt_pp_k<T, OT, EPI>,
                                                hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES) == hipSuccess;
   (void)attr;
   const bool wide = reinterpret_cast<uintptr_t>(c) % 16 == 0 && (ldc * (long)sizeof(OT)) % 16 == 0;
-  if (nt_sched() == 1)
+  if ((sched < 0 ? nt_sched() : sched) == 1)
     hipLaunchKernelGGL((gemm_nt_pp_k<T, OT, EPI>), dim3((M / TM) * (N / TN)), dim3(THREADS), LDS_BYTES, s,
                        (const T*)a, lda, (const T*)b, ldb, (OT*)c, ldc, M, N, K, (int)accumulate, (int)wide, (OT*)act, F);
   else
@@ -510,10 +510,10 @@ bool gemm_nt2_supported(int M, int N, int K, long lda, long ldb) {
 }
 
 void gemm_nt2(DType dt, DType odt, const void* a, long lda, const void* b, long ldb, void* c, long ldc, int M, int N,
-              int K, bool accumulate, hipStream_t s) {
+              int K, bool accumulate, hipStream_t s, int sched) {
   BLLM_DISPATCH(odt, OT, {
-    if (dt == DType::BF16) launch<bf16_t, OT>(a, lda, b, ldb, c, ldc, M, N, K, accumulate, s);
-    else launch<f16_t, OT>(a, lda, b, ldb, c, ldc, M, N, K, accumulate, s);
+    if (dt == DType::BF16) launch<bf16_t, OT>(a, lda, b, ldb, c, ldc, M, N, K, accumulate, s, nullptr, 0, sched);
+    else launch<f16_t, OT>(a, lda, b, ldb, c, ldc, M, N, K, accumulate, s, nullptr, 0, sched);
   });
 }
 
