@@ -397,7 +397,7 @@ def gemm_nt_swiglu(a, w):
 def gemm_nt_(a, b, c, accumulate: bool = False, sched: int = -1):
     """c (+)= a @ b^T with a [M, K], b [N, K] (both K-contiguous, a Linear's forward y = x W^T),
     fp32 accumulation on csrc/gemm_nt.hip (``sched`` 0: one barrier per K-tile, 1: ping-pong wave
-    rows, -1: BLLM_GEMM_NT_SCHED) or, for shapes it does not take, csrc/gemm_wgrad.hip."""
+    rows, 2: 4 waves of 128 x 128, -1: BLLM_GEMM_NT_SCHED) or, for shapes it does not take, csrc/gemm_wgrad.hip."""
     if _hip(a):
         _k().gemm_nt_(a, b, c, bool(accumulate), int(sched))
         return c

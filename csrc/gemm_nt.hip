@@ -25,6 +25,8 @@
 //    accumulating).
 #include <stdlib.h>
 
+#include <type_traits>
+
 #include "api.h"
 
 namespace bllm {
@@ -49,6 +51,24 @@ template <> struct Mf<f16_t> {
                                                   0, 0, 0);
   }
 };
+
+// MFMA with the accumulator tied in place in an AGPR ("+a"): hipcc otherwise renames the
+// 256 accumulators of the 4-wave kernel between unrolled steps and pays for it in
+// v_accvgpr_read/write copies.  Operand hazards: fragments come from ds_read (waited for by the
+// compiler's lgkmcnt, no VALU producer); a chain on one accumulator needs no padding; the first
+// compiler reader after the last MFMA is behind mfma_drain().
+template <typename T> struct MfA;
+template <> struct MfA<bf16_t> {
+  static __device__ __forceinline__ void run(f32x4& c, const s16x8& a, const s16x8& b) {
+    asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(a), "v"(b));
+  }
+};
+template <> struct MfA<f16_t> {
+  static __device__ __forceinline__ void run(f32x4& c, const s16x8& a, const s16x8& b) {
+    asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, %0" : "+a"(c) : "v"(a), "v"(b));
+  }
+};
+__device__ __forceinline__ void mfma_drain() { asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory"); }
 
 constexpr int TM = 256, TN = 256, TK = 64;
 constexpr int ROWB = TK * 2;             // 128 B per LDS row (one K-tile of one row)
@@ -478,8 +498,274 @@ __global__ __launch_bounds__(THREADS) void gemm_nt_pp_k(const T* __restrict__ A,
   epilogue<T, OT, EPI>(acc, smem, wm, wn, lane, C, ldc, m0, n0, g0, u0, accumulate, wide, act, F);
 }
 
+// ---- 4-wave schedule (BLLM_GEMM_NT_SCHED=2): the same 256 x 256 x 64 tile, LDS images and
+// swizzle on 4 waves (one per SIMD) of 128 x 128 outputs each (acc[8][8]: 256 accumulator
+// registers, which the compiler places in AGPRs), the layout gfx950's hipBLASLt
+// MT256x256x64_MI16x16x1 / MIWT8_8 / WG32_8_1 kernels use (read off their code object).  Per
+// wave and K-tile: 128 MFMAs, 32 fragment reads, 16 LDS-DMA pieces.  Every fragment of a K-tile
+// is held in registers (a0/b0: k-step 0, a1/b1: k-step 1, 128 VGPRs), so a buffer is free for
+// the tile two ahead as soon as its last fragment read has retired:
+//   section 1 (64 MFMAs on a0 x b0): reads of a1/b1 (buffer cur) one per MFMA over the first 16;
+//     after MFMA 31 lgkmcnt(0) + barrier (WAR: every wave's reads of cur retired), then the 16
+//     DMA pieces of tile t+2 into cur, one per 5 MFMAs;
+//   section 2 (64 MFMAs on a1 x b1): the rest of the DMA; after MFMA 47 vmcnt(16) + barrier
+//     (RAW: every wave's pieces of tile t+1 landed), then the reads of a0/b0 of tile t+1 (buffer
+//     nxt) one per MFMA over the last 16.
+// Program order is pinned with sched_barrier(0) after each MFMA step; the compiler inserts the
+// counted lgkmcnt waits for the fragment reads, the DMA (inline asm) is counted by hand.
+constexpr int THREADS4 = 256;
+
+template <typename T, typename OT, int EPI>
+__device__ __forceinline__ void epilogue4(f32x4 (&acc)[8][8], char* smem, int wm, int wn, int lane, OT* C, long ldc,
+                                          long m0, long n0, long g0, long u0, int accumulate, int wide, OT* act,
+                                          int F) {
+  OT* cbase = C + m0 * ldc + n0;
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  if (wide) {
+    constexpr int RB = TN * 4;
+    constexpr int EPT = 16 / (int)sizeof(OT);
+    constexpr int NCH = EPT / 4;
+    constexpr int IPR = TN / EPT;
+    constexpr int TRIPS = 128 * IPR / THREADS4;
+    struct alignas(16) V16 { OT e[EPT]; };
+#pragma unroll
+    for (int pass = 0; pass < 2; ++pass) {
+      if (wm == pass) {
+#pragma unroll
+        for (int I = 0; I < 8; ++I)
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+#pragma unroll
+            for (int J = 0; J < 8; ++J) {
+              const int lr = 16 * I + 4 * (lane >> 4) + e, col = wn * 128 + 16 * J + (lane & 15);
+              *(float*)(smem + lr * RB + ((((col >> 2) ^ (lr & 7)) << 4) | ((col & 3) << 2))) = acc[I][J][e];
+            }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+#pragma unroll 4
+      for (int tr = 0; tr < TRIPS; ++tr) {
+        const int q = (int)threadIdx.x + tr * THREADS4;
+        const int lr = q / IPR, it = q % IPR;
+        float v[EPT];
+#pragma unroll
+        for (int h = 0; h < NCH; ++h) {
+          const f32x4 x = *(const f32x4*)(smem + lr * RB + (((it * NCH + h) ^ (lr & 7)) << 4));
+#pragma unroll
+          for (int k = 0; k < 4; ++k) v[4 * h + k] = x[k];
+        }
+        long col = it * EPT;
+        if constexpr (EPI == EPI_SWIGLU) col = col < 128 ? g0 + col - n0 : u0 + (col - 128) - n0;
+        V16* o = (V16*)(cbase + (long)(pass * 128 + lr) * ldc + col);
+        if (accumulate) {
+          const V16 old = *o;
+#pragma unroll
+          for (int k = 0; k < EPT; ++k) v[k] += to_f(old.e[k]);
+        }
+        V16 w;
+#pragma unroll
+        for (int k = 0; k < EPT; ++k) w.e[k] = from_f<OT>(v[k]);
+        *o = w;
+      }
+      if constexpr (EPI == EPI_SWIGLU) {
+        constexpr int AIPR = 128 / EPT;
+        constexpr int ATRIPS = 128 * AIPR / THREADS4;
+#pragma unroll 4
+        for (int tr = 0; tr < ATRIPS; ++tr) {
+          const int q = (int)threadIdx.x + tr * THREADS4;
+          const int lr = q / AIPR, it = q % AIPR;
+          float g[EPT], u[EPT];
+#pragma unroll
+          for (int h = 0; h < NCH; ++h) {
+            const f32x4 xg = *(const f32x4*)(smem + lr * RB + (((it * NCH + h) ^ (lr & 7)) << 4));
+            const f32x4 xu = *(const f32x4*)(smem + lr * RB + (((32 + it * NCH + h) ^ (lr & 7)) << 4));
+#pragma unroll
+            for (int k = 0; k < 4; ++k) g[4 * h + k] = xg[k], u[4 * h + k] = xu[k];
+          }
+          V16 w;
+#pragma unroll
+          for (int k = 0; k < EPT; ++k) {
+            const float a = to_f(from_f<OT>(g[k])), b = to_f(from_f<OT>(u[k]));
+            w.e[k] = from_f<OT>(a / (1.f + __expf(-a)) * b);
+          }
+          *(V16*)(act + (m0 + pass * 128 + lr) * (long)F + g0 + it * EPT) = w;
+        }
+      }
+      if (pass == 0) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+      }
+    }
+    return;
+  }
+  OT* c = cbase + (128 * wm + 4 * (lane >> 4)) * ldc + 128 * wn + (lane & 15);
+  if (accumulate) {
+#pragma unroll
+    for (int I = 0; I < 8; ++I)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int J = 0; J < 8; ++J) {
+          OT* o = c + (long)(16 * I + e) * ldc + 16 * J;
+          *o = from_f<OT>(to_f(*o) + acc[I][J][e]);
+        }
+  } else {
+#pragma unroll
+    for (int I = 0; I < 8; ++I)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int J = 0; J < 8; ++J) c[(long)(16 * I + e) * ldc + 16 * J] = from_f<OT>(acc[I][J][e]);
+  }
+}
+
+template <typename T, typename OT, int EPI>
+__global__ __launch_bounds__(THREADS4, 1) void gemm_nt4_k(const T* __restrict__ A, long lda,
+                                                          const T* __restrict__ B, long ldb, OT* __restrict__ C,
+                                                          long ldc, int M, int N, int K, int accumulate, int wide,
+                                                          OT* __restrict__ act, int F) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int wm = wave >> 1, wn = wave & 1;
+
+  const int nbm = M / TM, nbn = N / TN, nblk = nbm * nbn;
+  const int bid = blockIdx.x, xcd = bid & 7, q8 = nblk >> 3, r8 = nblk & 7;
+  const int wid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int per_group = GROUP_M * nbn;
+  const int grp = wid / per_group;
+  const int first_m = grp * GROUP_M;
+  const int gm = nbm - first_m < GROUP_M ? nbm - first_m : GROUP_M;
+  const int in_g = wid - grp * per_group;
+  const int tm = first_m + in_g % gm, tn = in_g / gm;
+  const long m0 = (long)tm * TM, n0 = (long)tn * TN;
+  const long g0 = (long)tn * 128, u0 = (long)F + (long)tn * 128;
+
+  // ---- staging: wave w moves image rows 64w .. 64w+63 of A and of B, 8 pieces of 8 rows each;
+  //      lane l -> row 8p + (l >> 3) of the piece set, physical chunk l & 7 holding logical chunk
+  //      (l & 7) ^ ((row >> 1) & 7), which only depends on the piece's parity
+  const uint32_t lds0 = lds_u32(smem);
+  const long brow0 = EPI == EPI_SWIGLU ? (wave < 2 ? g0 + 64 * wave : u0 + 64 * (wave - 2)) : n0 + 64 * wave;
+  const T* Abase = A + (m0 + 64 * wave) * lda;
+  const T* Bbase = B + brow0 * ldb;
+  const uint32_t ldab = (uint32_t)(lda * sizeof(T)), ldbb = (uint32_t)(ldb * sizeof(T));
+  // per-piece lane offsets (row 8p + (l >> 3) of the wave's 64, swizzled chunk) in VGPRs; the
+  // tile's base pointer is wave-uniform (SGPRs), so a piece costs one m0 write and the DMA
+  uint32_t voA[8], voB[8];
+#pragma unroll
+  for (int p = 0; p < 8; ++p) {
+    const uint32_t r = 8u * p + (uint32_t)(lane >> 3), c = 16u * ((lane & 7) ^ ((r >> 1) & 7));
+    voA[p] = r * ldab + c;
+    voB[p] = r * ldbb + c;
+  }
+  // piece k of tile t (k < 8: A piece k, k >= 8: B piece k - 8) into buffer buf
+  auto dma = [&](int t, int buf, int k) {
+    const int p = k & 7;
+    const uint32_t d = lds0 + (k >= 8 ? 2 * IMGB : 0) + buf * IMGB + (64 * wave + 8 * p) * ROWB;
+    if (k < 8) glds16s(sgpr_ptr(Abase + (long)t * TK), voA[p], d);
+    else glds16s(sgpr_ptr(Bbase + (long)t * TK), voB[p], d);
+  };
+
+  // ---- fragment reads: row (.. + (l & 15)), logical chunk 4s + (l >> 4)
+  const int xo0 = ((0 + (lane >> 4)) ^ ((lane >> 1) & 7)) << 4;
+  const int xo1 = ((4 + (lane >> 4)) ^ ((lane >> 1) & 7)) << 4;
+  // (both buffers of an operand within one 64 KiB window: 4 base VGPRs, the rest immediates)
+  const char* pA0 = smem + (128 * wm + (lane & 15)) * ROWB + xo0;
+  const char* pA1 = smem + (128 * wm + (lane & 15)) * ROWB + xo1;
+  const char* pB0 = smem + 2 * IMGB + (128 * wn + (lane & 15)) * ROWB + xo0;
+  const char* pB1 = smem + 2 * IMGB + (128 * wn + (lane & 15)) * ROWB + xo1;
+  auto rdA = [&](int buf, int i, int s) -> s16x8 {
+    return *(const lds_s16x8*)((s ? pA1 : pA0) + buf * IMGB + 16 * i * ROWB);
+  };
+  auto rdB = [&](int buf, int j, int s) -> s16x8 {
+    return *(const lds_s16x8*)((s ? pB1 : pB0) + buf * IMGB + 16 * j * ROWB);
+  };
+
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{};
+  s16x8 a0[8], b0[8], a1[8], b1[8];
+
+  const int nt = K / TK;  // even, >= 2 (host: K % 128 == 0)
+#pragma unroll
+  for (int k = 0; k < 16; ++k) dma(0, 0, k);
+#pragma unroll
+  for (int k = 0; k < 16; ++k) dma(1, 1, k);
+  wait_vm<16>();
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+#pragma unroll
+  for (int i = 0; i < 8; ++i) a0[i] = rdA(0, i, 0), b0[i] = rdB(0, i, 0);
+
+  // MODE 0: DMA tile t+2 and read tile t+1; 1: read tile t+1 only (t = nt-2); 2: last tile
+  auto tile = [&](int t, auto mode_c, auto cur_c) {
+    constexpr int MODE = decltype(mode_c)::value;
+    constexpr int cur = decltype(cur_c)::value, nxt = cur ^ 1;
+    // section 1: a0 x b0; reads of k-step 1 (a1[0], b1[0..7], a1[1..7]) over the first 16 MFMAs
+#pragma unroll
+    for (int n = 0; n < 64; ++n) {
+      const int i = n >> 3, j = n & 7;
+      MfA<T>::run(acc[i][j], a0[i], b0[j]);
+      if (n == 0) a1[0] = rdA(cur, 0, 1);
+      else if (n <= 8) b1[n - 1] = rdB(cur, n - 1, 1);
+      else if (n < 16) a1[n - 8] = rdA(cur, n - 8, 1);
+      if constexpr (MODE == 0) {
+        if (n == 31) {
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          __builtin_amdgcn_s_barrier();
+          asm volatile("" ::: "memory");
+        }
+        if (n >= 32 && (n - 32) % 5 == 0) dma(t + 2, cur, (n - 32) / 5);   // pieces 0..6
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // section 2: a1 x b1; DMA pieces 7..15; RAW sync for tile t+1; its k-step 0 reads
+#pragma unroll
+    for (int n = 0; n < 64; ++n) {
+      const int i = n >> 3, j = n & 7;
+      if constexpr (MODE == 0) {
+        if (n >= 3 && n <= 43 && (n - 3) % 5 == 0) dma(t + 2, cur, 7 + (n - 3) / 5);   // pieces 7..15
+      }
+      if constexpr (MODE <= 1) {
+        if (n == 48) {
+          if constexpr (MODE == 0) wait_vm<16>();
+          else wait_vm0();
+          __builtin_amdgcn_s_barrier();
+          asm volatile("" ::: "memory");
+        }
+        if (n >= 48) {
+          const int r = n - 48;   // a0[0], b0[0..7], a0[1..7]
+          if (r == 0) a0[0] = rdA(nxt, 0, 0);
+          else if (r <= 8) b0[r - 1] = rdB(nxt, r - 1, 0);
+          else a0[r - 8] = rdA(nxt, r - 8, 0);
+        }
+      }
+      MfA<T>::run(acc[i][j], a1[i], b1[j]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using I2 = std::integral_constant<int, 2>;
+  // buffers are compile-time: tile pairs (nt is even), then the 2-tile tail
+  for (int t = 0; t + 2 < nt; t += 2) {
+    tile(t, I0{}, I0{});
+    tile(t + 1, I0{}, I1{});
+  }
+  tile(nt - 2, I1{}, I0{});
+  tile(nt - 1, I2{}, I1{});
+  mfma_drain();
+
+  epilogue4<T, OT, EPI>(acc, smem, wm, wn, lane, C, ldc, m0, n0, g0, u0, accumulate, wide, act, F);
+}
+
 // BLLM_GEMM_NT_SCHED (read per launch, so one process can A/B): 0 = one barrier per K-tile
-// (gemm_nt_k), 1 = ping-pong wave rows (gemm_nt_pp_k)
+// (gemm_nt_k), 1 = ping-pong wave rows (gemm_nt_pp_k), 2 = 4 waves of 128 x 128 (gemm_nt4_k)
 inline int nt_sched() {
   const char* e = getenv("BLLM_GEMM_NT_SCHED");
   return e ? atoi(e) : 0;
@@ -491,10 +777,16 @@ void launch(const void* a, long lda, const void* b, long ldb, void* c, long ldc,
   static const bool attr = hipFuncSetAttribute((const void*)gemm_nt_k<T, OT, EPI>,
                                                hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES) == hipSuccess &&
                            hipFuncSetAttribute((const void*)gemm_nt_pp_k<T, OT, EPI>,
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES) == hipSuccess &&
+                           hipFuncSetAttribute((const void*)gemm_nt4_k<T, OT, EPI>,
                                                hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES) == hipSuccess;
   (void)attr;
   const bool wide = reinterpret_cast<uintptr_t>(c) % 16 == 0 && (ldc * (long)sizeof(OT)) % 16 == 0;
-  if ((sched < 0 ? nt_sched() : sched) == 1)
+  const int sc = sched < 0 ? nt_sched() : sched;
+  if (sc == 2)
+    hipLaunchKernelGGL((gemm_nt4_k<T, OT, EPI>), dim3((M / TM) * (N / TN)), dim3(THREADS4), LDS_BYTES, s,
+                       (const T*)a, lda, (const T*)b, ldb, (OT*)c, ldc, M, N, K, (int)accumulate, (int)wide, (OT*)act, F);
+  else if (sc == 1)
     hipLaunchKernelGGL((gemm_nt_pp_k<T, OT, EPI>), dim3((M / TM) * (N / TN)), dim3(THREADS), LDS_BYTES, s,
                        (const T*)a, lda, (const T*)b, ldb, (OT*)c, ldc, M, N, K, (int)accumulate, (int)wide, (OT*)act, F);
   else

@@ -569,14 +569,14 @@ def test_wgrad_gemm_unaligned_output(accumulate):
 @pytest.mark.parametrize("odt", [None, torch.float32])
 @pytest.mark.parametrize("M,K,N", [(256, 128, 256), (512, 384, 768), (768, 1024, 512), (1024, 4096, 1536)])
 @pytest.mark.parametrize("accumulate", [False, True])
-@pytest.mark.parametrize("impl", ["gemm_nt", "gemm_nt_pingpong", "wgrad_slots"])
+@pytest.mark.parametrize("impl", ["gemm_nt", "gemm_nt_pingpong", "gemm_nt_4wave", "wgrad_slots"])
 def test_gemm_nt(dt, odt, M, K, N, accumulate, impl, monkeypatch):
     """Both-operands-K-contiguous GEMM (c = a . b^T, the forward layout) vs an fp32 matmul,
     strided rows: the 64-deep-K-tile kernel (csrc/gemm_nt.hip, default), its ping-pong schedule
-    (BLLM_GEMM_NT_SCHED=1) and the 32-deep-slot kernel of csrc/gemm_wgrad.hip
-    (BLLM_GEMM_NT_IMPL=1)."""
+    (BLLM_GEMM_NT_SCHED=1), its 4-wave 128 x 128-per-wave schedule (BLLM_GEMM_NT_SCHED=2) and
+    the 32-deep-slot kernel of csrc/gemm_wgrad.hip (BLLM_GEMM_NT_IMPL=1)."""
     monkeypatch.setenv("BLLM_GEMM_NT_IMPL", "1" if impl == "wgrad_slots" else "2")
-    monkeypatch.setenv("BLLM_GEMM_NT_SCHED", "1" if impl == "gemm_nt_pingpong" else "0")
+    monkeypatch.setenv("BLLM_GEMM_NT_SCHED", {"gemm_nt_pingpong": "1", "gemm_nt_4wave": "2"}.get(impl, "0"))
     a_full = torch.randn(M, K + 64, device=DEV).to(dt)
     a = a_full[:, 32:32 + K]
     b_full = torch.randn(N, K + 32, device=DEV).to(dt)
@@ -665,7 +665,7 @@ def test_linear_residual_hipblaslt(dt, N, K, O):
 
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("M,K,F", [(256, 128, 128), (512, 512, 768), (1024, 4096, 1792)])
-@pytest.mark.parametrize("sched", ["0", "1"])
+@pytest.mark.parametrize("sched", ["0", "1", "2"])
 def test_gemm_nt_swiglu(dt, M, K, F, sched, monkeypatch):
     """Gate/up GEMM with the SwiGLU forward in the epilogue (K10): gu against the fp32 oracle, act
     bitwise equal to the separate swiglu_fwd kernel applied to that gu; both schedules."""

@@ -52,7 +52,7 @@ def main():
             x = torch.rand(m, k, device="cuda", dtype=dt) * 2 - 1
             w = (torch.rand(n, k, device="cuda", dtype=dt) * 2 - 1) * 0.05
             ref = torch.mm(x, w.t())
-            outs = {k_: torch.empty(m, n, device="cuda", dtype=dt) for k_ in ("new", "pp", "old")}
+            outs = {k_: torch.empty(m, n, device="cuda", dtype=dt) for k_ in ("new", "pp", "w4", "old")}
             y = torch.empty(m, n, device="cuda", dtype=dt)
 
             def new():
@@ -65,12 +65,17 @@ def main():
                 os.environ["BLLM_GEMM_NT_SCHED"] = "1"
                 ops.gemm_nt_(x, w, outs["pp"])
 
+            def w4():
+                os.environ.pop("BLLM_GEMM_NT_IMPL", None)
+                os.environ["BLLM_GEMM_NT_SCHED"] = "2"
+                ops.gemm_nt_(x, w, outs["w4"])
+
             def old():
                 os.environ["BLLM_GEMM_NT_IMPL"] = "1"
                 ops.gemm_nt_(x, w, outs["old"])
 
             fns = {"hipblaslt": lambda: torch.mm(x, w.t(), out=y), "gemm_nt_new": new, "gemm_nt_pp": pp,
-                   "gemm_nt_old": old}
+                   "gemm_nt_4w": w4, "gemm_nt_old": old}
             times = {kk: [] for kk in fns}
             for _ in range(a.rounds):
                 for kk, fn in fns.items():
@@ -82,7 +87,7 @@ def main():
                 med = sorted(ts)[len(ts) // 2]
                 r[kk + "_us"] = round(med * 1e3, 1)
                 r[kk + "_tflops"] = round(fl / med / 1e9, 1)
-            for kk in ("new", "pp", "old"):
+            for kk in ("new", "pp", "w4", "old"):
                 r[f"rel_err_{kk}"] = ((outs[kk].float() - ref.float()).norm() / ref.float().norm()).item()
             print(json.dumps(r), flush=True)
             del x, w, ref, outs, y
