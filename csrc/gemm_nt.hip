@@ -28,6 +28,7 @@
 #include <type_traits>
 
 #include "api.h"
+#include "gemm4.h"
 
 namespace bllm {
 namespace {
@@ -52,24 +53,6 @@ template <> struct Mf<f16_t> {
   }
 };
 
-// MFMA with the accumulator tied in place in an AGPR ("+a"): hipcc otherwise renames the
-// 256 accumulators of the 4-wave kernel between unrolled steps and pays for it in
-// v_accvgpr_read/write copies.  Operand hazards: fragments come from ds_read (waited for by the
-// compiler's lgkmcnt, no VALU producer); a chain on one accumulator needs no padding; the first
-// compiler reader after the last MFMA is behind mfma_drain().
-template <typename T> struct MfA;
-template <> struct MfA<bf16_t> {
-  static __device__ __forceinline__ void run(f32x4& c, const s16x8& a, const s16x8& b) {
-    asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(a), "v"(b));
-  }
-};
-template <> struct MfA<f16_t> {
-  static __device__ __forceinline__ void run(f32x4& c, const s16x8& a, const s16x8& b) {
-    asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, %0" : "+a"(c) : "v"(a), "v"(b));
-  }
-};
-__device__ __forceinline__ void mfma_drain() { asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory"); }
-
 constexpr int TM = 256, TN = 256, TK = 64;
 constexpr int ROWB = TK * 2;             // 128 B per LDS row (one K-tile of one row)
 constexpr int IMGB = TM * ROWB;          // 32 KiB per operand image
@@ -86,7 +69,11 @@ struct FB { s16x8 f[2][2]; };
 // (image rows 0-127 / 128-255), the epilogue stores gu (both halves, as the plain GEMM would) and
 // act = silu(g) * u for its 128 columns, rounded exactly like the separate SwiGLU kernel
 // (elementwise.hip: g, u rounded to T first, then a / (1 + exp(-a)) * u in fp32).
-enum { EPI_NONE = 0, EPI_SWIGLU = 1 };
+using g4::EPI_NONE;
+using g4::EPI_SWIGLU;
+using g4::i32x4;
+using g4::MfA;
+using g4::THREADS4;
 
 // ---- epilogue: lane holds C[16I + 4(l>>4) + e][16J + (l&15)] of its wave's 128 x 64 block
 template <typename T, typename OT, int EPI>
@@ -513,117 +500,8 @@ __global__ __launch_bounds__(THREADS) void gemm_nt_pp_k(const T* __restrict__ A,
 //     nxt) one per MFMA over the last 16.
 // Program order is pinned with sched_barrier(0) after each MFMA step; the compiler inserts the
 // counted lgkmcnt waits for the fragment reads, the DMA (inline asm) is counted by hand.
-constexpr int THREADS4 = 256;
 
-template <typename T, typename OT, int EPI>
-__device__ __forceinline__ void epilogue4(f32x4 (&acc)[8][8], char* smem, int wm, int wn, int lane, OT* C, long ldc,
-                                          long m0, long n0, long g0, long u0, int accumulate, int wide, OT* act,
-                                          int F) {
-  OT* cbase = C + m0 * ldc + n0;
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-  if (wide) {
-    constexpr int RB = TN * 4;
-    constexpr int EPT = 16 / (int)sizeof(OT);
-    constexpr int NCH = EPT / 4;
-    constexpr int IPR = TN / EPT;
-    constexpr int TRIPS = 128 * IPR / THREADS4;
-    struct alignas(16) V16 { OT e[EPT]; };
-#pragma unroll
-    for (int pass = 0; pass < 2; ++pass) {
-      if (wm == pass) {
-#pragma unroll
-        for (int I = 0; I < 8; ++I)
-#pragma unroll
-          for (int e = 0; e < 4; ++e)
-#pragma unroll
-            for (int J = 0; J < 8; ++J) {
-              const int lr = 16 * I + 4 * (lane >> 4) + e, col = wn * 128 + 16 * J + (lane & 15);
-              *(float*)(smem + lr * RB + ((((col >> 2) ^ (lr & 7)) << 4) | ((col & 3) << 2))) = acc[I][J][e];
-            }
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-#pragma unroll 4
-      for (int tr = 0; tr < TRIPS; ++tr) {
-        const int q = (int)threadIdx.x + tr * THREADS4;
-        const int lr = q / IPR, it = q % IPR;
-        float v[EPT];
-#pragma unroll
-        for (int h = 0; h < NCH; ++h) {
-          const f32x4 x = *(const f32x4*)(smem + lr * RB + (((it * NCH + h) ^ (lr & 7)) << 4));
-#pragma unroll
-          for (int k = 0; k < 4; ++k) v[4 * h + k] = x[k];
-        }
-        long col = it * EPT;
-        if constexpr (EPI == EPI_SWIGLU) col = col < 128 ? g0 + col - n0 : u0 + (col - 128) - n0;
-        V16* o = (V16*)(cbase + (long)(pass * 128 + lr) * ldc + col);
-        if (accumulate) {
-          const V16 old = *o;
-#pragma unroll
-          for (int k = 0; k < EPT; ++k) v[k] += to_f(old.e[k]);
-        }
-        V16 w;
-#pragma unroll
-        for (int k = 0; k < EPT; ++k) w.e[k] = from_f<OT>(v[k]);
-        *o = w;
-      }
-      if constexpr (EPI == EPI_SWIGLU) {
-        constexpr int AIPR = 128 / EPT;
-        constexpr int ATRIPS = 128 * AIPR / THREADS4;
-#pragma unroll 4
-        for (int tr = 0; tr < ATRIPS; ++tr) {
-          const int q = (int)threadIdx.x + tr * THREADS4;
-          const int lr = q / AIPR, it = q % AIPR;
-          float g[EPT], u[EPT];
-#pragma unroll
-          for (int h = 0; h < NCH; ++h) {
-            const f32x4 xg = *(const f32x4*)(smem + lr * RB + (((it * NCH + h) ^ (lr & 7)) << 4));
-            const f32x4 xu = *(const f32x4*)(smem + lr * RB + (((32 + it * NCH + h) ^ (lr & 7)) << 4));
-#pragma unroll
-            for (int k = 0; k < 4; ++k) g[4 * h + k] = xg[k], u[4 * h + k] = xu[k];
-          }
-          V16 w;
-#pragma unroll
-          for (int k = 0; k < EPT; ++k) {
-            const float a = to_f(from_f<OT>(g[k])), b = to_f(from_f<OT>(u[k]));
-            w.e[k] = from_f<OT>(a / (1.f + __expf(-a)) * b);
-          }
-          *(V16*)(act + (m0 + pass * 128 + lr) * (long)F + g0 + it * EPT) = w;
-        }
-      }
-      if (pass == 0) {
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-      }
-    }
-    return;
-  }
-  OT* c = cbase + (128 * wm + 4 * (lane >> 4)) * ldc + 128 * wn + (lane & 15);
-  if (accumulate) {
-#pragma unroll
-    for (int I = 0; I < 8; ++I)
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-#pragma unroll
-        for (int J = 0; J < 8; ++J) {
-          OT* o = c + (long)(16 * I + e) * ldc + 16 * J;
-          *o = from_f<OT>(to_f(*o) + acc[I][J][e]);
-        }
-  } else {
-#pragma unroll
-    for (int I = 0; I < 8; ++I)
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-#pragma unroll
-        for (int J = 0; J < 8; ++J) c[(long)(16 * I + e) * ldc + 16 * J] = from_f<OT>(acc[I][J][e]);
-  }
-}
-
-template <typename T, typename OT, int EPI>
+template <typename T, typename OT, int EPI, int DV>
 __global__ __launch_bounds__(THREADS4, 1) void gemm_nt4_k(const T* __restrict__ A, long lda,
                                                           const T* __restrict__ B, long ldb, OT* __restrict__ C,
                                                           long ldc, int M, int N, int K, int accumulate, int wide,
@@ -662,11 +540,18 @@ __global__ __launch_bounds__(THREADS4, 1) void gemm_nt4_k(const T* __restrict__ 
     voB[p] = r * ldbb + c;
   }
   // piece k of tile t (k < 8: A piece k, k >= 8: B piece k - 8) into buffer buf
+  const i32x4 rsA = g4::make_rsrc(Abase), rsB = g4::make_rsrc(Bbase);
   auto dma = [&](int t, int buf, int k) {
     const int p = k & 7;
     const uint32_t d = lds0 + (k >= 8 ? 2 * IMGB : 0) + buf * IMGB + (64 * wave + 8 * p) * ROWB;
-    if (k < 8) glds16s(sgpr_ptr(Abase + (long)t * TK), voA[p], d);
-    else glds16s(sgpr_ptr(Bbase + (long)t * TK), voB[p], d);
+    if constexpr (DV == 0) {
+      if (k < 8) glds16s(sgpr_ptr(Abase + (long)t * TK), voA[p], d);
+      else glds16s(sgpr_ptr(Bbase + (long)t * TK), voB[p], d);
+    } else {
+      const uint32_t so = __builtin_amdgcn_readfirstlane((uint32_t)(t * TK * (int)sizeof(T)));
+      if (k < 8) g4::bdma16<DV>(rsA, voA[p], so, d);
+      else g4::bdma16<DV>(rsB, voB[p], so, d);
+    }
   };
 
   // ---- fragment reads: row (.. + (l & 15)), logical chunk 4s + (l >> 4)
@@ -702,66 +587,66 @@ __global__ __launch_bounds__(THREADS4, 1) void gemm_nt4_k(const T* __restrict__ 
 #pragma unroll
   for (int i = 0; i < 8; ++i) a0[i] = rdA(0, i, 0), b0[i] = rdB(0, i, 0);
 
-  // MODE 0: DMA tile t+2 and read tile t+1; 1: read tile t+1 only (t = nt-2); 2: last tile
-  auto tile = [&](int t, auto mode_c, auto cur_c) {
-    constexpr int MODE = decltype(mode_c)::value;
+  // One branch-free body for every tile (so hipcc keeps one register assignment and never copies
+  // an accumulator between MFMAs, which would read it before the MFMA's result has landed): the
+  // pieces "of tile t+2" re-load tile nt-1 when t+2 >= nt (valid memory, into a buffer nothing
+  // reads again) and the last tile's "next" fragments are read from a buffer whose contents go
+  // unused; every DMA is drained before the epilogue reuses LDS.
+  auto tile = [&](int t, auto cur_c) {
     constexpr int cur = decltype(cur_c)::value, nxt = cur ^ 1;
+    const int tf = t + 2 < nt ? t + 2 : nt - 1;
     // section 1: a0 x b0; reads of k-step 1 (a1[0], b1[0..7], a1[1..7]) over the first 16 MFMAs
 #pragma unroll
     for (int n = 0; n < 64; ++n) {
       const int i = n >> 3, j = n & 7;
-      MfA<T>::run(acc[i][j], a0[i], b0[j]);
+      MfA<T>::run(acc[i][j], b0[j], a0[i]);   // swapped: lane holds 4 columns of a row
       if (n == 0) a1[0] = rdA(cur, 0, 1);
       else if (n <= 8) b1[n - 1] = rdB(cur, n - 1, 1);
       else if (n < 16) a1[n - 8] = rdA(cur, n - 8, 1);
-      if constexpr (MODE == 0) {
-        if (n == 31) {
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-          __builtin_amdgcn_s_barrier();
-          asm volatile("" ::: "memory");
-        }
-        if (n >= 32 && (n - 32) % 5 == 0) dma(t + 2, cur, (n - 32) / 5);   // pieces 0..6
+      if (n == 31) {   // WAR: every wave's reads of buffer cur retired
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
       }
+      if (n >= 32 && (n - 32) % 5 == 0) dma(tf, cur, (n - 32) / 5);   // pieces 0..6
       __builtin_amdgcn_sched_barrier(0);
     }
     // section 2: a1 x b1; DMA pieces 7..15; RAW sync for tile t+1; its k-step 0 reads
 #pragma unroll
     for (int n = 0; n < 64; ++n) {
       const int i = n >> 3, j = n & 7;
-      if constexpr (MODE == 0) {
-        if (n >= 3 && n <= 43 && (n - 3) % 5 == 0) dma(t + 2, cur, 7 + (n - 3) / 5);   // pieces 7..15
+      if (n >= 3 && n <= 43 && (n - 3) % 5 == 0) dma(tf, cur, 7 + (n - 3) / 5);   // pieces 7..15
+      if (n == 48) {   // RAW: every wave's pieces of tile t+1 landed (16 of tile t+2 may fly)
+        wait_vm<16>();
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
       }
-      if constexpr (MODE <= 1) {
-        if (n == 48) {
-          if constexpr (MODE == 0) wait_vm<16>();
-          else wait_vm0();
-          __builtin_amdgcn_s_barrier();
-          asm volatile("" ::: "memory");
-        }
-        if (n >= 48) {
-          const int r = n - 48;   // a0[0], b0[0..7], a0[1..7]
-          if (r == 0) a0[0] = rdA(nxt, 0, 0);
-          else if (r <= 8) b0[r - 1] = rdB(nxt, r - 1, 0);
-          else a0[r - 8] = rdA(nxt, r - 8, 0);
-        }
+      if (n >= 48) {
+        const int r = n - 48;   // a0[0], b0[0..7], a0[1..7]
+        if (r == 0) a0[0] = rdA(nxt, 0, 0);
+        else if (r <= 8) b0[r - 1] = rdB(nxt, r - 1, 0);
+        else a0[r - 8] = rdA(nxt, r - 8, 0);
       }
-      MfA<T>::run(acc[i][j], a1[i], b1[j]);
+      MfA<T>::run(acc[i][j], b1[j], a1[i]);
       __builtin_amdgcn_sched_barrier(0);
     }
   };
   using I0 = std::integral_constant<int, 0>;
   using I1 = std::integral_constant<int, 1>;
-  using I2 = std::integral_constant<int, 2>;
-  // buffers are compile-time: tile pairs (nt is even), then the 2-tile tail
-  for (int t = 0; t + 2 < nt; t += 2) {
-    tile(t, I0{}, I0{});
-    tile(t + 1, I0{}, I1{});
+  for (int t = 0; t < nt; t += 2) {   // nt is even
+    tile(t, I0{});
+    tile(t + 1, I1{});
   }
-  tile(nt - 2, I1{}, I0{});
-  tile(nt - 1, I2{}, I1{});
-  mfma_drain();
+  // the last MFMAs' results land before anything reads an accumulator: drain, then pin every
+  // accumulator in its AGPR behind the drain (no copy of one can be scheduled above it)
+  wait_vm0();
+  g4::mfma_drain();
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) asm volatile("" : "+a"(acc[i][j]));
 
-  epilogue4<T, OT, EPI>(acc, smem, wm, wn, lane, C, ldc, m0, n0, g0, u0, accumulate, wide, act, F);
+  g4::epilogue4<T, OT, EPI>(acc, smem, wm, wn, lane, C, ldc, m0, n0, g0, u0, accumulate, wide, act, F);
 }
 
 // BLLM_GEMM_NT_SCHED (read per launch, so one process can A/B): 0 = one barrier per K-tile
@@ -778,15 +663,29 @@ void launch(const void* a, long lda, const void* b, long ldb, void* c, long ldc,
                                                hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES) == hipSuccess &&
                            hipFuncSetAttribute((const void*)gemm_nt_pp_k<T, OT, EPI>,
                                                hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES) == hipSuccess &&
-                           hipFuncSetAttribute((const void*)gemm_nt4_k<T, OT, EPI>,
+                           hipFuncSetAttribute((const void*)gemm_nt4_k<T, OT, EPI, 0>,
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES) == hipSuccess &&
+                           hipFuncSetAttribute((const void*)gemm_nt4_k<T, OT, EPI, 1>,
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES) == hipSuccess &&
+                           hipFuncSetAttribute((const void*)gemm_nt4_k<T, OT, EPI, 2>,
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES) == hipSuccess &&
+                           hipFuncSetAttribute((const void*)gemm_nt4_k<T, OT, EPI, 3>,
                                                hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES) == hipSuccess;
   (void)attr;
   const bool wide = reinterpret_cast<uintptr_t>(c) % 16 == 0 && (ldc * (long)sizeof(OT)) % 16 == 0;
   const int sc = sched < 0 ? nt_sched() : sched;
-  if (sc == 2)
-    hipLaunchKernelGGL((gemm_nt4_k<T, OT, EPI>), dim3((M / TM) * (N / TN)), dim3(THREADS4), LDS_BYTES, s,
-                       (const T*)a, lda, (const T*)b, ldb, (OT*)c, ldc, M, N, K, (int)accumulate, (int)wide, (OT*)act, F);
-  else if (sc == 1)
+  if (sc == 2) {
+    const char* e = getenv("BLLM_GEMM_NT4_DMA");
+    const int dv = e && *e ? atoi(e) : 0;
+#define BLLM_NT4(DVv)                                                                                                  \
+  hipLaunchKernelGGL((gemm_nt4_k<T, OT, EPI, DVv>), dim3((M / TM) * (N / TN)), dim3(THREADS4), LDS_BYTES, s,         \
+                     (const T*)a, lda, (const T*)b, ldb, (OT*)c, ldc, M, N, K, (int)accumulate, (int)wide, (OT*)act, F)
+    if (dv == 1) BLLM_NT4(1);
+    else if (dv == 2) BLLM_NT4(2);
+    else if (dv == 3) BLLM_NT4(3);
+    else BLLM_NT4(0);
+#undef BLLM_NT4
+  } else if (sc == 1)
     hipLaunchKernelGGL((gemm_nt_pp_k<T, OT, EPI>), dim3((M / TM) * (N / TN)), dim3(THREADS), LDS_BYTES, s,
                        (const T*)a, lda, (const T*)b, ldb, (OT*)c, ldc, M, N, K, (int)accumulate, (int)wide, (OT*)act, F);
   else

@@ -49,6 +49,7 @@
 #include <type_traits>
 
 #include "api.h"
+#include "gemm4.h"
 
 namespace bllm {
 namespace {
@@ -451,6 +452,159 @@ __global__ __launch_bounds__(Geo<VAR>::THREADS) void wgrad_gemm_k(const T* __res
   }
 }
 
+// ---- Variant 4: one wave per SIMD, 128 x 128 outputs per wave (the structure of
+// csrc/gemm_nt.hip's 4-wave schedule and of gfx950 hipBLASLt's MT256x256x64 kernels) on this
+// kernel's operand layout.  A K-tile is 64 tokens = two 32-row ring slots per operand (LDS slots
+// 2b, 2b+1 of buffer b; same images, swizzle and transposed fragment reads as variants 0-3);
+// every fragment of a K-tile sits in VGPRs (a0/b0 k-step 0, a1/b1 k-step 1), the MFMAs keep their
+// accumulators in place in AGPRs (g4::MfA), operands swapped so a lane holds 4 consecutive
+// columns of a row (g4::epilogue4).  Per wave and K-tile: 128 MFMAs, 64 ds_read_b64_tr_b16,
+// 16 LDS-DMA pieces (wave w moves token rows 16w .. 16w+15 of both operands):
+//   section 1 (a0 x b0): reads of a1/b1 over the first 16 MFMAs; after MFMA 31 lgkmcnt(0) +
+//     barrier (WAR on buffer cur), then the pieces of tile t+2 into cur, one per 5 MFMAs;
+//   section 2 (a1 x b1): the rest of the pieces; after MFMA 47 vmcnt(16) + barrier (RAW for tile
+//     t+1), then the reads of a0/b0 of tile t+1 over the last 16 MFMAs.
+// The body is branch-free for every tile (past the end the pieces re-load the last tile into a
+// buffer nothing reads again).  DV 0: global_load_lds with the tile's base pointer in SGPRs;
+// 1: buffer_load ... lds on a per-tile descriptor (BLLM_WGRAD4_DMA, default 1).
+template <typename T, typename OT, int DV>
+__global__ __launch_bounds__(g4::THREADS4, 1) void wgrad4_k(const T* __restrict__ A, long lda,
+                                                            const T* __restrict__ B, long ldb, OT* __restrict__ C,
+                                                            long ldc, long c_split, int M, int N, int K,
+                                                            int accumulate, int wide) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int wm = wave >> 1, wn = wave & 1;
+
+  const int nbm = M / BM, nbn = N / BN, nblk = nbm * nbn;
+  const int bid = blockIdx.x, xcd = bid & 7, q8 = nblk >> 3, r8 = nblk & 7;
+  const int wid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int per_group = GROUP_M * nbn;
+  const int grp = wid / per_group;
+  const int first_m = grp * GROUP_M;
+  const int gm = nbm - first_m < GROUP_M ? nbm - first_m : GROUP_M;
+  const int in_g = wid - grp * per_group;
+  const int tm = first_m + in_g % gm, tn = in_g / gm;
+  const long m0 = (long)tm * BM, n0 = (long)tn * BN;
+
+  const int S = gridDim.y, sp = blockIdx.y, nch = K / KCH;
+  const int c_lo = (int)((long)nch * sp / S), c_hi = (int)((long)nch * (sp + 1) / S);
+  const int nt = (c_hi - c_lo) * (KCH / 64);   // 64-deep K-tiles, even
+
+  // ---- staging: piece p of wave w = token rows kr, kr+1 (kr = 16w + 2p) of the K-tile; lane l
+  //      -> row kr + (l >> 5), physical chunk l & 31 holding logical chunk (l & 31) ^ swz(row & 31)
+  uint32_t voA[8], voB[8];
+#pragma unroll
+  for (int p = 0; p < 8; ++p) {
+    const int kr = 16 * wave + 2 * p + (lane >> 5), c = (lane & 31) ^ swz(kr & 31);
+    voA[p] = (uint32_t)((kr * lda + 8 * c) * (long)sizeof(T));
+    voB[p] = (uint32_t)((kr * ldb + 8 * c) * (long)sizeof(T));
+  }
+  const uint32_t lds0 = lds_u32(smem);
+  const T* Abase = A + (long)c_lo * KCH * lda + m0;
+  const T* Bbase = B + (long)c_lo * KCH * ldb + n0;
+  // piece k (< 8: A piece k, else B piece k - 8) of tile t into buffer buf (slots 2buf, 2buf+1)
+  auto dma = [&](int t, int buf, int k) {
+    const int p = k & 7, kr = 16 * wave + 2 * p;
+    const uint32_t d = lds0 + (k >= 8 ? B_BASE : 0) + (2 * buf + (kr >> 5)) * SLOTB + (kr & 31) * ROWB;
+    const T* base = k < 8 ? Abase + (long)t * 64 * lda : Bbase + (long)t * 64 * ldb;
+    if constexpr (DV == 0) glds16s(sgpr_ptr(base), k < 8 ? voA[p] : voB[p], d);
+    else g4::bdma16<1>(g4::make_rsrc(base), k < 8 ? voA[p] : voB[p], 0u, d);
+  };
+
+  // ---- fragment offsets (variants 0-3 with 128 columns per wave on both operands)
+  const int g = lane >> 4, qq = (lane & 15) >> 2, p4 = lane & 3;
+  const int f = 2 * (qq | ((g & 1) << 2));
+  const int rowb = (8 * g + qq) * ROWB + (p4 & 1) * 8 + (p4 >> 1) * 16;
+  const char* pa = smem + rowb + (wm * 16) * 16;
+  const char* pb = smem + B_BASE + rowb + (wn * 16) * 16;
+  // i-th 16-column fragment of slot sl: column chunk (2i) ^ f past the wave's base (f < 16, even)
+  auto rdA = [&](int sl, int i) -> g4::s16x8 { return frag(pa + sl * SLOTB + ((2 * i) ^ f) * 16); };
+  auto rdB = [&](int sl, int j) -> g4::s16x8 { return frag(pb + sl * SLOTB + ((2 * j) ^ f) * 16); };
+
+  g4::f32x4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = g4::f32x4{};
+  g4::s16x8 a0[8], b0[8], a1[8], b1[8];
+
+#pragma unroll
+  for (int k = 0; k < 16; ++k) dma(0, 0, k);
+#pragma unroll
+  for (int k = 0; k < 16; ++k) dma(1, 1, k);
+  vm_wait<16>();
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+#pragma unroll
+  for (int i = 0; i < 8; ++i) a0[i] = rdA(0, i), b0[i] = rdB(0, i);
+
+  auto tile = [&](int t, auto cur_c) {
+    constexpr int cur = decltype(cur_c)::value, nxt = cur ^ 1;
+    const int tf = t + 2 < nt ? t + 2 : nt - 1;
+#pragma unroll
+    for (int n = 0; n < 64; ++n) {
+      const int i = n >> 3, j = n & 7;
+      g4::MfA<T>::run(acc[i][j], b0[j], a0[i]);
+      if (n == 0) a1[0] = rdA(2 * cur + 1, 0);
+      else if (n <= 8) b1[n - 1] = rdB(2 * cur + 1, n - 1);
+      else if (n < 16) a1[n - 8] = rdA(2 * cur + 1, n - 8);
+      if (n == 31) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+      }
+      if (n >= 32 && (n - 32) % 5 == 0) dma(tf, cur, (n - 32) / 5);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int n = 0; n < 64; ++n) {
+      const int i = n >> 3, j = n & 7;
+      if (n >= 3 && n <= 43 && (n - 3) % 5 == 0) dma(tf, cur, 7 + (n - 3) / 5);
+      if (n == 48) {
+        vm_wait<16>();
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+      }
+      if (n >= 48) {
+        const int r = n - 48;
+        if (r == 0) a0[0] = rdA(2 * nxt, 0);
+        else if (r <= 8) b0[r - 1] = rdB(2 * nxt, r - 1);
+        else a0[r - 8] = rdA(2 * nxt, r - 8);
+      }
+      g4::MfA<T>::run(acc[i][j], b1[j], a1[i]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  for (int t = 0; t < nt; t += 2) {
+    tile(t, I0{});
+    tile(t + 1, I1{});
+  }
+  vm_wait<0>();
+  g4::mfma_drain();
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) asm volatile("" : "+a"(acc[i][j]));
+  g4::epilogue4<T, OT, g4::EPI_NONE>(acc, smem, wm, wn, lane, C + sp * c_split, ldc, m0, n0, 0, 0, accumulate, wide,
+                                     (OT*)nullptr, 0);
+}
+
+template <typename T, typename OT, int DV>
+void launch4(const void* a, long lda, const void* b, long ldb, void* c, long ldc, long c_split, int M, int N, int K,
+             int S, bool accumulate, hipStream_t s) {
+  static const bool attr = hipFuncSetAttribute((const void*)wgrad4_k<T, OT, DV>,
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES) == hipSuccess;
+  (void)attr;
+  const dim3 grid((M / BM) * (N / BN), S);
+  const bool wide = reinterpret_cast<uintptr_t>(c) % 16 == 0 && (ldc * (long)sizeof(OT)) % 16 == 0 &&
+                    (c_split * (long)sizeof(OT)) % 16 == 0;
+  hipLaunchKernelGGL((wgrad4_k<T, OT, DV>), grid, dim3(g4::THREADS4), LDS_BYTES, s, (const T*)a, lda, (const T*)b, ldb,
+                     (OT*)c, ldc, c_split, M, N, K, (int)accumulate, (int)wide);
+}
+
 template <typename T, typename OT, int VAR, bool AK = false, bool BKC = false>
 void launch_v(const void* a, long lda, const void* b, long ldb, void* c, long ldc, long c_split, int M, int N, int K,
               int S, bool accumulate, hipStream_t s) {
@@ -475,6 +629,12 @@ template <typename T, typename OT>
 void launch(const void* a, long lda, const void* b, long ldb, void* c, long ldc, long c_split, int M, int N, int K,
             int S, bool accumulate, hipStream_t s) {
   switch (variant()) {
+    case 4: {
+      const char* e = getenv("BLLM_WGRAD4_DMA");
+      if (e && *e == '0') launch4<T, OT, 0>(a, lda, b, ldb, c, ldc, c_split, M, N, K, S, accumulate, s);
+      else launch4<T, OT, 1>(a, lda, b, ldb, c, ldc, c_split, M, N, K, S, accumulate, s);
+      break;
+    }
     case 0: launch_v<T, OT, 0>(a, lda, b, ldb, c, ldc, c_split, M, N, K, S, accumulate, s); break;
     case 2: launch_v<T, OT, 2>(a, lda, b, ldb, c, ldc, c_split, M, N, K, S, accumulate, s); break;
     case 3: launch_v<T, OT, 3>(a, lda, b, ldb, c, ldc, c_split, M, N, K, S, accumulate, s); break;

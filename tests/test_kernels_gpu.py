@@ -522,7 +522,7 @@ def test_split_k_weight_grad(gdt, accumulate):
 @pytest.mark.parametrize("odt", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("K,M,N,S", [(128, 256, 256, 1), (384, 512, 768, 1), (2048, 768, 512, 3), (1024, 256, 1024, 2)])
 @pytest.mark.parametrize("accumulate", [False, True])
-@pytest.mark.parametrize("variant", ["0", "1", "2", "3"])
+@pytest.mark.parametrize("variant", ["0", "1", "2", "3", "4"])
 def test_wgrad_gemm(dt, odt, K, M, N, S, accumulate, variant, monkeypatch):
     """Token-major MFMA dW kernel c (+)= a^T b (strided a, split-K) vs an fp32 matmul, every
     schedule variant (BLLM_WGRAD_VARIANT is read per launch)."""

@@ -42,6 +42,8 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--models", default="llama,gpt2")
+    ap.add_argument("--nt4_dma", default="0", help="comma list of BLLM_GEMM_NT4_DMA variants of the 4-wave arm")
+    ap.add_argument("--arms", default="hipblaslt,new,pp,4w,old")
     a = ap.parse_args()
     ops.load_ext(required=True)
     dt = torch.bfloat16
@@ -52,7 +54,8 @@ def main():
             x = torch.rand(m, k, device="cuda", dtype=dt) * 2 - 1
             w = (torch.rand(n, k, device="cuda", dtype=dt) * 2 - 1) * 0.05
             ref = torch.mm(x, w.t())
-            outs = {k_: torch.empty(m, n, device="cuda", dtype=dt) for k_ in ("new", "pp", "w4", "old")}
+            dvs = a.nt4_dma.split(",")
+            outs = {k_: torch.empty(m, n, device="cuda", dtype=dt) for k_ in ["new", "pp", "old"] + ["w4_" + d for d in dvs]}
             y = torch.empty(m, n, device="cuda", dtype=dt)
 
             def new():
@@ -65,17 +68,24 @@ def main():
                 os.environ["BLLM_GEMM_NT_SCHED"] = "1"
                 ops.gemm_nt_(x, w, outs["pp"])
 
-            def w4():
-                os.environ.pop("BLLM_GEMM_NT_IMPL", None)
-                os.environ["BLLM_GEMM_NT_SCHED"] = "2"
-                ops.gemm_nt_(x, w, outs["w4"])
+            def w4(dv):
+                def f():
+                    os.environ.pop("BLLM_GEMM_NT_IMPL", None)
+                    os.environ["BLLM_GEMM_NT_SCHED"] = "2"
+                    os.environ["BLLM_GEMM_NT4_DMA"] = dv
+                    ops.gemm_nt_(x, w, outs["w4_" + dv])
+                return f
 
             def old():
                 os.environ["BLLM_GEMM_NT_IMPL"] = "1"
                 ops.gemm_nt_(x, w, outs["old"])
 
             fns = {"hipblaslt": lambda: torch.mm(x, w.t(), out=y), "gemm_nt_new": new, "gemm_nt_pp": pp,
-                   "gemm_nt_4w": w4, "gemm_nt_old": old}
+                   "gemm_nt_old": old}
+            fns.update({"gemm_nt_4w_" + d: w4(d) for d in dvs})
+            want = a.arms.split(",")
+            fns = {k_: f for k_, f in fns.items()
+                   if k_ == "hipblaslt" and "hipblaslt" in want or k_.startswith("gemm_nt_") and k_.split("_")[2] in want}
             times = {kk: [] for kk in fns}
             for _ in range(a.rounds):
                 for kk, fn in fns.items():
@@ -87,8 +97,9 @@ def main():
                 med = sorted(ts)[len(ts) // 2]
                 r[kk + "_us"] = round(med * 1e3, 1)
                 r[kk + "_tflops"] = round(fl / med / 1e9, 1)
-            for kk in ("new", "pp", "w4", "old"):
-                r[f"rel_err_{kk}"] = ((outs[kk].float() - ref.float()).norm() / ref.float().norm()).item()
+            for kk in outs:
+                if any(f.endswith(kk) for f in fns):
+                    r[f"rel_err_{kk}"] = ((outs[kk].float() - ref.float()).norm() / ref.float().norm()).item()
             print(json.dumps(r), flush=True)
             del x, w, ref, outs, y
             torch.cuda.empty_cache()
