@@ -649,6 +649,215 @@ __global__ __launch_bounds__(THREADS4, 1) void gemm_nt4_k(const T* __restrict__ 
   g4::epilogue4<T, OT, EPI>(acc, smem, wm, wn, lane, C, ldc, m0, n0, g0, u0, accumulate, wide, act, F);
 }
 
+// ---- persistent 4-wave schedule (BLLM_GEMM_NT_SCHED=3): the loop of gemm_nt4_k, but one
+// workgroup per CU walks output tiles tid, tid + G, ... (the same XCD-contiguous, GROUP_M-deep
+// tile order), and the K-tile stream never drains between output tiles: the pieces "of K-tile
+// t+2" issued in the last two K-tiles of a tile are K-tiles 0 and 1 of the workgroup's NEXT tile,
+// and the fragments read at the end of the last K-tile are that tile's first.  The epilogue
+// therefore writes straight from the accumulators (lane: 4 consecutive columns of one row ->
+// one 8-B bf16/fp16 or 16-B fp32 store per accumulator) while the next tile's first 64 KiB land
+// in LDS, instead of staging through LDS with the pipeline drained.
+template <typename T, typename OT, int DV>
+__global__ __launch_bounds__(THREADS4, 1) void gemm_nt4p_k(const T* __restrict__ A, long lda,
+                                                           const T* __restrict__ B, long ldb, OT* __restrict__ C,
+                                                           long ldc, int M, int N, int K, int accumulate, int vec) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int nbm = M / TM, nbn = N / TN, nblk = nbm * nbn, G = gridDim.x;
+  const int q8 = nblk >> 3, r8 = nblk & 7, per_group = GROUP_M * nbn;
+  auto coords = [&](int tid, long& m0, long& n0) {
+    const int xcd = tid & 7;
+    const int wid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (tid >> 3);
+    const int grp = wid / per_group, first_m = grp * GROUP_M;
+    const int gm = nbm - first_m < GROUP_M ? nbm - first_m : GROUP_M;
+    const int in_g = wid - grp * per_group;
+    m0 = (long)(first_m + in_g % gm) * TM;
+    n0 = (long)(in_g / gm) * TN;
+  };
+
+  const uint32_t lds0 = lds_u32(smem);
+  const uint32_t ldab = (uint32_t)(lda * sizeof(T)), ldbb = (uint32_t)(ldb * sizeof(T));
+  uint32_t voA[8], voB[8];
+#pragma unroll
+  for (int p = 0; p < 8; ++p) {
+    const uint32_t r = 8u * p + (uint32_t)(lane >> 3), c = 16u * ((lane & 7) ^ ((r >> 1) & 7));
+    voA[p] = r * ldab + c;
+    voB[p] = r * ldbb + c;
+  }
+  const int nt = K / TK;  // even, >= 2
+  constexpr uint32_t TKB = TK * (uint32_t)sizeof(T);
+
+  int tid = blockIdx.x;
+  long m0, n0;
+  coords(tid, m0, n0);
+  const T* Ac = A + (m0 + 64 * wave) * lda;   // this wave's staged rows of the current tile
+  const T* Bc = B + (n0 + 64 * wave) * ldb;
+  const T* An = Ac;                           // ... and of the next tile (= current when none)
+  const T* Bn = Bc;
+  int tid_n = tid + G;
+  long m0n = m0, n0n = n0;
+  auto set_next = [&]() {
+    tid_n = tid + G;
+    if (tid_n < nblk) {
+      coords(tid_n, m0n, n0n);
+      An = A + (m0n + 64 * wave) * lda;
+      Bn = B + (n0n + 64 * wave) * ldb;
+    } else {
+      An = Ac, Bn = Bc;
+    }
+  };
+  set_next();
+  // piece k of K-tile t of the stream (t < nt: current tile; nt, nt+1: the next tile's 0, 1, or
+  // re-loads of the current tile's last K-tile when there is none) into buffer buf
+  auto dma = [&](int t, int buf, int k) {
+    const int p = k & 7;
+    const uint32_t d = lds0 + (k >= 8 ? 2 * IMGB : 0) + buf * IMGB + (64 * wave + 8 * p) * ROWB;
+    const bool nx = t >= nt;
+    const int tt = !nx ? t : (tid_n < nblk ? t - nt : nt - 1);
+    const T* base = k < 8 ? (nx ? An : Ac) : (nx ? Bn : Bc);
+    if constexpr (DV == 0) {
+      glds16s(sgpr_ptr(base + (long)tt * TK), k < 8 ? voA[p] : voB[p], d);
+    } else {
+      const uint32_t so = __builtin_amdgcn_readfirstlane((uint32_t)tt * TKB);
+      g4::bdma16<DV>(g4::make_rsrc(base), k < 8 ? voA[p] : voB[p], so, d);
+    }
+  };
+
+  const int xo0 = ((0 + (lane >> 4)) ^ ((lane >> 1) & 7)) << 4;
+  const int xo1 = ((4 + (lane >> 4)) ^ ((lane >> 1) & 7)) << 4;
+  const char* pA0 = smem + (128 * wm + (lane & 15)) * ROWB + xo0;
+  const char* pA1 = smem + (128 * wm + (lane & 15)) * ROWB + xo1;
+  const char* pB0 = smem + 2 * IMGB + (128 * wn + (lane & 15)) * ROWB + xo0;
+  const char* pB1 = smem + 2 * IMGB + (128 * wn + (lane & 15)) * ROWB + xo1;
+  auto rdA = [&](int buf, int i, int s) -> s16x8 {
+    return *(const lds_s16x8*)((s ? pA1 : pA0) + buf * IMGB + 16 * i * ROWB);
+  };
+  auto rdB = [&](int buf, int j, int s) -> s16x8 {
+    return *(const lds_s16x8*)((s ? pB1 : pB0) + buf * IMGB + 16 * j * ROWB);
+  };
+
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{};
+  s16x8 a0[8], b0[8], a1[8], b1[8];
+
+#pragma unroll
+  for (int k = 0; k < 16; ++k) dma(0, 0, k);
+#pragma unroll
+  for (int k = 0; k < 16; ++k) dma(1, 1, k);
+  wait_vm<16>();
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+#pragma unroll
+  for (int i = 0; i < 8; ++i) a0[i] = rdA(0, i, 0), b0[i] = rdB(0, i, 0);
+
+  auto ktile = [&](int t, auto cur_c) {
+    constexpr int cur = decltype(cur_c)::value, nxt = cur ^ 1;
+#pragma unroll
+    for (int n = 0; n < 64; ++n) {
+      const int i = n >> 3, j = n & 7;
+      MfA<T>::run(acc[i][j], b0[j], a0[i]);
+      if (n == 0) a1[0] = rdA(cur, 0, 1);
+      else if (n <= 8) b1[n - 1] = rdB(cur, n - 1, 1);
+      else if (n < 16) a1[n - 8] = rdA(cur, n - 8, 1);
+      if (n == 31) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+      }
+      if (n >= 32 && (n - 32) % 5 == 0) dma(t + 2, cur, (n - 32) / 5);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int n = 0; n < 64; ++n) {
+      const int i = n >> 3, j = n & 7;
+      if (n >= 3 && n <= 43 && (n - 3) % 5 == 0) dma(t + 2, cur, 7 + (n - 3) / 5);
+      if (n == 48) {
+        wait_vm<16>();
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+      }
+      if (n >= 48) {
+        const int r = n - 48;
+        if (r == 0) a0[0] = rdA(nxt, 0, 0);
+        else if (r <= 8) b0[r - 1] = rdB(nxt, r - 1, 0);
+        else a0[r - 8] = rdA(nxt, r - 8, 0);
+      }
+      MfA<T>::run(acc[i][j], b1[j], a1[i]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  for (;;) {
+    for (int t = 0; t < nt; t += 2) {
+      ktile(t, I0{});
+      ktile(t + 1, I1{});
+    }
+    g4::mfma_drain();
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) asm volatile("" : "+a"(acc[i][j]));
+    // epilogue straight from the accumulators: acc[i][j] = row 16i + (l & 15), columns
+    // 16j + 4(l >> 4) .. +3 of the wave's 128 x 128 block
+    OT* cw = C + (m0 + 128 * wm + (lane & 15)) * ldc + n0 + 128 * wn + 4 * (lane >> 4);
+    if (vec) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          OT* o = cw + (long)(16 * i) * ldc + 16 * j;
+          float v0 = acc[i][j][0], v1 = acc[i][j][1], v2 = acc[i][j][2], v3 = acc[i][j][3];
+          if constexpr (sizeof(OT) == 2) {
+            if (accumulate) {
+              const uint2 old = *(const uint2*)o;
+              v0 += to_f(__builtin_bit_cast(OT, (short)(old.x & 0xFFFF)));
+              v1 += to_f(__builtin_bit_cast(OT, (short)(old.x >> 16)));
+              v2 += to_f(__builtin_bit_cast(OT, (short)(old.y & 0xFFFF)));
+              v3 += to_f(__builtin_bit_cast(OT, (short)(old.y >> 16)));
+            }
+            uint2 w;
+            w.x = (uint32_t)(uint16_t)__builtin_bit_cast(short, from_f<OT>(v0)) |
+                  ((uint32_t)(uint16_t)__builtin_bit_cast(short, from_f<OT>(v1)) << 16);
+            w.y = (uint32_t)(uint16_t)__builtin_bit_cast(short, from_f<OT>(v2)) |
+                  ((uint32_t)(uint16_t)__builtin_bit_cast(short, from_f<OT>(v3)) << 16);
+            *(uint2*)o = w;
+          } else {
+            f32x4 w{v0, v1, v2, v3};
+            if (accumulate) w += *(const f32x4*)o;
+            *(f32x4*)o = w;
+          }
+        }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            OT* o = cw + (long)(16 * i) * ldc + 16 * j + e;
+            *o = from_f<OT>((accumulate ? to_f(*o) : 0.f) + acc[i][j][e]);
+          }
+    }
+    if (tid_n >= nblk) break;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        acc[i][j] = f32x4{};
+        asm volatile("" : "+a"(acc[i][j]));
+      }
+    asm volatile("s_nop 7" ::: "memory");
+    tid = tid_n, m0 = m0n, n0 = n0n, Ac = An, Bc = Bn;
+    set_next();
+  }
+  wait_vm0();   // the re-load pieces of the last two stream K-tiles land before the wave ends
+}
+
 // BLLM_GEMM_NT_SCHED (read per launch, so one process can A/B): 0 = one barrier per K-tile
 // (gemm_nt_k), 1 = ping-pong wave rows (gemm_nt_pp_k), 2 = 4 waves of 128 x 128 (gemm_nt4_k)
 inline int nt_sched() {
@@ -674,7 +883,25 @@ void launch(const void* a, long lda, const void* b, long ldb, void* c, long ldc,
   (void)attr;
   const bool wide = reinterpret_cast<uintptr_t>(c) % 16 == 0 && (ldc * (long)sizeof(OT)) % 16 == 0;
   const int sc = sched < 0 ? nt_sched() : sched;
-  if (sc == 2) {
+  if (sc == 3 && EPI == EPI_NONE) {
+    static const bool attr3 = hipFuncSetAttribute((const void*)gemm_nt4p_k<T, OT, 1>,
+                                                  hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES) == hipSuccess;
+    (void)attr3;
+    static int ncu = 0;
+    if (!ncu) {
+      int dev = 0;
+      (void)hipGetDevice(&dev);
+      hipDeviceProp_t prop;
+      ncu = hipGetDeviceProperties(&prop, dev) == hipSuccess ? prop.multiProcessorCount : 256;
+      ncu = ncu < 8 ? 8 : ncu / 8 * 8;
+    }
+    const int nblk = (M / TM) * (N / TN);
+    const int grid = nblk < ncu ? nblk : ncu;
+    const bool vec = sizeof(OT) == 2 ? (reinterpret_cast<uintptr_t>(c) % 8 == 0 && (ldc * (long)sizeof(OT)) % 8 == 0)
+                                     : (reinterpret_cast<uintptr_t>(c) % 16 == 0 && (ldc * (long)sizeof(OT)) % 16 == 0);
+    hipLaunchKernelGGL((gemm_nt4p_k<T, OT, 1>), dim3(grid), dim3(THREADS4), LDS_BYTES, s, (const T*)a, lda,
+                       (const T*)b, ldb, (OT*)c, ldc, M, N, K, (int)accumulate, (int)vec);
+  } else if (sc == 2 || sc == 3) {
     const char* e = getenv("BLLM_GEMM_NT4_DMA");
     const int dv = e && *e ? atoi(e) : 0;
 #define BLLM_NT4(DVv)                                                                                                  \

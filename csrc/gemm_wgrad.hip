@@ -620,15 +620,19 @@ void launch_v(const void* a, long lda, const void* b, long ldb, void* c, long ld
 
 constexpr int DEFAULT_VARIANT = 2;
 
-int variant() {
+// Default: variant 4 (one wave per SIMD, 128 x 128 per wave) — 1.02-1.06x variant 2 on the
+// Llama-3-8B / Llama-3.2-1B / GPT2-774M weight gradients at 40,960 tokens
+// (profiles/r3/wgrad4_vs_v2.jsonl) — except for deep split-K (S >= 8: GPT2-774M's 1280 x 1280
+// o-projection, 200 workgroups), where variant 2 was 12 % faster.
+int variant(int S) {
   const char* e = getenv("BLLM_WGRAD_VARIANT");  // per launch (A/B in one process); ~100 ns
-  return e && *e ? atoi(e) : DEFAULT_VARIANT;
+  return e && *e ? atoi(e) : (S >= 8 ? DEFAULT_VARIANT : 4);
 }
 
 template <typename T, typename OT>
 void launch(const void* a, long lda, const void* b, long ldb, void* c, long ldc, long c_split, int M, int N, int K,
             int S, bool accumulate, hipStream_t s) {
-  switch (variant()) {
+  switch (variant(S)) {
     case 4: {
       const char* e = getenv("BLLM_WGRAD4_DMA");
       if (e && *e == '0') launch4<T, OT, 0>(a, lda, b, ldb, c, ldc, c_split, M, N, K, S, accumulate, s);

@@ -569,14 +569,15 @@ def test_wgrad_gemm_unaligned_output(accumulate):
 @pytest.mark.parametrize("odt", [None, torch.float32])
 @pytest.mark.parametrize("M,K,N", [(256, 128, 256), (512, 384, 768), (768, 1024, 512), (1024, 4096, 1536)])
 @pytest.mark.parametrize("accumulate", [False, True])
-@pytest.mark.parametrize("impl", ["gemm_nt", "gemm_nt_pingpong", "gemm_nt_4wave", "wgrad_slots"])
+@pytest.mark.parametrize("impl", ["gemm_nt", "gemm_nt_pingpong", "gemm_nt_4wave", "gemm_nt_persistent", "wgrad_slots"])
 def test_gemm_nt(dt, odt, M, K, N, accumulate, impl, monkeypatch):
     """Both-operands-K-contiguous GEMM (c = a . b^T, the forward layout) vs an fp32 matmul,
     strided rows: the 64-deep-K-tile kernel (csrc/gemm_nt.hip, default), its ping-pong schedule
     (BLLM_GEMM_NT_SCHED=1), its 4-wave 128 x 128-per-wave schedule (BLLM_GEMM_NT_SCHED=2) and
     the 32-deep-slot kernel of csrc/gemm_wgrad.hip (BLLM_GEMM_NT_IMPL=1)."""
     monkeypatch.setenv("BLLM_GEMM_NT_IMPL", "1" if impl == "wgrad_slots" else "2")
-    monkeypatch.setenv("BLLM_GEMM_NT_SCHED", {"gemm_nt_pingpong": "1", "gemm_nt_4wave": "2"}.get(impl, "0"))
+    monkeypatch.setenv("BLLM_GEMM_NT_SCHED",
+                       {"gemm_nt_pingpong": "1", "gemm_nt_4wave": "2", "gemm_nt_persistent": "3"}.get(impl, "0"))
     a_full = torch.randn(M, K + 64, device=DEV).to(dt)
     a = a_full[:, 32:32 + K]
     b_full = torch.randn(N, K + 32, device=DEV).to(dt)
@@ -585,6 +586,25 @@ def test_gemm_nt(dt, odt, M, K, N, accumulate, impl, monkeypatch):
     expect = a.float() @ b.float().t() + (c.float() if accumulate else 0)
     ops.gemm_nt_(a, b, c, accumulate)
     check_close(c, expect, odt or dt, k=3.0, name="gemm_nt")
+
+
+@pytest.mark.parametrize("odt", [None, torch.float32])
+@pytest.mark.parametrize("M,K,N", [(8192, 256, 4096), (4352, 128, 4096), (2048, 512, 33 * 256)])
+@pytest.mark.parametrize("accumulate", [False, True])
+def test_gemm_nt_persistent_multi_tile(odt, M, K, N, accumulate, monkeypatch):
+    """Persistent 4-wave schedule (BLLM_GEMM_NT_SCHED=3) with more output tiles than workgroups
+    (each workgroup walks several tiles, the K-tile stream running across tile boundaries; uneven
+    tile counts per workgroup) vs an fp32 matmul, strided A rows."""
+    monkeypatch.setenv("BLLM_GEMM_NT_IMPL", "2")
+    monkeypatch.setenv("BLLM_GEMM_NT_SCHED", "3")
+    dt = torch.bfloat16
+    a_full = torch.randn(M, K + 64, device=DEV).to(dt)
+    a = a_full[:, 32:32 + K]
+    b = torch.randn(N, K, device=DEV).to(dt)
+    c = torch.randn(M, N, device=DEV).to(odt or dt)
+    expect = a.float() @ b.float().t() + (c.float() if accumulate else 0)
+    ops.gemm_nt_(a, b, c, accumulate)
+    check_close(c, expect, odt or dt, k=3.0, name="gemm_nt persistent")
 
 
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])

@@ -44,18 +44,22 @@ def main():
     ap.add_argument("--models", default="llama,gpt2")
     ap.add_argument("--nt4_dma", default="0", help="comma list of BLLM_GEMM_NT4_DMA variants of the 4-wave arm")
     ap.add_argument("--arms", default="hipblaslt,new,pp,4w,old")
+    ap.add_argument("--only", default="", help="comma list of gemm names to run (e.g. gate_up)")
     a = ap.parse_args()
     ops.load_ext(required=True)
     dt = torch.bfloat16
     for model in a.models.split(","):
         tokens, shapes = SHAPES[model]
         for name, (k, n) in shapes.items():
+            if a.only and name not in a.only.split(","):
+                continue
             m = 8192 if name == "head_chunk" else tokens   # the fused head runs 8192-row chunks
             x = torch.rand(m, k, device="cuda", dtype=dt) * 2 - 1
             w = (torch.rand(n, k, device="cuda", dtype=dt) * 2 - 1) * 0.05
             ref = torch.mm(x, w.t())
             dvs = a.nt4_dma.split(",")
-            outs = {k_: torch.empty(m, n, device="cuda", dtype=dt) for k_ in ["new", "pp", "old"] + ["w4_" + d for d in dvs]}
+            outs = {k_: torch.empty(m, n, device="cuda", dtype=dt)
+                    for k_ in ["new", "pp", "old", "p4"] + ["w4_" + d for d in dvs]}
             y = torch.empty(m, n, device="cuda", dtype=dt)
 
             def new():
@@ -76,6 +80,11 @@ def main():
                     ops.gemm_nt_(x, w, outs["w4_" + dv])
                 return f
 
+            def p4():
+                os.environ.pop("BLLM_GEMM_NT_IMPL", None)
+                os.environ["BLLM_GEMM_NT_SCHED"] = "3"
+                ops.gemm_nt_(x, w, outs["p4"])
+
             def old():
                 os.environ["BLLM_GEMM_NT_IMPL"] = "1"
                 ops.gemm_nt_(x, w, outs["old"])
@@ -83,6 +92,7 @@ def main():
             fns = {"hipblaslt": lambda: torch.mm(x, w.t(), out=y), "gemm_nt_new": new, "gemm_nt_pp": pp,
                    "gemm_nt_old": old}
             fns.update({"gemm_nt_4w_" + d: w4(d) for d in dvs})
+            fns["gemm_nt_4p"] = p4
             want = a.arms.split(",")
             fns = {k_: f for k_, f in fns.items()
                    if k_ == "hipblaslt" and "hipblaslt" in want or k_.startswith("gemm_nt_") and k_.split("_")[2] in want}
