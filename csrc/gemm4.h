@@ -24,10 +24,18 @@ template <> struct MfA<bf16_t> {
   static __device__ __forceinline__ void run(f32x4& c, const s16x8& a, const s16x8& b) {
     asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(a), "v"(b));
   }
+  // c = 0 in place (srcC the inline constant 0, A = B = 0): resets an accumulator without
+  // letting hipcc re-home it
+  static __device__ __forceinline__ void zero(f32x4& c, const s16x8& z) {
+    asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %1, 0" : "+a"(c) : "v"(z));
+  }
 };
 template <> struct MfA<f16_t> {
   static __device__ __forceinline__ void run(f32x4& c, const s16x8& a, const s16x8& b) {
     asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, %0" : "+a"(c) : "v"(a), "v"(b));
+  }
+  static __device__ __forceinline__ void zero(f32x4& c, const s16x8& z) {
+    asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %1, 0" : "+a"(c) : "v"(z));
   }
 };
 __device__ __forceinline__ void mfma_drain() { asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory"); }

@@ -657,10 +657,10 @@ __global__ __launch_bounds__(THREADS4, 1) void gemm_nt4_k(const T* __restrict__ 
 // therefore writes straight from the accumulators (lane: 4 consecutive columns of one row ->
 // one 8-B bf16/fp16 or 16-B fp32 store per accumulator) while the next tile's first 64 KiB land
 // in LDS, instead of staging through LDS with the pipeline drained.
-template <typename T, typename OT, int DV>
+template <typename T, typename OT, int DV, bool ACC>
 __global__ __launch_bounds__(THREADS4, 1) void gemm_nt4p_k(const T* __restrict__ A, long lda,
                                                            const T* __restrict__ B, long ldb, OT* __restrict__ C,
-                                                           long ldc, int M, int N, int K, int accumulate, int vec) {
+                                                           long ldc, int M, int N, int K) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int wm = wave >> 1, wn = wave & 1;
@@ -803,55 +803,54 @@ __global__ __launch_bounds__(THREADS4, 1) void gemm_nt4p_k(const T* __restrict__
 #pragma unroll
       for (int j = 0; j < 8; ++j) asm volatile("" : "+a"(acc[i][j]));
     // epilogue straight from the accumulators: acc[i][j] = row 16i + (l & 15), columns
-    // 16j + 4(l >> 4) .. +3 of the wave's 128 x 128 block
+    // 16j + 4(l >> 4) .. +3 of the wave's 128 x 128 block (the accumulate test hoisted out of the
+    // element loops: a per-element select makes hipcc branch around every load)
     OT* cw = C + (m0 + 128 * wm + (lane & 15)) * ldc + n0 + 128 * wn + 4 * (lane >> 4);
-    if (vec) {
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          OT* o = cw + (long)(16 * i) * ldc + 16 * j;
-          float v0 = acc[i][j][0], v1 = acc[i][j][1], v2 = acc[i][j][2], v3 = acc[i][j][3];
-          if constexpr (sizeof(OT) == 2) {
-            if (accumulate) {
-              const uint2 old = *(const uint2*)o;
-              v0 += to_f(__builtin_bit_cast(OT, (short)(old.x & 0xFFFF)));
-              v1 += to_f(__builtin_bit_cast(OT, (short)(old.x >> 16)));
-              v2 += to_f(__builtin_bit_cast(OT, (short)(old.y & 0xFFFF)));
-              v3 += to_f(__builtin_bit_cast(OT, (short)(old.y >> 16)));
-            }
-            uint2 w;
-            w.x = (uint32_t)(uint16_t)__builtin_bit_cast(short, from_f<OT>(v0)) |
-                  ((uint32_t)(uint16_t)__builtin_bit_cast(short, from_f<OT>(v1)) << 16);
-            w.y = (uint32_t)(uint16_t)__builtin_bit_cast(short, from_f<OT>(v2)) |
-                  ((uint32_t)(uint16_t)__builtin_bit_cast(short, from_f<OT>(v3)) << 16);
-            *(uint2*)o = w;
-          } else {
-            f32x4 w{v0, v1, v2, v3};
-            if (accumulate) w += *(const f32x4*)o;
-            *(f32x4*)o = w;
-          }
-        }
-    } else {
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            OT* o = cw + (long)(16 * i) * ldc + 16 * j + e;
-            *o = from_f<OT>((accumulate ? to_f(*o) : 0.f) + acc[i][j][e]);
-          }
-    }
-    if (tid_n >= nblk) break;
+    auto st4 = [&](OT* o, f32x4 v) {
+      if constexpr (sizeof(OT) == 2) {
+        typedef OT o4 __attribute__((ext_vector_type(4)));
+        *(o4*)o = __builtin_convertvector(v, o4);   // v_cvt_pk_{bf16,f16}_f32 pairs, one 8-B store
+      } else {
+        *(f32x4*)o = v;
+      }
+    };
+    auto ld4 = [&](const OT* o) -> f32x4 {
+      if constexpr (sizeof(OT) == 2) {
+        const uint2 u = *(const uint2*)o;
+        return f32x4{to_f(__builtin_bit_cast(OT, (short)(u.x & 0xFFFF))), to_f(__builtin_bit_cast(OT, (short)(u.x >> 16))),
+                     to_f(__builtin_bit_cast(OT, (short)(u.y & 0xFFFF))), to_f(__builtin_bit_cast(OT, (short)(u.y >> 16)))};
+      } else {
+        return *(const f32x4*)o;
+      }
+    };
+    // (branch-free: ACC is a template parameter and the host only picks this kernel for rows
+    //  aligned to the store width, so hipcc never hoists all 256 accumulator reads above a
+    //  branch — which it does otherwise, and spills)
 #pragma unroll
     for (int i = 0; i < 8; ++i)
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        acc[i][j] = f32x4{};
-        asm volatile("" : "+a"(acc[i][j]));
+        OT* o = cw + (long)(16 * i) * ldc + 16 * j;
+        if constexpr (ACC) st4(o, acc[i][j] + ld4(o));
+        else st4(o, acc[i][j]);
       }
-    asm volatile("s_nop 7" ::: "memory");
+    if (tid_n >= nblk) break;
+    __builtin_amdgcn_sched_barrier(0);
+    {
+      // (z through an asm: the zero MFMAs read it as an operand, and a VALU write of an MFMA
+      //  operand needs wait states hipcc does not pad for an asm MFMA)
+      s16x8 z = s16x8{};
+      asm volatile("s_nop 4" : "+v"(z));
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) MfA<T>::zero(acc[i][j], z);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    // the next tile's first fragments (buffer 0, landed behind the last K-tile's RAW barrier) are
+    // read again here so that no fragment register is live across the epilogue
+#pragma unroll
+    for (int i = 0; i < 8; ++i) a0[i] = rdA(0, i, 0), b0[i] = rdB(0, i, 0);
     tid = tid_n, m0 = m0n, n0 = n0n, Ac = An, Bc = Bn;
     set_next();
   }
@@ -883,8 +882,12 @@ void launch(const void* a, long lda, const void* b, long ldb, void* c, long ldc,
   (void)attr;
   const bool wide = reinterpret_cast<uintptr_t>(c) % 16 == 0 && (ldc * (long)sizeof(OT)) % 16 == 0;
   const int sc = sched < 0 ? nt_sched() : sched;
-  if (sc == 3 && EPI == EPI_NONE) {
-    static const bool attr3 = hipFuncSetAttribute((const void*)gemm_nt4p_k<T, OT, 1>,
+  const bool vec3 = sizeof(OT) == 2 ? (reinterpret_cast<uintptr_t>(c) % 8 == 0 && (ldc * (long)sizeof(OT)) % 8 == 0)
+                                    : (reinterpret_cast<uintptr_t>(c) % 16 == 0 && (ldc * (long)sizeof(OT)) % 16 == 0);
+  if (sc == 3 && EPI == EPI_NONE && vec3) {
+    static const bool attr3 = hipFuncSetAttribute((const void*)gemm_nt4p_k<T, OT, 1, false>,
+                                                  hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES) == hipSuccess &&
+                              hipFuncSetAttribute((const void*)gemm_nt4p_k<T, OT, 1, true>,
                                                   hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES) == hipSuccess;
     (void)attr3;
     static int ncu = 0;
@@ -897,10 +900,12 @@ void launch(const void* a, long lda, const void* b, long ldb, void* c, long ldc,
     }
     const int nblk = (M / TM) * (N / TN);
     const int grid = nblk < ncu ? nblk : ncu;
-    const bool vec = sizeof(OT) == 2 ? (reinterpret_cast<uintptr_t>(c) % 8 == 0 && (ldc * (long)sizeof(OT)) % 8 == 0)
-                                     : (reinterpret_cast<uintptr_t>(c) % 16 == 0 && (ldc * (long)sizeof(OT)) % 16 == 0);
-    hipLaunchKernelGGL((gemm_nt4p_k<T, OT, 1>), dim3(grid), dim3(THREADS4), LDS_BYTES, s, (const T*)a, lda,
-                       (const T*)b, ldb, (OT*)c, ldc, M, N, K, (int)accumulate, (int)vec);
+    if (accumulate)
+      hipLaunchKernelGGL((gemm_nt4p_k<T, OT, 1, true>), dim3(grid), dim3(THREADS4), LDS_BYTES, s, (const T*)a, lda,
+                         (const T*)b, ldb, (OT*)c, ldc, M, N, K);
+    else
+      hipLaunchKernelGGL((gemm_nt4p_k<T, OT, 1, false>), dim3(grid), dim3(THREADS4), LDS_BYTES, s, (const T*)a, lda,
+                         (const T*)b, ldb, (OT*)c, ldc, M, N, K);
   } else if (sc == 2 || sc == 3) {
     const char* e = getenv("BLLM_GEMM_NT4_DMA");
     const int dv = e && *e ? atoi(e) : 0;
