@@ -657,7 +657,19 @@ __global__ __launch_bounds__(THREADS4, 1) void gemm_nt4_k(const T* __restrict__ 
 // therefore writes straight from the accumulators (lane: 4 consecutive columns of one row ->
 // one 8-B bf16/fp16 or 16-B fp32 store per accumulator) while the next tile's first 64 KiB land
 // in LDS, instead of staging through LDS with the pipeline drained.
-template <typename T, typename OT, int DV, bool ACC>
+// SV (BLLM_GEMM_NT4P_SV, A/B): where the WAR barrier, the 16 pieces and the RAW barrier sit in
+// the 128-MFMA K-tile.  0: WAR after MFMA 31, pieces every 5 MFMAs from 32, RAW at 112 (reads of
+// the next fragments one per MFMA over the last 16); 1: WAR after 23, pieces every 4 from 24,
+// RAW at 112; 2: as 1 with RAW at 120 (two reads per MFMA over the last 8); 3: as 0, RAW at 120.
+template <int SV> struct Sched4 {
+  static constexpr int WAR = (SV == 1 || SV == 2) ? 23 : 31;   // barrier after this MFMA
+  static constexpr int D0 = WAR + 1, DS = (SV == 1 || SV == 2) ? 4 : 5;   // first piece, stride
+  static constexpr int RAW = (SV >= 2) ? 120 : 112;             // before this MFMA (of 128)
+  // piece index issued before/after MFMA m (0..127), -1 if none
+  static constexpr int piece(int m) { return m >= D0 && (m - D0) % DS == 0 && (m - D0) / DS < 16 ? (m - D0) / DS : -1; }
+};
+
+template <typename T, typename OT, int DV, bool ACC, int SV>
 __global__ __launch_bounds__(THREADS4, 1) void gemm_nt4p_k(const T* __restrict__ A, long lda,
                                                            const T* __restrict__ B, long ldb, OT* __restrict__ C,
                                                            long ldc, int M, int N, int K) {
@@ -754,6 +766,7 @@ __global__ __launch_bounds__(THREADS4, 1) void gemm_nt4p_k(const T* __restrict__
 #pragma unroll
   for (int i = 0; i < 8; ++i) a0[i] = rdA(0, i, 0), b0[i] = rdB(0, i, 0);
 
+  using SC = Sched4<SV>;
   auto ktile = [&](int t, auto cur_c) {
     constexpr int cur = decltype(cur_c)::value, nxt = cur ^ 1;
 #pragma unroll
@@ -763,28 +776,32 @@ __global__ __launch_bounds__(THREADS4, 1) void gemm_nt4p_k(const T* __restrict__
       if (n == 0) a1[0] = rdA(cur, 0, 1);
       else if (n <= 8) b1[n - 1] = rdB(cur, n - 1, 1);
       else if (n < 16) a1[n - 8] = rdA(cur, n - 8, 1);
-      if (n == 31) {
+      if (n == SC::WAR) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
       }
-      if (n >= 32 && (n - 32) % 5 == 0) dma(t + 2, cur, (n - 32) / 5);
+      if (SC::piece(n) >= 0) dma(t + 2, cur, SC::piece(n));
       __builtin_amdgcn_sched_barrier(0);
     }
 #pragma unroll
     for (int n = 0; n < 64; ++n) {
       const int i = n >> 3, j = n & 7;
-      if (n >= 3 && n <= 43 && (n - 3) % 5 == 0) dma(t + 2, cur, 7 + (n - 3) / 5);
-      if (n == 48) {
+      if (SC::piece(64 + n) >= 0) dma(t + 2, cur, SC::piece(64 + n));
+      if (64 + n == SC::RAW) {
         wait_vm<16>();
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
       }
-      if (n >= 48) {
-        const int r = n - 48;
-        if (r == 0) a0[0] = rdA(nxt, 0, 0);
-        else if (r <= 8) b0[r - 1] = rdB(nxt, r - 1, 0);
-        else a0[r - 8] = rdA(nxt, r - 8, 0);
+      constexpr int NR = 128 - SC::RAW;   // MFMAs carrying the 16 reads (16 or 8)
+      if (64 + n >= SC::RAW) {
+#pragma unroll
+        for (int q = 0; q < 16 / NR; ++q) {
+          const int r = (64 + n - SC::RAW) * (16 / NR) + q;   // a0[0], b0[0..7], a0[1..7]
+          if (r == 0) a0[0] = rdA(nxt, 0, 0);
+          else if (r <= 8) b0[r - 1] = rdB(nxt, r - 1, 0);
+          else a0[r - 8] = rdA(nxt, r - 8, 0);
+        }
       }
       MfA<T>::run(acc[i][j], b1[j], a1[i]);
       __builtin_amdgcn_sched_barrier(0);
@@ -885,11 +902,6 @@ void launch(const void* a, long lda, const void* b, long ldb, void* c, long ldc,
   const bool vec3 = sizeof(OT) == 2 ? (reinterpret_cast<uintptr_t>(c) % 8 == 0 && (ldc * (long)sizeof(OT)) % 8 == 0)
                                     : (reinterpret_cast<uintptr_t>(c) % 16 == 0 && (ldc * (long)sizeof(OT)) % 16 == 0);
   if (sc == 3 && EPI == EPI_NONE && vec3) {
-    static const bool attr3 = hipFuncSetAttribute((const void*)gemm_nt4p_k<T, OT, 1, false>,
-                                                  hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES) == hipSuccess &&
-                              hipFuncSetAttribute((const void*)gemm_nt4p_k<T, OT, 1, true>,
-                                                  hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES) == hipSuccess;
-    (void)attr3;
     static int ncu = 0;
     if (!ncu) {
       int dev = 0;
@@ -900,12 +912,28 @@ void launch(const void* a, long lda, const void* b, long ldb, void* c, long ldc,
     }
     const int nblk = (M / TM) * (N / TN);
     const int grid = nblk < ncu ? nblk : ncu;
-    if (accumulate)
-      hipLaunchKernelGGL((gemm_nt4p_k<T, OT, 1, true>), dim3(grid), dim3(THREADS4), LDS_BYTES, s, (const T*)a, lda,
-                         (const T*)b, ldb, (OT*)c, ldc, M, N, K);
-    else
-      hipLaunchKernelGGL((gemm_nt4p_k<T, OT, 1, false>), dim3(grid), dim3(THREADS4), LDS_BYTES, s, (const T*)a, lda,
-                         (const T*)b, ldb, (OT*)c, ldc, M, N, K);
+    const char* ev = getenv("BLLM_GEMM_NT4P_SV");
+    const int sv = ev && *ev ? atoi(ev) : 0;
+#define BLLM_NT4P(ACCv, SVv)                                                                                            \
+  do {                                                                                                                  \
+    static const bool at_ = hipFuncSetAttribute((const void*)gemm_nt4p_k<T, OT, 1, ACCv, SVv>,                          \
+                                                hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES) == hipSuccess; \
+    (void)at_;                                                                                                          \
+    hipLaunchKernelGGL((gemm_nt4p_k<T, OT, 1, ACCv, SVv>), dim3(grid), dim3(THREADS4), LDS_BYTES, s, (const T*)a, lda, \
+                       (const T*)b, ldb, (OT*)c, ldc, M, N, K);                                                        \
+  } while (0)
+    if (accumulate) {
+      BLLM_NT4P(true, 0);
+    } else if (sv == 1) {
+      BLLM_NT4P(false, 1);
+    } else if (sv == 2) {
+      BLLM_NT4P(false, 2);
+    } else if (sv == 3) {
+      BLLM_NT4P(false, 3);
+    } else {
+      BLLM_NT4P(false, 0);
+    }
+#undef BLLM_NT4P
   } else if (sc == 2 || sc == 3) {
     const char* e = getenv("BLLM_GEMM_NT4_DMA");
     const int dv = e && *e ? atoi(e) : 0;

@@ -605,6 +605,207 @@ void launch4(const void* a, long lda, const void* b, long ldb, void* c, long ldc
                      (OT*)c, ldc, c_split, M, N, K, (int)accumulate, (int)wide);
 }
 
+// ---- Variant 5: variant 4 made persistent (as csrc/gemm_nt.hip's BLLM_GEMM_NT_SCHED=3): one
+// workgroup per CU walks the work items (output tile x split-K slice) w, w + G, ..., the K-tile
+// stream runs across work items (the last two K-tiles of an item prefetch the next item's first
+// two), and the epilogue stores straight from the accumulators (lane: 4 consecutive columns of a
+// row), while the next item's first K-tile is already landing.  ACC is a template parameter and
+// rows must be aligned to the store width (host), so the epilogue is branch-free.
+template <typename T, typename OT, bool ACC>
+__global__ __launch_bounds__(g4::THREADS4, 1) void wgrad4p_k(const T* __restrict__ A, long lda,
+                                                             const T* __restrict__ B, long ldb, OT* __restrict__ C,
+                                                             long ldc, long c_split, int M, int N, int K, int S) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int nbm = M / BM, nbn = N / BN, nblk = nbm * nbn, nwork = nblk * S, G = gridDim.x;
+  const int q8 = nblk >> 3, r8 = nblk & 7, per_group = GROUP_M * nbn, nch = K / KCH;
+  // work item w: split sp = w / nblk (all tiles of a split, then the next), tile = w % nblk
+  struct Item { long m0, n0; int sp, c_lo, nt; };
+  auto item = [&](int w) {
+    Item it;
+    it.sp = w / nblk;
+    const int tid = w - it.sp * nblk, xcd = tid & 7;
+    const int wid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (tid >> 3);
+    const int grp = wid / per_group, first_m = grp * GROUP_M;
+    const int gm = nbm - first_m < GROUP_M ? nbm - first_m : GROUP_M;
+    const int in_g = wid - grp * per_group;
+    it.m0 = (long)(first_m + in_g % gm) * BM;
+    it.n0 = (long)(in_g / gm) * BN;
+    it.c_lo = (int)((long)nch * it.sp / S);
+    it.nt = ((int)((long)nch * (it.sp + 1) / S) - it.c_lo) * (KCH / 64);
+    return it;
+  };
+
+  uint32_t voA[8], voB[8];
+#pragma unroll
+  for (int p = 0; p < 8; ++p) {
+    const int kr = 16 * wave + 2 * p + (lane >> 5), c = (lane & 31) ^ swz(kr & 31);
+    voA[p] = (uint32_t)((kr * lda + 8 * c) * (long)sizeof(T));
+    voB[p] = (uint32_t)((kr * ldb + 8 * c) * (long)sizeof(T));
+  }
+  const uint32_t lds0 = lds_u32(smem);
+  int w = blockIdx.x;
+  Item cur = item(w);
+  const T* Ac = A + (long)cur.c_lo * KCH * lda + cur.m0;
+  const T* Bc = B + (long)cur.c_lo * KCH * ldb + cur.n0;
+  int w_n = w + G;
+  Item nx = cur;
+  const T* An = Ac;
+  const T* Bn = Bc;
+  auto set_next = [&]() {
+    w_n = w + G;
+    if (w_n < nwork) {
+      nx = item(w_n);
+      An = A + (long)nx.c_lo * KCH * lda + nx.m0;
+      Bn = B + (long)nx.c_lo * KCH * ldb + nx.n0;
+    } else {
+      An = Ac, Bn = Bc;
+    }
+  };
+  set_next();
+  auto dma = [&](int t, int buf, int k) {
+    const int p = k & 7, kr = 16 * wave + 2 * p;
+    const uint32_t d = lds0 + (k >= 8 ? B_BASE : 0) + (2 * buf + (kr >> 5)) * SLOTB + (kr & 31) * ROWB;
+    const bool nxt = t >= cur.nt;
+    const int tt = !nxt ? t : (w_n < nwork ? t - cur.nt : cur.nt - 1);
+    const T* base = k < 8 ? (nxt ? An : Ac) + (long)tt * 64 * lda : (nxt ? Bn : Bc) + (long)tt * 64 * ldb;
+    g4::bdma16<1>(g4::make_rsrc(base), k < 8 ? voA[p] : voB[p], 0u, d);
+  };
+
+  const int g = lane >> 4, qq = (lane & 15) >> 2, p4 = lane & 3;
+  const int f = 2 * (qq | ((g & 1) << 2));
+  const int rowb = (8 * g + qq) * ROWB + (p4 & 1) * 8 + (p4 >> 1) * 16;
+  const char* pa = smem + rowb + (wm * 16) * 16;
+  const char* pb = smem + B_BASE + rowb + (wn * 16) * 16;
+  auto rdA = [&](int sl, int i) -> g4::s16x8 { return frag(pa + sl * SLOTB + ((2 * i) ^ f) * 16); };
+  auto rdB = [&](int sl, int j) -> g4::s16x8 { return frag(pb + sl * SLOTB + ((2 * j) ^ f) * 16); };
+
+  g4::f32x4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = g4::f32x4{};
+  g4::s16x8 a0[8], b0[8], a1[8], b1[8];
+
+#pragma unroll
+  for (int k = 0; k < 16; ++k) dma(0, 0, k);
+#pragma unroll
+  for (int k = 0; k < 16; ++k) dma(1, 1, k);
+  vm_wait<16>();
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+#pragma unroll
+  for (int i = 0; i < 8; ++i) a0[i] = rdA(0, i), b0[i] = rdB(0, i);
+
+  auto tile = [&](int t, auto cur_c) {
+    constexpr int cb = decltype(cur_c)::value, nb = cb ^ 1;
+#pragma unroll
+    for (int n = 0; n < 64; ++n) {
+      const int i = n >> 3, j = n & 7;
+      g4::MfA<T>::run(acc[i][j], b0[j], a0[i]);
+      if (n == 0) a1[0] = rdA(2 * cb + 1, 0);
+      else if (n <= 8) b1[n - 1] = rdB(2 * cb + 1, n - 1);
+      else if (n < 16) a1[n - 8] = rdA(2 * cb + 1, n - 8);
+      if (n == 31) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+      }
+      if (n >= 32 && (n - 32) % 5 == 0) dma(t + 2, cb, (n - 32) / 5);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int n = 0; n < 64; ++n) {
+      const int i = n >> 3, j = n & 7;
+      if (n >= 3 && n <= 43 && (n - 3) % 5 == 0) dma(t + 2, cb, 7 + (n - 3) / 5);
+      if (n == 48) {
+        vm_wait<16>();
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+      }
+      if (n >= 48) {
+        const int r = n - 48;
+        if (r == 0) a0[0] = rdA(2 * nb, 0);
+        else if (r <= 8) b0[r - 1] = rdB(2 * nb, r - 1);
+        else a0[r - 8] = rdA(2 * nb, r - 8);
+      }
+      g4::MfA<T>::run(acc[i][j], b1[j], a1[i]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  for (;;) {
+    for (int t = 0; t < cur.nt; t += 2) {
+      tile(t, I0{});
+      tile(t + 1, I1{});
+    }
+    g4::mfma_drain();
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) asm volatile("" : "+a"(acc[i][j]));
+    OT* cw = C + cur.sp * c_split + (cur.m0 + 128 * wm + (lane & 15)) * ldc + cur.n0 + 128 * wn + 4 * (lane >> 4);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        OT* o = cw + (long)(16 * i) * ldc + 16 * j;
+        typedef OT o4 __attribute__((ext_vector_type(4)));
+        g4::f32x4 v = acc[i][j];
+        if constexpr (ACC) v += __builtin_convertvector(*(const o4*)o, g4::f32x4);
+        *(o4*)o = __builtin_convertvector(v, o4);
+      }
+    if (w_n >= nwork) break;
+    __builtin_amdgcn_sched_barrier(0);
+    {
+      g4::s16x8 z = g4::s16x8{};
+      asm volatile("s_nop 4" : "+v"(z));
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) g4::MfA<T>::zero(acc[i][j], z);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) a0[i] = rdA(0, i), b0[i] = rdB(0, i);
+    w = w_n, cur = nx, Ac = An, Bc = Bn;
+    set_next();
+  }
+  vm_wait<0>();
+}
+
+template <typename T, typename OT>
+bool launch4p(const void* a, long lda, const void* b, long ldb, void* c, long ldc, long c_split, int M, int N, int K,
+              int S, bool accumulate, hipStream_t s) {
+  const long al = sizeof(OT) == 2 ? 8 : 16;
+  if (reinterpret_cast<uintptr_t>(c) % al || (ldc * (long)sizeof(OT)) % al || (c_split * (long)sizeof(OT)) % al)
+    return false;
+  static int ncu = 0;
+  if (!ncu) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    hipDeviceProp_t prop;
+    ncu = hipGetDeviceProperties(&prop, dev) == hipSuccess ? prop.multiProcessorCount : 256;
+    ncu = ncu < 8 ? 8 : ncu / 8 * 8;
+  }
+  const int nwork = (M / BM) * (N / BN) * S;
+  const int grid = nwork < ncu ? nwork : ncu;
+#define BLLM_W4P(ACCv)                                                                                                 \
+  do {                                                                                                                 \
+    static const bool at_ = hipFuncSetAttribute((const void*)wgrad4p_k<T, OT, ACCv>,                                   \
+                                                hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES) == hipSuccess; \
+    (void)at_;                                                                                                         \
+    hipLaunchKernelGGL((wgrad4p_k<T, OT, ACCv>), dim3(grid), dim3(g4::THREADS4), LDS_BYTES, s, (const T*)a, lda,      \
+                       (const T*)b, ldb, (OT*)c, ldc, c_split, M, N, K, S);                                           \
+  } while (0)
+  if (accumulate) BLLM_W4P(true);
+  else BLLM_W4P(false);
+#undef BLLM_W4P
+  return true;
+}
+
 template <typename T, typename OT, int VAR, bool AK = false, bool BKC = false>
 void launch_v(const void* a, long lda, const void* b, long ldb, void* c, long ldc, long c_split, int M, int N, int K,
               int S, bool accumulate, hipStream_t s) {
@@ -633,6 +834,10 @@ template <typename T, typename OT>
 void launch(const void* a, long lda, const void* b, long ldb, void* c, long ldc, long c_split, int M, int N, int K,
             int S, bool accumulate, hipStream_t s) {
   switch (variant(S)) {
+    case 5:
+      if (launch4p<T, OT>(a, lda, b, ldb, c, ldc, c_split, M, N, K, S, accumulate, s)) break;
+      launch4<T, OT, 1>(a, lda, b, ldb, c, ldc, c_split, M, N, K, S, accumulate, s);
+      break;
     case 4: {
       const char* e = getenv("BLLM_WGRAD4_DMA");
       if (e && *e == '0') launch4<T, OT, 0>(a, lda, b, ldb, c, ldc, c_split, M, N, K, S, accumulate, s);

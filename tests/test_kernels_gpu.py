@@ -522,7 +522,7 @@ def test_split_k_weight_grad(gdt, accumulate):
 @pytest.mark.parametrize("odt", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("K,M,N,S", [(128, 256, 256, 1), (384, 512, 768, 1), (2048, 768, 512, 3), (1024, 256, 1024, 2)])
 @pytest.mark.parametrize("accumulate", [False, True])
-@pytest.mark.parametrize("variant", ["0", "1", "2", "3", "4"])
+@pytest.mark.parametrize("variant", ["0", "1", "2", "3", "4", "5"])
 def test_wgrad_gemm(dt, odt, K, M, N, S, accumulate, variant, monkeypatch):
     """Token-major MFMA dW kernel c (+)= a^T b (strided a, split-K) vs an fp32 matmul, every
     schedule variant (BLLM_WGRAD_VARIANT is read per launch)."""
@@ -535,6 +535,23 @@ def test_wgrad_gemm(dt, odt, K, M, N, S, accumulate, variant, monkeypatch):
     expect = a.float().t() @ b.float() + (c.float() if accumulate else 0)
     ops.wgrad_gemm_(a, b, c, accumulate, S)
     check_close(c, expect, odt, k=3.0, name="wgrad")
+
+
+@pytest.mark.parametrize("odt", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("K,M,N,S", [(256, 4096, 4096, 2), (640, 4352, 2048, 1), (1024, 2048, 4096, 4)])
+@pytest.mark.parametrize("accumulate", [False, True])
+def test_wgrad_gemm_persistent_multi_item(odt, K, M, N, S, accumulate, monkeypatch):
+    """Persistent dW kernel (BLLM_WGRAD_VARIANT=5) with more work items (tile x split) than
+    workgroups, uneven items per workgroup, the K-tile stream crossing items of different splits."""
+    monkeypatch.setenv("BLLM_WGRAD_VARIANT", "5")
+    a_full = torch.randn(K, M + 64, device=DEV).to(torch.bfloat16)
+    a = a_full[:, 32:32 + M]
+    b = torch.randn(K, N, device=DEV).to(torch.bfloat16)
+    c = torch.randn(M, N, device=DEV).to(odt)
+    assert ops.wgrad_gemm_ok(a, b, c)
+    expect = a.float().t() @ b.float() + (c.float() if accumulate else 0)
+    ops.wgrad_gemm_(a, b, c, accumulate, S)
+    check_close(c, expect, odt, k=3.0, name="wgrad persistent")
 
 
 def test_wgrad_gemm_in_weight_grad_path():

@@ -45,6 +45,7 @@ def main():
     ap.add_argument("--nt4_dma", default="0", help="comma list of BLLM_GEMM_NT4_DMA variants of the 4-wave arm")
     ap.add_argument("--arms", default="hipblaslt,new,pp,4w,old")
     ap.add_argument("--only", default="", help="comma list of gemm names to run (e.g. gate_up)")
+    ap.add_argument("--nt4p_sv", default="0", help="comma list of BLLM_GEMM_NT4P_SV variants of the persistent arm")
     a = ap.parse_args()
     ops.load_ext(required=True)
     dt = torch.bfloat16
@@ -58,8 +59,9 @@ def main():
             w = (torch.rand(n, k, device="cuda", dtype=dt) * 2 - 1) * 0.05
             ref = torch.mm(x, w.t())
             dvs = a.nt4_dma.split(",")
+            svs = a.nt4p_sv.split(",")
             outs = {k_: torch.empty(m, n, device="cuda", dtype=dt)
-                    for k_ in ["new", "pp", "old", "p4"] + ["w4_" + d for d in dvs]}
+                    for k_ in ["new", "pp", "old"] + ["w4_" + d for d in dvs] + ["p4_" + v for v in svs]}
             y = torch.empty(m, n, device="cuda", dtype=dt)
 
             def new():
@@ -80,10 +82,13 @@ def main():
                     ops.gemm_nt_(x, w, outs["w4_" + dv])
                 return f
 
-            def p4():
-                os.environ.pop("BLLM_GEMM_NT_IMPL", None)
-                os.environ["BLLM_GEMM_NT_SCHED"] = "3"
-                ops.gemm_nt_(x, w, outs["p4"])
+            def p4(sv):
+                def f():
+                    os.environ.pop("BLLM_GEMM_NT_IMPL", None)
+                    os.environ["BLLM_GEMM_NT_SCHED"] = "3"
+                    os.environ["BLLM_GEMM_NT4P_SV"] = sv
+                    ops.gemm_nt_(x, w, outs["p4_" + sv])
+                return f
 
             def old():
                 os.environ["BLLM_GEMM_NT_IMPL"] = "1"
@@ -92,7 +97,7 @@ def main():
             fns = {"hipblaslt": lambda: torch.mm(x, w.t(), out=y), "gemm_nt_new": new, "gemm_nt_pp": pp,
                    "gemm_nt_old": old}
             fns.update({"gemm_nt_4w_" + d: w4(d) for d in dvs})
-            fns["gemm_nt_4p"] = p4
+            fns.update({"gemm_nt_4p_" + v: p4(v) for v in svs})
             want = a.arms.split(",")
             fns = {k_: f for k_, f in fns.items()
                    if k_ == "hipblaslt" and "hipblaslt" in want or k_.startswith("gemm_nt_") and k_.split("_")[2] in want}
