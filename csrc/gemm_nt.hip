@@ -669,10 +669,16 @@ template <int SV> struct Sched4 {
   static constexpr int piece(int m) { return m >= D0 && (m - D0) % DS == 0 && (m - D0) / DS < 16 ? (m - D0) / DS : -1; }
 };
 
-template <typename T, typename OT, int DV, bool ACC, int SV>
+// EPI_SWIGLU (B = [W_gate; W_up], N = 2F): tile tn covers gate/up column pairs 128tn .. +127;
+// the B image interleaves them in 16-row blocks (image rows 128w' + 32b + [0, 16) gate pairs
+// 64w' + 16b + [0, 16), the next 16 rows the matching up rows), so a lane's acc[i][2k] and
+// acc[i][2k+1] hold 4 gate and the same 4 up columns of one row: the epilogue stores both halves
+// of gu and act = silu(g) * u (g, u rounded to T first, as the separate swiglu_fwd kernel).
+template <typename T, typename OT, int DV, bool ACC, int SV, int EPI = EPI_NONE>
 __global__ __launch_bounds__(THREADS4, 1) void gemm_nt4p_k(const T* __restrict__ A, long lda,
                                                            const T* __restrict__ B, long ldb, OT* __restrict__ C,
-                                                           long ldc, int M, int N, int K) {
+                                                           long ldc, int M, int N, int K, OT* __restrict__ act = nullptr,
+                                                           int F = 0) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int wm = wave >> 1, wn = wave & 1;
@@ -695,16 +701,25 @@ __global__ __launch_bounds__(THREADS4, 1) void gemm_nt4p_k(const T* __restrict__
   for (int p = 0; p < 8; ++p) {
     const uint32_t r = 8u * p + (uint32_t)(lane >> 3), c = 16u * ((lane & 7) ^ ((r >> 1) & 7));
     voA[p] = r * ldab + c;
-    voB[p] = r * ldbb + c;
+    if constexpr (EPI == EPI_SWIGLU) {   // image row R -> gate / up row of the tile (see above)
+      const uint32_t R = 64u * wave + r, lb = (R & 127) >> 4;
+      const uint32_t src = (R >> 7) * 64 + (lb >> 1) * 16 + (R & 15) + ((lb & 1) ? (uint32_t)F : 0u);
+      voB[p] = src * ldbb + c;
+    } else {
+      voB[p] = r * ldbb + c;
+    }
   }
   const int nt = K / TK;  // even, >= 2
   constexpr uint32_t TKB = TK * (uint32_t)sizeof(T);
+  // B rows a wave stages for the tile at column n0: its 64 contiguous rows, or (SwiGLU) the
+  // tile's gate/up pairs n0 / 2 .. (voB carries the row map)
+  auto brow = [&](long n0_) -> long { return EPI == EPI_SWIGLU ? n0_ / 2 : n0_ + 64 * wave; };
 
   int tid = blockIdx.x;
   long m0, n0;
   coords(tid, m0, n0);
   const T* Ac = A + (m0 + 64 * wave) * lda;   // this wave's staged rows of the current tile
-  const T* Bc = B + (n0 + 64 * wave) * ldb;
+  const T* Bc = B + brow(n0) * ldb;
   const T* An = Ac;                           // ... and of the next tile (= current when none)
   const T* Bn = Bc;
   int tid_n = tid + G;
@@ -714,7 +729,7 @@ __global__ __launch_bounds__(THREADS4, 1) void gemm_nt4p_k(const T* __restrict__
     if (tid_n < nblk) {
       coords(tid_n, m0n, n0n);
       An = A + (m0n + 64 * wave) * lda;
-      Bn = B + (n0n + 64 * wave) * ldb;
+      Bn = B + brow(n0n) * ldb;
     } else {
       An = Ac, Bn = Bc;
     }
@@ -843,14 +858,38 @@ __global__ __launch_bounds__(THREADS4, 1) void gemm_nt4p_k(const T* __restrict__
     // (branch-free: ACC is a template parameter and the host only picks this kernel for rows
     //  aligned to the store width, so hipcc never hoists all 256 accumulator reads above a
     //  branch — which it does otherwise, and spills)
+    if constexpr (EPI == EPI_SWIGLU) {
+      typedef OT o4 __attribute__((ext_vector_type(4)));
+      const long g0 = n0 / 2;
+      const long r0 = m0 + 128 * wm + (lane & 15);
+      const int pc = 64 * wn + 4 * (lane >> 4);
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
+      for (int i = 0; i < 8; ++i)
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        OT* o = cw + (long)(16 * i) * ldc + 16 * j;
-        if constexpr (ACC) st4(o, acc[i][j] + ld4(o));
-        else st4(o, acc[i][j]);
-      }
+        for (int k = 0; k < 4; ++k) {
+          const long r = r0 + 16 * i;
+          const long col = g0 + pc + 16 * k;
+          const o4 gb = __builtin_convertvector(acc[i][2 * k], o4), ub = __builtin_convertvector(acc[i][2 * k + 1], o4);
+          *(o4*)(C + r * ldc + col) = gb;
+          *(o4*)(C + r * ldc + F + col) = ub;
+          o4 w;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float a = to_f(gb[e]), b = to_f(ub[e]);
+            w[e] = from_f<OT>(a / (1.f + __expf(-a)) * b);
+          }
+          *(o4*)(act + r * (long)F + col) = w;
+        }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          OT* o = cw + (long)(16 * i) * ldc + 16 * j;
+          if constexpr (ACC) st4(o, acc[i][j] + ld4(o));
+          else st4(o, acc[i][j]);
+        }
+    }
     if (tid_n >= nblk) break;
     __builtin_amdgcn_sched_barrier(0);
     {
@@ -881,6 +920,26 @@ inline int nt_sched() {
   return e ? atoi(e) : 0;
 }
 
+template <typename T, typename OT>
+void launch_swiglu4p(const void* a, long lda, const void* b, long ldb, void* c, long ldc, int M, int N, int K,
+                     void* act, int F, hipStream_t s) {
+    static int ncu_s = 0;
+  if (!ncu_s) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    hipDeviceProp_t prop;
+    ncu_s = hipGetDeviceProperties(&prop, dev) == hipSuccess ? prop.multiProcessorCount : 256;
+    ncu_s = ncu_s < 8 ? 8 : ncu_s / 8 * 8;
+  }
+  static const bool at_s = hipFuncSetAttribute((const void*)gemm_nt4p_k<T, OT, 1, false, 0, EPI_SWIGLU>,
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES) == hipSuccess;
+  (void)at_s;
+  const int nblk = (M / TM) * (N / TN);
+  const int grid = nblk < ncu_s ? nblk : ncu_s;
+  hipLaunchKernelGGL((gemm_nt4p_k<T, OT, 1, false, 0, EPI_SWIGLU>), dim3(grid), dim3(THREADS4), LDS_BYTES, s,
+                     (const T*)a, lda, (const T*)b, ldb, (OT*)c, ldc, M, N, K, (OT*)act, F);
+}
+
 template <typename T, typename OT, int EPI = EPI_NONE>
 void launch(const void* a, long lda, const void* b, long ldb, void* c, long ldc, int M, int N, int K, bool accumulate,
             hipStream_t s, void* act = nullptr, int F = 0, int sched = -1) {
@@ -901,6 +960,12 @@ void launch(const void* a, long lda, const void* b, long ldb, void* c, long ldc,
   const int sc = sched < 0 ? nt_sched() : sched;
   const bool vec3 = sizeof(OT) == 2 ? (reinterpret_cast<uintptr_t>(c) % 8 == 0 && (ldc * (long)sizeof(OT)) % 8 == 0)
                                     : (reinterpret_cast<uintptr_t>(c) % 16 == 0 && (ldc * (long)sizeof(OT)) % 16 == 0);
+  if constexpr (EPI == EPI_SWIGLU && sizeof(OT) == 2) {
+    if (sc == 3 && vec3 && F % 4 == 0) {
+      launch_swiglu4p<T, OT>(a, lda, b, ldb, c, ldc, M, N, K, act, F, s);
+      return;
+    }
+  }
   if (sc == 3 && EPI == EPI_NONE && vec3) {
     static int ncu = 0;
     if (!ncu) {

@@ -701,8 +701,8 @@ def test_linear_residual_hipblaslt(dt, N, K, O):
 
 
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
-@pytest.mark.parametrize("M,K,F", [(256, 128, 128), (512, 512, 768), (1024, 4096, 1792)])
-@pytest.mark.parametrize("sched", ["0", "1", "2"])
+@pytest.mark.parametrize("M,K,F", [(256, 128, 128), (512, 512, 768), (1024, 4096, 1792), (4096, 256, 4096)])
+@pytest.mark.parametrize("sched", ["0", "1", "2", "3"])
 def test_gemm_nt_swiglu(dt, M, K, F, sched, monkeypatch):
     """Gate/up GEMM with the SwiGLU forward in the epilogue (K10): gu against the fp32 oracle, act
     bitwise equal to the separate swiglu_fwd kernel applied to that gu; both schedules."""

@@ -46,9 +46,13 @@ def main():
     ap.add_argument("--arms", default="hipblaslt,new,pp,4w,old")
     ap.add_argument("--only", default="", help="comma list of gemm names to run (e.g. gate_up)")
     ap.add_argument("--nt4p_sv", default="0", help="comma list of BLLM_GEMM_NT4P_SV variants of the persistent arm")
+    ap.add_argument("--swiglu", action="store_true",
+                    help="gate/up + SwiGLU: hipBLASLt GEMM + separate swiglu_fwd vs the fused kernel (sched 2, 3)")
     a = ap.parse_args()
     ops.load_ext(required=True)
     dt = torch.bfloat16
+    if a.swiglu:
+        return bench_swiglu(a)
     for model in a.models.split(","):
         tokens, shapes = SHAPES[model]
         for name, (k, n) in shapes.items():
@@ -118,6 +122,39 @@ def main():
             print(json.dumps(r), flush=True)
             del x, w, ref, outs, y
             torch.cuda.empty_cache()
+
+
+def bench_swiglu(a):
+    dt = torch.bfloat16
+    for model, (tokens, K, F) in {"llama": (40960, 4096, 14336), "llama32_1b": (40960, 2048, 8192)}.items():
+        x = torch.rand(tokens, K, device="cuda", dtype=dt) * 2 - 1
+        w = (torch.rand(2 * F, K, device="cuda", dtype=dt) * 2 - 1) * 0.05
+        gu = torch.empty(tokens, 2 * F, device="cuda", dtype=dt)
+
+        def sep():
+            torch.mm(x, w.t(), out=gu)
+            return ops.swiglu_fwd(gu)
+
+        def fused(sc):
+            def f():
+                os.environ["BLLM_GEMM_NT_SCHED"] = sc
+                return ops.gemm_nt_swiglu(x, w)
+            return f
+        fns = {"hipblaslt+swiglu_fwd": sep, "fused_sched2": fused("2"), "fused_sched3": fused("3")}
+        times = {k: [] for k in fns}
+        for _ in range(a.rounds):
+            for k, fn in fns.items():
+                times[k].append(timeit(fn, a.iters))
+        ref = sep()
+        r = {"model": model, "M_K_F": [tokens, K, F]}
+        for k, ts in times.items():
+            r[k + "_us"] = round(sorted(ts)[len(ts) // 2] * 1e3, 1)
+        for k in ("fused_sched2", "fused_sched3"):
+            _, act = fns[k]()
+            r["act_equal_" + k] = bool(torch.equal(act, ref))
+        print(json.dumps(r), flush=True)
+        del x, w, gu
+        torch.cuda.empty_cache()
 
 
 if __name__ == "__main__":
