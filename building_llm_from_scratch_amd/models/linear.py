@@ -210,8 +210,10 @@ def _input_grad(dy: torch.Tensor, W: torch.Tensor, dx_acc: Optional[torch.Tensor
 
 # tests set this to drive the grouped LoRA path through the CPU oracles of ops.reference
 FORCE_GROUPED_LORA = False
-# gate/up GEMM + SwiGLU epilogue (FusedLinear.forward_swiglu)
+# gate/up GEMM + SwiGLU epilogue (FusedLinear.forward_swiglu) and QKV GEMM + RoPE epilogue
+# (FusedLinear.forward_rope), both on csrc/gemm_nt.hip's persistent 4-wave kernel
 FUSED_SWIGLU = os.environ.get("BLLM_FUSED_SWIGLU", "0") != "0"
+FUSED_ROPE = os.environ.get("BLLM_FUSED_ROPE", "0") != "0"
 
 
 class FusedLinear:
@@ -352,6 +354,17 @@ class FusedLinear:
         if not ops.gemm_nt_swiglu_ok(x, W):
             return None
         return ops.gemm_nt_swiglu(x, W)
+
+    def forward_rope(self, x: torch.Tensor, cos, sin, T: int, H: int, G: int, hd: int):
+        """QKV projection with RoPE applied to the q and k heads in the GEMM epilogue (K4; no bias,
+        no LoRA): returns the rotated qkv, or None when the fused kernel does not apply (head dim
+        128 only; BLLM_FUSED_ROPE=0 turns it off) and the caller runs the GEMM + ``rope_``."""
+        if self.has_lora or self.b_params is not None or not FUSED_ROPE:
+            return None
+        W = self.W()
+        if not ops.gemm_nt_rope_ok(x, W, hd) or W.shape[0] != (H + 2 * G) * hd:
+            return None
+        return ops.gemm_nt_rope(x, W, cos, sin, T, H, G, hd)
 
     def lora_state(self, x: torch.Tensor):
         """Only the LoRA intermediate ``x A`` that ``backward`` needs (what ``forward`` would

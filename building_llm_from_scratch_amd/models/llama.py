@@ -154,8 +154,12 @@ class LlamaBlockCompute(UnitCompute):
         cos, sin = rc.rope
         x2d = x.reshape(N, d)
         h1, r1 = ops.rmsnorm_fwd(x2d, u.data(b.norm1.weight), eps)
-        qkv, xa_qkv = self.qkv.forward(h1)
-        ops.rope_(qkv, cos, sin, T, H, G, hd)
+        qkv = self.qkv.forward_rope(h1, cos, sin, T, H, G, hd)   # K4: RoPE in the GEMM epilogue
+        if qkv is not None:
+            xa_qkv = None
+        else:
+            qkv, xa_qkv = self.qkv.forward(h1)
+            ops.rope_(qkv, cos, sin, T, H, G, hd)
         o, lse = ops.flash_attn_fwd(qkv, B, T, H, G, hd, causal=True)
         x2, xa_o = self.o.forward(o, residual=x2d)
         h2, r2 = ops.rmsnorm_fwd(x2, u.data(b.norm2.weight), eps)

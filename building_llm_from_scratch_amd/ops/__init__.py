@@ -380,6 +380,24 @@ def gemm_nt_swiglu_ok(a: torch.Tensor, w: torch.Tensor) -> bool:
             and 256 * a.stride(0) * 2 < 2 ** 31 and 256 * w.stride(0) * 2 < 2 ** 31)
 
 
+def gemm_nt_rope_ok(a: torch.Tensor, w: torch.Tensor, hd: int) -> bool:
+    """Shapes the QKV + RoPE-epilogue kernel (csrc/gemm_nt.hip, persistent 4-wave) takes: head dim
+    128, bf16/fp16, M, N multiples of 256, K of 128, 16-B aligned unit-stride rows."""
+    return hd == 128 and gemm_nt_ok(a, w)
+
+
+def gemm_nt_rope(a, w, cos, sin, T: int, H: int, G: int, hd: int):
+    """qkv = a . w^T ([N, (H + 2G) hd]) with RoPE applied to its q and k heads (the first
+    (H + G) hd columns) at position row % T — the QKV projection with the rotation in the GEMM
+    epilogue (K4); on CPU the matmul + ``rope_`` oracle (same rounding: the GEMM output first)."""
+    if _hip(a):
+        qkv = torch.empty(a.shape[0], w.shape[0], dtype=a.dtype, device=a.device)
+        _k().gemm_nt_rope_(a, w, qkv, cos, sin, int(T), int((H + G) * hd), int(hd))
+        return qkv
+    qkv = (a.float() @ w.float().t()).to(a.dtype)
+    return ref.rope_(qkv, cos, sin, T, H, G, hd)
+
+
 def gemm_nt_swiglu(a, w):
     """(gu, act) = (a . w^T, silu(gu[:, :F]) * gu[:, F:]) for w = [W_gate; W_up] — the gate/up
     projection with the SwiGLU forward in its epilogue (csrc/gemm_nt.hip, GPU); on CPU the

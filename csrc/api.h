@@ -175,6 +175,11 @@ void gemm_nt2(DType dt, DType odt, const void* a, long lda, const void* b, long 
 // gate/up projection with the SwiGLU forward in the epilogue: gu[M, 2F] = a . [Wg; Wu]^T and
 // act[M, F] = silu(gu[:, :F]) * gu[:, F:] (bitwise the separate swiglu_fwd)
 bool gemm_nt_swiglu_supported(int M, int F, int K, long lda, long ldb, long ldgu);
+// qkv [M, N] = a [M, K] . w [N, K]^T with RoPE applied to columns < nrot (head dim 128) at
+// position row % Tq in the epilogue of the persistent 4-wave kernel (csrc/gemm_nt.hip)
+bool gemm_nt_rope_supported(int M, int N, int K, long lda, long ldb, long ldc, int hd);
+void gemm_nt_rope(DType dt, const void* a, long lda, const void* w, long ldw, void* c, long ldc, int M, int N, int K,
+                  const float* cosT, const float* sinT, int Tq, int nrot, hipStream_t s);
 void gemm_nt_swiglu(DType dt, const void* a, long lda, const void* w, long ldw, void* gu, long ldgu, void* act, int M,
                     int F, int K, hipStream_t s);
 

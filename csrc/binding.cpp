@@ -399,6 +399,31 @@ void gemm_nt_swiglu_(const Tensor& a, const Tensor& w, Tensor& gu, Tensor& act) 
                        act.data_ptr(), (int)M, (int)F, (int)K, stream());
 }
 
+// QKV projection with RoPE in the epilogue (K4, csrc/gemm_nt.hip): qkv[M, N] = a . w^T, columns
+// below nrot rotated at position row % T (tables fp32 [>= T, 64], head dim 128)
+void gemm_nt_rope_(const Tensor& a, const Tensor& w, Tensor& qkv, const Tensor& cos, const Tensor& sin, int64_t T,
+                   int64_t nrot, int64_t hd) {
+  TORCH_CHECK(a.is_cuda() && w.is_cuda() && qkv.is_cuda() && cos.is_cuda() && sin.is_cuda(), "gemm_nt_rope: GPU tensors");
+  c10::DeviceGuard g(a.device());
+  TORCH_CHECK(a.dim() == 2 && w.dim() == 2 && qkv.dim() == 2, "gemm_nt_rope: 2-D operands");
+  const int64_t M = a.size(0), K = a.size(1), N = w.size(0);
+  TORCH_CHECK(w.size(1) == K && qkv.size(0) == M && qkv.size(1) == N, "gemm_nt_rope: shapes");
+  TORCH_CHECK(a.scalar_type() == w.scalar_type() && qkv.scalar_type() == a.scalar_type() &&
+                  (a.scalar_type() == at::kBFloat16 || a.scalar_type() == at::kHalf), "gemm_nt_rope: bf16/fp16");
+  TORCH_CHECK(cos.scalar_type() == at::kFloat && sin.scalar_type() == at::kFloat && cos.is_contiguous() &&
+                  sin.is_contiguous() && cos.size(1) == hd / 2 && sin.sizes() == cos.sizes() && cos.size(0) >= T,
+              "gemm_nt_rope: fp32 [>= T, hd/2] tables");
+  TORCH_CHECK(a.stride(1) == 1 && w.stride(1) == 1 && qkv.stride(1) == 1 && a.stride(0) % 8 == 0 &&
+                  w.stride(0) % 8 == 0, "gemm_nt_rope: unit column strides, 16-B rows");
+  TORCH_CHECK((reinterpret_cast<uintptr_t>(a.data_ptr()) | reinterpret_cast<uintptr_t>(w.data_ptr())) % 16 == 0 &&
+                  reinterpret_cast<uintptr_t>(qkv.data_ptr()) % 8 == 0, "gemm_nt_rope: aligned operands");
+  TORCH_CHECK(nrot % hd == 0 && nrot <= N && T > 0, "gemm_nt_rope: nrot");
+  TORCH_CHECK(bllm::gemm_nt_rope_supported((int)M, (int)N, (int)K, a.stride(0), w.stride(0), qkv.stride(0), (int)hd),
+              "gemm_nt_rope: unsupported shape ", M, "x", N, "x", K, " hd ", hd);
+  bllm::gemm_nt_rope(dt_of(a), a.data_ptr(), a.stride(0), w.data_ptr(), w.stride(0), qkv.data_ptr(), qkv.stride(0),
+                     (int)M, (int)N, (int)K, cos.data_ptr<float>(), sin.data_ptr<float>(), (int)T, (int)nrot, stream());
+}
+
 // qkv [B, (H+2G)*hd] (one decode token per row); kc / vc [B, G, Tmax, hd] valid below *pos;
 // appends the token's k / v at *pos and attends over pos + 1 keys -> out [B, H*hd]
 Tensor attn_decode_append(const Tensor& qkv, Tensor& kc, Tensor& vc, const Tensor& pos, int64_t H, int64_t G) {
@@ -914,6 +939,7 @@ TORCH_LIBRARY(bllm, m) {
   m.def("gemm_nn_(Tensor a, Tensor b, Tensor(a!) c, bool accumulate) -> ()");
   m.def("gemm_nt_(Tensor a, Tensor b, Tensor(a!) c, bool accumulate, int sched=-1) -> ()");
   m.def("gemm_nt_swiglu_(Tensor a, Tensor w, Tensor(a!) gu, Tensor(b!) act) -> ()");
+  m.def("gemm_nt_rope_(Tensor a, Tensor w, Tensor(a!) qkv, Tensor cos, Tensor sin, int T, int nrot, int hd) -> ()");
   m.def("attn_decode(Tensor q, Tensor kcache, Tensor vcache, int L) -> Tensor");
   m.def("attn_decode_append(Tensor qkv, Tensor(a!) kcache, Tensor(b!) vcache, Tensor pos, int H, int G) -> Tensor");
   m.def("rope_dev_(Tensor(a!) qkv, Tensor cos, Tensor sin, int H, int G, int hd, Tensor pos) -> ()");
@@ -956,6 +982,7 @@ TORCH_LIBRARY_IMPL(bllm, CUDA, m) {
   m.impl("gemm_nn_", &gemm_nn_);
   m.impl("gemm_nt_", &gemm_nt_);
   m.impl("gemm_nt_swiglu_", &gemm_nt_swiglu_);
+  m.impl("gemm_nt_rope_", &gemm_nt_rope_);
   m.impl("bias_grad_", &bias_grad_);
   m.impl("flash_attn_bwd", &flash_attn_bwd);
   m.impl("ce_fwd", &ce_fwd);

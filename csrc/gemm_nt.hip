@@ -71,6 +71,7 @@ struct FB { s16x8 f[2][2]; };
 // (elementwise.hip: g, u rounded to T first, then a / (1 + exp(-a)) * u in fp32).
 using g4::EPI_NONE;
 using g4::EPI_SWIGLU;
+using g4::EPI_ROPE;
 using g4::i32x4;
 using g4::MfA;
 using g4::THREADS4;
@@ -674,11 +675,17 @@ template <int SV> struct Sched4 {
 // 64w' + 16b + [0, 16), the next 16 rows the matching up rows), so a lane's acc[i][2k] and
 // acc[i][2k+1] hold 4 gate and the same 4 up columns of one row: the epilogue stores both halves
 // of gu and act = silu(g) * u (g, u rounded to T first, as the separate swiglu_fwd kernel).
+// EPI_ROPE (the Llama QKV projection, head dim 128 = one wave's 128 columns): columns below nrot
+// (the q and k heads) leave rotated, out1 = x1 cos - x2 sin, out2 = x2 cos + x1 sin for the pairs
+// (d, d + 64) of the head — acc[i][k] and acc[i][k + 4] of the same lane — at position row % Tq,
+// x rounded to T first, exactly as the separate rope_k pass computes it on the stored GEMM output.
 template <typename T, typename OT, int DV, bool ACC, int SV, int EPI = EPI_NONE>
 __global__ __launch_bounds__(THREADS4, 1) void gemm_nt4p_k(const T* __restrict__ A, long lda,
                                                            const T* __restrict__ B, long ldb, OT* __restrict__ C,
                                                            long ldc, int M, int N, int K, OT* __restrict__ act = nullptr,
-                                                           int F = 0) {
+                                                           int F = 0, const float* __restrict__ cosT = nullptr,
+                                                           const float* __restrict__ sinT = nullptr, int Tq = 1,
+                                                           int nrot = 0) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int wm = wave >> 1, wn = wave & 1;
@@ -858,7 +865,34 @@ __global__ __launch_bounds__(THREADS4, 1) void gemm_nt4p_k(const T* __restrict__
     // (branch-free: ACC is a template parameter and the host only picks this kernel for rows
     //  aligned to the store width, so hipcc never hoists all 256 accumulator reads above a
     //  branch — which it does otherwise, and spills)
-    if constexpr (EPI == EPI_SWIGLU) {
+    if constexpr (EPI == EPI_ROPE) {
+      typedef OT o4 __attribute__((ext_vector_type(4)));
+      const long c0 = n0 + 128 * wn;                          // this wave's head
+      const bool rot = c0 < nrot;                             // wave-uniform; applied as a select
+      const long r0 = m0 + 128 * wm + (lane & 15);
+      const int d0 = 4 * (lane >> 4);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const long r = r0 + 16 * i;
+        const int pos = (int)(r % Tq);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int d = 16 * k + d0;
+          const f32x4 cs = *(const f32x4*)(cosT + (long)pos * 64 + d), sn = *(const f32x4*)(sinT + (long)pos * 64 + d);
+          const o4 xa = __builtin_convertvector(acc[i][k], o4), xb = __builtin_convertvector(acc[i][k + 4], o4);
+          o4 oa, ob;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float x1 = to_f(xa[e]), x2 = to_f(xb[e]);
+            const float c = rot ? cs[e] : 1.f, sj = rot ? sn[e] : 0.f;
+            oa[e] = from_f<OT>(x1 * c - x2 * sj);
+            ob[e] = from_f<OT>(x2 * c + x1 * sj);
+          }
+          *(o4*)(C + r * ldc + c0 + d) = oa;
+          *(o4*)(C + r * ldc + c0 + 64 + d) = ob;
+        }
+      }
+    } else if constexpr (EPI == EPI_SWIGLU) {
       typedef OT o4 __attribute__((ext_vector_type(4)));
       const long g0 = n0 / 2;
       const long r0 = m0 + 128 * wm + (lane & 15);
@@ -1020,6 +1054,37 @@ void launch(const void* a, long lda, const void* b, long ldb, void* c, long ldc,
 
 }  // namespace
 
+bool gemm_nt_rope_supported(int M, int N, int K, long lda, long ldb, long ldc, int hd) {
+  return hd == 128 && M > 0 && N > 0 && M % TM == 0 && N % TN == 0 && K % (2 * TK) == 0 && ldc % 4 == 0 &&
+         (long)TM * lda * 2 < (1L << 31) && (long)TN * ldb * 2 < (1L << 31);
+}
+
+void gemm_nt_rope(DType dt, const void* a, long lda, const void* w, long ldw, void* c, long ldc, int M, int N, int K,
+                  const float* cosT, const float* sinT, int Tq, int nrot, hipStream_t s) {
+  static int ncu = 0;
+  if (!ncu) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    hipDeviceProp_t prop;
+    ncu = hipGetDeviceProperties(&prop, dev) == hipSuccess ? prop.multiProcessorCount : 256;
+    ncu = ncu < 8 ? 8 : ncu / 8 * 8;
+  }
+  const int nblk = (M / TM) * (N / TN);
+  const int grid = nblk < ncu ? nblk : ncu;
+#define BLLM_ROPE4P(TT)                                                                                                \
+  do {                                                                                                                 \
+    static const bool at_ = hipFuncSetAttribute((const void*)gemm_nt4p_k<TT, TT, 1, false, 0, EPI_ROPE>,              \
+                                                hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES) == hipSuccess; \
+    (void)at_;                                                                                                         \
+    hipLaunchKernelGGL((gemm_nt4p_k<TT, TT, 1, false, 0, EPI_ROPE>), dim3(grid), dim3(THREADS4), LDS_BYTES, s,         \
+                       (const TT*)a, lda, (const TT*)w, ldw, (TT*)c, ldc, M, N, K, (TT*)nullptr, 0, cosT, sinT, Tq,    \
+                       nrot);                                                                                          \
+  } while (0)
+  if (dt == DType::BF16) BLLM_ROPE4P(bf16_t);
+  else BLLM_ROPE4P(f16_t);
+#undef BLLM_ROPE4P
+}
+
 bool gemm_nt2_supported(int M, int N, int K, long lda, long ldb) {
   return M > 0 && N > 0 && K > 0 && M % TM == 0 && N % TN == 0 && K % (2 * TK) == 0 &&
          (long)TM * lda * 2 < (1L << 31) && (long)TN * ldb * 2 < (1L << 31);
@@ -1039,8 +1104,10 @@ bool gemm_nt_swiglu_supported(int M, int F, int K, long lda, long ldb, long ldgu
 
 void gemm_nt_swiglu(DType dt, const void* a, long lda, const void* w, long ldw, void* gu, long ldgu, void* act, int M,
                     int F, int K, hipStream_t s) {
-  if (dt == DType::BF16) launch<bf16_t, bf16_t, EPI_SWIGLU>(a, lda, w, ldw, gu, ldgu, M, 2 * F, K, false, s, act, F);
-  else launch<f16_t, f16_t, EPI_SWIGLU>(a, lda, w, ldw, gu, ldgu, M, 2 * F, K, false, s, act, F);
+  // the persistent 4-wave schedule unless BLLM_GEMM_NT_SCHED picks another one (A/B)
+  const int sc = getenv("BLLM_GEMM_NT_SCHED") ? -1 : 3;
+  if (dt == DType::BF16) launch<bf16_t, bf16_t, EPI_SWIGLU>(a, lda, w, ldw, gu, ldgu, M, 2 * F, K, false, s, act, F, sc);
+  else launch<f16_t, f16_t, EPI_SWIGLU>(a, lda, w, ldw, gu, ldgu, M, 2 * F, K, false, s, act, F, sc);
 }
 
 }  // namespace bllm

@@ -701,6 +701,29 @@ def test_linear_residual_hipblaslt(dt, N, K, O):
 
 
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("M,K,T,H,G", [(512, 256, 256, 4, 2), (2048, 512, 1024, 32, 8), (8192, 128, 1024, 16, 8)])
+def test_gemm_nt_rope(dt, M, K, T, H, G):
+    """QKV projection with RoPE in the persistent GEMM's epilogue (K4) against the same GEMM
+    (BLLM_GEMM_NT_SCHED=3) followed by the separate rope_ pass — equal to 1 ulp (same rounding
+    points; the fp32 rotation may contract differently) — and against the fp32 oracle."""
+    hd = 128
+    N = (H + 2 * G) * hd
+    a = torch.randn(M, K, device=DEV).to(dt)
+    w = (torch.randn(N, K, device=DEV) / K ** 0.5).to(dt)
+    cos, sin = ops.rope_tables(hd, T, 500000.0, None, device=DEV)
+    assert ops.gemm_nt_rope_ok(a, w, hd)
+    got = ops.gemm_nt_rope(a, w, cos, sin, T, H, G, hd)
+    sep = torch.empty(M, N, device=DEV, dtype=dt)
+    ops.gemm_nt_(a, w, sep, False, 3)
+    ops.rope_(sep, cos, sin, T, H, G, hd)
+    ulp = (got.float() - sep.float()).abs() / sep.float().abs().clamp_min(1e-3)
+    assert (ulp <= (2 ** -7 if dt == torch.bfloat16 else 2 ** -10)).all(), ulp.max().item()
+    assert torch.equal(got[:, (H + G) * hd:], sep[:, (H + G) * hd:])      # v heads untouched
+    oracle = ref.rope_((a.float() @ w.float().t()).to(dt), cos, sin, T, H, G, hd)
+    check_close(got, oracle.float(), dt, k=4.0, name="gemm_nt_rope")
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("M,K,F", [(256, 128, 128), (512, 512, 768), (1024, 4096, 1792), (4096, 256, 4096)])
 @pytest.mark.parametrize("sched", ["0", "1", "2", "3"])
 def test_gemm_nt_swiglu(dt, M, K, F, sched, monkeypatch):
