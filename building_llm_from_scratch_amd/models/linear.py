@@ -122,7 +122,7 @@ def _dgrad_wt_ok(dy: torch.Tensor, W: torch.Tensor) -> bool:
 
 # The forward-layout GEMMs (y = x W^T, dX on the transposed weight copy, the fused head's logits
 # and dh).  BLLM_GEMM_NT: 0 = hipBLASLt; 1 = csrc/gemm_nt.hip wherever its shape rules hold
-# (schedule from BLLM_GEMM_NT_SCHED); auto = per shape, whichever of hipBLASLt and the three
+# (schedule from BLLM_GEMM_NT_SCHED); auto = per shape, whichever of hipBLASLt and the four
 # gemm_nt schedules timed fastest on this device (measured once per shape and process, like
 # TunableOp; never inside a graph capture)
 GEMM_NT_MODE = os.environ.get("BLLM_GEMM_NT", "0")
@@ -135,7 +135,7 @@ def _time_nt(a, b, out) -> int:
     c = torch.empty(a.shape[0], b.shape[0], dtype=out.dtype if out is not None else a.dtype, device=a.device)
     arms = {-1: lambda: torch.mm(a, b.t(), out=c) if c.dtype == a.dtype else c.copy_(torch.mm(a, b.t())),
             0: lambda: ops.gemm_nt_(a, b, c, False, 0), 1: lambda: ops.gemm_nt_(a, b, c, False, 1),
-            2: lambda: ops.gemm_nt_(a, b, c, False, 2)}
+            2: lambda: ops.gemm_nt_(a, b, c, False, 2), 3: lambda: ops.gemm_nt_(a, b, c, False, 3)}
     times = {k: [] for k in arms}
     for fn in arms.values():
         fn()

@@ -155,6 +155,23 @@ def bench_swiglu(a):
         print(json.dumps(r), flush=True)
         del x, w, gu
         torch.cuda.empty_cache()
+    # QKV + RoPE: hipBLASLt GEMM + rope_ vs the fused persistent kernel (Llama-3-8B at 40 x 1024)
+    tokens, K, H, G, hd, T = 40960, 4096, 32, 8, 128, 1024
+    x = torch.rand(tokens, K, device="cuda", dtype=dt) * 2 - 1
+    w = (torch.rand((H + 2 * G) * hd, K, device="cuda", dtype=dt) * 2 - 1) * 0.05
+    cos, sin = ops.rope_tables(hd, T, 500000.0, None, device="cuda")
+    q = torch.empty(tokens, w.shape[0], device="cuda", dtype=dt)
+
+    def sep_r():
+        torch.mm(x, w.t(), out=q)
+        ops.rope_(q, cos, sin, T, H, G, hd)
+    fns = {"hipblaslt+rope": sep_r, "fused_rope": lambda: ops.gemm_nt_rope(x, w, cos, sin, T, H, G, hd)}
+    times = {k: [] for k in fns}
+    for _ in range(a.rounds):
+        for k, fn in fns.items():
+            times[k].append(timeit(fn, a.iters))
+    print(json.dumps({"model": "llama", "op": "qkv+rope", **{k + "_us": round(sorted(v)[len(v) // 2] * 1e3, 1)
+                                                              for k, v in times.items()}}), flush=True)
 
 
 if __name__ == "__main__":
