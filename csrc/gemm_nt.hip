@@ -662,7 +662,10 @@ __global__ __launch_bounds__(THREADS4, 1) void gemm_nt4_k(const T* __restrict__ 
 // the 128-MFMA K-tile.  0: WAR after MFMA 31, pieces every 5 MFMAs from 32, RAW at 112 (reads of
 // the next fragments one per MFMA over the last 16); 1: WAR after 23, pieces every 4 from 24,
 // RAW at 112; 2: as 1 with RAW at 120 (two reads per MFMA over the last 8); 3: as 0, RAW at 120.
+// 4: as 0 with the MFMA order j-major (the B fragment, MFMA src A, fixed over 8 consecutive MFMAs,
+// as in hipBLASLt's loop) and the fragment reads ordered to match (b[0], a[0..7], b[1..7]).
 template <int SV> struct Sched4 {
+  static constexpr bool JMAJ = SV == 4;
   static constexpr int WAR = (SV == 1 || SV == 2) ? 23 : 31;   // barrier after this MFMA
   static constexpr int D0 = WAR + 1, DS = (SV == 1 || SV == 2) ? 4 : 5;   // first piece, stride
   static constexpr int RAW = (SV >= 2) ? 120 : 112;             // before this MFMA (of 128)
@@ -685,17 +688,17 @@ __global__ __launch_bounds__(THREADS4, 1) void gemm_nt4p_k(const T* __restrict__
                                                            long ldc, int M, int N, int K, OT* __restrict__ act = nullptr,
                                                            int F = 0, const float* __restrict__ cosT = nullptr,
                                                            const float* __restrict__ sinT = nullptr, int Tq = 1,
-                                                           int nrot = 0) {
+                                                           int nrot = 0, int group_m = GROUP_M) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int wm = wave >> 1, wn = wave & 1;
   const int nbm = M / TM, nbn = N / TN, nblk = nbm * nbn, G = gridDim.x;
-  const int q8 = nblk >> 3, r8 = nblk & 7, per_group = GROUP_M * nbn;
+  const int q8 = nblk >> 3, r8 = nblk & 7, per_group = group_m * nbn;
   auto coords = [&](int tid, long& m0, long& n0) {
     const int xcd = tid & 7;
     const int wid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (tid >> 3);
-    const int grp = wid / per_group, first_m = grp * GROUP_M;
-    const int gm = nbm - first_m < GROUP_M ? nbm - first_m : GROUP_M;
+    const int grp = wid / per_group, first_m = grp * group_m;
+    const int gm = nbm - first_m < group_m ? nbm - first_m : group_m;
     const int in_g = wid - grp * per_group;
     m0 = (long)(first_m + in_g % gm) * TM;
     n0 = (long)(in_g / gm) * TN;
@@ -789,15 +792,25 @@ __global__ __launch_bounds__(THREADS4, 1) void gemm_nt4p_k(const T* __restrict__
   for (int i = 0; i < 8; ++i) a0[i] = rdA(0, i, 0), b0[i] = rdB(0, i, 0);
 
   using SC = Sched4<SV>;
+  // read r (0..15) of a k-step's fragments, in the order the MFMAs consume them
+  auto rd16 = [&](s16x8 (&fa)[8], s16x8 (&fb)[8], int buf, int s, int r) {
+    if constexpr (SC::JMAJ) {
+      if (r == 0) fb[0] = rdB(buf, 0, s);
+      else if (r <= 8) fa[r - 1] = rdA(buf, r - 1, s);
+      else fb[r - 8] = rdB(buf, r - 8, s);
+    } else {
+      if (r == 0) fa[0] = rdA(buf, 0, s);
+      else if (r <= 8) fb[r - 1] = rdB(buf, r - 1, s);
+      else fa[r - 8] = rdA(buf, r - 8, s);
+    }
+  };
   auto ktile = [&](int t, auto cur_c) {
     constexpr int cur = decltype(cur_c)::value, nxt = cur ^ 1;
 #pragma unroll
     for (int n = 0; n < 64; ++n) {
-      const int i = n >> 3, j = n & 7;
+      const int i = SC::JMAJ ? (n & 7) : (n >> 3), j = SC::JMAJ ? (n >> 3) : (n & 7);
       MfA<T>::run(acc[i][j], b0[j], a0[i]);
-      if (n == 0) a1[0] = rdA(cur, 0, 1);
-      else if (n <= 8) b1[n - 1] = rdB(cur, n - 1, 1);
-      else if (n < 16) a1[n - 8] = rdA(cur, n - 8, 1);
+      if (n < 16) rd16(a1, b1, cur, 1, n);
       if (n == SC::WAR) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
@@ -808,7 +821,7 @@ __global__ __launch_bounds__(THREADS4, 1) void gemm_nt4p_k(const T* __restrict__
     }
 #pragma unroll
     for (int n = 0; n < 64; ++n) {
-      const int i = n >> 3, j = n & 7;
+      const int i = SC::JMAJ ? (n & 7) : (n >> 3), j = SC::JMAJ ? (n >> 3) : (n & 7);
       if (SC::piece(64 + n) >= 0) dma(t + 2, cur, SC::piece(64 + n));
       if (64 + n == SC::RAW) {
         wait_vm<16>();
@@ -818,12 +831,7 @@ __global__ __launch_bounds__(THREADS4, 1) void gemm_nt4p_k(const T* __restrict__
       constexpr int NR = 128 - SC::RAW;   // MFMAs carrying the 16 reads (16 or 8)
       if (64 + n >= SC::RAW) {
 #pragma unroll
-        for (int q = 0; q < 16 / NR; ++q) {
-          const int r = (64 + n - SC::RAW) * (16 / NR) + q;   // a0[0], b0[0..7], a0[1..7]
-          if (r == 0) a0[0] = rdA(nxt, 0, 0);
-          else if (r <= 8) b0[r - 1] = rdB(nxt, r - 1, 0);
-          else a0[r - 8] = rdA(nxt, r - 8, 0);
-        }
+        for (int q = 0; q < 16 / NR; ++q) rd16(a0, b0, nxt, 0, (64 + n - SC::RAW) * (16 / NR) + q);
       }
       MfA<T>::run(acc[i][j], b1[j], a1[i]);
       __builtin_amdgcn_sched_barrier(0);
@@ -1013,13 +1021,17 @@ void launch(const void* a, long lda, const void* b, long ldb, void* c, long ldc,
     const int grid = nblk < ncu ? nblk : ncu;
     const char* ev = getenv("BLLM_GEMM_NT4P_SV");
     const int sv = ev && *ev ? atoi(ev) : 0;
+    const char* eg = getenv("BLLM_GEMM_NT4P_GM");   // tile-group depth (A/B); default GROUP_M
+    // 4 measured 0.3-12 % faster than 8 (16, 32 slower) on the Llama-3-8B / GPT2-774M shapes
+    // (profiles/r3/gemm_nt4p_sv4_gm.jsonl)
+    const int gmz = eg && atoi(eg) > 0 ? atoi(eg) : 4;
 #define BLLM_NT4P(ACCv, SVv)                                                                                            \
   do {                                                                                                                  \
     static const bool at_ = hipFuncSetAttribute((const void*)gemm_nt4p_k<T, OT, 1, ACCv, SVv>,                          \
                                                 hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES) == hipSuccess; \
     (void)at_;                                                                                                          \
     hipLaunchKernelGGL((gemm_nt4p_k<T, OT, 1, ACCv, SVv>), dim3(grid), dim3(THREADS4), LDS_BYTES, s, (const T*)a, lda, \
-                       (const T*)b, ldb, (OT*)c, ldc, M, N, K);                                                        \
+                       (const T*)b, ldb, (OT*)c, ldc, M, N, K, (OT*)nullptr, 0, nullptr, nullptr, 1, 0, gmz);      \
   } while (0)
     if (accumulate) {
       BLLM_NT4P(true, 0);
@@ -1029,6 +1041,8 @@ void launch(const void* a, long lda, const void* b, long ldb, void* c, long ldc,
       BLLM_NT4P(false, 2);
     } else if (sv == 3) {
       BLLM_NT4P(false, 3);
+    } else if (sv == 4) {
+      BLLM_NT4P(false, 4);
     } else {
       BLLM_NT4P(false, 0);
     }

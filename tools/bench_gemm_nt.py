@@ -43,9 +43,10 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--models", default="llama,gpt2")
     ap.add_argument("--nt4_dma", default="0", help="comma list of BLLM_GEMM_NT4_DMA variants of the 4-wave arm")
-    ap.add_argument("--arms", default="hipblaslt,new,pp,4w,old")
+    ap.add_argument("--arms", default="hipblaslt,new,pp,4w,old,4p,4g")
     ap.add_argument("--only", default="", help="comma list of gemm names to run (e.g. gate_up)")
     ap.add_argument("--nt4p_sv", default="0", help="comma list of BLLM_GEMM_NT4P_SV variants of the persistent arm")
+    ap.add_argument("--nt4p_gm", default="", help="comma list of BLLM_GEMM_NT4P_GM (tile-group depth) arms, SV 0")
     ap.add_argument("--swiglu", action="store_true",
                     help="gate/up + SwiGLU: hipBLASLt GEMM + separate swiglu_fwd vs the fused kernel (sched 2, 3)")
     a = ap.parse_args()
@@ -64,8 +65,10 @@ def main():
             ref = torch.mm(x, w.t())
             dvs = a.nt4_dma.split(",")
             svs = a.nt4p_sv.split(",")
+            gms = [g for g in a.nt4p_gm.split(",") if g]
             outs = {k_: torch.empty(m, n, device="cuda", dtype=dt)
-                    for k_ in ["new", "pp", "old"] + ["w4_" + d for d in dvs] + ["p4_" + v for v in svs]}
+                    for k_ in ["new", "pp", "old"] + ["w4_" + d for d in dvs] + ["p4_" + v for v in svs]
+                    + ["g4_" + g for g in gms]}
             y = torch.empty(m, n, device="cuda", dtype=dt)
 
             def new():
@@ -102,6 +105,17 @@ def main():
                    "gemm_nt_old": old}
             fns.update({"gemm_nt_4w_" + d: w4(d) for d in dvs})
             fns.update({"gemm_nt_4p_" + v: p4(v) for v in svs})
+
+            def g4(gm):
+                def f():
+                    os.environ.pop("BLLM_GEMM_NT_IMPL", None)
+                    os.environ["BLLM_GEMM_NT_SCHED"] = "3"
+                    os.environ["BLLM_GEMM_NT4P_SV"] = "0"
+                    os.environ["BLLM_GEMM_NT4P_GM"] = gm
+                    ops.gemm_nt_(x, w, outs["g4_" + gm])
+                    os.environ.pop("BLLM_GEMM_NT4P_GM", None)
+                return f
+            fns.update({"gemm_nt_4g_" + g: g4(g) for g in gms})
             want = a.arms.split(",")
             fns = {k_: f for k_, f in fns.items()
                    if k_ == "hipblaslt" and "hipblaslt" in want or k_.startswith("gemm_nt_") and k_.split("_")[2] in want}
