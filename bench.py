@@ -76,7 +76,7 @@ PEAK_BF16 = 2.5e15
 PRESETS = {
     "llama3_8b_fsdp": dict(model="llama3", num_params="8B", parallel="fsdp", actv_ckpt="auto", batch_size=40,
                            data="pretrain", mixed_precision=None, lora_rank=0),
-    "gpt2_774m_ddp": dict(model="GPT2", num_params="774M", parallel="ddp", actv_ckpt="none", batch_size=24,
+    "gpt2_774m_ddp": dict(model="GPT2", num_params="774M", parallel="ddp", actv_ckpt="none", batch_size=64,
                           data="pretrain", mixed_precision=None, lora_rank=0),
     "llama32_1b_lora_alpaca": dict(model="llama3_2", num_params="1B", parallel="ddp", actv_ckpt="none",
                                    batch_size=96, data="alpaca", mixed_precision=None, lora_rank=16),
