@@ -10,8 +10,10 @@ import sqlite3
 def classify(n):
     if n.startswith(("Cijk", "Custom_Cijk")):
         return "gemm (hipBLASLt)"
-    if "wgrad_gemm_k" in n:
+    if "wgrad_gemm_k" in n or "wgrad4_k" in n or "wgrad4p_k" in n:
         return "wgrad_mfma (dW GEMM, csrc/gemm_wgrad.hip)"
+    if "gemm_nt" in n:
+        return "gemm_nt (forward-layout GEMM, csrc/gemm_nt.hip)"
     if "sum_partials" in n:
         return "sum_partials (split-K)"
     if "transpose16" in n:
