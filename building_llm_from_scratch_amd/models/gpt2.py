@@ -198,15 +198,21 @@ class GPTBlockCompute(UnitCompute):
         x2 = ops.dropout_add(x2d, a, p, rc.seed, offs[1])
         del a
         h2, m2, r2 = self._ln(x2, b.norm2)
-        f, xa_fc = self.fc.forward(h2)
-        if recompute and not self.proj.has_lora and RECOMPUTE_FUSED:
+        rebuild_g = recompute and not self.proj.has_lora and RECOMPUTE_FUSED
+        fused = None if rebuild_g else self.fc.forward_bias_gelu(h2)   # K9: bias + GELU in the epilogue
+        if fused is not None:
+            (f, g), xa_fc = fused, None
+        else:
+            f, xa_fc = self.fc.forward(h2)
+            g = None
+        if rebuild_g:
             # backward rebuilds g inside the GELU backward pass (ops.gelu_bwd_act)
             g, x3, xa_pr = None, None, None
         elif recompute:
-            g = ops.gelu_fwd(f)
+            g = ops.gelu_fwd(f) if g is None else g
             x3, xa_pr = None, self.proj.lora_state(g)
         else:
-            g = ops.gelu_fwd(f)
+            g = ops.gelu_fwd(f) if g is None else g
             m, xa_pr = self.proj.forward(g)
             x3 = ops.dropout_add(x2, m, p, rc.seed, offs[2])
         if not save:

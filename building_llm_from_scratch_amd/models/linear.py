@@ -214,6 +214,8 @@ FORCE_GROUPED_LORA = False
 # (FusedLinear.forward_rope), both on csrc/gemm_nt.hip's persistent 4-wave kernel
 FUSED_SWIGLU = os.environ.get("BLLM_FUSED_SWIGLU", "0") != "0"
 FUSED_ROPE = os.environ.get("BLLM_FUSED_ROPE", "0") != "0"
+# GPT-2 c_fc GEMM + bias + GELU epilogue (FusedLinear.forward_bias_gelu)
+FUSED_GELU = os.environ.get("BLLM_FUSED_GELU", "0") != "0"
 
 
 class FusedLinear:
@@ -354,6 +356,17 @@ class FusedLinear:
         if not ops.gemm_nt_swiglu_ok(x, W):
             return None
         return ops.gemm_nt_swiglu(x, W)
+
+    def forward_bias_gelu(self, x: torch.Tensor):
+        """c_fc with its bias and the exact GELU in the GEMM epilogue (K9; no LoRA): returns
+        ``(f, g)`` = (pre-activation, activation) or None when the fused kernel does not apply
+        (BLLM_FUSED_GELU=0 turns it off) and the caller runs the GEMM + ``gelu_fwd``."""
+        if self.has_lora or self.b_params is None or not FUSED_GELU:
+            return None
+        W, b = self.W(), self.b()
+        if not ops.gemm_nt_bias_gelu_ok(x, W, b):
+            return None
+        return ops.gemm_nt_bias_gelu(x, W, b)
 
     def forward_rope(self, x: torch.Tensor, cos, sin, T: int, H: int, G: int, hd: int):
         """QKV projection with RoPE applied to the q and k heads in the GEMM epilogue (K4; no bias,

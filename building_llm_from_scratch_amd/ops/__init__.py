@@ -398,6 +398,23 @@ def gemm_nt_rope(a, w, cos, sin, T: int, H: int, G: int, hd: int):
     return ref.rope_(qkv, cos, sin, T, H, G, hd)
 
 
+def gemm_nt_bias_gelu_ok(a: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor]) -> bool:
+    """Shapes the c_fc + bias + GELU-epilogue kernel takes (persistent 4-wave GEMM)."""
+    return bias is not None and bias.dtype == a.dtype and bias.numel() == w.shape[0] and gemm_nt_ok(a, w)
+
+
+def gemm_nt_bias_gelu(a, w, bias):
+    """(f, g) = (a . w^T + bias, gelu(f)) — GPT-2's c_fc with the bias and the exact-erf GELU in
+    the GEMM epilogue (K9); on CPU the matmul + ``gelu_fwd`` oracle (f rounded first)."""
+    if _hip(a):
+        f = torch.empty(a.shape[0], w.shape[0], dtype=a.dtype, device=a.device)
+        g = torch.empty_like(f)
+        _k().gemm_nt_bias_gelu_(a, w, bias.contiguous(), f, g)
+        return f, g
+    f = (a.float() @ w.float().t() + bias.float()).to(a.dtype)
+    return f, gelu_fwd(f)
+
+
 def gemm_nt_swiglu(a, w):
     """(gu, act) = (a . w^T, silu(gu[:, :F]) * gu[:, F:]) for w = [W_gate; W_up] — the gate/up
     projection with the SwiGLU forward in its epilogue (csrc/gemm_nt.hip, GPU); on CPU the

@@ -178,6 +178,10 @@ bool gemm_nt_swiglu_supported(int M, int F, int K, long lda, long ldb, long ldgu
 // qkv [M, N] = a [M, K] . w [N, K]^T with RoPE applied to columns < nrot (head dim 128) at
 // position row % Tq in the epilogue of the persistent 4-wave kernel (csrc/gemm_nt.hip)
 bool gemm_nt_rope_supported(int M, int N, int K, long lda, long ldb, long ldc, int hd);
+// GPT-2 c_fc with bias + exact GELU in the epilogue: f = a . w^T + bias, g = gelu(f) (both [M, N])
+bool gemm_nt_bias_gelu_supported(int M, int N, int K, long lda, long ldb, long ldc);
+void gemm_nt_bias_gelu(DType dt, const void* a, long lda, const void* w, long ldw, const void* bias, void* f, void* g,
+                       long ldc, int M, int N, int K, hipStream_t s);
 void gemm_nt_rope(DType dt, const void* a, long lda, const void* w, long ldw, void* c, long ldc, int M, int N, int K,
                   const float* cosT, const float* sinT, int Tq, int nrot, hipStream_t s);
 void gemm_nt_swiglu(DType dt, const void* a, long lda, const void* w, long ldw, void* gu, long ldgu, void* act, int M,

@@ -424,6 +424,28 @@ void gemm_nt_rope_(const Tensor& a, const Tensor& w, Tensor& qkv, const Tensor& 
                      (int)M, (int)N, (int)K, cos.data_ptr<float>(), sin.data_ptr<float>(), (int)T, (int)nrot, stream());
 }
 
+// GPT-2 c_fc with bias + exact GELU in the epilogue (K9, csrc/gemm_nt.hip): f = a . w^T + bias,
+// g = gelu(f); f and g contiguous [M, N]
+void gemm_nt_bias_gelu_(const Tensor& a, const Tensor& w, const Tensor& bias, Tensor& f, Tensor& g) {
+  TORCH_CHECK(a.is_cuda() && w.is_cuda() && bias.is_cuda() && f.is_cuda() && g.is_cuda(), "gemm_nt_bias_gelu: GPU");
+  c10::DeviceGuard dg(a.device());
+  const int64_t M = a.size(0), K = a.size(1), N = w.size(0);
+  TORCH_CHECK(a.dim() == 2 && w.dim() == 2 && w.size(1) == K && bias.numel() == N && bias.is_contiguous() &&
+                  f.sizes() == g.sizes() && f.size(0) == M && f.size(1) == N && f.is_contiguous() && g.is_contiguous(),
+              "gemm_nt_bias_gelu: shapes");
+  TORCH_CHECK(a.scalar_type() == w.scalar_type() && bias.scalar_type() == a.scalar_type() &&
+                  f.scalar_type() == a.scalar_type() && g.scalar_type() == a.scalar_type() &&
+                  (a.scalar_type() == at::kBFloat16 || a.scalar_type() == at::kHalf), "gemm_nt_bias_gelu: bf16/fp16");
+  TORCH_CHECK(a.stride(1) == 1 && w.stride(1) == 1 && a.stride(0) % 8 == 0 && w.stride(0) % 8 == 0 &&
+                  (reinterpret_cast<uintptr_t>(a.data_ptr()) | reinterpret_cast<uintptr_t>(w.data_ptr())) % 16 == 0 &&
+                  (reinterpret_cast<uintptr_t>(bias.data_ptr()) | reinterpret_cast<uintptr_t>(f.data_ptr()) |
+                   reinterpret_cast<uintptr_t>(g.data_ptr())) % 8 == 0, "gemm_nt_bias_gelu: alignment");
+  TORCH_CHECK(bllm::gemm_nt_bias_gelu_supported((int)M, (int)N, (int)K, a.stride(0), w.stride(0), f.stride(0)),
+              "gemm_nt_bias_gelu: unsupported shape ", M, "x", N, "x", K);
+  bllm::gemm_nt_bias_gelu(dt_of(a), a.data_ptr(), a.stride(0), w.data_ptr(), w.stride(0), bias.data_ptr(),
+                          f.data_ptr(), g.data_ptr(), f.stride(0), (int)M, (int)N, (int)K, stream());
+}
+
 // qkv [B, (H+2G)*hd] (one decode token per row); kc / vc [B, G, Tmax, hd] valid below *pos;
 // appends the token's k / v at *pos and attends over pos + 1 keys -> out [B, H*hd]
 Tensor attn_decode_append(const Tensor& qkv, Tensor& kc, Tensor& vc, const Tensor& pos, int64_t H, int64_t G) {
@@ -940,6 +962,7 @@ TORCH_LIBRARY(bllm, m) {
   m.def("gemm_nt_(Tensor a, Tensor b, Tensor(a!) c, bool accumulate, int sched=-1) -> ()");
   m.def("gemm_nt_swiglu_(Tensor a, Tensor w, Tensor(a!) gu, Tensor(b!) act) -> ()");
   m.def("gemm_nt_rope_(Tensor a, Tensor w, Tensor(a!) qkv, Tensor cos, Tensor sin, int T, int nrot, int hd) -> ()");
+  m.def("gemm_nt_bias_gelu_(Tensor a, Tensor w, Tensor bias, Tensor(a!) f, Tensor(b!) g) -> ()");
   m.def("attn_decode(Tensor q, Tensor kcache, Tensor vcache, int L) -> Tensor");
   m.def("attn_decode_append(Tensor qkv, Tensor(a!) kcache, Tensor(b!) vcache, Tensor pos, int H, int G) -> Tensor");
   m.def("rope_dev_(Tensor(a!) qkv, Tensor cos, Tensor sin, int H, int G, int hd, Tensor pos) -> ()");
@@ -983,6 +1006,7 @@ TORCH_LIBRARY_IMPL(bllm, CUDA, m) {
   m.impl("gemm_nt_", &gemm_nt_);
   m.impl("gemm_nt_swiglu_", &gemm_nt_swiglu_);
   m.impl("gemm_nt_rope_", &gemm_nt_rope_);
+  m.impl("gemm_nt_bias_gelu_", &gemm_nt_bias_gelu_);
   m.impl("bias_grad_", &bias_grad_);
   m.impl("flash_attn_bwd", &flash_attn_bwd);
   m.impl("ce_fwd", &ce_fwd);

@@ -12,7 +12,7 @@ typedef int i32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int TN = 256;          // output tile columns (and rows)
 constexpr int THREADS4 = 256;    // 4 waves
-enum { EPI_NONE = 0, EPI_SWIGLU = 1, EPI_ROPE = 2 };
+enum { EPI_NONE = 0, EPI_SWIGLU = 1, EPI_ROPE = 2, EPI_BIAS_GELU = 3 };
 
 // MFMA with the accumulator tied in place in an AGPR ("+a"): hipcc otherwise renames the
 // 256 accumulators of the 4-wave kernel between unrolled steps and pays for it in

@@ -72,6 +72,7 @@ struct FB { s16x8 f[2][2]; };
 using g4::EPI_NONE;
 using g4::EPI_SWIGLU;
 using g4::EPI_ROPE;
+using g4::EPI_BIAS_GELU;
 using g4::i32x4;
 using g4::MfA;
 using g4::THREADS4;
@@ -688,7 +689,8 @@ __global__ __launch_bounds__(THREADS4, 1) void gemm_nt4p_k(const T* __restrict__
                                                            long ldc, int M, int N, int K, OT* __restrict__ act = nullptr,
                                                            int F = 0, const float* __restrict__ cosT = nullptr,
                                                            const float* __restrict__ sinT = nullptr, int Tq = 1,
-                                                           int nrot = 0, int group_m = GROUP_M) {
+                                                           int nrot = 0, int group_m = GROUP_M,
+                                                           const OT* __restrict__ bias = nullptr) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int wm = wave >> 1, wn = wave & 1;
@@ -873,7 +875,30 @@ __global__ __launch_bounds__(THREADS4, 1) void gemm_nt4p_k(const T* __restrict__
     // (branch-free: ACC is a template parameter and the host only picks this kernel for rows
     //  aligned to the store width, so hipcc never hoists all 256 accumulator reads above a
     //  branch — which it does otherwise, and spills)
-    if constexpr (EPI == EPI_ROPE) {
+    if constexpr (EPI == EPI_BIAS_GELU) {
+      // GPT-2 c_fc: f = acc + bias (rounded to T: the saved pre-activation) and g = GELU(f) with
+      // the exact erf form of the separate gelu_fwd kernel (act)
+      typedef OT o4 __attribute__((ext_vector_type(4)));
+      const long r0 = m0 + 128 * wm + (lane & 15);
+      const long cb = n0 + 128 * wn + 4 * (lane >> 4);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const f32x4 bv = __builtin_convertvector(*(const o4*)(bias + cb + 16 * j), f32x4);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const long off = (r0 + 16 * i) * ldc + cb + 16 * j;
+          const o4 fb = __builtin_convertvector(acc[i][j] + bv, o4);
+          *(o4*)(C + off) = fb;
+          o4 gb;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float x = to_f(fb[e]);
+            gb[e] = from_f<OT>(0.5f * x * (1.f + erff(x * 0.70710678118654752f)));
+          }
+          *(o4*)(act + off) = gb;
+        }
+      }
+    } else if constexpr (EPI == EPI_ROPE) {
       typedef OT o4 __attribute__((ext_vector_type(4)));
       const long c0 = n0 + 128 * wn;                          // this wave's head
       const bool rot = c0 < nrot;                             // wave-uniform; applied as a select
@@ -1097,6 +1122,37 @@ void gemm_nt_rope(DType dt, const void* a, long lda, const void* w, long ldw, vo
   if (dt == DType::BF16) BLLM_ROPE4P(bf16_t);
   else BLLM_ROPE4P(f16_t);
 #undef BLLM_ROPE4P
+}
+
+bool gemm_nt_bias_gelu_supported(int M, int N, int K, long lda, long ldb, long ldc) {
+  return M > 0 && N > 0 && M % TM == 0 && N % TN == 0 && K % (2 * TK) == 0 && ldc % 4 == 0 &&
+         (long)TM * lda * 2 < (1L << 31) && (long)TN * ldb * 2 < (1L << 31);
+}
+
+void gemm_nt_bias_gelu(DType dt, const void* a, long lda, const void* w, long ldw, const void* bias, void* f, void* g,
+                       long ldc, int M, int N, int K, hipStream_t s) {
+  static int ncu = 0;
+  if (!ncu) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    hipDeviceProp_t prop;
+    ncu = hipGetDeviceProperties(&prop, dev) == hipSuccess ? prop.multiProcessorCount : 256;
+    ncu = ncu < 8 ? 8 : ncu / 8 * 8;
+  }
+  const int nblk = (M / TM) * (N / TN);
+  const int grid = nblk < ncu ? nblk : ncu;
+#define BLLM_GELU4P(TT)                                                                                                \
+  do {                                                                                                                 \
+    static const bool at_ = hipFuncSetAttribute((const void*)gemm_nt4p_k<TT, TT, 1, false, 0, EPI_BIAS_GELU>,         \
+                                                hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES) == hipSuccess; \
+    (void)at_;                                                                                                         \
+    hipLaunchKernelGGL((gemm_nt4p_k<TT, TT, 1, false, 0, EPI_BIAS_GELU>), dim3(grid), dim3(THREADS4), LDS_BYTES, s,    \
+                       (const TT*)a, lda, (const TT*)w, ldw, (TT*)f, ldc, M, N, K, (TT*)g, 0, nullptr, nullptr, 1, 0, \
+                       4, (const TT*)bias);                                                                            \
+  } while (0)
+  if (dt == DType::BF16) BLLM_GELU4P(bf16_t);
+  else BLLM_GELU4P(f16_t);
+#undef BLLM_GELU4P
 }
 
 bool gemm_nt2_supported(int M, int N, int K, long lda, long ldb) {

@@ -701,6 +701,20 @@ def test_linear_residual_hipblaslt(dt, N, K, O):
 
 
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("M,K,N", [(512, 256, 1024), (8192, 1280, 5120), (4096, 384, 768)])
+def test_gemm_nt_bias_gelu(dt, M, K, N):
+    """GPT-2 c_fc with bias + exact GELU in the persistent GEMM's epilogue (K9): f against the fp32
+    oracle, g bitwise equal to the separate gelu_fwd kernel applied to that f."""
+    a = torch.randn(M, K, device=DEV).to(dt)
+    w = (torch.randn(N, K, device=DEV) / K ** 0.5).to(dt)
+    bias = torch.randn(N, device=DEV).to(dt)
+    assert ops.gemm_nt_bias_gelu_ok(a, w, bias)
+    f, g = ops.gemm_nt_bias_gelu(a, w, bias)
+    check_close(f, a.float() @ w.float().t() + bias.float(), dt, k=3.0, name="gemm_nt_bias_gelu f")
+    assert torch.equal(g, ops.gelu_fwd(f))
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("M,K,T,H,G", [(512, 256, 256, 4, 2), (2048, 512, 1024, 32, 8), (8192, 128, 1024, 16, 8)])
 def test_gemm_nt_rope(dt, M, K, T, H, G):
     """QKV projection with RoPE in the persistent GEMM's epilogue (K4) against the same GEMM

@@ -281,6 +281,32 @@ def test_fused_rope_and_swiglu_epilogues_in_model(ckpt, monkeypatch):
         assert _rel(g1[k], g0[k]) < 2e-2, (k, _rel(g1[k], g0[k]))
 
 
+@pytest.mark.parametrize("ckpt", ["none", "selective", "full"])
+def test_fused_bias_gelu_epilogue_in_model(ckpt, monkeypatch):
+    """BLLM_FUSED_GELU: GPT-2's c_fc with bias + GELU in the GEMM epilogue gives the loss and
+    gradients of hipBLASLt's bias GEMM + the separate gelu_fwd pass to rounding (no dropout)."""
+    from building_llm_from_scratch_amd.models import linear
+    ops.load_ext(required=True)
+    cfg = _cfgs()["gpt2"].replace(dtype=torch.bfloat16)
+    idx = torch.randint(0, cfg.vocab_size, (2, 257), device="cuda")
+    res, calls = {}, []
+    orig = ops.gemm_nt_bias_gelu
+    monkeypatch.setattr(ops, "gemm_nt_bias_gelu", lambda *a: (calls.append(1), orig(*a))[1])
+    for fused in (False, True):
+        monkeypatch.setattr(linear, "FUSED_GELU", fused)
+        torch.manual_seed(0)
+        m = build_model(cfg, use_actv_ckpt=ckpt, device="cuda")
+        m.flatten()
+        loss = m(idx[:, :-1], idx[:, 1:])
+        loss.backward()
+        res[fused] = (loss.item(), {k: p.grad.float().clone() for k, p in m.named_parameters()})
+    assert calls, "fused c_fc + bias + GELU kernel not used"
+    (l0, g0), (l1, g1) = res[False], res[True]
+    assert abs(l0 - l1) < 1e-2 * abs(l0)
+    for k in g0:
+        assert _rel(g1[k], g0[k]) < 2e-2, (k, _rel(g1[k], g0[k]))
+
+
 @pytest.mark.parametrize("mode", ["sched0", "sched1", "sched2", "sched3", "auto"])
 def test_gemm_nt_kernel_in_model(mode, monkeypatch):
     """BLLM_GEMM_NT: the forward-layout GEMMs (projections, the dX GEMMs on the transposed weight
