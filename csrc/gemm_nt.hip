@@ -1050,26 +1050,31 @@ void launch(const void* a, long lda, const void* b, long ldb, void* c, long ldc,
     // 4 measured 0.3-12 % faster than 8 (16, 32 slower) on the Llama-3-8B / GPT2-774M shapes
     // (profiles/r3/gemm_nt4p_sv4_gm.jsonl)
     const int gmz = eg && atoi(eg) > 0 ? atoi(eg) : 4;
-#define BLLM_NT4P(ACCv, SVv)                                                                                            \
+#define BLLM_NT4P(ACCv, SVv, DVv)                                                                                       \
   do {                                                                                                                  \
-    static const bool at_ = hipFuncSetAttribute((const void*)gemm_nt4p_k<T, OT, 1, ACCv, SVv>,                          \
+    static const bool at_ = hipFuncSetAttribute((const void*)gemm_nt4p_k<T, OT, DVv, ACCv, SVv>,                        \
                                                 hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES) == hipSuccess; \
     (void)at_;                                                                                                          \
-    hipLaunchKernelGGL((gemm_nt4p_k<T, OT, 1, ACCv, SVv>), dim3(grid), dim3(THREADS4), LDS_BYTES, s, (const T*)a, lda, \
-                       (const T*)b, ldb, (OT*)c, ldc, M, N, K, (OT*)nullptr, 0, nullptr, nullptr, 1, 0, gmz);      \
+    hipLaunchKernelGGL((gemm_nt4p_k<T, OT, DVv, ACCv, SVv>), dim3(grid), dim3(THREADS4), LDS_BYTES, s, (const T*)a,   \
+                       lda, (const T*)b, ldb, (OT*)c, ldc, M, N, K, (OT*)nullptr, 0, nullptr, nullptr, 1, 0, gmz);  \
   } while (0)
+    // sv 5 / 6: schedule 0 with the pieces issued sc0 sc1 / nt (cache-policy A/B)
     if (accumulate) {
-      BLLM_NT4P(true, 0);
+      BLLM_NT4P(true, 0, 1);
     } else if (sv == 1) {
-      BLLM_NT4P(false, 1);
+      BLLM_NT4P(false, 1, 1);
     } else if (sv == 2) {
-      BLLM_NT4P(false, 2);
+      BLLM_NT4P(false, 2, 1);
     } else if (sv == 3) {
-      BLLM_NT4P(false, 3);
+      BLLM_NT4P(false, 3, 1);
     } else if (sv == 4) {
-      BLLM_NT4P(false, 4);
+      BLLM_NT4P(false, 4, 1);
+    } else if (sv == 5) {
+      BLLM_NT4P(false, 0, 2);
+    } else if (sv == 6) {
+      BLLM_NT4P(false, 0, 3);
     } else {
-      BLLM_NT4P(false, 0);
+      BLLM_NT4P(false, 0, 1);
     }
 #undef BLLM_NT4P
   } else if (sc == 2 || sc == 3) {
