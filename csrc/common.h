@@ -88,6 +88,22 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
   return t;
 }
 
+// ---------------------------------------------------------------- GELU derivative
+// d/dx [x Phi(x)] = Phi(x) + x phi(x) for the exact (erf) GELU, branch-free: Phi from
+// Abramowitz-Stegun 7.1.26 (|erf error| <= 1.5e-7, about one fp32 ulp of Phi) sharing its
+// exp(-x^2 / 2) with phi.  libm's erff branches by range (divergent in a wave) and made the GELU
+// backward passes VALU-bound (~100 instructions per element); this is ~15, all full-rate but one
+// v_exp and one v_rcp.
+__device__ __forceinline__ float gelu_grad(float x) {
+  const float z = fabsf(x) * 0.70710678118654752f;
+  const float t = __frcp_rn(1.f + 0.3275911f * z);
+  const float poly = t * (0.254829592f + t * (-0.284496736f + t * (1.421413741f + t * (-1.453152027f + t * 1.061405429f))));
+  const float e = __expf(-0.5f * x * x);
+  const float tail = 0.5f * poly * e;                  // 1 - Phi(|x|)
+  const float cdf = x >= 0.f ? 1.f - tail : tail;
+  return cdf + x * (e * 0.39894228040143268f);
+}
+
 // ---------------------------------------------------------------- dropout RNG
 __device__ __forceinline__ uint32_t mix32(uint32_t x) {
   x ^= x >> 16;

@@ -177,9 +177,7 @@ __global__ __launch_bounds__(256) void gelu_bwd_k(const T* __restrict__ f, const
 #pragma unroll
     for (int j = 0; j < VEC; ++j) {
       const float x = to_f(a.v[j]);
-      const float cdf = 0.5f * (1.f + erff(x * 0.70710678118654752f));
-      const float pdf = __expf(-0.5f * x * x) * 0.39894228040143268f;
-      o.v[j] = from_f<T>(to_f(d.v[j]) * (cdf + x * pdf));
+      o.v[j] = from_f<T>(to_f(d.v[j]) * gelu_grad(x));
     }
     stv<T, VEC>(df + i * VEC, o);
   }
@@ -334,6 +332,8 @@ int colsum_bands(int N, int F) {
 //         gelu_fwd_k (act may alias src: the activation-checkpoint recompute of GPT-2 then
 //         needs no GELU forward pass for the c_proj dW)
 // part == nullptr: no column sums (frozen / absent bias).
+// OP 2 = OP 1 that also writes the activation (act != nullptr), a separate instantiation so the
+// erff of that rebuild is not branched around per element when there is none
 template <typename T, int OP>
 __global__ __launch_bounds__(256) void bwd_colsum_k(const T* src, const T* __restrict__ aux,
                                                     T* __restrict__ out, float* __restrict__ part, int N, int F,
@@ -359,12 +359,10 @@ __global__ __launch_bounds__(256) void bwd_colsum_k(const T* src, const T* __res
 #pragma unroll
       for (int j = 0; j < VEC; ++j) {
         const float x = to_f(a.v[j]);
-        const float cdf = 0.5f * (1.f + erff(x * 0.70710678118654752f));
-        const float pdf = __expf(-0.5f * x * x) * 0.39894228040143268f;
-        o.v[j] = from_f<T>(to_f(v.v[j]) * (cdf + x * pdf));
-        g.v[j] = from_f<T>(0.5f * x * (1.f + erff(x * 0.70710678118654752f)));
+        o.v[j] = from_f<T>(to_f(v.v[j]) * gelu_grad(x));
+        if constexpr (OP == 2) g.v[j] = from_f<T>(0.5f * x * (1.f + erff(x * 0.70710678118654752f)));   // = gelu_fwd
       }
-      if (act) st16(act + e, g);
+      if constexpr (OP == 2) st16(act + e, g);
     }
     st16(out + e, o);
     if (!part) return;
@@ -384,14 +382,14 @@ __global__ __launch_bounds__(256) void bwd_colsum_k(const T* src, const T* __res
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       v[k] = ld16(src + (long)(r + k) * F + cv * VEC);
-      if constexpr (OP == 1) a[k] = ld16(aux + (long)(r + k) * F + cv * VEC);
+      if constexpr (OP >= 1) a[k] = ld16(aux + (long)(r + k) * F + cv * VEC);
     }
 #pragma unroll
     for (int k = 0; k < 4; ++k) row(r + k, v[k], a[k]);
   }
   for (; r < r1; ++r) {
     Vec16<T> v = ld16(src + (long)r * F + cv * VEC), a;
-    if constexpr (OP == 1) a = ld16(aux + (long)r * F + cv * VEC);
+    if constexpr (OP >= 1) a = ld16(aux + (long)r * F + cv * VEC);
     row(r, v, a);
   }
   if (!part) return;
@@ -413,8 +411,12 @@ void bwd_bias_grad(DType dt, DType odt, int op, const void* src, const void* aux
       hipLaunchKernelGGL((bwd_colsum_k<T, 0>), grid, dim3(256), 0, s, (const T*)src, (const T*)aux, (T*)out, part, N, F,
                          rows_per, seed, offset, thr, inv_keep, (T*)nullptr);
     else
-      hipLaunchKernelGGL((bwd_colsum_k<T, 1>), grid, dim3(256), 0, s, (const T*)src, (const T*)aux, (T*)out, part, N, F,
-                         rows_per, seed, offset, thr, inv_keep, (T*)act);
+      if (act)
+        hipLaunchKernelGGL((bwd_colsum_k<T, 2>), grid, dim3(256), 0, s, (const T*)src, (const T*)aux, (T*)out, part, N,
+                           F, rows_per, seed, offset, thr, inv_keep, (T*)act);
+      else
+        hipLaunchKernelGGL((bwd_colsum_k<T, 1>), grid, dim3(256), 0, s, (const T*)src, (const T*)aux, (T*)out, part, N,
+                           F, rows_per, seed, offset, thr, inv_keep, (T*)nullptr);
   });
   if (part) col_reduce(part, odt, db, P, F, accumulate, s);
 }
