@@ -8,7 +8,7 @@
 namespace bllm {
 
 // norms.hip
-int norm_bwd_num_wg(int N);
+int norm_bwd_num_wg(int N, int d);
 int norm_max_dim(DType dt);
 void rmsnorm_fwd(DType dt, const void* x, const void* w, void* y, float* rstd, int N, int d, float eps, hipStream_t s);
 void layernorm_fwd(DType dt, const void* x, const void* w, const void* b, void* y, float* mean, float* rstd, int N,

@@ -87,7 +87,7 @@ std::tuple<Tensor, Tensor> rmsnorm_bwd(const Tensor& dy, const Tensor& x, const 
     acc = dx_acc->data_ptr();
   }
   auto dx = at::empty_like(x);
-  const int nwg = bllm::norm_bwd_num_wg(N);
+  const int nwg = bllm::norm_bwd_num_wg(N, d);
   auto part = at::empty({nwg, d}, x.options().dtype(at::kFloat));
   Tensor dw = vec_out(dw_out, x, d, "dw_out");
   bllm::rmsnorm_bwd(dt_of(x), dy.data_ptr(), x.data_ptr(), w.data_ptr(), rstd.data_ptr<float>(), acc, dx.data_ptr(),
@@ -127,7 +127,7 @@ std::tuple<Tensor, Tensor, Tensor> layernorm_bwd(const Tensor& dy, const Tensor&
     acc = dx_acc->data_ptr();
   }
   auto dx = at::empty_like(x);
-  const int nwg = bllm::norm_bwd_num_wg(N);
+  const int nwg = bllm::norm_bwd_num_wg(N, d);
   auto pw = at::empty({nwg, d}, x.options().dtype(at::kFloat));
   auto pb = at::empty({nwg, d}, x.options().dtype(at::kFloat));
   TORCH_CHECK(dw_out.has_value() == db_out.has_value(), "layernorm_bwd: give both dw_out and db_out or neither");
