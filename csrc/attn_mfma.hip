@@ -321,26 +321,45 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd_mfma_k(const T* __restrict_
         // keys (r, r+1) with r even are adjacent: one hash serves both when the row base is even.
         // The keep bits also go to the backward's mask (bit (r&3) + 8(r>>2) + 4hh of the word of
         // this query and 32-key sub-tile; the two lane halves' bits are merged by one swap).
+        // Element e0 + o (o = (r&3) + 8(r>>2) <= 27) of this sub-tile row is hashed as pair
+        // pb + off: the 64-bit base and both candidate window seeds are formed once per sub-tile,
+        // each pair then costs a 32-bit add, a carry select and one mix32 (same values as
+        // DropSlab::pair_hash: the low word wraps at most once, into the next window).
         const uint64_t rowbase = dslab + (uint64_t)qi[u] * T_;
 #pragma unroll
         for (int kt = 0; kt < NV; ++kt) {
           uint32_t kbits = 0;
-          if (dpair) {
+          const uint64_t e0 = rowbase + (uint64_t)(k0 + kt * 32 + 4 * hh);
+          const uint32_t plo = (uint32_t)(e0 >> 1), phi = (uint32_t)(e0 >> 33);
+          const uint32_t smA = phi == ds.hi0 ? ds.sm0 : ds.sm1;
+          const uint32_t smB = phi + 1u == ds.hi0 ? ds.sm0 : ds.sm1;
+          auto hash_at = [&](uint32_t off) {
+            const uint32_t lo = plo + off;
+            return mix32(lo ^ (lo < plo ? smB : smA));
+          };
+          if (dpair) {  // e0 even: keys (r, r+1) share pair pb + o/2
 #pragma unroll
             for (int r = 0; r < 16; r += 2) {
-              const int key = k0 + kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
-              const uint32_t hv = ds.pair_hash((rowbase + key) >> 1);
+              const uint32_t hv = hash_at((uint32_t)(((r & 3) + 8 * (r >> 2)) >> 1));
               const bool k0b = (hv & 0xFFFFu) >= thr, k1b = (hv >> 16) >= thr;
               s[u][kt][r] = k0b ? s[u][kt][r] * inv_keep : 0.f;
               s[u][kt][r + 1] = k1b ? s[u][kt][r + 1] * inv_keep : 0.f;
               kbits |= ((uint32_t)k0b << ((r & 3) + 8 * (r >> 2))) |
                        ((uint32_t)k1b << (((r + 1) & 3) + 8 * (r >> 2)));
             }
-          } else {
+          } else {  // odd T or offset: element e0 + o is half (o+par)&1 of pair pb + (o+par)/2
+            const int par = (int)(e0 & 1);
+            uint32_t hv[4][3];
+#pragma unroll
+            for (int g = 0; g < 4; ++g)
+#pragma unroll
+              for (int j = 0; j < 3; ++j) hv[g][j] = hash_at((uint32_t)(4 * g + j));
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-              const int key = k0 + kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
-              const bool kb_ = ds.bits16(rowbase + key) >= thr;
+              const int cr = r & 3;  // compile-time hash indices; par picks between them
+              const uint32_t h = par ? hv[r >> 2][(cr + 1) >> 1] : hv[r >> 2][cr >> 1];
+              const bool hi = par ? ((cr + 1) & 1) : (cr & 1);
+              const bool kb_ = (hi ? (h >> 16) : (h & 0xFFFFu)) >= thr;
               s[u][kt][r] = kb_ ? s[u][kt][r] * inv_keep : 0.f;
               kbits |= (uint32_t)kb_ << ((r & 3) + 8 * (r >> 2));
             }
