@@ -464,17 +464,20 @@ bool attn_mfma_head_dim(int hd) { return hd == 64 || hd == 128; }
 // 2 WGs/CU, one 32-query block per wave (round-2 default); 1 = 32-key tiles, 3-slot ring;
 // 2 = 32-key tiles, 2-slot ring (up to 3 WGs/CU); 4 = two 32-query blocks per wave (QB = 2),
 // 64-key tiles (hd 64), 32-key tiles at hd 128 (register budget of 2 waves per SIMD);
-// 5 = QB = 2 with 64-key tiles and one workgroup per CU at hd 128
-static int fwd_variant_from_env() {
+// 5 = QB = 2 with 64-key tiles and one workgroup per CU at hd 128.
+// Unset: variant 2 for hd 64 with dropout on grids of >= 2048 workgroups (GPT2-774M B=24:
+// 0.179 -> 0.163 ms -- the hash work wants the third co-resident workgroup), else variant 0.
+static int fwd_variant_from_env(int hd, float p, long nwg) {
   const char* e = getenv("BLLM_ATTN_FWD_VARIANT");
-  return e ? atoi(e) : 0;
+  if (e) return atoi(e);
+  return (hd == 64 && p > 0.f && nwg >= 2048) ? 2 : 0;
 }
 
 void attn_fwd_mfma(DType dt, const void* qkv, void* o, float* lse, int B, int T_, int H, int G, int hd, bool causal,
                    float p, uint64_t seed, uint64_t offset, uint32_t* keep_mask, hipStream_t s) {
   const uint32_t thr = drop_threshold16(p);
   const float ik = drop_inv_keep(p);
-  const int fwd_variant = fwd_variant_from_env();
+  const int fwd_variant = fwd_variant_from_env(hd, p, (long)((T_ + FWD_BQ - 1) / FWD_BQ) * H * B);
 #define LAUNCH_V(TT, HDD, BK, NB, OC, QBB)                                                                \
   do {                                                                                                        \
     const int lds = NB * 2 * BK * HDD * 2;                                                                    \

@@ -276,6 +276,20 @@ def test_flash_attention_deferred_rescale(dt, hd, step):
     _close(dqkv, dqkv0, dt, 4, name="dqkv")
 
 
+@pytest.mark.parametrize("variant", ["1", "2"])
+@pytest.mark.parametrize("hd", [64, 128])
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_flash_attention_fwd_variants(variant, hd, p, monkeypatch):
+    """The 32-key-tile forwards (BLLM_ATTN_FWD_VARIANT 1 / 2; 2 is the default for large hd-64
+    dropout grids) against the oracle, and their keep-mask words equal the oracle's hash."""
+    monkeypatch.setenv("BLLM_ATTN_FWD_VARIANT", variant)
+    for B, T, H, G in ((2, 33, 4, 2), (1, 300, 4, 2), (2, 256, 4, 4)):
+        test_flash_attention(torch.bfloat16, B, T, H, G, hd, p, True)
+        test_flash_attention(torch.bfloat16, B, T, H, G, hd, p, False)
+        if p > 0:
+            test_flash_attention_keep_mask(hd, B, T, H, G, True)
+
+
 def test_flash_attention_fp32_is_flash_not_materialised():
     """GPT-2 in the reference's default fp32 (args.py:77) at T = 4096, 12 heads: the fp32 kernels'
     footprint is O(T) -- the materialised oracle would need 12 x 4096^2 x 4 B = 805 MB per sequence."""

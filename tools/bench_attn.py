@@ -45,6 +45,7 @@ def main():
               ("gpt2-774M-nodrop", 4, 1024, 20, 20, 64, 0.0),
               ("gpt2-774M-B24", 24, 1024, 20, 20, 64, 0.1),
               ("gpt2-774M-B24-nodrop", 24, 1024, 20, 20, 64, 0.0),
+              ("gpt2-774M-B64", 64, 1024, 20, 20, 64, 0.1),
               ("gpt2-124M", 4, 1024, 12, 12, 64, 0.0)]
     if a.shapes:
         keep = a.shapes.split(",")
@@ -80,11 +81,14 @@ def main():
             for v in vs:
                 t_med = sorted(times[v])[len(times[v]) // 2]
                 same = all(torch.equal(x, y) for x, y in zip(outs[v][1:], outs[v0][1:]))
+                mask_same = len(outs[v]) < 3 or torch.equal(outs[v][2], outs[v0][2])
+                lse_err = (outs[v][1] - outs[v0][1]).abs().max().item()
                 err = ((outs[v][0].float() - outs[v0][0].float()).norm() / outs[v0][0].float().norm()).item()
                 print(json.dumps(dict(shape=name, fwd_variant=v, fwd_ms_med=round(t_med, 4),
                                       fwd_ms_all=[round(x, 4) for x in times[v]],
                                       fwd_tflops=round(flop / t_med / 1e9, 1),
-                                      rel_err_vs_first=err, lse_mask_equal=same)))
+                                      rel_err_vs_first=err, lse_mask_equal=same, keep_mask_equal=mask_same,
+                                      lse_max_abs_diff=lse_err)))
         res.append(dict(shape=name, B=B, T=T, causal=causal, keep_mask=km is not None, fwd_ms=round(tf, 4), bwd_ms=round(tb, 4),
                         fwd_tflops=round(flop / tf / 1e9, 1), bwd_tflops_5mm=round(2.5 * flop / tb / 1e9, 1)))
     for r in res:
