@@ -115,6 +115,10 @@ def parse(argv=None):
     ap.add_argument("--profile", action="store_true", help="print a per-phase timing breakdown to stderr")
     ap.add_argument("--overlap_optimizer", action="store_true",
                     help="run AdamW on a side HIP stream under the next forward")
+    ap.add_argument("--data", default=None, choices=["pretrain", "random_ids", "alpaca"],
+                    help="pretrain (default for pretraining presets): synthetic Gutenberg text -> offline "
+                         "tokenizer -> memmap cache -> DataloaderPT windows (DistributedSampler at N>1), the "
+                         "reference's data path; random_ids: device-resident random token ids (A/B only)")
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
                     help="cpu: tiny config on gloo (distributed plumbing check, not a measurement)")
     ap.add_argument("--pg_timeout_min", type=float, default=20.0)
@@ -211,6 +215,69 @@ def alpaca_loader(a, cfg, rank, world):
     return forever()
 
 
+def pretrain_loader(a, cfg, dist, rank, world):
+    """The reference's pretraining data path (train.py:162-172, datautils/dataloader.py:42-62):
+    synthetic Gutenberg-shaped text (data/synthetic.py, ``combined_1.txt`` format) + " <eos> ",
+    tokenised ONCE into the uint32 memmap cache by rank 0 before the timer (the other ranks map
+    it), split 90/10 by characters, DatasetPT windows with stride = context, and a
+    DistributedSampler over the N ranks (set_epoch per pass).  Returns (batch iterator,
+    description, sampler-order function for the disjointness check)."""
+    import tempfile
+
+    from building_llm_from_scratch_amd.data.loaders import DataloaderPT
+    from building_llm_from_scratch_amd.data.synthetic import make_gutenberg_corpus
+    from building_llm_from_scratch_amd.data.tokenizer import build_tokenizer
+    from building_llm_from_scratch_amd.utils.misc import read_text_file
+    B, T = a.batch_size, a.seq_len
+    # enough text for every timed + warm-up window of every rank (byte tokenizer: ~1 token per
+    # character; BPE would give fewer tokens and the sampler simply starts another epoch)
+    need = (a.warmup + a.steps + 4) * B * (T + 1) * world / 0.9
+    mb = round(min(256.0, max(0.5, need / 2 ** 20 * 1.05)), 2)
+    root = os.path.join(tempfile.gettempdir(), f"bllm_bench_gutenberg_{os.getuid()}_{mb}mb")
+    path = os.path.join(root, "combined_1.txt")
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if local == 0 and not os.path.exists(path):
+        tmp = f"{root}.{os.getpid()}.tmp"
+        make_gutenberg_corpus(tmp, n_files=1, mb_per_file=mb, seed=123)
+        os.makedirs(root, exist_ok=True)
+        os.replace(os.path.join(tmp, "combined_1.txt"), path)
+        os.rmdir(tmp)
+    dist.barrier()
+    tok = build_tokenizer(a.model, cfg, None)
+    ldr = DataloaderPT(tok, batch_size=B, max_length=T, stride=T, eos_text=cfg.eos_text,
+                       run_type="multi_gpu" if world > 1 else "single_gpu", cache_dir=os.path.join(root, "tokens"))
+    text = read_text_file(path) + " " + cfg.eos_text + " "
+    if rank == 0:
+        ldr.create_dataloaders(text, num_workers=0)      # fills the memmap cache
+    dist.barrier()
+    train, _ = ldr.create_dataloaders(text, num_workers=0, generator=torch_gen(1000 + rank))
+    n_tok = train.dataset.tokens.numel()
+
+    def forever():
+        ep = 0
+        while True:
+            if hasattr(train.sampler, "set_epoch"):
+                train.sampler.set_epoch(ep)
+            yield from train
+            ep += 1
+
+    def order(epoch=0):   # window indices this rank consumes in ``epoch``, in order
+        if hasattr(train.sampler, "set_epoch"):
+            train.sampler.set_epoch(epoch)
+        return list(iter(train.sampler))
+    desc = (f"synthetic Gutenberg-shaped text ({mb} MB, data/synthetic.py) -> {type(tok).__name__} "
+            f"({n_tok} train tokens, memmap cache) -> DataloaderPT windows (stride {T}) -> "
+            + ("DistributedSampler over %d ranks" % world if world > 1 else "shuffled sampler (1 rank)"))
+    return forever(), desc, order, len(train.dataset)
+
+
+def torch_gen(seed):
+    import torch
+    g = torch.Generator()
+    g.manual_seed(seed)
+    return g
+
+
 def _free_port() -> int:
     import socket
     with socket.socket() as s:
@@ -273,7 +340,10 @@ def main(argv=None):
     torch.manual_seed(123)
     plan = None
     ckpt_mode = "selective" if a.actv_ckpt == "auto" else a.actv_ckpt
-    model = build_model(cfg, use_actv_ckpt=ckpt_mode, device=dev)
+    # built on the meta device: every engine initialises the weights unit by unit on this rank's
+    # device under per-unit seeds (models/base.py:init_unit_), so no rank materialises the whole
+    # model and nothing is broadcast (FSDP keeps only its shard of each unit)
+    model = build_model(cfg, use_actv_ckpt=ckpt_mode, device="meta")
     if a.ckpt_segments:
         model.set_actv_ckpt(a.actv_ckpt, a.ckpt_segments)
     B, T = a.batch_size, a.seq_len
@@ -293,8 +363,15 @@ def main(argv=None):
                           reshard_after_forward=bool(a.reshard_after_forward), prefetch=a.fsdp_prefetch)
     opt = FusedAdamW(model, lr=3e-4, weight_decay=0.1, engine=engine, overlap=a.overlap_optimizer)
 
+    data_desc, sampler_order, n_windows = None, None, None
     if a.data == "alpaca":
         batches = alpaca_loader(a, cfg, rank, world)
+
+        def next_batch(i):
+            x, y = next(batches)
+            return x.to(dev, non_blocking=True), y.to(dev, non_blocking=True)
+    elif a.data == "pretrain":
+        batches, data_desc, sampler_order, n_windows = pretrain_loader(a, cfg, dist, rank, world)
 
         def next_batch(i):
             x, y = next(batches)
@@ -336,9 +413,12 @@ def main(argv=None):
                 plan = new
                 model.set_block_modes(plan.modes)
                 torch.cuda.reset_peak_memory_stats(dev)
+    comm = getattr(engine, "comm", None)
     sync()
     dist.barrier()
     sync()
+    if comm is not None:
+        comm.reset(enabled=True)     # exposed collective waits of the timed steps only
     tokens = 0
     t0 = time.perf_counter()
     for i in range(a.steps):
@@ -347,9 +427,14 @@ def main(argv=None):
     dist.barrier()
     sync()
     elapsed = time.perf_counter() - t0
+    comm_by_kind = comm.summary() if comm is not None else {}
+    if comm is not None:
+        comm.enabled = False
+    comm_ms = sum(v["ms"] for v in comm_by_kind.values()) / a.steps
     peak = float(torch.cuda.max_memory_allocated(dev)) if cuda else 0.0
-    # every rank's (time, tokens, peak): rank 0 reports the max time, the token sum and the spread
-    mine = torch.tensor([elapsed, float(tokens), peak], device=dev, dtype=torch.float64)
+    # every rank's (time, tokens, peak, exposed comm ms/step): rank 0 reports the max time, the
+    # token sum and the spread
+    mine = torch.tensor([elapsed, float(tokens), peak, comm_ms], device=dev, dtype=torch.float64)
     allr = [torch.zeros_like(mine) for _ in range(world)]
     dist.all_gather(allr, mine)
     per_rank = torch.stack(allr).cpu().tolist()
@@ -366,6 +451,21 @@ def main(argv=None):
     # recomputed blocks only (checkpoint_sequential leaves the last segment un-checkpointed)
     extra = cfg.recompute_flops_per_token(int(round(T_eff))) * n_ckpt / cfg.n_layers
     recompute = (flops_tok + extra) / flops_tok
+    # data sharding check: the windows each rank consumed in the first pass of the sampler
+    data_check = None
+    if sampler_order is not None:
+        per = a.batch_size * (a.warmup + a.steps)
+        mine_w = sampler_order(0)[:per]
+        allw = [None] * world
+        dist.all_gather_object(allw, mine_w)
+        sets = [set(w) for w in allw]
+        union = set().union(*sets)
+        data_check = {"sampler": "DistributedSampler" if world > 1 else "RandomSampler",
+                      "windows": n_windows, "windows_per_rank_used": len(mine_w),
+                      "disjoint_across_ranks": len(union) == sum(len(x) for x in sets)
+                      or per * world > n_windows}
+    comm_kinds = [None] * world
+    dist.all_gather_object(comm_kinds, comm_by_kind)
     prof = profile_phases(model, opt, next_batch, dev) if (a.profile and rank == 0 and cuda) else None
     if rank == 0:
         headline = a.preset == "llama3_8b_fsdp" and cuda and not a.layers
@@ -403,8 +503,9 @@ def main(argv=None):
             "vs_baseline": (tps / BASELINE_TOKENS_PER_S) if BASELINE_TOKENS_PER_S else None,
             "dtype": dtype,
             "data": ("synthetic Alpaca-shaped records, offline byte tokenizer, reference collate (variable T)"
-                     if a.data == "alpaca" else "synthetic token ids (Gutenberg-pretraining shape)")
-                    + ", random-init weights",
+                     if a.data == "alpaca" else (data_desc if a.data == "pretrain"
+                                                 else "synthetic random token ids (Gutenberg-pretraining shape)"))
+                    + ", random-init weights (seeded per unit, meta-built)",
             "config": {
                 "model": name + (f" ({cfg.n_layers} layers, INVALID)" if a.layers else "")
                 + ("" if cuda else " (tiny cpu config, INVALID as a measurement)"),
@@ -432,8 +533,18 @@ def main(argv=None):
             "per_rank": {"ms_per_step_min": round(1000 * min(r[0] for r in per_rank) / a.steps, 2),
                          "ms_per_step_max": round(ms, 2),
                          "ms_per_step": [round(1000 * r[0] / a.steps, 2) for r in per_rank],
-                         "peak_mem_gib": [gib(r[2]) for r in per_rank] if cuda else None},
+                         "peak_mem_gib": [gib(r[2]) for r in per_rank] if cuda else None,
+                         "comm_exposed_ms": [round(r[3], 3) for r in per_rank]},
+            # per-step time each rank's compute stream sat waiting on a collective (parallel/
+            # commstats.py); max over ranks.  0 at world 1 (no-shard engines issue none)
+            "comm_exposed_ms": round(max(r[3] for r in per_rank), 3),
+            "comm": {"by_kind_rank0": comm_kinds[0],
+                     "fsdp_prefetch": getattr(engine, "prefetch", None) if a.parallel == "fsdp" else None,
+                     "bucket_mib": getattr(engine, "bucket_mb", None),
+                     "deferred_init": bool(getattr(engine, "deferred_init", False))},
         }
+        if data_check is not None:
+            out["data_check"] = data_check
         if getattr(engine, "prefetch", None) is not None and not getattr(engine, "no_shard", True):
             out["config"]["fsdp_prefetch"] = engine.prefetch
         if plan is not None:

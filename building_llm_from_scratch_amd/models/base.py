@@ -32,6 +32,13 @@ import torch.nn as nn
 
 from .flat import FlatUnit
 
+DEFAULT_INIT_SEED = 123   # the reference's set_seed(123) (utils.py:55)
+
+
+def unit_seed(seed: int, index: int) -> int:
+    """Seed of unit ``index`` in a meta-built model's per-unit initialisation."""
+    return (int(seed) * 1_000_003 + 7919 * (index + 1)) % (2 ** 63)
+
 
 class LocalEngine:
     """No-op distributed engine (single process)."""
@@ -279,6 +286,8 @@ class _HeadLogitsFn(torch.autograd.Function):
 class BaseLM(nn.Module):
     """Common machinery for GPTModel / Llama models."""
 
+    init_seed = DEFAULT_INIT_SEED   # seed of the per-unit init of a meta-built model
+
     def __init__(self, cfg, use_actv_ckpt=False):
         super().__init__()
         self.cfg = cfg
@@ -342,12 +351,21 @@ class BaseLM(nn.Module):
         return self._comps
 
     # -- flat storage ------------------------------------------------------------------
-    def flatten(self, device=None, dtype=None, pad_to: int = 1, grad_dtype=None, arena=None):
+    def flatten(self, device=None, dtype=None, pad_to: int = 1, grad_dtype=None, arena=None, on_unit=None,
+                init_seed: Optional[int] = None):
         """(Re)build every unit's flat buffers from the current parameters (call after
         LoRA replacement / weight loading; idempotent).  ``arena`` (optional) maps a unit
         index to ``(param_view, grad_view)`` slices of model-wide contiguous buffers that the
-        trainable flat must live in (DDP / ZeRO buckets)."""
+        trainable flat must live in (DDP / ZeRO buckets).
+
+        A model built on the ``meta`` device has no values yet: each unit is initialised right
+        after its flat is allocated, by its modules' own ``reset_parameters`` under a seed
+        derived from ``init_seed`` and the unit index (``init_unit_``) — the same values on every
+        rank, with no broadcast.  ``on_unit(unit)`` runs after each unit is built, BEFORE the
+        next one is allocated: FSDP shards and frees the unit there, so a rank never holds
+        more than one unit at full size."""
         p0 = next(self.parameters())
+        meta = any(p.is_meta for p in self.parameters())
         device = torch.device(device) if device is not None else p0.device
         dtype = dtype or p0.dtype
         comps = self.build_computes()
@@ -357,6 +375,10 @@ class BaseLM(nn.Module):
             u.flatten(c.layout(), device, dtype, pad_to=pad_to, grad_dtype=grad_dtype,
                       train_storage=ts, train_grad_storage=gs)
             c.bind(u)
+            if meta and device.type != "meta":   # (meta -> meta: shape-only plans, no values)
+                self.init_unit_(u, self.init_seed if init_seed is None else init_seed)
+            if on_unit is not None:
+                on_unit(u)
         object.__setattr__(self, "_comps", comps)
         object.__setattr__(self, "_anchor", torch.zeros((), device=device, requires_grad=True))
         self._after_flatten(device)
@@ -364,6 +386,24 @@ class BaseLM(nn.Module):
 
     def _after_flatten(self, device):
         pass
+
+    @torch.no_grad()
+    def init_unit_(self, unit: FlatUnit, seed: int = None):
+        """Seeded in-place initialisation of one unit's parameters: every module owning one of
+        them runs its ``reset_parameters`` (nn.Linear / nn.Embedding / nn.LayerNorm defaults,
+        RMSNorm ones, LoRA kaiming A / zero B), in module order, under
+        ``torch.manual_seed(unit_seed(seed, unit.index))``.  Deterministic per (seed, unit), so
+        every rank computes the same values for the units it shards."""
+        seed = self.init_seed if seed is None else seed
+        ids = {id(p) for fb in unit.buffers() for p in fb.params}
+        torch.manual_seed(unit_seed(seed, unit.index))
+        for mod in self.modules():
+            own = [p for p in mod.parameters(recurse=False) if id(p) in ids]
+            if not own:
+                continue
+            if not hasattr(mod, "reset_parameters"):
+                raise TypeError(f"{type(mod).__name__} has no reset_parameters: cannot initialise a meta-built model")
+            mod.reset_parameters()
 
     def _ensure_flat(self):
         if self._comps is None:

@@ -84,7 +84,10 @@ class FlatBuffer:
     def bind(self):
         """Re-point every parameter's ``.data`` at its view (and ``.grad`` if allocated)."""
         for p in self.params:
-            p.data = self.view(self.data, p)
+            if p.is_meta:   # set_data cannot change a tensor's device type: swap the impl in place
+                torch.utils.swap_tensors(p, nn.Parameter(self.view(self.data, p), requires_grad=p.requires_grad))
+            else:
+                p.data = self.view(self.data, p)
             if self.grad is not None:
                 p.grad = self.view(self.grad, p)
 
@@ -127,7 +130,8 @@ class FlatUnit:
                 continue
             with torch.no_grad():
                 for p in fb.params:
-                    fb.view(fb.data, p).copy_(p.data.to(device=device, dtype=dtype))
+                    if not p.is_meta:   # meta-built model: values come from BaseLM.init_unit_
+                        fb.view(fb.data, p).copy_(p.data.to(device=device, dtype=dtype))
                     self._owner[id(p)] = fb
             fb.bind()
         if self.train is not None:

@@ -37,6 +37,10 @@ class RMSNorm(nn.Module):
         self.emb_dim = emb_dim
         self.weight = nn.Parameter(torch.ones(emb_dim, dtype=dtype, device=device))
 
+    def reset_parameters(self):   # (seeded per-unit init of a meta-built model, base.py:init_unit_)
+        with torch.no_grad():
+            self.weight.fill_(1.0)
+
     def forward(self, x):  # reference-style eager path (used only by tests / users)
         xf = x.float()
         y = xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + self.eps)

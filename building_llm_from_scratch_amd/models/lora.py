@@ -25,8 +25,13 @@ class LoRALayer(nn.Module):
         self.alpha = alpha
         self.scaling = alpha / rank
         self.A = nn.Parameter(torch.empty(in_dim, rank, dtype=dtype, device=device))
-        nn.init.kaiming_uniform_(self.A, a=math.sqrt(5))
         self.B = nn.Parameter(torch.zeros(rank, out_dim, dtype=dtype, device=device))
+        self.reset_parameters()
+
+    def reset_parameters(self):
+        nn.init.kaiming_uniform_(self.A, a=math.sqrt(5))
+        with torch.no_grad():
+            self.B.zero_()
 
     def forward(self, x):
         return self.scaling * (x @ self.A @ self.B)

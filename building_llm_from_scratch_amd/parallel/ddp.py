@@ -30,12 +30,17 @@ class DDPEngine(LocalEngine):
         self.rank = dist.get_rank(pg)
         self.model = model
         dtype = next(model.parameters()).dtype
+        # meta-built model: every rank initialises the same values (seeded per unit), no broadcast
+        self.deferred_init = any(p.is_meta for p in model.parameters())
         self.arena = Arena(model, device, dtype, self.world_size, bucket_mb * 2 ** 20)
+        self.bucket_mb = bucket_mb
+        from .commstats import CommStats
+        self.comm = CommStats(device)
         self.reduce_dtype = reduce_dtype if reduce_dtype not in (None, dtype) else None
         # a single rank has nothing to average with: no broadcast, no all-reduce (same hooks)
         from . import force_comm
         self.no_comm = self.world_size == 1 and not force_comm()
-        if broadcast and not self.no_comm:
+        if broadcast and not self.no_comm and not self.deferred_init:
             self._broadcast_params()
         self.grad_prescale = 1.0 / self.world_size
         self.sync_grads = True
@@ -80,7 +85,8 @@ class DDPEngine(LocalEngine):
                 if n > 0:  # units that saw no backward this step (e.g. frozen paths)
                     self._launch(b)
             for w, tmp, g in self._works:
-                w.wait()
+                with self.comm.waiting("all_reduce"):
+                    w.wait()
                 if tmp is not None:
                     g.copy_(tmp)
         self._works = []

@@ -71,14 +71,22 @@ class FSDPEngine(LocalEngine):
         self._prefetch_tokens = None
         self.grad_prescale = 1.0 / self.world_size
         self.is_cuda = self.device.type == "cuda"
+        from .commstats import CommStats
+        self.comm = CommStats(self.device)
         from . import force_comm
         self.no_shard = self.world_size == 1 and not force_comm()
         dtype = next(model.parameters()).dtype
         self.reduce_dtype = reduce_dtype if reduce_dtype not in (None, dtype) else None
-        model.flatten(device=device, dtype=dtype, pad_to=self.world_size * ALIGN)
-        self.units = model.units
+        # A model built on the meta device is initialised unit by unit inside flatten (seeded per
+        # unit: every rank computes the same values, models/base.py:init_unit_), and each unit is
+        # sharded and freed before the next is allocated: no rank ever holds the whole model and
+        # nothing is broadcast.  An eagerly built model (e.g. weights loaded on rank 0) is
+        # broadcast unit by unit from rank 0 instead.
+        meta = any(p.is_meta for p in model.parameters())
+        self.deferred_init = meta
         W, r = self.world_size, self.rank
-        for u in self.units:
+
+        def shard_unit(u):
             st = u.state
             st["bufs"] = []
             for fb in u.buffers():
@@ -90,7 +98,8 @@ class FSDPEngine(LocalEngine):
                         fb.grad_shard = fb.grad
                     st["bufs"].append(fb)
                     continue
-                dist.broadcast(fb.data, src=0, group=pg)          # identical init on every rank
+                if not meta:
+                    dist.broadcast(fb.data, src=0, group=pg)      # identical init on every rank
                 fb.shard = fb.data[r * n:(r + 1) * n].clone()
                 if fb is u.train:
                     fb.grad_shard = torch.zeros(n, dtype=fb.grad.dtype, device=device)
@@ -102,6 +111,9 @@ class FSDPEngine(LocalEngine):
             st["gathered"] = self.no_shard
             st["gather_work"] = None
             st["sharded"] = not self.no_shard   # read by FusedLinear._kaug_ok (no persistent W copies)
+
+        model.flatten(device=device, dtype=dtype, pad_to=self.world_size * ALIGN, on_unit=shard_unit)
+        self.units = model.units
         self._rs_works: List = []
         self._in_backward = False
         model.set_engine(self)
@@ -140,12 +152,14 @@ class FSDPEngine(LocalEngine):
     def _wait_gather(self, u):
         st = u.state
         if st["gather_work"] is not None:
-            for w in st["gather_work"]:
-                w.wait()
+            with self.comm.waiting("all_gather"):
+                for w in st["gather_work"]:
+                    w.wait()
             st["gather_work"] = None
             st["gathered"] = True
         if not st["gathered"]:
-            self._issue_gather(u, async_op=False)
+            with self.comm.waiting("all_gather"):
+                self._issue_gather(u, async_op=False)
 
     def _reshard(self, u):
         st = u.state
@@ -158,10 +172,23 @@ class FSDPEngine(LocalEngine):
         st["gathered"] = False
 
     def _size_prefetch(self):
-        rc = self.model.rctx
-        tokens = rc.B * rc.T
-        if tokens == self._prefetch_tokens:
+        """Size the auto prefetch depth ONCE, at the first training forward, from the MAX of the
+        ranks' token counts.  The depth decides how many all-gathers a rank issues before each
+        reduce-scatter in backward, so it must be identical on every rank: sizing from a rank's
+        own B*T (padded instruction batches differ per rank) would put the collectives of one
+        RCCL group in different orders on different ranks.  Every rank reaches its first
+        training forward at the same step (the loop is lockstep), so the one MAX all-reduce is
+        collective-safe; later shape changes keep the depth."""
+        if self._prefetch_tokens is not None:
             return
+        rc = self.model.rctx
+        if not (rc.grad_forward and self.model.training):
+            return
+        tokens = int(rc.B * rc.T)
+        if not self.no_shard and self.world_size > 1:
+            t = torch.tensor([tokens], dtype=torch.int64, device=self.device if self.is_cuda else "cpu")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.pg)
+            tokens = int(t.item())
         from .commplan import fsdp_prefetch_depth
         self._prefetch_tokens = tokens
         blocks = [u for u in self.units if u.name.startswith(("trf_blocks", "blocks"))] or self.units
@@ -172,7 +199,7 @@ class FSDPEngine(LocalEngine):
 
     # ------------------------------------------------------------------ hooks
     def pre_forward(self, unit):
-        if self.prefetch_auto and unit.index == 0:
+        if self.prefetch_auto and unit.index == 0 and self._prefetch_tokens is None:
             self._size_prefetch()
         self._wait_gather(unit)
         for nxt in range(unit.index + 1, min(unit.index + 1 + self.prefetch, len(self.units))):
@@ -226,7 +253,8 @@ class FSDPEngine(LocalEngine):
         without stalling the stream on the one just issued)."""
         while len(self._rs_works) > keep:
             w, fb, full, part = self._rs_works.pop(0)
-            w.wait()
+            with self.comm.waiting("reduce_scatter"):
+                w.wait()
             if part is not None:
                 fb.grad_shard.copy_(part)
             _free(fb.grad)
@@ -242,7 +270,8 @@ class FSDPEngine(LocalEngine):
 
     def all_reduce_grad_sq_norm(self, sq: torch.Tensor) -> torch.Tensor:
         if not self.no_shard:
-            dist.all_reduce(sq, group=self.pg)
+            with self.comm.waiting("all_reduce"):
+                dist.all_reduce(sq, group=self.pg)
         return sq
 
     # the next forward starts with the embedding (1 GiB bf16 for Llama-3-8B) and the first

@@ -31,11 +31,16 @@ class ZeroEngine(LocalEngine):
         self.rank = dist.get_rank(pg)
         self.model = model
         dtype = next(model.parameters()).dtype
+        # meta-built model: every rank initialises the same values (seeded per unit), no broadcast
+        self.deferred_init = any(p.is_meta for p in model.parameters())
         self.reduce_dtype = reduce_dtype if reduce_dtype not in (None, dtype) else None
         self.arena = Arena(model, device, dtype, self.world_size, bucket_mb * 2 ** 20)
+        self.bucket_mb = bucket_mb
+        from .commstats import CommStats
+        self.comm = CommStats(device)
         from . import force_comm
         self.no_comm = self.world_size == 1 and not force_comm()  # one rank: its shard is the whole bucket
-        if not self.no_comm:
+        if not self.no_comm and not self.deferred_init:
             dist.broadcast(self.arena.param, src=0, group=pg)
             for u in model.units:
                 if u.frozen is not None:
@@ -90,7 +95,8 @@ class ZeroEngine(LocalEngine):
             if n > 0:
                 self._launch(b)
         for w, b, full, part in self._works:
-            w.wait()
+            with self.comm.waiting("reduce_scatter"):
+                w.wait()
             if part is not None:
                 self.grad_shards[b].copy_(part)
         self._works = []
@@ -102,7 +108,8 @@ class ZeroEngine(LocalEngine):
 
     def all_reduce_grad_sq_norm(self, sq: torch.Tensor) -> torch.Tensor:
         if not self.no_comm:
-            dist.all_reduce(sq, group=self.pg)
+            with self.comm.waiting("all_reduce"):
+                dist.all_reduce(sq, group=self.pg)
         return sq
 
     def after_slot_update(self, slot):
@@ -119,7 +126,8 @@ class ZeroEngine(LocalEngine):
     def pre_forward(self, unit):
         b = self.arena.bucket_of.get(unit.index)
         if b is not None and b in self._ag_works:
-            self._ag_works.pop(b).wait()
+            with self.comm.waiting("all_gather"):
+                self._ag_works.pop(b).wait()
 
     def sync(self):
         for w in self._ag_works.values():

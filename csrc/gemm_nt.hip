@@ -690,11 +690,15 @@ __global__ __launch_bounds__(THREADS4, 1) void gemm_nt4p_k(const T* __restrict__
                                                            int F = 0, const float* __restrict__ cosT = nullptr,
                                                            const float* __restrict__ sinT = nullptr, int Tq = 1,
                                                            int nrot = 0, int group_m = GROUP_M,
-                                                           const OT* __restrict__ bias = nullptr) {
+                                                           const OT* __restrict__ bias = nullptr, int su = 0) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int wm = wave >> 1, wn = wave & 1;
   const int nbm = M / TM, nbn = N / TN, nblk = nbm * nbn, G = gridDim.x;
+  // K stagger: workgroup b walks its K-tiles starting at (b mod su) and wraps, so the 256
+  // co-running workgroups do not all stream the same 128-B column slice of their rows at once
+  // (rows of A and B are 2^k bytes apart: same-offset reads camp on the same HBM channels)
+  const int kst0 = su > 0 ? (int)(blockIdx.x % (unsigned)su) % (K / TK) : 0;
   const int q8 = nblk >> 3, r8 = nblk & 7, per_group = group_m * nbn;
   auto coords = [&](int tid, long& m0, long& n0) {
     const int xcd = tid & 7;
@@ -753,7 +757,9 @@ __global__ __launch_bounds__(THREADS4, 1) void gemm_nt4p_k(const T* __restrict__
     const int p = k & 7;
     const uint32_t d = lds0 + (k >= 8 ? 2 * IMGB : 0) + buf * IMGB + (64 * wave + 8 * p) * ROWB;
     const bool nx = t >= nt;
-    const int tt = !nx ? t : (tid_n < nblk ? t - nt : nt - 1);
+    int tt = !nx ? t : (tid_n < nblk ? t - nt : nt - 1);
+    tt += kst0;
+    if (tt >= nt) tt -= nt;
     const T* base = k < 8 ? (nx ? An : Ac) : (nx ? Bn : Bc);
     if constexpr (DV == 0) {
       glds16s(sgpr_ptr(base + (long)tt * TK), k < 8 ? voA[p] : voB[p], d);
@@ -1050,13 +1056,16 @@ void launch(const void* a, long lda, const void* b, long ldb, void* c, long ldc,
     // 4 measured 0.3-12 % faster than 8 (16, 32 slower) on the Llama-3-8B / GPT2-774M shapes
     // (profiles/r3/gemm_nt4p_sv4_gm.jsonl)
     const int gmz = eg && atoi(eg) > 0 ? atoi(eg) : 4;
+    const char* es = getenv("BLLM_GEMM_NT4P_SU");   // K stagger (A/B)
+    const int su = es && *es ? atoi(es) : 0;
 #define BLLM_NT4P(ACCv, SVv, DVv)                                                                                       \
   do {                                                                                                                  \
     static const bool at_ = hipFuncSetAttribute((const void*)gemm_nt4p_k<T, OT, DVv, ACCv, SVv>,                        \
                                                 hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES) == hipSuccess; \
     (void)at_;                                                                                                          \
     hipLaunchKernelGGL((gemm_nt4p_k<T, OT, DVv, ACCv, SVv>), dim3(grid), dim3(THREADS4), LDS_BYTES, s, (const T*)a,   \
-                       lda, (const T*)b, ldb, (OT*)c, ldc, M, N, K, (OT*)nullptr, 0, nullptr, nullptr, 1, 0, gmz);  \
+                       lda, (const T*)b, ldb, (OT*)c, ldc, M, N, K, (OT*)nullptr, 0, nullptr, nullptr, 1, 0, gmz,   \
+                       (const OT*)nullptr, su);                                                                      \
   } while (0)
     // sv 5 / 6: schedule 0 with the pieces issued sc0 sc1 / nt (cache-policy A/B)
     if (accumulate) {

@@ -99,3 +99,31 @@ def test_bench_presets(preset, n):
         assert str(out["config"]["seq_len"]).startswith("variable")
     if preset == "llama2_7b_fsdp_mp":
         assert out["config"]["mixed_precision"] == "bf16"
+
+
+@pytest.mark.parametrize("parallel", ["fsdp", "ddp", "zero1"])
+def test_bench_world8_self_diagnosing_fields(parallel):
+    """World 8 (gloo): the line carries what a first multi-GPU run needs to be read —
+    every rank's exposed collective wait per step, the prefetch depth / bucket size the engine
+    chose, a meta-built (no broadcast) init — and the headline's data path is the reference's
+    (DataloaderPT windows through a DistributedSampler) with disjoint windows per rank."""
+    out = _run(8, ["--parallel", parallel], spawn=True)
+    assert len(out["per_rank"]["comm_exposed_ms"]) == 8
+    assert out["comm_exposed_ms"] == max(out["per_rank"]["comm_exposed_ms"]) and out["comm_exposed_ms"] > 0
+    kinds = out["comm"]["by_kind_rank0"]
+    if parallel == "fsdp":
+        assert out["comm"]["fsdp_prefetch"] >= 1 and kinds["all_gather"]["waits"] > 0
+        assert kinds["reduce_scatter"]["waits"] > 0 and kinds["all_reduce"]["waits"] == 2   # clip, per step
+    else:
+        assert out["comm"]["bucket_mib"] == 256.0
+    assert out["comm"]["deferred_init"] is True
+    assert "DataloaderPT" in out["data"] and "DistributedSampler over 8 ranks" in out["data"]
+    dc = out["data_check"]
+    assert dc["sampler"] == "DistributedSampler" and dc["disjoint_across_ranks"] is True
+    assert dc["windows_per_rank_used"] == 2 * 3    # micro-batch 2 x (1 warm-up + 2 timed steps)
+
+
+def test_bench_random_ids_arm():
+    """``--data random_ids``: the A/B arm with device-resident random token ids."""
+    out = _run(1, ["--data", "random_ids"])
+    assert out["data"].startswith("synthetic random token ids") and "data_check" not in out

@@ -113,8 +113,10 @@ def _full_size_worker(q):
                 assert s[("all_reduce", "clip")]["count"] == 1
             else:
                 assert ("all_reduce", "clip") not in s                        # grads replicated: local norm
-            # construction: one broadcast of the whole arena (X4), no per-forward buffer broadcast (X5)
-            assert [e["op"] for e in rec.log] == ["broadcast"]
+            # construction of a meta-built model: NO collective (every rank initialises the same
+            # values, seeded per unit; reference X4 broadcasts the whole model), and no
+            # per-forward buffer broadcast (X5)
+            assert rec.log == []
         # Llama-3-8B FSDP full shard, bf16, full checkpointing
         cfg = get_config("llama3", "8B").replace(dtype=torch.bfloat16)
         m = build_model(cfg, use_actv_ckpt="full", device="meta")
