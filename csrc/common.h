@@ -96,7 +96,9 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
 // v_exp and one v_rcp.
 __device__ __forceinline__ float gelu_grad(float x) {
   const float z = fabsf(x) * 0.70710678118654752f;
-  const float t = __frcp_rn(1.f + 0.3275911f * z);
+  // v_rcp_f32 (1 ulp): __frcp_rn lowers to the IEEE division sequence (div_scale / div_fmas /
+  // div_fixup, ~10 instructions), more than the rest of the function; A&S 7.1.26 is 1.5e-7 anyway
+  const float t = __builtin_amdgcn_rcpf(1.f + 0.3275911f * z);
   const float poly = t * (0.254829592f + t * (-0.284496736f + t * (1.421413741f + t * (-1.453152027f + t * 1.061405429f))));
   const float e = __expf(-0.5f * x * x);
   const float tail = 0.5f * poly * e;                  // 1 - Phi(|x|)

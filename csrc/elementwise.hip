@@ -10,25 +10,6 @@ namespace bllm {
 
 BLLM_DEBUG_WORD(elementwise)
 
-// BLLM_SWIGLU_ROWS=0 selects the grid-stride SwiGLU kernels (A/B tuning)
-static bool swiglu_rows() {
-  static const bool v = [] {
-    const char* e = getenv("BLLM_SWIGLU_ROWS");
-    return !(e && e[0] == '0');
-  }();
-  return v;
-}
-
-// BLLM_SWIGLU_U=2|4|8: 16-B load groups in flight per lane in the row-per-workgroup SwiGLU kernels (A/B)
-static int swiglu_u() {
-  static const int v = [] {
-    const char* e = getenv("BLLM_SWIGLU_U");
-    const int u = e ? atoi(e) : 4;
-    return (u == 2 || u == 8) ? u : 4;
-  }();
-  return v;
-}
-
 static inline int ew_grid(long nvec) {
   long g = (nvec + 255) / 256;
   return (int)(g < 2048 ? (g > 0 ? g : 1) : 2048);
@@ -280,68 +261,44 @@ __global__ __launch_bounds__(256) void rope_scalar_k(T* __restrict__ qkv, const 
 // bias grads (reference nn.Linear bias).  Pass 1: workgroup (x = 256 threads x 8-column
 // vectors, y = a row band) writes fp32 partial sums; pass 2 sums the bands in a fixed order and
 // writes / accumulates the gradient in its dtype (deterministic, no atomics).
-template <typename T>
-__global__ __launch_bounds__(256) void colsum_partial_k(const T* __restrict__ dy, float* __restrict__ part, int N,
-                                                        int F, int rows_per) {
-  constexpr int VEC = 16 / sizeof(T);
-  const int cv = blockIdx.x * 256 + threadIdx.x;   // column vector index
-  if (cv * VEC >= F) return;
-  const int r0 = blockIdx.y * rows_per, r1 = min(N, r0 + rows_per);
-  float acc[VEC];
-#pragma unroll
-  for (int j = 0; j < VEC; ++j) acc[j] = 0.f;
-  int r = r0;
-  for (; r + 4 <= r1; r += 4) {  // 4 independent 16-B loads in flight per lane
-    Vec16<T> v[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) v[k] = ld16(dy + (long)(r + k) * F + cv * VEC);
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-#pragma unroll
-      for (int j = 0; j < VEC; ++j) acc[j] += to_f(v[k].v[j]);
-  }
-  for (; r < r1; ++r) {
-    const Vec16<T> v = ld16(dy + (long)r * F + cv * VEC);
-#pragma unroll
-    for (int j = 0; j < VEC; ++j) acc[j] += to_f(v.v[j]);
-  }
-  float* o = part + (long)blockIdx.y * F + cv * VEC;
-#pragma unroll
-  for (int j = 0; j < VEC; ++j) o[j] = acc[j];
-}
-
 // row bands: narrow outputs (F <= 2048, e.g. GPT-2's 1280-wide biases: one 160-lane workgroup
 // per band) get 4x more bands so enough waves stream dy; partials stay small (1024 x F fp32)
 int colsum_bands(int N, int F) {
-  static const int small_cap = [] {  // BLLM_COLSUM_BANDS=<n> overrides the narrow-output cap (A/B)
-    const char* e = getenv("BLLM_COLSUM_BANDS");
-    const int n = e ? atoi(e) : 0;
-    return n > 0 ? n : 1024;
-  }();
-  const int cap = F <= 2048 ? small_cap : 256;
+  const int cap = F <= 2048 ? 1024 : 256;
   return N >= 16 * cap ? cap : (N + 15) / 16;
 }
 
 // Elementwise backward + bias-gradient column sums in one pass (GPT-2: the dropout backward in
 // front of the out_proj / c_proj bias grads, the GELU backward in front of the c_fc bias grad,
 // reference GPT2.py:58-62 + nn.Linear bias).  Same band split, per-lane row order and fp32
-// partials as colsum_partial_k over the rounded outputs (db within one ulp of its dtype of the separate path's);
-// the separate colsum pass's re-read of the [N, F] gradient is gone.
+// partials as the plain column sum (OP 3, bias_grad) over the rounded outputs, so db is bitwise
+// the separate path's; the separate colsum pass's re-read of the [N, F] gradient is gone.
 //   OP 0: out = dropout_bwd(src)  (keep bits by the counter hash at element index r * F + c)
 //   OP 1: out = src * gelu'(aux)   (exact erf GELU); with act, also act = gelu(aux), bitwise as
 //         gelu_fwd_k (act may alias src: the activation-checkpoint recompute of GPT-2 then
 //         needs no GELU forward pass for the c_proj dW)
+//   OP 3: column sums of src only (bias_grad: nothing stored but the partials)
 // part == nullptr: no column sums (frozen / absent bias).
 // OP 2 = OP 1 that also writes the activation (act != nullptr), a separate instantiation so the
-// erff of that rebuild is not branched around per element when there is none
+// erff of that rebuild is not branched around per element when there is none.
+// Mapping: each wave owns 64 column vectors (no partially filled workgroups at F = 1280 / 5120
+// bf16) and one quarter of the band's rows (rows r0 + w, r0 + w + 4, ...); the next group of
+// BR rows is loaded before the current one is processed (register double buffer), so every wave
+// keeps 2 x BR x (1 or 2) 16-B loads in flight instead of draining between groups (the
+// load-all / compute / store loop ran GPT2-774M's c_fc GELU backward at ~3 TB/s).  The four
+// waves' column sums meet in LDS; one fp32 partial row per band as before.
 template <typename T, int OP>
 __global__ __launch_bounds__(256) void bwd_colsum_k(const T* src, const T* __restrict__ aux,
                                                     T* __restrict__ out, float* __restrict__ part, int N, int F,
                                                     int rows_per, uint64_t seed, uint64_t offset, uint32_t thr,
                                                     float inv_keep, T* act) {
   constexpr int VEC = 16 / sizeof(T);
-  const int cv = blockIdx.x * 256 + threadIdx.x;
-  if (cv * VEC >= F) return;
+  constexpr int BR = 4;                      // rows per group per wave
+  constexpr bool AUX = OP == 1 || OP == 2;
+  __shared__ float red[4][64 * VEC];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int cv = blockIdx.x * 64 + lane;
+  const bool on = cv * VEC < F;
   const int r0 = blockIdx.y * rows_per, r1 = min(N, r0 + rows_per);
   float acc[VEC];
 #pragma unroll
@@ -349,7 +306,9 @@ __global__ __launch_bounds__(256) void bwd_colsum_k(const T* src, const T* __res
   auto row = [&](int r, const Vec16<T>& v, const Vec16<T>& a) {
     const long e = (long)r * F + cv * VEC;
     Vec16<T> o;
-    if constexpr (OP == 0) {
+    if constexpr (OP == 3) {
+      o = v;
+    } else if constexpr (OP == 0) {
       uint32_t bits[VEC];
       drop_bits_run<VEC>(seed, offset + (uint64_t)e, bits);
 #pragma unroll
@@ -364,38 +323,55 @@ __global__ __launch_bounds__(256) void bwd_colsum_k(const T* src, const T* __res
       }
       if constexpr (OP == 2) st16(act + e, g);
     }
-    st16(out + e, o);
-    if (!part) return;
+    if constexpr (OP != 3) st16(out + e, o);
 #pragma unroll
     for (int j = 0; j < VEC; ++j) {
       // opaque copy: for fp32 (from_f = identity) the compiler would otherwise fuse the output
       // product into the column sum (one FMA), skipping the rounding the stored output had --
-      // the sums are over the stored (rounded) values, as colsum_partial_k's
+      // the sums are over the stored (rounded) values, as the plain column sum (OP 3)
       float ov = to_f(o.v[j]);
       asm volatile("" : "+v"(ov));
       acc[j] += ov;
     }
   };
-  int r = r0;
-  for (; r + 4 <= r1; r += 4) {  // 4 independent row loads (x2 with the GELU input) in flight per lane
-    Vec16<T> v[4], a[4];
+  if (on) {
+    Vec16<T> v[BR], a[BR], vn[BR], an[BR];
+    auto load = [&](int rb, Vec16<T> (&dv)[BR], Vec16<T> (&da)[BR]) {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      v[k] = ld16(src + (long)(r + k) * F + cv * VEC);
-      if constexpr (OP >= 1) a[k] = ld16(aux + (long)(r + k) * F + cv * VEC);
+      for (int k = 0; k < BR; ++k) {
+        const int r = rb + 4 * k;            // wave-uniform
+        if (r < r1) {
+          dv[k] = ld16(src + (long)r * F + cv * VEC);
+          if constexpr (AUX) da[k] = ld16(aux + (long)r * F + cv * VEC);
+        }
+      }
+    };
+    int rb = r0 + w;
+    if (rb < r1) load(rb, v, a);
+    while (rb < r1) {
+      const int rn = rb + 4 * BR;
+      if (rn < r1) load(rn, vn, an);
+#pragma unroll
+      for (int k = 0; k < BR; ++k)
+        if (rb + 4 * k < r1) row(rb + 4 * k, v[k], a[k]);
+#pragma unroll
+      for (int k = 0; k < BR; ++k) {
+        v[k] = vn[k];
+        if constexpr (AUX) a[k] = an[k];
+      }
+      rb = rn;
     }
-#pragma unroll
-    for (int k = 0; k < 4; ++k) row(r + k, v[k], a[k]);
-  }
-  for (; r < r1; ++r) {
-    Vec16<T> v = ld16(src + (long)r * F + cv * VEC), a;
-    if constexpr (OP >= 1) a = ld16(aux + (long)r * F + cv * VEC);
-    row(r, v, a);
   }
   if (!part) return;
-  float* o = part + (long)blockIdx.y * F + cv * VEC;
 #pragma unroll
-  for (int j = 0; j < VEC; ++j) o[j] = acc[j];
+  for (int j = 0; j < VEC; ++j) red[w][lane * VEC + j] = acc[j];
+  __syncthreads();
+  if (w == 0 && on) {
+    float* o = part + (long)blockIdx.y * F + cv * VEC;
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) o[j] = ((red[0][lane * VEC + j] + red[1][lane * VEC + j]) + red[2][lane * VEC + j]) +
+                                         red[3][lane * VEC + j];
+  }
 }
 
 void bwd_bias_grad(DType dt, DType odt, int op, const void* src, const void* aux, void* out, float* part, void* db,
@@ -406,7 +382,7 @@ void bwd_bias_grad(DType dt, DType odt, int op, const void* src, const void* aux
   const float inv_keep = drop_inv_keep(p);
   BLLM_DISPATCH(dt, T, {
     constexpr int VEC = 16 / sizeof(T);
-    dim3 grid((F / VEC + 255) / 256, P);
+    dim3 grid((F / VEC + 63) / 64, P);
     if (op == 0)
       hipLaunchKernelGGL((bwd_colsum_k<T, 0>), grid, dim3(256), 0, s, (const T*)src, (const T*)aux, (T*)out, part, N, F,
                          rows_per, seed, offset, thr, inv_keep, (T*)nullptr);
@@ -428,8 +404,9 @@ void bias_grad(DType dt, DType odt, const void* dy, float* part, void* out, int 
   const int rows_per = (N + P - 1) / P;
   BLLM_DISPATCH(dt, T, {
     constexpr int VEC = 16 / sizeof(T);
-    dim3 grid((F / VEC + 255) / 256, P);
-    hipLaunchKernelGGL(colsum_partial_k<T>, grid, dim3(256), 0, s, (const T*)dy, part, N, F, rows_per);
+    dim3 grid((F / VEC + 63) / 64, P);
+    hipLaunchKernelGGL((bwd_colsum_k<T, 3>), grid, dim3(256), 0, s, (const T*)dy, (const T*)nullptr, (T*)nullptr,
+                       part, N, F, rows_per, 0ull, 0ull, 0u, 0.f, (T*)nullptr);
   });
   col_reduce(part, odt, out, P, F, accumulate, s);
 }
@@ -440,45 +417,29 @@ void bias_grad(DType dt, DType odt, const void* dy, float* part, void* out, int 
   if (cond) { constexpr int VEC = 16 / sizeof(T); __VA_ARGS__; } \
   else { constexpr int VEC = 1; __VA_ARGS__; }
 
+// row-per-workgroup kernels (4 16-B load groups in flight per lane) for the wide rows of the
+// Llama MLPs; the grid-stride kernels otherwise (narrow / odd rows, debug shapes)
 void swiglu_fwd(DType dt, const void* gu, void* act, long N, int F, hipStream_t s) {
   BLLM_DISPATCH(dt, T, {
     EW_VEC(T, F % (16 / sizeof(T)) == 0, {
-      if (swiglu_rows() && F / VEC >= 512 && N <= 0x7fffffffL) {
-        const int u = swiglu_u();
-        if (u == 2)
-          hipLaunchKernelGGL((swiglu_fwd_rows_k<T, VEC, 2>), dim3((unsigned)N), dim3(256), 0, s, (const T*)gu,
-                             (T*)act, F);
-        else if (u == 8)
-          hipLaunchKernelGGL((swiglu_fwd_rows_k<T, VEC, 8>), dim3((unsigned)N), dim3(256), 0, s, (const T*)gu,
-                             (T*)act, F);
-        else
-          hipLaunchKernelGGL((swiglu_fwd_rows_k<T, VEC, 4>), dim3((unsigned)N), dim3(256), 0, s, (const T*)gu,
-                             (T*)act, F);
-      } else {
+      if (F / VEC >= 512 && N <= 0x7fffffffL)
+        hipLaunchKernelGGL((swiglu_fwd_rows_k<T, VEC, 4>), dim3((unsigned)N), dim3(256), 0, s, (const T*)gu,
+                           (T*)act, F);
+      else
         hipLaunchKernelGGL((swiglu_fwd_k<T, VEC>), dim3(ew_grid(N * F / VEC)), dim3(256), 0, s, (const T*)gu,
                            (T*)act, N, F);
-      }
     });
   });
 }
 void swiglu_bwd(DType dt, const void* gu, const void* dact, void* dgu, void* act, long N, int F, hipStream_t s) {
   BLLM_DISPATCH(dt, T, {
     EW_VEC(T, F % (16 / sizeof(T)) == 0, {
-      if (swiglu_rows() && F / VEC >= 512 && N <= 0x7fffffffL) {
-        const int u = swiglu_u();
-        if (u == 2)
-          hipLaunchKernelGGL((swiglu_bwd_rows_k<T, VEC, 2>), dim3((unsigned)N), dim3(256), 0, s, (const T*)gu,
-                             (const T*)dact, (T*)dgu, (T*)act, F);
-        else if (u == 8)
-          hipLaunchKernelGGL((swiglu_bwd_rows_k<T, VEC, 8>), dim3((unsigned)N), dim3(256), 0, s, (const T*)gu,
-                             (const T*)dact, (T*)dgu, (T*)act, F);
-        else
-          hipLaunchKernelGGL((swiglu_bwd_rows_k<T, VEC, 4>), dim3((unsigned)N), dim3(256), 0, s, (const T*)gu,
-                             (const T*)dact, (T*)dgu, (T*)act, F);
-      } else {
+      if (F / VEC >= 512 && N <= 0x7fffffffL)
+        hipLaunchKernelGGL((swiglu_bwd_rows_k<T, VEC, 4>), dim3((unsigned)N), dim3(256), 0, s, (const T*)gu,
+                           (const T*)dact, (T*)dgu, (T*)act, F);
+      else
         hipLaunchKernelGGL((swiglu_bwd_k<T, VEC>), dim3(ew_grid(N * F / VEC)), dim3(256), 0, s, (const T*)gu,
                            (const T*)dact, (T*)dgu, (T*)act, N, F);
-      }
     });
   });
 }

@@ -665,11 +665,15 @@ __global__ __launch_bounds__(THREADS4, 1) void gemm_nt4_k(const T* __restrict__ 
 // RAW at 112; 2: as 1 with RAW at 120 (two reads per MFMA over the last 8); 3: as 0, RAW at 120.
 // 4: as 0 with the MFMA order j-major (the B fragment, MFMA src A, fixed over 8 consecutive MFMAs,
 // as in hipBLASLt's loop) and the fragment reads ordered to match (b[0], a[0..7], b[1..7]).
+// 5: the placement of gfx950 hipBLASLt's MT256x256x64 loop (read off its code object): WAR after
+// MFMA 25, pieces every 5 from 26, RAW before MFMA 106, next-fragment reads one per MFMA from there.
 template <int SV> struct Sched4 {
   static constexpr bool JMAJ = SV == 4;
-  static constexpr int WAR = (SV == 1 || SV == 2) ? 23 : 31;   // barrier after this MFMA
+  static constexpr int WAR = (SV == 1 || SV == 2) ? 23 : (SV == 5 ? 25 : 31);   // barrier after this MFMA
   static constexpr int D0 = WAR + 1, DS = (SV == 1 || SV == 2) ? 4 : 5;   // first piece, stride
-  static constexpr int RAW = (SV >= 2) ? 120 : 112;             // before this MFMA (of 128)
+  static constexpr int RAW = SV == 5 ? 106 : ((SV >= 2) ? 120 : 112);     // before this MFMA (of 128)
+  // next-tile fragment reads per MFMA from RAW on (1, or 2 when fewer than 16 MFMAs remain)
+  static constexpr int RPM = 128 - RAW >= 16 ? 1 : 16 / (128 - RAW);
   // piece index issued before/after MFMA m (0..127), -1 if none
   static constexpr int piece(int m) { return m >= D0 && (m - D0) % DS == 0 && (m - D0) / DS < 16 ? (m - D0) / DS : -1; }
 };
@@ -690,15 +694,11 @@ __global__ __launch_bounds__(THREADS4, 1) void gemm_nt4p_k(const T* __restrict__
                                                            int F = 0, const float* __restrict__ cosT = nullptr,
                                                            const float* __restrict__ sinT = nullptr, int Tq = 1,
                                                            int nrot = 0, int group_m = GROUP_M,
-                                                           const OT* __restrict__ bias = nullptr, int su = 0) {
+                                                           const OT* __restrict__ bias = nullptr) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int wm = wave >> 1, wn = wave & 1;
   const int nbm = M / TM, nbn = N / TN, nblk = nbm * nbn, G = gridDim.x;
-  // K stagger: workgroup b walks its K-tiles starting at (b mod su) and wraps, so the 256
-  // co-running workgroups do not all stream the same 128-B column slice of their rows at once
-  // (rows of A and B are 2^k bytes apart: same-offset reads camp on the same HBM channels)
-  const int kst0 = su > 0 ? (int)(blockIdx.x % (unsigned)su) % (K / TK) : 0;
   const int q8 = nblk >> 3, r8 = nblk & 7, per_group = group_m * nbn;
   auto coords = [&](int tid, long& m0, long& n0) {
     const int xcd = tid & 7;
@@ -751,22 +751,34 @@ __global__ __launch_bounds__(THREADS4, 1) void gemm_nt4p_k(const T* __restrict__
     }
   };
   set_next();
-  // piece k of K-tile t of the stream (t < nt: current tile; nt, nt+1: the next tile's 0, 1, or
-  // re-loads of the current tile's last K-tile when there is none) into buffer buf
-  auto dma = [&](int t, int buf, int k) {
+  // buffer descriptors of this wave's staged rows: current tile and next tile (uniform, built once
+  // per output tile, not per piece)
+  i32x4 srAc = g4::make_rsrc(Ac), srBc = g4::make_rsrc(Bc), srAn = g4::make_rsrc(An), srBn = g4::make_rsrc(Bn);
+  // descriptors + K offset of the K-tile the pieces of the current step stream (selected once per
+  // K-tile by dsel(), placed among the first MFMAs, ahead of the WAR barrier: the pieces behind the
+  // barrier then cost one m0 write and the DMA each)
+  i32x4 rsA = srAc, rsB = srBc;
+  uint32_t soK = 0;
+  auto dsel = [&](int t) {   // t: K-tile of the stream (>= nt: the next output tile's t - nt)
+    const bool nx = t >= nt;
+    const int tt = !nx ? t : (tid_n < nblk ? t - nt : nt - 1);
+    const i32x4 a = nx ? srAn : srAc, b = nx ? srBn : srBc;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {   // (uniform; pinned to SGPRs for the asm "s" operand)
+      rsA[e] = __builtin_amdgcn_readfirstlane(a[e]);
+      rsB[e] = __builtin_amdgcn_readfirstlane(b[e]);
+    }
+    soK = __builtin_amdgcn_readfirstlane((uint32_t)tt * TKB);
+  };
+  // piece k of the selected K-tile into buffer buf
+  auto dmap = [&](int buf, int k) {
     const int p = k & 7;
     const uint32_t d = lds0 + (k >= 8 ? 2 * IMGB : 0) + buf * IMGB + (64 * wave + 8 * p) * ROWB;
-    const bool nx = t >= nt;
-    int tt = !nx ? t : (tid_n < nblk ? t - nt : nt - 1);
-    tt += kst0;
-    if (tt >= nt) tt -= nt;
-    const T* base = k < 8 ? (nx ? An : Ac) : (nx ? Bn : Bc);
-    if constexpr (DV == 0) {
-      glds16s(sgpr_ptr(base + (long)tt * TK), k < 8 ? voA[p] : voB[p], d);
-    } else {
-      const uint32_t so = __builtin_amdgcn_readfirstlane((uint32_t)tt * TKB);
-      g4::bdma16<DV>(g4::make_rsrc(base), k < 8 ? voA[p] : voB[p], so, d);
-    }
+    g4::bdma16<DV>(k < 8 ? rsA : rsB, k < 8 ? voA[p] : voB[p], soK, d);
+  };
+  auto dma = [&](int t, int buf, int k) {   // (prologue)
+    dsel(t);
+    dmap(buf, k);
   };
 
   const int xo0 = ((0 + (lane >> 4)) ^ ((lane >> 1) & 7)) << 4;
@@ -819,27 +831,27 @@ __global__ __launch_bounds__(THREADS4, 1) void gemm_nt4p_k(const T* __restrict__
       const int i = SC::JMAJ ? (n & 7) : (n >> 3), j = SC::JMAJ ? (n >> 3) : (n & 7);
       MfA<T>::run(acc[i][j], b0[j], a0[i]);
       if (n < 16) rd16(a1, b1, cur, 1, n);
+      if (n == 2) dsel(t + 2);
       if (n == SC::WAR) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
       }
-      if (SC::piece(n) >= 0) dma(t + 2, cur, SC::piece(n));
+      if (SC::piece(n) >= 0) dmap(cur, SC::piece(n));
       __builtin_amdgcn_sched_barrier(0);
     }
 #pragma unroll
     for (int n = 0; n < 64; ++n) {
       const int i = SC::JMAJ ? (n & 7) : (n >> 3), j = SC::JMAJ ? (n >> 3) : (n & 7);
-      if (SC::piece(64 + n) >= 0) dma(t + 2, cur, SC::piece(64 + n));
+      if (SC::piece(64 + n) >= 0) dmap(cur, SC::piece(64 + n));
       if (64 + n == SC::RAW) {
         wait_vm<16>();
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
       }
-      constexpr int NR = 128 - SC::RAW;   // MFMAs carrying the 16 reads (16 or 8)
-      if (64 + n >= SC::RAW) {
+      if (64 + n >= SC::RAW && (64 + n - SC::RAW) * SC::RPM < 16) {
 #pragma unroll
-        for (int q = 0; q < 16 / NR; ++q) rd16(a0, b0, nxt, 0, (64 + n - SC::RAW) * (16 / NR) + q);
+        for (int q = 0; q < SC::RPM; ++q) rd16(a0, b0, nxt, 0, (64 + n - SC::RAW) * SC::RPM + q);
       }
       MfA<T>::run(acc[i][j], b1[j], a1[i]);
       __builtin_amdgcn_sched_barrier(0);
@@ -982,6 +994,8 @@ __global__ __launch_bounds__(THREADS4, 1) void gemm_nt4p_k(const T* __restrict__
     for (int i = 0; i < 8; ++i) a0[i] = rdA(0, i, 0), b0[i] = rdB(0, i, 0);
     tid = tid_n, m0 = m0n, n0 = n0n, Ac = An, Bc = Bn;
     set_next();
+    srAc = srAn, srBc = srBn;
+    srAn = g4::make_rsrc(An), srBn = g4::make_rsrc(Bn);
   }
   wait_vm0();   // the re-load pieces of the last two stream K-tiles land before the wave ends
 }
@@ -1056,16 +1070,13 @@ void launch(const void* a, long lda, const void* b, long ldb, void* c, long ldc,
     // 4 measured 0.3-12 % faster than 8 (16, 32 slower) on the Llama-3-8B / GPT2-774M shapes
     // (profiles/r3/gemm_nt4p_sv4_gm.jsonl)
     const int gmz = eg && atoi(eg) > 0 ? atoi(eg) : 4;
-    const char* es = getenv("BLLM_GEMM_NT4P_SU");   // K stagger (A/B)
-    const int su = es && *es ? atoi(es) : 0;
 #define BLLM_NT4P(ACCv, SVv, DVv)                                                                                       \
   do {                                                                                                                  \
     static const bool at_ = hipFuncSetAttribute((const void*)gemm_nt4p_k<T, OT, DVv, ACCv, SVv>,                        \
                                                 hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES) == hipSuccess; \
     (void)at_;                                                                                                          \
     hipLaunchKernelGGL((gemm_nt4p_k<T, OT, DVv, ACCv, SVv>), dim3(grid), dim3(THREADS4), LDS_BYTES, s, (const T*)a,   \
-                       lda, (const T*)b, ldb, (OT*)c, ldc, M, N, K, (OT*)nullptr, 0, nullptr, nullptr, 1, 0, gmz,   \
-                       (const OT*)nullptr, su);                                                                      \
+                       lda, (const T*)b, ldb, (OT*)c, ldc, M, N, K, (OT*)nullptr, 0, nullptr, nullptr, 1, 0, gmz);  \
   } while (0)
     // sv 5 / 6: schedule 0 with the pieces issued sc0 sc1 / nt (cache-policy A/B)
     if (accumulate) {
@@ -1078,6 +1089,8 @@ void launch(const void* a, long lda, const void* b, long ldb, void* c, long ldc,
       BLLM_NT4P(false, 3, 1);
     } else if (sv == 4) {
       BLLM_NT4P(false, 4, 1);
+    } else if (sv == 7) {
+      BLLM_NT4P(false, 5, 1);
     } else if (sv == 5) {
       BLLM_NT4P(false, 0, 2);
     } else if (sv == 6) {

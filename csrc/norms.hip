@@ -12,23 +12,11 @@
 
 namespace bllm {
 
-static int getenv_int(const char* k, int dflt) {
-  const char* e = getenv(k);
-  return e && *e ? atoi(e) : dflt;
-}
-
 constexpr int ROWS_PER_WG = 4;  // 4 waves x 1 row
 // backward workgroups (rows are grid-strided over them): 1024 = 4 WGs / 16 waves per CU on 256 CUs,
 // enough loads in flight for a d=4096 row pass; each WG adds one fp32 dW partial row (16 MiB at
-// d=4096), which col_reduce_k streams once.  BLLM_NORM_BWD_WG overrides (A/B tuning).
-static int max_bwd_wg() {
-  static const int v = [] {
-    const char* e = getenv("BLLM_NORM_BWD_WG");
-    const int n = e ? atoi(e) : 0;
-    return n > 0 ? n : 1024;
-  }();
-  return v;
-}
+// d=4096), which col_reduce_k streams once
+constexpr int MAX_BWD_WG = 1024;
 
 template <typename T, int NV, bool LN>
 __global__ __launch_bounds__(256) void norm_fwd_k(const T* __restrict__ x, const T* __restrict__ w,
@@ -207,110 +195,6 @@ __global__ __launch_bounds__(256) void norm_bwd_k(const T* __restrict__ dy, cons
   }
 }
 
-// Short rows (d <= 64 * NV * VEC, e.g. GPT-2's 1280, Llama-3.2-1B's 2048): one WAVE per row, 4
-// rows in flight per workgroup, the per-row reductions are wave shuffles only (the workgroup
-// kernel above pays an LDS round trip + barrier per row, which made it latency-bound there);
-// wave w of workgroup b owns partial row 4b + w of part_w / part_b, so the partial buffer and
-// col_reduce are unchanged (P = 4 x workgroups).  Opt-in (BLLM_NORM_BWD_WAVE=1): measured
-// end to end within noise of the workgroup kernel (GPT2-774M 183.5k vs 184.1k tok/s, Llama-3.2-1B
-// LoRA 162.4k vs 162.2k; profiles/r3/session2_norm_ab/), so that kernel's per-row barrier is not
-// what bounds it.
-template <typename T, int NV, bool LN>
-__global__ __launch_bounds__(256) void norm_bwd_wave_k(const T* __restrict__ dy, const T* __restrict__ x,
-                                                       const T* __restrict__ w, const float* __restrict__ mean,
-                                                       const float* __restrict__ rstd, const T* __restrict__ dx_acc,
-                                                       T* __restrict__ dx, float* __restrict__ part_w,
-                                                       float* __restrict__ part_b, int N, int d) {
-  constexpr int VEC = 16 / sizeof(T);
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int nvec = d / VEC;
-  const int prow = blockIdx.x * 4 + wv, nprow = gridDim.x * 4;
-  float aw[NV][VEC], ab[LN ? NV : 1][VEC];
-  Vec16<T> wvv[NV];
-#pragma unroll
-  for (int i = 0; i < NV; ++i) {
-    const int c = lane + 64 * i;
-    if (c < nvec) wvv[i] = ld16(w + c * VEC);
-#pragma unroll
-    for (int j = 0; j < VEC; ++j) {
-      aw[i][j] = 0.f;
-      if (LN) ab[LN ? i : 0][j] = 0.f;
-    }
-  }
-  for (int row = prow; row < N; row += nprow) {
-    const T* xr = x + (size_t)row * d;
-    const T* dyr = dy + (size_t)row * d;
-    const float rs = rstd[row];
-    const float mu = LN ? mean[row] : 0.f;
-    Vec16<T> xv[NV], dv[NV];
-#pragma unroll
-    for (int i = 0; i < NV; ++i) {
-      const int c = lane + 64 * i;
-      if (c < nvec) {
-        xv[i] = ld16(xr + c * VEC);
-        dv[i] = ld16(dyr + c * VEC);
-      }
-    }
-    float sg = 0.f, sgx = 0.f;
-#pragma unroll
-    for (int i = 0; i < NV; ++i) {
-      const int c = lane + 64 * i;
-      if (c < nvec) {
-#pragma unroll
-        for (int j = 0; j < VEC; ++j) {
-          const float dd = to_f(dv[i].v[j]);
-          const float xh = (to_f(xv[i].v[j]) - mu) * rs;
-          const float gg = dd * to_f(wvv[i].v[j]);
-          aw[i][j] += dd * xh;
-          if (LN) ab[LN ? i : 0][j] += dd;
-          sg += gg;
-          sgx += gg * xh;
-        }
-      }
-    }
-    sgx = wave_sum(sgx) / d;
-    if (LN) sg = wave_sum(sg) / d;
-    T* dxr = dx + (size_t)row * d;
-    const T* ar = dx_acc ? dx_acc + (size_t)row * d : nullptr;
-#pragma unroll
-    for (int i = 0; i < NV; ++i) {
-      const int c = lane + 64 * i;
-      if (c < nvec) {
-        Vec16<T> o, av;
-        if (ar) av = ld16(ar + c * VEC);
-#pragma unroll
-        for (int j = 0; j < VEC; ++j) {
-          const float xh = (to_f(xv[i].v[j]) - mu) * rs;
-          const float gg = to_f(dv[i].v[j]) * to_f(wvv[i].v[j]);
-          float r = rs * (gg - (LN ? sg : 0.f) - xh * sgx);
-          if (ar) r += to_f(av.v[j]);
-          o.v[j] = from_f<T>(r);
-        }
-        st16(dxr + c * VEC, o);
-      }
-    }
-  }
-#pragma unroll
-  for (int i = 0; i < NV; ++i) {
-    const int c = lane + 64 * i;
-    if (c < nvec) {
-      float* pw = part_w + (size_t)prow * d + c * VEC;
-#pragma unroll
-      for (int j = 0; j < VEC; j += 4)
-        *reinterpret_cast<float4*>(pw + j) = make_float4(aw[i][j], aw[i][j + 1], aw[i][j + 2], aw[i][j + 3]);
-      if (LN) {
-        float* pb = part_b + (size_t)prow * d + c * VEC;
-#pragma unroll
-        for (int j = 0; j < VEC; j += 4)
-          *reinterpret_cast<float4*>(pb + j) = make_float4(ab[LN ? i : 0][j], ab[LN ? i : 0][j + 1],
-                                                           ab[LN ? i : 0][j + 2], ab[LN ? i : 0][j + 3]);
-      }
-    }
-  }
-}
-
-// out[c] = sum_p part[p][c]   (16 columns x 16 row-groups per workgroup -> d/16 workgroups
-// so the partial matrix is streamed by many CUs; fixed summation order, deterministic)
 template <typename OT>
 __global__ __launch_bounds__(256) void col_reduce_k(const float* __restrict__ part, OT* __restrict__ out, int P,
                                                     int d, bool accumulate) {
@@ -365,16 +249,6 @@ static void bwd_dispatch(const void* dy, const void* x, const void* w, const flo
                          bool accumulate, int N, int d, int nwg, hipStream_t s) {
   constexpr int VEC = 16 / sizeof(T);
   const int nvec = d / VEC;
-  if (nvec <= 256 && nwg % 4 == 0 && getenv_int("BLLM_NORM_BWD_WAVE", 0)) {   // one wave per row
-    const int nv = ceil_div(nvec, 64);
-#define LW(NVV) hipLaunchKernelGGL((norm_bwd_wave_k<T, NVV, LN>), dim3(nwg / 4), dim3(256), 0, s, (const T*)dy,      \
-                                   (const T*)x, (const T*)w, mean, rstd, (const T*)dx_acc, (T*)dx, part_w, part_b, N, d)
-    if (nv <= 1) LW(1); else if (nv <= 2) LW(2); else if (nv <= 3) LW(3); else LW(4);
-#undef LW
-    col_reduce(part_w, odt, dw, nwg, d, accumulate, s);
-    if (LN) col_reduce(part_b, odt, db, nwg, d, accumulate, s);
-    return;
-  }
   // threads per row: a multiple of 64 covering the row in <= 4 waves; NV vectors per thread
   const int bt = nvec >= 256 ? 256 : ceil_div(nvec, 64) * 64;
   const int nv = ceil_div(nvec, bt);
@@ -387,18 +261,10 @@ static void bwd_dispatch(const void* dy, const void* x, const void* w, const flo
   if (LN) col_reduce(part_b, odt, db, nwg, d, accumulate, s);
 }
 
-// partial rows of the dW / dB sums = workgroups (wide rows) or 4 x workgroups (the wave-per-row
-// kernel for rows of <= 2048 16-bit elements: 4096 partial rows = 1024 workgroups of 4 waves, 16
-// waves per CU, a multiple of 4 so every wave owns one)
+// partial rows of the dW / dB sums = backward workgroups
 int norm_bwd_num_wg(int N, int d) {
-  if (d <= 2048 && getenv_int("BLLM_NORM_BWD_WAVE", 0)) {
-    const int e = getenv_int("BLLM_NORM_BWD_WG", 4096);
-    const int m = (e > 4 ? e : 4) / 4 * 4;
-    return N >= m ? m : (N >= 4 ? N / 4 * 4 : N);
-  }
-  int n = N;
-  const int m = max_bwd_wg();
-  return n < m ? n : m;
+  (void)d;
+  return N < MAX_BWD_WG ? N : MAX_BWD_WG;
 }
 
 // max supported row length per dtype (NV <= 16): 8192 (bf16/f16), 4096 (f32)

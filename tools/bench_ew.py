@@ -1,8 +1,7 @@
 """Micro-benchmark of the HBM-bound Llama-3-8B elementwise/norm kernels at the bench shape
 (24 x 1024 tokens): SwiGLU fwd/bwd on [N, 2*14336] and RMSNorm bwd (with the residual-gradient
 add) on [N, 4096], bf16; plus the GPT2-774M bias-gradient column sums ([N, 1280], [N, 5120]).  Prints one JSON line with us/call and achieved GB/s per op.
-Kernel-path A/B knobs are read from the environment by the extension (BLLM_SWIGLU_ROWS,
-BLLM_NORM_BWD_WG), so compare configurations by running this once per setting.
+Compare kernel changes by running this once per build.
 """
 import json
 import os
@@ -43,7 +42,20 @@ def main():
     g5 = torch.randn(N, 5120, device=dev).to(dt)     # GPT2-774M fc1 bias grad
     db1 = torch.zeros(1280, device=dev, dtype=dt)
     db5 = torch.zeros(5120, device=dev, dtype=dt)
-    res = {"env": {k: os.environ.get(k) for k in ("BLLM_SWIGLU_ROWS", "BLLM_NORM_BWD_WG", "BLLM_SWIGLU_U")}}
+    res = {}
+    # GPT2-774M at the preset's micro-batch 64 x 1024: the fused backward + bias column sums
+    N64 = 64 * 1024
+    f64 = torch.randn(N64, 5120, device=dev).to(dt)
+    dg64 = torch.randn(N64, 5120, device=dev).to(dt)
+    dm64 = torch.randn(N64, 1280, device=dev).to(dt)
+    for name, fn, nbytes in (
+        ("gpt2_b64_gelu_bwd_bias_5120", lambda: ops.gelu_bwd_bias(f64, dg64, db5, True), 3 * N64 * 5120 * 2),
+        ("gpt2_b64_dropout_bwd_bias_1280", lambda: ops.dropout_bwd_bias(dm64, 0.1, 7, 0, db1, True), 2 * N64 * 1280 * 2),
+        ("gpt2_b64_gelu_bwd_5120", lambda: ops.gelu_bwd(f64, dg64), 3 * N64 * 5120 * 2),
+    ):
+        us = _time(fn)
+        res[name] = {"us": round(us, 1), "GBps": round(nbytes / us / 1e3, 1)}
+    del f64, dg64, dm64
     for name, fn, nbytes in (
         ("swiglu_fwd", lambda: ops.swiglu_fwd(gu), 3 * N * F * 2),
         ("swiglu_bwd", lambda: ops.swiglu_bwd(gu, da), 5 * N * F * 2),

@@ -47,7 +47,6 @@ def main():
     ap.add_argument("--only", default="", help="comma list of gemm names to run (e.g. gate_up)")
     ap.add_argument("--nt4p_sv", default="0", help="comma list of BLLM_GEMM_NT4P_SV variants of the persistent arm")
     ap.add_argument("--nt4p_gm", default="", help="comma list of BLLM_GEMM_NT4P_GM (tile-group depth) arms, SV 0")
-    ap.add_argument("--nt4p_su", default="", help="comma list of BLLM_GEMM_NT4P_SU (K stagger) arms, SV 0")
     ap.add_argument("--swiglu", action="store_true",
                     help="gate/up + SwiGLU: hipBLASLt GEMM + separate swiglu_fwd vs the fused kernel (sched 2, 3)")
     a = ap.parse_args()
@@ -67,10 +66,9 @@ def main():
             dvs = a.nt4_dma.split(",")
             svs = a.nt4p_sv.split(",")
             gms = [g for g in a.nt4p_gm.split(",") if g]
-            sus = [g for g in a.nt4p_su.split(",") if g]
             outs = {k_: torch.empty(m, n, device="cuda", dtype=dt)
                     for k_ in ["new", "pp", "old"] + ["w4_" + d for d in dvs] + ["p4_" + v for v in svs]
-                    + ["g4_" + g for g in gms] + ["s4_" + g for g in sus]}
+                    + ["g4_" + g for g in gms]}
             y = torch.empty(m, n, device="cuda", dtype=dt)
 
             def new():
@@ -119,16 +117,6 @@ def main():
                 return f
             fns.update({"gemm_nt_4g_" + g: g4(g) for g in gms})
 
-            def s4(su):
-                def f():
-                    os.environ.pop("BLLM_GEMM_NT_IMPL", None)
-                    os.environ["BLLM_GEMM_NT_SCHED"] = "3"
-                    os.environ["BLLM_GEMM_NT4P_SV"] = "0"
-                    os.environ["BLLM_GEMM_NT4P_SU"] = su
-                    ops.gemm_nt_(x, w, outs["s4_" + su])
-                    os.environ.pop("BLLM_GEMM_NT4P_SU", None)
-                return f
-            fns.update({"gemm_nt_4s_" + g: s4(g) for g in sus})
             want = a.arms.split(",")
             fns = {k_: f for k_, f in fns.items()
                    if k_ == "hipblaslt" and "hipblaslt" in want or k_.startswith("gemm_nt_") and k_.split("_")[2] in want}

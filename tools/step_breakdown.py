@@ -25,7 +25,7 @@ BLLM_CLASSES = {
     "swiglu_fwd_k": "swiglu_fwd", "swiglu_fwd_rows_k": "swiglu_fwd", "swiglu_bwd_k": "swiglu_bwd", "swiglu_bwd_rows_k": "swiglu_bwd",
     "gelu_fwd_k": "gelu_fwd", "gelu_bwd_k": "gelu_bwd",
     "bwd_colsum_k": "bwd_colsum (GELU / dropout backward + bias column sums, csrc/elementwise.hip)",
-    "colsum_partial_k": "col_reduce", "col_reduce_k": "col_reduce",
+    "col_reduce_k": "col_reduce",
     "dropout_add_k": "dropout", "rope_k": "rope", "rope_scalar_k": "rope",
     "norm_fwd_k": "norm_fwd", "norm_bwd_k": "norm_bwd", "norm_bwd_wave_k": "norm_bwd",
     "ce_fwd_k": "ce_fwd", "ce_bwd_k": "ce_bwd",
