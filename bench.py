@@ -115,13 +115,19 @@ def parse(argv=None):
     ap.add_argument("--profile", action="store_true", help="print a per-phase timing breakdown to stderr")
     ap.add_argument("--overlap_optimizer", action="store_true",
                     help="run AdamW on a side HIP stream under the next forward")
-    ap.add_argument("--data", default=None, choices=["pretrain", "random_ids", "alpaca"],
+    ap.add_argument("--data", default=None, choices=["pretrain", "random_ids", "fixed_ids", "alpaca"],
                     help="pretrain (default for pretraining presets): synthetic Gutenberg text -> offline "
                          "tokenizer -> memmap cache -> DataloaderPT windows (DistributedSampler at N>1), the "
-                         "reference's data path; random_ids: device-resident random token ids (A/B only)")
+                         "reference's data path; random_ids: device-resident random token ids (A/B only); "
+                         "fixed_ids: one seeded GLOBAL batch per step, rank r trains rows [rB, (r+1)B), and "
+                         "the JSON gets the per-step loss trace, so a world-N run can be compared with world 1 "
+                         "at N x B (rehearsal check, not a measurement)")
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
                     help="cpu: tiny config on gloo (distributed plumbing check, not a measurement)")
     ap.add_argument("--pg_timeout_min", type=float, default=20.0)
+    ap.add_argument("--one_device", action="store_true",
+                    help="(rehearsal only) every rank on cuda:0 over gloo (RCCL refuses two ranks on one "
+                         "GPU): the world-N sharded path on a one-GPU box; invalidates the metric")
     ap.add_argument("--force_comm", action="store_true",
                     help="world 1: run the engines' N>1 collective path (RCCL copies) instead of the "
                          "world-1 shortcut (BLLM_FORCE_COMM=1) — a one-GPU rehearsal of the multi-GPU path")
@@ -151,16 +157,18 @@ def init_dist(a):
     if world != a.gpus:
         raise SystemExit(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={world}")
     if a.device == "cuda":
+        local = 0 if a.one_device else local
         torch.cuda.set_device(local)
         dev = torch.device("cuda", local)
     else:
         dev = torch.device("cpu")
     kw = dict(timeout=timedelta(minutes=a.pg_timeout_min))
-    if dev.type == "cuda":
+    rccl = dev.type == "cuda" and not a.one_device
+    if rccl:
         from building_llm_from_scratch_amd.parallel import nccl_pg_options
         kw["device_id"] = dev
         kw["pg_options"] = nccl_pg_options()
-    backend = "nccl" if dev.type == "cuda" else "gloo"
+    backend = "nccl" if rccl else "gloo"
     if launched:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group(backend, **kw)
@@ -299,7 +307,7 @@ def launch(argv=None):
     if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
         import torch
         import torch.multiprocessing as mp
-        if a.device == "cuda":
+        if a.device == "cuda" and not a.one_device:
             n = torch.cuda.device_count()   # counts devices without initialising HIP in this process
             if n < a.gpus:
                 raise SystemExit(f"bench.py: --gpus {a.gpus} but only {n} GPU(s) visible")
@@ -376,6 +384,15 @@ def main(argv=None):
         def next_batch(i):
             x, y = next(batches)
             return x.to(dev, non_blocking=True), y.to(dev, non_blocking=True)
+    elif a.data == "fixed_ids":
+        g = torch.Generator(device=dev)
+        g.manual_seed(1000)
+        data = [torch.randint(0, cfg.vocab_size, (world * B, T + 1), device=dev, generator=g)[rank * B:(rank + 1) * B]
+                for _ in range(4)]
+
+        def next_batch(i):
+            b = data[i % len(data)]
+            return b[:, :-1], b[:, 1:]
     else:
         g = torch.Generator(device=dev)
         g.manual_seed(1000 + rank)
@@ -386,6 +403,7 @@ def main(argv=None):
             return b[:, :-1], b[:, 1:]
 
     tokens = 0
+    loss_trace = [] if a.data == "fixed_ids" else None
 
     def step(i):
         nonlocal tokens
@@ -396,6 +414,10 @@ def main(argv=None):
         opt.clip_grad_norm_(1.0)
         opt.step()
         tokens += x.numel()
+        if loss_trace is not None:   # mean over ranks == the world-1 loss of the whole global batch
+            lt = loss.detach().float().reshape(1)
+            dist.all_reduce(lt)
+            loss_trace.append(lt.item() / world)
         return loss
 
     probe_peak = None
@@ -468,7 +490,7 @@ def main(argv=None):
     dist.all_gather_object(comm_kinds, comm_by_kind)
     prof = profile_phases(model, opt, next_batch, dev) if (a.profile and rank == 0 and cuda) else None
     if rank == 0:
-        headline = a.preset == "llama3_8b_fsdp" and cuda and not a.layers
+        headline = a.preset == "llama3_8b_fsdp" and cuda and not a.layers and not a.one_device
         name = NICE.get(a.model, f"{cfg.name}-{cfg.size}")
         if cuda:
             dtype = "bf16" if cfg.dtype == torch.bfloat16 else str(cfg.dtype).replace("torch.", "")
@@ -508,6 +530,7 @@ def main(argv=None):
                     + ", random-init weights (seeded per unit, meta-built)",
             "config": {
                 "model": name + (f" ({cfg.n_layers} layers, INVALID)" if a.layers else "")
+                + (" (all ranks on one GPU over gloo, INVALID)" if a.one_device else "")
                 + ("" if cuda else " (tiny cpu config, INVALID as a measurement)"),
                 "global_batch": world * B,
                 "micro_batch_per_gpu": B,
@@ -545,6 +568,8 @@ def main(argv=None):
         }
         if data_check is not None:
             out["data_check"] = data_check
+        if loss_trace is not None:
+            out["loss_trace"] = [round(v, 6) for v in loss_trace]
         if getattr(engine, "prefetch", None) is not None and not getattr(engine, "no_shard", True):
             out["config"]["fsdp_prefetch"] = engine.prefetch
         if plan is not None:

@@ -110,8 +110,9 @@ def _ln_bwd(unit, norm, dy, x, mean, rstd, dx_acc, acc):
     return dx
 
 
-# BLLM_FUSED_BIAS=0: bias gradients by the separate column-sum pass (A/B)
-FUSED_BIAS = os.environ.get("BLLM_FUSED_BIAS", "1") != "0"
+# bias gradients ride along in the dropout / GELU backward passes (ops.*_bwd_bias); tests set
+# this to False to check them against the separate column-sum pass
+FUSED_BIAS = True
 # BLLM_RECOMPUTE_FUSED=0: the checkpoint recompute runs its GELU forward as a separate pass (A/B)
 RECOMPUTE_FUSED = os.environ.get("BLLM_RECOMPUTE_FUSED", "1") != "0"
 

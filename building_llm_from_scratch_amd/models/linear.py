@@ -121,21 +121,21 @@ def _dgrad_wt_ok(dy: torch.Tensor, W: torch.Tensor) -> bool:
 
 
 # The forward-layout GEMMs (y = x W^T, dX on the transposed weight copy, the fused head's logits
-# and dh).  BLLM_GEMM_NT: 0 = hipBLASLt; 1 = csrc/gemm_nt.hip wherever its shape rules hold
-# (schedule from BLLM_GEMM_NT_SCHED); auto = per shape, whichever of hipBLASLt and the four
-# gemm_nt schedules timed fastest on this device (measured once per shape and process, like
-# TunableOp; never inside a graph capture)
+# and dh).  BLLM_GEMM_NT: 0 = hipBLASLt (default: it measures faster on these shapes,
+# profiles/r4/kernel_experiments.md); 1 = csrc/gemm_nt.hip's persistent kernel wherever its shape
+# rules hold; auto = per shape, whichever of the two timed faster on this device (measured once
+# per shape and process, like TunableOp; rank 0's pick is broadcast when a process group is up,
+# so every rank runs the same kernel; never inside a graph capture)
 GEMM_NT_MODE = os.environ.get("BLLM_GEMM_NT", "0")
 GEMM_NT = GEMM_NT_MODE not in ("0", "")
 _NT_PICK: dict = {}
 
 
-def _time_nt(a, b, out) -> int:
-    """-1 (hipBLASLt) or the gemm_nt schedule that ran this shape fastest (median of 3 x 3)."""
+def _time_nt(a, b, out) -> bool:
+    """True when csrc/gemm_nt.hip ran this shape faster than hipBLASLt (median of 3 x 3)."""
     c = torch.empty(a.shape[0], b.shape[0], dtype=out.dtype if out is not None else a.dtype, device=a.device)
-    arms = {-1: lambda: torch.mm(a, b.t(), out=c) if c.dtype == a.dtype else c.copy_(torch.mm(a, b.t())),
-            0: lambda: ops.gemm_nt_(a, b, c, False, 0), 1: lambda: ops.gemm_nt_(a, b, c, False, 1),
-            2: lambda: ops.gemm_nt_(a, b, c, False, 2), 3: lambda: ops.gemm_nt_(a, b, c, False, 3)}
+    arms = {False: lambda: torch.mm(a, b.t(), out=c) if c.dtype == a.dtype else c.copy_(torch.mm(a, b.t())),
+            True: lambda: ops.gemm_nt_(a, b, c, False)}
     times = {k: [] for k in arms}
     for fn in arms.values():
         fn()
@@ -148,33 +148,37 @@ def _time_nt(a, b, out) -> int:
             e.record()
             e.synchronize()
             times[k].append(s.elapsed_time(e))
-    med = {k: sorted(v)[1] for k, v in times.items()}
-    return min(med, key=med.get)
+    pick = sorted(times[True])[1] < sorted(times[False])[1]
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized():   # one decision for every rank
+        t = torch.tensor([int(pick)], device=a.device if dist.get_backend() == "nccl" else "cpu")
+        dist.broadcast(t, src=0)
+        pick = bool(t.item())
+    return pick
 
 
-def nt_choice(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None) -> int:
-    """-1 = hipBLASLt, else the gemm_nt schedule mm_nt uses for this call."""
+def nt_choice(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None) -> bool:
+    """Whether mm_nt runs this call on csrc/gemm_nt.hip (else hipBLASLt)."""
     if not GEMM_NT or not ops.gemm_nt_ok(a, b, out):
-        return -1
+        return False
     if GEMM_NT_MODE != "auto":
-        return int(os.environ.get("BLLM_GEMM_NT_SCHED", "0") or 0)
+        return True
     key = (tuple(a.shape), a.stride(0), tuple(b.shape), b.stride(0), a.dtype,
            None if out is None else (out.dtype, out.stride(0)), a.device)
     pick = _NT_PICK.get(key)
     if pick is None:
         if torch.cuda.is_current_stream_capturing():
-            return -1
+            return False
         pick = _NT_PICK[key] = _time_nt(a, b, out)
     return pick
 
 
 def mm_nt(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """a @ b^T for b stored [N, K] (both operands K-contiguous)."""
-    sched = nt_choice(a, b, out)
-    if sched >= 0:
+    if nt_choice(a, b, out):
         if out is None:
             out = torch.empty(a.shape[0], b.shape[0], dtype=a.dtype, device=a.device)
-        ops.gemm_nt_(a, b, out, False, sched)
+        ops.gemm_nt_(a, b, out, False)
         return out
     return torch.mm(a, b.t(), out=out) if out is not None else torch.mm(a, b.t())
 

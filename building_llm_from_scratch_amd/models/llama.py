@@ -348,8 +348,7 @@ class HeadComputeMixin:
     def _fused_lora_ok(self) -> bool:
         hd = self.head
         return (hd.has_lora and len(hd.specs) == 1 and hd.b_params is None
-                and not hd.unit.trainable(hd.W_params[0])
-                and os.environ.get("BLLM_LORA_HEAD_FUSED", "1") != "0")
+                and not hd.unit.trainable(hd.W_params[0]))
 
     def _waug(self, W, Bm):
         """[W | B^T] ([V, d + r]) in a buffer kept across steps; both parts re-copied per call

@@ -429,12 +429,12 @@ def gemm_nt_swiglu(a, w):
     return gu, swiglu_fwd(gu)
 
 
-def gemm_nt_(a, b, c, accumulate: bool = False, sched: int = -1):
+def gemm_nt_(a, b, c, accumulate: bool = False):
     """c (+)= a @ b^T with a [M, K], b [N, K] (both K-contiguous, a Linear's forward y = x W^T),
-    fp32 accumulation on csrc/gemm_nt.hip (``sched`` 0: one barrier per K-tile, 1: ping-pong wave
-    rows, 2: 4 waves of 128 x 128, -1: BLLM_GEMM_NT_SCHED) or, for shapes it does not take, csrc/gemm_wgrad.hip."""
+    fp32 accumulation on the persistent kernel of csrc/gemm_nt.hip or, for shapes it does not
+    take, csrc/gemm_wgrad.hip."""
     if _hip(a):
-        _k().gemm_nt_(a, b, c, bool(accumulate), int(sched))
+        _k().gemm_nt_(a, b, c, bool(accumulate))
         return c
     r = a.float() @ b.float().t()
     if accumulate:

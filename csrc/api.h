@@ -161,17 +161,12 @@ void wgrad_gemm(DType dt, DType odt, const void* a, long lda, const void* b, lon
 bool gemm_nn_supported(int M, int N, int K);
 void gemm_nn(DType dt, DType odt, const void* a, long lda, const void* b, long ldb, void* c, long ldc, int M, int N,
              int K, bool accumulate, hipStream_t s);
-// same kernel, both operands K-contiguous: C[M, N] (+)= A[M, K] B[N, K]^T (forward y = x W^T);
-// shape rules of gemm_nn_supported
-void gemm_nt(DType dt, DType odt, const void* a, long lda, const void* b, long ldb, void* c, long ldc, int M, int N,
-             int K, bool accumulate, hipStream_t s);
 
-// gemm_nt.hip — forward-layout kernel with 64-deep K-tiles (full 128-B rows): C[M, N] (+)= A[M, K] B[N, K]^T;
-// M, N multiples of 256, K of 128; used by gemm_nt_ unless BLLM_GEMM_NT_IMPL=1.  sched: 0 = one
-// barrier per K-tile, 1 = ping-pong wave rows, -1 = BLLM_GEMM_NT_SCHED (default 0)
+// gemm_nt.hip — persistent 4-wave forward-layout kernel with 64-deep K-tiles (full 128-B rows):
+// C[M, N] (+)= A[M, K] B[N, K]^T; M, N multiples of 256, K of 128
 bool gemm_nt2_supported(int M, int N, int K, long lda, long ldb);
 void gemm_nt2(DType dt, DType odt, const void* a, long lda, const void* b, long ldb, void* c, long ldc, int M, int N,
-              int K, bool accumulate, hipStream_t s, int sched = -1);
+              int K, bool accumulate, hipStream_t s);
 // gate/up projection with the SwiGLU forward in the epilogue: gu[M, 2F] = a . [Wg; Wu]^T and
 // act[M, F] = silu(gu[:, :F]) * gu[:, F:] (bitwise the separate swiglu_fwd)
 bool gemm_nt_swiglu_supported(int M, int F, int K, long lda, long ldb, long ldgu);

@@ -827,42 +827,15 @@ __global__ __launch_bounds__(256) void attn_bwd_kv_reduce_k(const float* __restr
   }
 }
 
-// dK/dV variant: 0 = 2-slot ring at 2 workgroups per CU (one wave's waits hide under the other
-// wave's MFMAs), 1 = 3-slot ring (prefetch distance 2) at 1 workgroup per CU.
-// BLLM_ATTN_KV_VARIANT selects one for A/B measurement.
-// 2 = as 0 with the GQA heads of a kv head fused into one workgroup (no partials / reduction).
-// Unset: 2 when the fused grid still has >= 4 workgroups per CU (measured: Llama-3-8B B=24
-// 1.51 -> 1.12 ms), else 0 (B=4 has only 256 fused workgroups: 0.25 ms unfused vs 0.35 fused).
-static int kv_variant_from_env() {
-  const char* e = getenv("BLLM_ATTN_KV_VARIANT");
-  return e ? atoi(e) : -1;
-}
+// GQA heads of a kv head fused into one dK/dV workgroup (no per-head fp32 partials, no
+// reduction pass) when the fused grid still has >= 4 workgroups per CU (Llama-3-8B B=24
+// 1.51 -> 1.12 ms); below that the per-head grid wins (B=4: 256 fused workgroups, 0.25 ms unfused
+// vs 0.35 fused).  Dropped variants (3-slot ring at one workgroup per CU, 64-key dQ tiles) are
+// in profiles/r2_kernel_experiments.md.
 static bool fuse_gqa_heads(int B, int T_, int H, int G) {
-  static const int kv_variant = kv_variant_from_env();
   if (H == G) return false;
-  if (kv_variant >= 0) return kv_variant == 2;
   const long nkb = (T_ + BWD_BKV - 1) / BWD_BKV;
   return nkb * G * (long)B >= 1024;
-}
-// dQ variant: 0 = 32-key tiles, 3-slot ring, 2 workgroups per CU; 1 = 64-key tiles, 1 per CU
-// dK/dV staging: 1 = one dual-use LDS image per Q / dO tile and a 4-slot ring (DUAL kernels),
-// 0 = separate row and transposed images, 2-slot ring.  Unset: dual at hd 128 (Llama-3-8B
-// B=24 backward 1.143 -> 1.100 ms) and at hd 64 with a dropout keep mask, else separate images
-// (Llama-3.2-1B 0.548 vs 0.568 ms); BLLM_ATTN_KV_DUAL overrides.
-static int kv_dual_from_env() {
-  const char* e = getenv("BLLM_ATTN_KV_DUAL");
-  return e ? atoi(e) : -1;
-}
-// V fragments in LDS (VLDS kernels, with the dual images and a 2-slot ring).  Unset: on at
-// hd 128 (no spills; Llama-3-8B B=24 backward 1.158 -> 1.009 ms), off at hd 64 (no register
-// pressure there); BLLM_ATTN_KV_VLDS overrides.
-static int kv_vlds_from_env() {
-  const char* e = getenv("BLLM_ATTN_KV_VLDS");
-  return e ? atoi(e) : -1;
-}
-static int q_variant_from_env() {
-  const char* e = getenv("BLLM_ATTN_Q_VARIANT");
-  return e ? atoi(e) : 0;
 }
 
 bool attn_bwd_kv_partials(int B, int T_, int H, int G) { return H != G && !fuse_gqa_heads(B, T_, H, G); }
@@ -908,19 +881,22 @@ static void launch_kv(const BwdArgs& a, bool drop, dim3 grid) {
   else if (drop) launch_kv1<TT, HDD, true, NB, OC, FG, DU, false, VL>(a, grid);
   else launch_kv1<TT, HDD, false, NB, OC, FG, DU, false, VL>(a, grid);
 }
+// dQ: 32-key tiles, 3-slot ring, 2 workgroups per CU.  dK/dV: hd 128 -> one dual-use LDS image
+// per Q / dO tile, V fragments in LDS, 2-slot ring (Llama-3-8B B=24 1.158 -> 1.009 ms); hd 64 ->
+// dual images only with the forward's dropout keep mask (GPT2-774M B=24 0.430 -> 0.420 ms; they
+// lose without dropout or with fused GQA heads: 0.367 -> 0.376, Llama-3.2-1B 0.575 -> 0.602 ms,
+// profiles/r2_attn_hd64_dual.md), 4-slot ring; else separate row / transposed images, 2-slot ring
 template <typename TT, int HDD>
-static void launch_bwd(const BwdArgs& a, bool drop, int q_variant, int kv_variant, bool fuseg, bool kv_dual,
-                       bool kv_vlds, dim3 grid_q, dim3 grid_kv) {
-  if (q_variant == 0) launch_dq<TT, HDD, 32, 3, 2>(a, drop, grid_q);
-  else launch_dq<TT, HDD, 64, 3, 1>(a, drop, grid_q);
-  if (kv_vlds && kv_dual) {  // dual images, 2-slot ring, V fragments in LDS
+static void launch_bwd(const BwdArgs& a, bool drop, bool fuseg, dim3 grid_q, dim3 grid_kv) {
+  launch_dq<TT, HDD, 32, 3, 2>(a, drop, grid_q);
+  if constexpr (HDD == 128) {
     if (fuseg) launch_kv<TT, HDD, 2, 2, true, true, true>(a, drop, grid_kv);
     else launch_kv<TT, HDD, 2, 2, false, true, true>(a, drop, grid_kv);
-  } else if (fuseg && kv_dual) launch_kv<TT, HDD, 4, 2, true, true>(a, drop, grid_kv);
-  else if (kv_dual && kv_variant != 1) launch_kv<TT, HDD, 4, 2, false, true>(a, drop, grid_kv);
-  else if (fuseg) launch_kv<TT, HDD, 2, 2, true, false>(a, drop, grid_kv);
-  else if (kv_variant != 1) launch_kv<TT, HDD, 2, 2, false, false>(a, drop, grid_kv);
-  else launch_kv<TT, HDD, 3, 1, false, false>(a, drop, grid_kv);
+  } else {
+    if (drop && a.kmask && !fuseg) launch_kv<TT, HDD, 4, 2, false, true>(a, drop, grid_kv);
+    else if (fuseg) launch_kv<TT, HDD, 2, 2, true, false>(a, drop, grid_kv);
+    else launch_kv<TT, HDD, 2, 2, false, false>(a, drop, grid_kv);
+  }
 }
 
 void attn_bwd_mfma(DType dt, const void* qkv, const void* o, const float* lse, const void* dout, void* dqkv,
@@ -928,29 +904,18 @@ void attn_bwd_mfma(DType dt, const void* qkv, const void* o, const float* lse, c
                    float p, uint64_t seed, uint64_t offset, const uint32_t* keep_mask, const float* rcos,
                    const float* rsin, hipStream_t s) {
   (void)dq_acc;
-  static const int kv_variant = kv_variant_from_env();
-  static const int q_variant = q_variant_from_env();
   const int nkb = (T_ + BWD_BKV - 1) / BWD_BKV;
-  // kv variant 2 (GQA, large grids): the dK/dV workgroup sweeps the H/G heads of its kv head
   const bool fuseg = fuse_gqa_heads(B, T_, H, G);
-  // dual images: hd 128, and hd 64 with the forward's keep mask (GPT-2 774M B=24 dK/dV+dQ
-  // 0.430 -> 0.420 ms; without dropout or with fused GQA heads they lose: 0.367 -> 0.376,
-  // Llama-3.2-1B 0.575 -> 0.602 ms — profiles/r2_attn_hd64_dual.md)
-  static const int kv_dual_env = kv_dual_from_env();
-  const bool kv_dual = kv_dual_env >= 0 ? kv_dual_env != 0
-                                        : (hd == 128 || (p > 0.f && keep_mask != nullptr && !fuseg));
-  static const int kv_vlds_env = kv_vlds_from_env();
-  const bool kv_vlds = kv_vlds_env >= 0 ? kv_vlds_env > 0 : hd == 128;
   dim3 grid_kv(nkb * (fuseg ? G : H) * B), grid_q(((T_ + DQ_BQ - 1) / DQ_BQ) * H * B);
   const bool drop = p > 0.f;
   const BwdArgs a{qkv, o, dout, lse, delta, dkv_part, dqkv, T_, H, G, B, causal, drop_threshold16(p),
                   drop_inv_keep(p), seed, offset, drop ? keep_mask : nullptr, rcos, rsin, s};
   if (dt == DType::BF16) {
-    if (hd == 128) launch_bwd<bf16_t, 128>(a, drop, q_variant, kv_variant, fuseg, kv_dual, kv_vlds, grid_q, grid_kv);
-    else launch_bwd<bf16_t, 64>(a, drop, q_variant, kv_variant, fuseg, kv_dual, kv_vlds, grid_q, grid_kv);
+    if (hd == 128) launch_bwd<bf16_t, 128>(a, drop, fuseg, grid_q, grid_kv);
+    else launch_bwd<bf16_t, 64>(a, drop, fuseg, grid_q, grid_kv);
   } else {
-    if (hd == 128) launch_bwd<f16_t, 128>(a, drop, q_variant, kv_variant, fuseg, kv_dual, kv_vlds, grid_q, grid_kv);
-    else launch_bwd<f16_t, 64>(a, drop, q_variant, kv_variant, fuseg, kv_dual, kv_vlds, grid_q, grid_kv);
+    if (hd == 128) launch_bwd<f16_t, 128>(a, drop, fuseg, grid_q, grid_kv);
+    else launch_bwd<f16_t, 64>(a, drop, fuseg, grid_q, grid_kv);
   }
   if (H != G && !fuseg) {
     const long BT = (long)B * T_;

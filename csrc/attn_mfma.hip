@@ -14,11 +14,10 @@
 // (element j of lane half h = key 16s + 8(j>>2) + 4h + (j&3)); the V^T operand is read
 // with the matching key permutation: two transposed reads of 4 keys each.
 //
-// Workgroup = 4 waves; each wave owns QB 32-query blocks (QB = 1: 128 queries per workgroup;
-// QB = 2: 256): every K fragment and V^T fragment read from LDS feeds QB MFMAs, so QB = 2 halves
-// the LDS read bytes, the DMA landing waits and the barriers per FLOP (at QB = 1 the K + V
-// reads of a tile, 32 KiB per wave at hd 128, match the MFMA time of the tile).  K/V tiles of
-// 64 keys, register DMA (global_load_lds) of tile t+1 under the MFMAs of tile t,
+// Workgroup = 4 waves; each wave owns one 32-query block (128 queries per workgroup; two blocks
+// per wave, which halves the LDS reads per FLOP, measured slower on every shape:
+// profiles/r3/attn_fwd_qb2.md -- the per-query arrays below keep a block index for that layout).
+// K/V tiles of 64 keys, register DMA (global_load_lds) of tile t+1 under the MFMAs of tile t,
 // double-buffered LDS.  GQA reads kv head h / (H/G)
 // directly; causal tiles above the diagonal are skipped; q-blocks are launched
 // heaviest-first.  LDS images are XOR-swizzled: K in 16-B chunks (conflict-free
@@ -84,7 +83,7 @@ template <typename T> __device__ __forceinline__ uint32_t pack2(float a, float b
 // per-lane offsets, 2x(LD) saddr DMA issues with precomputed per-lane source offsets, and
 // ~130 VALU of online softmax (scale folded into the exp2 FMA; the O rescale is skipped when
 // no lane's running max moved, which is the common case after the first tiles).
-template <typename T, int HD, bool DROP, int FWD_BK, int NBUF, int OCC, int QB>
+template <typename T, int HD, bool DROP, int FWD_BK, int NBUF, int OCC>
 __global__ __launch_bounds__(256, OCC) void attn_fwd_mfma_k(const T* __restrict__ qkv, T* __restrict__ out,
                                                           float* __restrict__ lse, int T_, int H, int G, int B_,
                                                           bool causal, uint32_t thr, float inv_keep, uint64_t seed,
@@ -98,10 +97,11 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd_mfma_k(const T* __restrict_
   constexpr int LD = FWD_BK * CH / 256;     // 1-KiB pieces per wave per tile (K and V each)
   constexpr int NPW = 2 * LD;
   constexpr int NKT = FWD_BK / 32;          // 32-key MFMA tiles per step
+  constexpr int QB = 1;                     // 32-query blocks per wave
   constexpr int WQ = 32 * QB;               // queries per wave
   constexpr int BQ = FWD_BQ * QB;           // queries per workgroup
   static_assert(NBUF == 2 || NBUF == 3, "ring depth");
-  static_assert(QB == 1 || QB == 2, "q-blocks per wave");
+
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   // heaviest (latest, for causal) q-blocks first over the whole grid; the q-blocks of one
@@ -460,42 +460,32 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd_mfma_k(const T* __restrict_
 
 bool attn_mfma_head_dim(int hd) { return hd == 64 || hd == 128; }
 
-// forward variant (BLLM_ATTN_FWD_VARIANT, for A/B measurement): 0 = 64-key tiles, 2-slot ring,
-// 2 WGs/CU, one 32-query block per wave (round-2 default); 1 = 32-key tiles, 3-slot ring;
-// 2 = 32-key tiles, 2-slot ring (up to 3 WGs/CU); 4 = two 32-query blocks per wave (QB = 2),
-// 64-key tiles (hd 64), 32-key tiles at hd 128 (register budget of 2 waves per SIMD);
-// 5 = QB = 2 with 64-key tiles and one workgroup per CU at hd 128.
-// Unset: variant 2 for hd 64 with dropout on grids of >= 2048 workgroups (GPT2-774M B=24:
-// 0.179 -> 0.163 ms -- the hash work wants the third co-resident workgroup), else variant 0.
-static int fwd_variant_from_env(int hd, float p, long nwg) {
-  const char* e = getenv("BLLM_ATTN_FWD_VARIANT");
-  if (e) return atoi(e);
-  return (hd == 64 && p > 0.f && nwg >= 2048) ? 2 : 0;
-}
+// forward tiling: 64-key tiles, 2-slot ring, 2 workgroups per CU; for hd 64 with dropout on grids
+// of >= 2048 workgroups 32-key tiles with up to 3 workgroups per CU (GPT2-774M B=24 0.179 ->
+// 0.163 ms: the hash work wants the third co-resident workgroup).  Dropped: 32-key tiles with a
+// 3-slot ring, two 32-query blocks per wave (slower on every shape, profiles/r3/attn_fwd_qb2.md).
+static bool fwd_small_tiles(int hd, float p, long nwg) { return hd == 64 && p > 0.f && nwg >= 2048; }
 
 void attn_fwd_mfma(DType dt, const void* qkv, void* o, float* lse, int B, int T_, int H, int G, int hd, bool causal,
                    float p, uint64_t seed, uint64_t offset, uint32_t* keep_mask, hipStream_t s) {
   const uint32_t thr = drop_threshold16(p);
   const float ik = drop_inv_keep(p);
-  const int fwd_variant = fwd_variant_from_env(hd, p, (long)((T_ + FWD_BQ - 1) / FWD_BQ) * H * B);
-#define LAUNCH_V(TT, HDD, BK, NB, OC, QBB)                                                                \
+  const bool small = fwd_small_tiles(hd, p, (long)((T_ + FWD_BQ - 1) / FWD_BQ) * H * B);
+#define LAUNCH_V(TT, HDD, BK, NB, OC)                                                                      \
   do {                                                                                                        \
     const int lds = NB * 2 * BK * HDD * 2;                                                                    \
-    const dim3 grid(((T_ + FWD_BQ * QBB - 1) / (FWD_BQ * QBB)) * H * B), block(256);                          \
+    const dim3 grid(((T_ + FWD_BQ - 1) / FWD_BQ) * H * B), block(256);                                        \
     if (p > 0.f)                                                                                              \
-      hipLaunchKernelGGL((attn_fwd_mfma_k<TT, HDD, true, BK, NB, OC, QBB>), grid, block, lds, s,          \
+      hipLaunchKernelGGL((attn_fwd_mfma_k<TT, HDD, true, BK, NB, OC>), grid, block, lds, s,          \
                          (const TT*)qkv, (TT*)o, lse, T_, H, G, B, causal, thr, ik, seed, offset, keep_mask); \
     else                                                                                                      \
-      hipLaunchKernelGGL((attn_fwd_mfma_k<TT, HDD, false, BK, NB, OC, QBB>), grid, block, lds, s,         \
+      hipLaunchKernelGGL((attn_fwd_mfma_k<TT, HDD, false, BK, NB, OC>), grid, block, lds, s,         \
                          (const TT*)qkv, (TT*)o, lse, T_, H, G, B, causal, thr, ik, seed, offset, nullptr); \
   } while (0)
 #define LAUNCH(TT, HDD)                                                                                       \
   do {                                                                                                        \
-    if (fwd_variant == 1) LAUNCH_V(TT, HDD, 32, 3, 2, 1);                                                     \
-    else if (fwd_variant == 2) LAUNCH_V(TT, HDD, 32, 2, 3, 1);                                                \
-    else if (fwd_variant == 4) LAUNCH_V(TT, HDD, 32, 3, 2, 2);                                                \
-    else if (fwd_variant == 5) LAUNCH_V(TT, HDD, 64, 2, (HDD == 64 ? 2 : 1), 2);                             \
-    else LAUNCH_V(TT, HDD, 64, 2, 2, 1);                                                                      \
+    if (small) LAUNCH_V(TT, HDD, 32, 2, 3);                                                                   \
+    else LAUNCH_V(TT, HDD, 64, 2, 2);                                                                         \
   } while (0)
   if (dt == DType::BF16) {
     if (hd == 128) LAUNCH(bf16_t, 128); else LAUNCH(bf16_t, 64);

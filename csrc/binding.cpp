@@ -350,7 +350,7 @@ void gemm_nn_(const Tensor& a, const Tensor& b, Tensor& c, bool accumulate) {
 }
 
 // c[M, N] (+)= a[M, K] . b[N, K]^T on the MFMA kernel (both operands K-contiguous)
-void gemm_nt_(const Tensor& a, const Tensor& b, Tensor& c, bool accumulate, int64_t sched) {
+void gemm_nt_(const Tensor& a, const Tensor& b, Tensor& c, bool accumulate) {
   TORCH_CHECK(a.is_cuda() && b.is_cuda() && c.is_cuda(), "gemm_nt: GPU tensors");
   c10::DeviceGuard g(a.device());
   TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && c.dim() == 2, "gemm_nt: 2-D operands");
@@ -365,15 +365,10 @@ void gemm_nt_(const Tensor& a, const Tensor& b, Tensor& c, bool accumulate, int6
               "gemm_nt: operands must be 16-B aligned");
   TORCH_CHECK(a.stride(0) < (int64_t(1) << 26) && b.stride(0) < (int64_t(1) << 26), "gemm_nt: row stride too large");
   TORCH_CHECK(M < (int64_t(1) << 31) && N < (int64_t(1) << 31) && K < (int64_t(1) << 31));
-  const char* impl = getenv("BLLM_GEMM_NT_IMPL");  // "1": the 32-deep-slot kernel of gemm_wgrad.hip (A/B)
-  if (!(impl && impl[0] == '1') && bllm::gemm_nt2_supported((int)M, (int)N, (int)K, a.stride(0), b.stride(0))) {
-    bllm::gemm_nt2(dt_of(a), dt_of(c), a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0), c.data_ptr(),
-                   c.stride(0), (int)M, (int)N, (int)K, accumulate, stream(), (int)sched);
-    return;
-  }
-  TORCH_CHECK(bllm::gemm_nn_supported((int)M, (int)N, (int)K), "gemm_nt: unsupported shape ", M, "x", N, "x", K);
-  bllm::gemm_nt(dt_of(a), dt_of(c), a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0), c.data_ptr(), c.stride(0),
-                (int)M, (int)N, (int)K, accumulate, stream());
+  TORCH_CHECK(bllm::gemm_nt2_supported((int)M, (int)N, (int)K, a.stride(0), b.stride(0)),
+              "gemm_nt: unsupported shape ", M, "x", N, "x", K);
+  bllm::gemm_nt2(dt_of(a), dt_of(c), a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0), c.data_ptr(),
+                 c.stride(0), (int)M, (int)N, (int)K, accumulate, stream());
 }
 
 // gate/up projection + SwiGLU forward in one kernel (csrc/gemm_nt.hip): gu[M, 2F] = a . w^T with
@@ -884,13 +879,11 @@ const LtPlan& lt_plan(int dev, hipDataType dt, int64_t N, int64_t K, int64_t O, 
       (void)hipEventRecord(e1, st);
       (void)hipEventSynchronize(e1);
       (void)hipEventElapsedTime(&ms, e0, e1);
-      if (getenv("BLLM_LT_VERBOSE")) printf("[lt] N=%ld K=%ld O=%ld cand %d: %.1f us\n", (long)N, (long)K, (long)O, i, ms * 1e3f / 3);
       if (ms < best) { best = ms; besti = i; }
     }
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
     p.algo = res[besti].algo;
-    if (getenv("BLLM_LT_VERBOSE")) printf("[lt] N=%ld K=%ld O=%ld -> cand %d of %d\n", (long)N, (long)K, (long)O, besti, n);
   }
   std::lock_guard<std::mutex> g(lt_mu);
   return cache.emplace(key, p).first->second;
@@ -959,7 +952,7 @@ TORCH_LIBRARY(bllm, m) {
   m.def("sum_partials_(Tensor part, Tensor(a!) out, bool accumulate) -> ()");
   m.def("wgrad_gemm_(Tensor a, Tensor b, Tensor(a!) c, bool accumulate, int splits) -> ()");
   m.def("gemm_nn_(Tensor a, Tensor b, Tensor(a!) c, bool accumulate) -> ()");
-  m.def("gemm_nt_(Tensor a, Tensor b, Tensor(a!) c, bool accumulate, int sched=-1) -> ()");
+  m.def("gemm_nt_(Tensor a, Tensor b, Tensor(a!) c, bool accumulate) -> ()");
   m.def("gemm_nt_swiglu_(Tensor a, Tensor w, Tensor(a!) gu, Tensor(b!) act) -> ()");
   m.def("gemm_nt_rope_(Tensor a, Tensor w, Tensor(a!) qkv, Tensor cos, Tensor sin, int T, int nrot, int hd) -> ()");
   m.def("gemm_nt_bias_gelu_(Tensor a, Tensor w, Tensor bias, Tensor(a!) f, Tensor(b!) g) -> ()");

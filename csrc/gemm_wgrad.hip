@@ -34,16 +34,13 @@
 //    ring in two 128-row passes and leaves as 16-B row-contiguous global stores (and 16-B loads
 //    when accumulating) instead of 128 scattered 2-/4-byte stores per lane.
 //
-// Variants (BLLM_WGRAD_VARIANT, read per launch so one process can A/B them):
-//   0  fragments read after each barrier
-//   1  next slot's fragments read under the current slot's MFMAs
-//   2  as 1, LDS-DMA issued by waves 0-3 only (see Geo::LOADERS) — default: 1.02-1.13x variant 1
-//      (Llama-3-8B gate/up 1.33 -> 1.40 PF, LM head 1.18 -> 1.34 PF)
-//   3  as 2 on v_mfma_f32_32x32x16 (acc[4][2] of 32 x 32, own LDS swizzle) — correct, but 3-10 %
-//      slower than 2 on every benchmark shape (profiles/r2_kernel_experiments.md); kept for A/B
-// Measured and dropped (tools/bench_wgrad.py, profiles/r1_wgrad_kernel.md): 4 waves of 128 x 128
-// (one wave per SIMD) -25 %; LDS-DMA pieces interleaved between MFMA groups instead of one burst
-// after the barrier -5 %.
+// Two schedules (the others -- fragments read after each barrier, DMA by all 8 waves,
+// 32x32x16 MFMAs, a persistent variant of wgrad4_k -- measured slower and were deleted;
+// profiles/r2_kernel_experiments.md, profiles/r3/kernel_experiments.md):
+//   wgrad_gemm_k  8 waves of 128 x 64, next slot's fragments read under the current slot's
+//                 MFMAs, LDS-DMA issued by waves 0-3 only -- deep split-K (S >= 8: few, short
+//                 tiles) and the K-contiguous-A dX kernel (gemm_nn);
+//   wgrad4_k      4 waves (one per SIMD) of 128 x 128 (below) -- every other weight gradient.
 #include <stdlib.h>
 
 #include <type_traits>
@@ -93,28 +90,21 @@ constexpr int B_BASE = NSLOT * SLOTB;       // A slots [0, 64 KiB), B slots [64,
 constexpr int LDS_BYTES = 2 * NSLOT * SLOTB;
 constexpr int GROUP_M = 8;
 
-// wave layout / schedule per variant
-template <int VAR> struct Geo {
+// wave layout / schedule of wgrad_gemm_k
+struct Geo {
   static constexpr int NW = 8;                         // waves per workgroup
   static constexpr int THREADS = NW * 64;
   static constexpr int WAVES_N = 4;                    // waves along N (2 along M)
   static constexpr int FN = BN / WAVES_N / 16;         // 16-wide n fragments per wave
-  // Variant 2: only waves 0-3 (one per SIMD) issue the slot's LDS-DMA, so each SIMD's other
-  // wave (4-7) goes straight from the barrier to its MFMAs and keeps the matrix pipe busy while
-  // its partner spends ~60 issue cycles per piece; variants 0/1 split the pieces over all 8.
-  static constexpr int LOADERS = VAR >= 2 ? 4 : 8;
+  // only waves 0-3 (one per SIMD) issue the slot's LDS-DMA, so each SIMD's other wave (4-7) goes
+  // straight from the barrier to its MFMAs and keeps the matrix pipe busy while its partner
+  // spends ~60 issue cycles per piece (1.02-1.13x splitting the pieces over all 8)
+  static constexpr int LOADERS = 4;
   static constexpr int DJ = (SLOTB / 1024) / LOADERS;  // LDS-DMA pieces per operand per slot per loader
   static constexpr int PER_STAGE = 2 * DJ;             // vmcnt units one staged slot adds (loaders)
-  static constexpr bool PREFETCH = VAR >= 1;           // next slot's fragments under this slot's MFMAs
-  // Variant 3: v_mfma_f32_32x32x16 (acc[4][2] of 32 x 32) — half the MFMA instructions and half
-  // the operand-register reads per FLOP of 16x16x32; same fragment count per k-step.
-  static constexpr bool M32 = VAR == 3;
 };
 
 __device__ __forceinline__ int swz(int r) { return 2 * ((r & 3) | (((r >> 3) & 1) << 2)); }
-// 32x32 fragments: a 32-lane half reads 4 k-rows x 64 B (two 16-column blocks), so XOR the
-// 4-chunk block index by (r & 3) — the 4 rows land on 4 distinct 64-B bank groups
-__device__ __forceinline__ int swz32(int r) { return 4 * (r & 3); }
 
 __device__ __forceinline__ s16x8 frag(const char* p) {
   const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p));
@@ -131,12 +121,12 @@ template <int N> __device__ __forceinline__ void vm_wait() { asm volatile("s_wai
 //             covers 16 distinct bank quads), fragments read with ds_read_b128.
 __device__ __forceinline__ int fA(int q) { return (0x78 >> (2 * q)) & 3; }
 
-template <typename T, typename OT, int VAR, bool AK = false, bool BKC = false>
-__global__ __launch_bounds__(Geo<VAR>::THREADS) void wgrad_gemm_k(const T* __restrict__ A, long lda,
+template <typename T, typename OT, bool AK = false>
+__global__ __launch_bounds__(Geo::THREADS) void wgrad_gemm_k(const T* __restrict__ A, long lda,
                                                                   const T* __restrict__ B, long ldb,
                                                                   OT* __restrict__ C, long ldc, long c_split,
                                                                   int M, int N, int K, int accumulate, int wide) {
-  using G = Geo<VAR>;
+  using G = Geo;
   constexpr int FN = G::FN, DJ = G::DJ, PS = G::PER_STAGE;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
@@ -163,13 +153,8 @@ __global__ __launch_bounds__(Geo<VAR>::THREADS) void wgrad_gemm_k(const T* __res
   uint32_t voffA[DJ], voffB[DJ];
 #pragma unroll
   for (int j = 0; j < DJ; ++j) {
-    const int r = (wave * DJ + j) * 2 + (lane >> 5), c = (lane & 31) ^ (G::M32 ? swz32(r) : swz(r));
-    if constexpr (BKC) {  // B [N, K] K-contiguous: staged like a K-contiguous A
-      const int rb = (wave * DJ + j) * 16 + (lane >> 2), cb = (lane & 3) ^ fA((rb >> 2) & 3);
-      voffB[j] = (uint32_t)((rb * ldb + 8 * cb) * (long)sizeof(T));
-    } else {
-      voffB[j] = (uint32_t)((r * ldb + 8 * c) * (long)sizeof(T));
-    }
+    const int r = (wave * DJ + j) * 2 + (lane >> 5), c = (lane & 31) ^ swz(r);
+    voffB[j] = (uint32_t)((r * ldb + 8 * c) * (long)sizeof(T));
     if constexpr (AK) {  // piece = 16 m-rows x 64 B; lane -> row l/4, physical chunk l%4
       const int ra = (wave * DJ + j) * 16 + (lane >> 2), ca = (lane & 3) ^ fA((ra >> 2) & 3);
       voffA[j] = (uint32_t)((ra * lda + 8 * ca) * (long)sizeof(T));
@@ -179,7 +164,7 @@ __global__ __launch_bounds__(Geo<VAR>::THREADS) void wgrad_gemm_k(const T* __res
   }
   const uint32_t lds0 = lds_u32(smem);
   const T* Abase = AK ? A + m0 * lda + (long)c_lo * KCH : A + (long)c_lo * KCH * lda + m0;
-  const T* Bbase = BKC ? B + n0 * ldb + (long)c_lo * KCH : B + (long)c_lo * KCH * ldb + n0;
+  const T* Bbase = B + (long)c_lo * KCH * ldb + n0;
   // piece q of a stage: q even = A piece q/2, q odd = B piece q/2 (issue order A0 B0 A1 B1 ..)
   auto piece = [&](const void* a, const void* b, int q, int slot) {
     const int j = q >> 1;
@@ -187,9 +172,9 @@ __global__ __launch_bounds__(Geo<VAR>::THREADS) void wgrad_gemm_k(const T* __res
     else glds16s(a, voffA[j], lds0 + slot * SLOTB + (wave * DJ + j) * 1024);
   };
   auto stage = [&](int kt, int slot) {
-    if (G::LOADERS < G::NW && wave >= G::LOADERS) return;  // wave-uniform (readfirstlane'd)
+    if (wave >= G::LOADERS) return;  // wave-uniform (readfirstlane'd)
     const void* a = sgpr_ptr(Abase + (AK ? (long)kt * BK : (long)kt * BK * lda));
-    const void* b = sgpr_ptr(Bbase + (BKC ? (long)kt * BK : (long)kt * BK * ldb));
+    const void* b = sgpr_ptr(Bbase + (long)kt * BK * ldb);
 #pragma unroll
     for (int q = 0; q < PS; ++q) piece(a, b, q, slot);
   };
@@ -204,13 +189,6 @@ __global__ __launch_bounds__(Geo<VAR>::THREADS) void wgrad_gemm_k(const T* __res
   for (int i = 0; i < 8; ++i)
     aoff[i] = AK ? (wm * 128 + 16 * i + (lane & 15)) * 64 + (((lane >> 4) ^ fA((lane & 15) >> 2)) << 4)
                  : rowb + (wm * 16 + ((2 * i) ^ f)) * 16;
-  if constexpr (G::M32) {
-    // lane (g, q, p): k-rows 8(g>>1) + q (+4) of k-half i>>2, columns 16(g&1) + 4p.. of 32-wide
-    // m tile i&3 (a[i]) / n tile j&1 of k-half j>>1 (b[j]) — the 32x32x16 operand layout
-    const int rb32 = (8 * (g >> 1) + qq) * ROWB + (p & 1) * 8 + (p >> 1) * 16 + 2 * (g & 1) * 16;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) aoff[i] = rb32 + (i >> 2) * 16 * ROWB + (wm * 16 + 4 * ((i & 3) ^ qq)) * 16;
-  }
   // A fragment: 8 k-values of one m row (row read) or of one m column (two transposed reads)
   auto fragA = [&](const char* p) -> s16x8 {
     if constexpr (AK) return *(const __attribute__((address_space(3))) s16x8*)(p);
@@ -218,28 +196,17 @@ __global__ __launch_bounds__(Geo<VAR>::THREADS) void wgrad_gemm_k(const T* __res
   };
 #pragma unroll
   for (int j = 0; j < FN; ++j)
-    boff[j] = BKC ? B_BASE + (wn * 16 * FN + 16 * j + (lane & 15)) * 64 + (((lane >> 4) ^ fA((lane & 15) >> 2)) << 4)
-                  : B_BASE + rowb + ((wn * 2 * FN + 2 * j) ^ f) * 16;
-  // B fragment: 8 k-values of one n column (two transposed reads) or of one n row (BKC)
-  auto fragB = [&](const char* p) -> s16x8 {
-    if constexpr (BKC) return *(const __attribute__((address_space(3))) s16x8*)(p);
-    else return frag(p);
-  };
-  if constexpr (G::M32) {
-    const int rb32 = (8 * (g >> 1) + qq) * ROWB + (p & 1) * 8 + (p >> 1) * 16 + 2 * (g & 1) * 16;
-#pragma unroll
-    for (int j = 0; j < FN; ++j) boff[j] = B_BASE + rb32 + (j >> 1) * 16 * ROWB + ((wn * 8 + 4 * (j & 1)) ^ (4 * qq)) * 16;
-  }
+    boff[j] = B_BASE + rowb + ((wn * 2 * FN + 2 * j) ^ f) * 16;
+  // B fragment: 8 k-values of one n column (two transposed reads)
+  auto fragB = [&](const char* p) -> s16x8 { return frag(p); };
 
-  using Acc = std::conditional_t<G::M32, f32x16, f32x4>;
-  constexpr int AI = G::M32 ? 4 : 8, AJ = G::M32 ? 2 : FN;
-  Acc acc[AI][AJ];
+  f32x4 acc[8][FN];
 #pragma unroll
-  for (int i = 0; i < AI; ++i)
+  for (int i = 0; i < 8; ++i)
 #pragma unroll
-    for (int j = 0; j < AJ; ++j) acc[i][j] = Acc{};
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{};
 
-  if constexpr (G::PREFETCH) {
+  {
     // Fragments of slot kt+1 are read into the second register set WHILE slot kt's MFMAs
     // run, so no wave waits on LDS latency after a barrier: the MFMA pipe stays fed across it.
     // Ring: DMA of k-slot kt+4 refills LDS slot kt as soon as every wave holds slot kt in VGPRs.
@@ -271,13 +238,8 @@ __global__ __launch_bounds__(Geo<VAR>::THREADS) void wgrad_gemm_k(const T* __res
       for (int i = 0; i < 8; ++i) {
         if constexpr (!LAST) Gn.a[i] = fragA(nxt + aoff[i]);
         __builtin_amdgcn_s_setprio(1);
-        if constexpr (G::M32) {
 #pragma unroll
-          for (int j = 0; j < 2; ++j) acc[i & 3][j] = Mfma<T>::run(F.a[i], F.b[(i >> 2) * 2 + j], acc[i & 3][j]);
-        } else {
-#pragma unroll
-          for (int j = 0; j < FN; ++j) acc[i][j] = Mfma<T>::run(F.a[i], F.b[j], acc[i][j]);
-        }
+        for (int j = 0; j < FN; ++j) acc[i][j] = Mfma<T>::run(F.a[i], F.b[j], acc[i][j]);
         __builtin_amdgcn_s_setprio(0);
       }
     };
@@ -306,40 +268,6 @@ __global__ __launch_bounds__(Geo<VAR>::THREADS) void wgrad_gemm_k(const T* __res
     it(W1{}, Nn{}, Nn{}, kt + 1, F1, F0);
     it(W0{}, Nn{}, Nn{}, kt + 2, F0, F1);
     it(W0{}, Nn{}, Y{}, kt + 3, F1, F0);
-  } else if constexpr (!G::M32) {
-  stage(0, 0);
-  stage(1, 1);
-  stage(2, 2);
-
-  auto step = [&](int kt, int slot) {
-    const int rem = nk - 1 - kt;  // slots still in flight behind this one
-    if (rem >= 2) vm_wait<2 * PS>();
-    else if (rem == 1) vm_wait<PS>();
-    else vm_wait<0>();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of slot kt-1 are done
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");  // no LDS read of slot kt is hoisted above the barrier
-    if (kt + 3 < nk) stage(kt + 3, (slot + 3) & (NSLOT - 1));
-    const char* base = smem + slot * SLOTB;
-    s16x8 bf[FN];
-#pragma unroll
-    for (int j = 0; j < FN; ++j) bf[j] = fragB(base + boff[j]);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const s16x8 af = fragA(base + aoff[i]);
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int j = 0; j < FN; ++j) acc[i][j] = Mfma<T>::run(af, bf[j], acc[i][j]);
-      __builtin_amdgcn_s_setprio(0);
-    }
-  };
-
-  for (int kt = 0; kt < nk; kt += NSLOT) {
-    step(kt + 0, 0);
-    step(kt + 1, 1);
-    step(kt + 2, 2);
-    step(kt + 3, 3);
-  }
   }
 
   // ---- epilogue: lane holds C[16i + 4(l>>4) + e][16j + (l&15)] of the wave's 128 x 64 block
@@ -360,27 +288,15 @@ __global__ __launch_bounds__(Geo<VAR>::THREADS) void wgrad_gemm_k(const T* __res
 #pragma unroll
     for (int pass = 0; pass < 2; ++pass) {
       if (wm == pass) {
-        if constexpr (G::M32) {  // 32x32 layout: row 8(e>>2) + 4(l>>5) + (e&3), column l&31
 #pragma unroll
-          for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < 8; ++i)
 #pragma unroll
-            for (int e = 0; e < 16; ++e)
+          for (int e = 0; e < 4; ++e)
 #pragma unroll
-              for (int j = 0; j < 2; ++j) {
-                const int lr = 32 * i + 8 * (e >> 2) + 4 * (lane >> 5) + (e & 3), col = wn * 64 + 32 * j + (lane & 31);
-                *(float*)(smem + lr * RB + ((((col >> 2) ^ (lr & 7)) << 4) | ((col & 3) << 2))) = acc[i][j][e];
-              }
-        } else {
-#pragma unroll
-          for (int i = 0; i < 8; ++i)
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-#pragma unroll
-              for (int j = 0; j < FN; ++j) {
-                const int lr = 16 * i + 4 * (lane >> 4) + e, col = wn * 16 * FN + 16 * j + (lane & 15);
-                *(float*)(smem + lr * RB + ((((col >> 2) ^ (lr & 7)) << 4) | ((col & 3) << 2))) = acc[i][j][e];
-              }
-        }
+            for (int j = 0; j < FN; ++j) {
+              const int lr = 16 * i + 4 * (lane >> 4) + e, col = wn * 16 * FN + 16 * j + (lane & 15);
+              *(float*)(smem + lr * RB + ((((col >> 2) ^ (lr & 7)) << 4) | ((col & 3) << 2))) = acc[i][j][e];
+            }
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
@@ -417,19 +333,6 @@ __global__ __launch_bounds__(Geo<VAR>::THREADS) void wgrad_gemm_k(const T* __res
   }
   // (unaligned output: element stores; the accumulate test is hoisted out of the element loops —
   //  a per-element select makes hipcc branch around every load and wait for each separately)
-  if constexpr (G::M32) {
-    OT* c = cbase + (wm * 128 + 4 * (lane >> 5)) * ldc + wn * 64 + (lane & 31);
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int e = 0; e < 16; ++e)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          OT* o = c + (long)(32 * i + 8 * (e >> 2) + (e & 3)) * ldc + 32 * j;
-          *o = from_f<OT>((accumulate ? to_f(*o) : 0.f) + acc[i][j][e]);
-        }
-    return;
-  } else {
   OT* c = cbase + (wm * 128 + 4 * (lane >> 4)) * ldc + wn * 16 * FN + (lane & 15);
   if (accumulate) {
 #pragma unroll
@@ -449,13 +352,12 @@ __global__ __launch_bounds__(Geo<VAR>::THREADS) void wgrad_gemm_k(const T* __res
 #pragma unroll
         for (int j = 0; j < FN; ++j) c[(long)(16 * i + e) * ldc + 16 * j] = from_f<OT>(acc[i][j][e]);
   }
-  }
 }
 
 // ---- Variant 4: one wave per SIMD, 128 x 128 outputs per wave (the structure of
 // csrc/gemm_nt.hip's 4-wave schedule and of gfx950 hipBLASLt's MT256x256x64 kernels) on this
 // kernel's operand layout.  A K-tile is 64 tokens = two 32-row ring slots per operand (LDS slots
-// 2b, 2b+1 of buffer b; same images, swizzle and transposed fragment reads as variants 0-3);
+// 2b, 2b+1 of buffer b; same images, swizzle and transposed fragment reads as wgrad_gemm_k);
 // every fragment of a K-tile sits in VGPRs (a0/b0 k-step 0, a1/b1 k-step 1), the MFMAs keep their
 // accumulators in place in AGPRs (g4::MfA), operands swapped so a lane holds 4 consecutive
 // columns of a row (g4::epilogue4).  Per wave and K-tile: 128 MFMAs, 64 ds_read_b64_tr_b16,
@@ -465,9 +367,8 @@ __global__ __launch_bounds__(Geo<VAR>::THREADS) void wgrad_gemm_k(const T* __res
 //   section 2 (a1 x b1): the rest of the pieces; after MFMA 47 vmcnt(16) + barrier (RAW for tile
 //     t+1), then the reads of a0/b0 of tile t+1 over the last 16 MFMAs.
 // The body is branch-free for every tile (past the end the pieces re-load the last tile into a
-// buffer nothing reads again).  DV 0: global_load_lds with the tile's base pointer in SGPRs;
-// 1: buffer_load ... lds on a per-tile descriptor (BLLM_WGRAD4_DMA, default 1).
-template <typename T, typename OT, int DV>
+// buffer nothing reads again).  Pieces are buffer_load ... lds on a per-K-tile descriptor.
+template <typename T, typename OT>
 __global__ __launch_bounds__(g4::THREADS4, 1) void wgrad4_k(const T* __restrict__ A, long lda,
                                                             const T* __restrict__ B, long ldb, OT* __restrict__ C,
                                                             long ldc, long c_split, int M, int N, int K,
@@ -508,11 +409,10 @@ __global__ __launch_bounds__(g4::THREADS4, 1) void wgrad4_k(const T* __restrict_
     const int p = k & 7, kr = 16 * wave + 2 * p;
     const uint32_t d = lds0 + (k >= 8 ? B_BASE : 0) + (2 * buf + (kr >> 5)) * SLOTB + (kr & 31) * ROWB;
     const T* base = k < 8 ? Abase + (long)t * 64 * lda : Bbase + (long)t * 64 * ldb;
-    if constexpr (DV == 0) glds16s(sgpr_ptr(base), k < 8 ? voA[p] : voB[p], d);
-    else g4::bdma16<1>(g4::make_rsrc(base), k < 8 ? voA[p] : voB[p], 0u, d);
+    g4::bdma16<1>(g4::make_rsrc(base), k < 8 ? voA[p] : voB[p], 0u, d);
   };
 
-  // ---- fragment offsets (variants 0-3 with 128 columns per wave on both operands)
+  // ---- fragment offsets (those of wgrad_gemm_k with 128 columns per wave on both operands)
   const int g = lane >> 4, qq = (lane & 15) >> 2, p4 = lane & 3;
   const int f = 2 * (qq | ((g & 1) << 2));
   const int rowb = (8 * g + qq) * ROWB + (p4 & 1) * 8 + (p4 >> 1) * 16;
@@ -592,263 +492,40 @@ __global__ __launch_bounds__(g4::THREADS4, 1) void wgrad4_k(const T* __restrict_
                                      (OT*)nullptr, 0);
 }
 
-template <typename T, typename OT, int DV>
+template <typename T, typename OT>
 void launch4(const void* a, long lda, const void* b, long ldb, void* c, long ldc, long c_split, int M, int N, int K,
              int S, bool accumulate, hipStream_t s) {
-  static const bool attr = hipFuncSetAttribute((const void*)wgrad4_k<T, OT, DV>,
+  static const bool attr = hipFuncSetAttribute((const void*)wgrad4_k<T, OT>,
                                                hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES) == hipSuccess;
   (void)attr;
   const dim3 grid((M / BM) * (N / BN), S);
   const bool wide = reinterpret_cast<uintptr_t>(c) % 16 == 0 && (ldc * (long)sizeof(OT)) % 16 == 0 &&
                     (c_split * (long)sizeof(OT)) % 16 == 0;
-  hipLaunchKernelGGL((wgrad4_k<T, OT, DV>), grid, dim3(g4::THREADS4), LDS_BYTES, s, (const T*)a, lda, (const T*)b, ldb,
+  hipLaunchKernelGGL((wgrad4_k<T, OT>), grid, dim3(g4::THREADS4), LDS_BYTES, s, (const T*)a, lda, (const T*)b, ldb,
                      (OT*)c, ldc, c_split, M, N, K, (int)accumulate, (int)wide);
 }
 
-// ---- Variant 5: variant 4 made persistent (as csrc/gemm_nt.hip's BLLM_GEMM_NT_SCHED=3): one
-// workgroup per CU walks the work items (output tile x split-K slice) w, w + G, ..., the K-tile
-// stream runs across work items (the last two K-tiles of an item prefetch the next item's first
-// two), and the epilogue stores straight from the accumulators (lane: 4 consecutive columns of a
-// row), while the next item's first K-tile is already landing.  ACC is a template parameter and
-// rows must be aligned to the store width (host), so the epilogue is branch-free.
-template <typename T, typename OT, bool ACC>
-__global__ __launch_bounds__(g4::THREADS4, 1) void wgrad4p_k(const T* __restrict__ A, long lda,
-                                                             const T* __restrict__ B, long ldb, OT* __restrict__ C,
-                                                             long ldc, long c_split, int M, int N, int K, int S) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-  const int wm = wave >> 1, wn = wave & 1;
-  const int nbm = M / BM, nbn = N / BN, nblk = nbm * nbn, nwork = nblk * S, G = gridDim.x;
-  const int q8 = nblk >> 3, r8 = nblk & 7, per_group = GROUP_M * nbn, nch = K / KCH;
-  // work item w: split sp = w / nblk (all tiles of a split, then the next), tile = w % nblk
-  struct Item { long m0, n0; int sp, c_lo, nt; };
-  auto item = [&](int w) {
-    Item it;
-    it.sp = w / nblk;
-    const int tid = w - it.sp * nblk, xcd = tid & 7;
-    const int wid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (tid >> 3);
-    const int grp = wid / per_group, first_m = grp * GROUP_M;
-    const int gm = nbm - first_m < GROUP_M ? nbm - first_m : GROUP_M;
-    const int in_g = wid - grp * per_group;
-    it.m0 = (long)(first_m + in_g % gm) * BM;
-    it.n0 = (long)(in_g / gm) * BN;
-    it.c_lo = (int)((long)nch * it.sp / S);
-    it.nt = ((int)((long)nch * (it.sp + 1) / S) - it.c_lo) * (KCH / 64);
-    return it;
-  };
-
-  uint32_t voA[8], voB[8];
-#pragma unroll
-  for (int p = 0; p < 8; ++p) {
-    const int kr = 16 * wave + 2 * p + (lane >> 5), c = (lane & 31) ^ swz(kr & 31);
-    voA[p] = (uint32_t)((kr * lda + 8 * c) * (long)sizeof(T));
-    voB[p] = (uint32_t)((kr * ldb + 8 * c) * (long)sizeof(T));
-  }
-  const uint32_t lds0 = lds_u32(smem);
-  int w = blockIdx.x;
-  Item cur = item(w);
-  const T* Ac = A + (long)cur.c_lo * KCH * lda + cur.m0;
-  const T* Bc = B + (long)cur.c_lo * KCH * ldb + cur.n0;
-  int w_n = w + G;
-  Item nx = cur;
-  const T* An = Ac;
-  const T* Bn = Bc;
-  auto set_next = [&]() {
-    w_n = w + G;
-    if (w_n < nwork) {
-      nx = item(w_n);
-      An = A + (long)nx.c_lo * KCH * lda + nx.m0;
-      Bn = B + (long)nx.c_lo * KCH * ldb + nx.n0;
-    } else {
-      An = Ac, Bn = Bc;
-    }
-  };
-  set_next();
-  auto dma = [&](int t, int buf, int k) {
-    const int p = k & 7, kr = 16 * wave + 2 * p;
-    const uint32_t d = lds0 + (k >= 8 ? B_BASE : 0) + (2 * buf + (kr >> 5)) * SLOTB + (kr & 31) * ROWB;
-    const bool nxt = t >= cur.nt;
-    const int tt = !nxt ? t : (w_n < nwork ? t - cur.nt : cur.nt - 1);
-    const T* base = k < 8 ? (nxt ? An : Ac) + (long)tt * 64 * lda : (nxt ? Bn : Bc) + (long)tt * 64 * ldb;
-    g4::bdma16<1>(g4::make_rsrc(base), k < 8 ? voA[p] : voB[p], 0u, d);
-  };
-
-  const int g = lane >> 4, qq = (lane & 15) >> 2, p4 = lane & 3;
-  const int f = 2 * (qq | ((g & 1) << 2));
-  const int rowb = (8 * g + qq) * ROWB + (p4 & 1) * 8 + (p4 >> 1) * 16;
-  const char* pa = smem + rowb + (wm * 16) * 16;
-  const char* pb = smem + B_BASE + rowb + (wn * 16) * 16;
-  auto rdA = [&](int sl, int i) -> g4::s16x8 { return frag(pa + sl * SLOTB + ((2 * i) ^ f) * 16); };
-  auto rdB = [&](int sl, int j) -> g4::s16x8 { return frag(pb + sl * SLOTB + ((2 * j) ^ f) * 16); };
-
-  g4::f32x4 acc[8][8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = g4::f32x4{};
-  g4::s16x8 a0[8], b0[8], a1[8], b1[8];
-
-#pragma unroll
-  for (int k = 0; k < 16; ++k) dma(0, 0, k);
-#pragma unroll
-  for (int k = 0; k < 16; ++k) dma(1, 1, k);
-  vm_wait<16>();
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-#pragma unroll
-  for (int i = 0; i < 8; ++i) a0[i] = rdA(0, i), b0[i] = rdB(0, i);
-
-  auto tile = [&](int t, auto cur_c) {
-    constexpr int cb = decltype(cur_c)::value, nb = cb ^ 1;
-#pragma unroll
-    for (int n = 0; n < 64; ++n) {
-      const int i = n >> 3, j = n & 7;
-      g4::MfA<T>::run(acc[i][j], b0[j], a0[i]);
-      if (n == 0) a1[0] = rdA(2 * cb + 1, 0);
-      else if (n <= 8) b1[n - 1] = rdB(2 * cb + 1, n - 1);
-      else if (n < 16) a1[n - 8] = rdA(2 * cb + 1, n - 8);
-      if (n == 31) {
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-      }
-      if (n >= 32 && (n - 32) % 5 == 0) dma(t + 2, cb, (n - 32) / 5);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-#pragma unroll
-    for (int n = 0; n < 64; ++n) {
-      const int i = n >> 3, j = n & 7;
-      if (n >= 3 && n <= 43 && (n - 3) % 5 == 0) dma(t + 2, cb, 7 + (n - 3) / 5);
-      if (n == 48) {
-        vm_wait<16>();
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-      }
-      if (n >= 48) {
-        const int r = n - 48;
-        if (r == 0) a0[0] = rdA(2 * nb, 0);
-        else if (r <= 8) b0[r - 1] = rdB(2 * nb, r - 1);
-        else a0[r - 8] = rdA(2 * nb, r - 8);
-      }
-      g4::MfA<T>::run(acc[i][j], b1[j], a1[i]);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  };
-  using I0 = std::integral_constant<int, 0>;
-  using I1 = std::integral_constant<int, 1>;
-  for (;;) {
-    for (int t = 0; t < cur.nt; t += 2) {
-      tile(t, I0{});
-      tile(t + 1, I1{});
-    }
-    g4::mfma_drain();
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) asm volatile("" : "+a"(acc[i][j]));
-    OT* cw = C + cur.sp * c_split + (cur.m0 + 128 * wm + (lane & 15)) * ldc + cur.n0 + 128 * wn + 4 * (lane >> 4);
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        OT* o = cw + (long)(16 * i) * ldc + 16 * j;
-        typedef OT o4 __attribute__((ext_vector_type(4)));
-        g4::f32x4 v = acc[i][j];
-        if constexpr (ACC) v += __builtin_convertvector(*(const o4*)o, g4::f32x4);
-        *(o4*)o = __builtin_convertvector(v, o4);
-      }
-    if (w_n >= nwork) break;
-    __builtin_amdgcn_sched_barrier(0);
-    {
-      g4::s16x8 z = g4::s16x8{};
-      asm volatile("s_nop 4" : "+v"(z));
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) g4::MfA<T>::zero(acc[i][j], z);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) a0[i] = rdA(0, i), b0[i] = rdB(0, i);
-    w = w_n, cur = nx, Ac = An, Bc = Bn;
-    set_next();
-  }
-  vm_wait<0>();
-}
-
-template <typename T, typename OT>
-bool launch4p(const void* a, long lda, const void* b, long ldb, void* c, long ldc, long c_split, int M, int N, int K,
-              int S, bool accumulate, hipStream_t s) {
-  const long al = sizeof(OT) == 2 ? 8 : 16;
-  if (reinterpret_cast<uintptr_t>(c) % al || (ldc * (long)sizeof(OT)) % al || (c_split * (long)sizeof(OT)) % al)
-    return false;
-  static int ncu = 0;
-  if (!ncu) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    hipDeviceProp_t prop;
-    ncu = hipGetDeviceProperties(&prop, dev) == hipSuccess ? prop.multiProcessorCount : 256;
-    ncu = ncu < 8 ? 8 : ncu / 8 * 8;
-  }
-  const int nwork = (M / BM) * (N / BN) * S;
-  const int grid = nwork < ncu ? nwork : ncu;
-#define BLLM_W4P(ACCv)                                                                                                 \
-  do {                                                                                                                 \
-    static const bool at_ = hipFuncSetAttribute((const void*)wgrad4p_k<T, OT, ACCv>,                                   \
-                                                hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES) == hipSuccess; \
-    (void)at_;                                                                                                         \
-    hipLaunchKernelGGL((wgrad4p_k<T, OT, ACCv>), dim3(grid), dim3(g4::THREADS4), LDS_BYTES, s, (const T*)a, lda,      \
-                       (const T*)b, ldb, (OT*)c, ldc, c_split, M, N, K, S);                                           \
-  } while (0)
-  if (accumulate) BLLM_W4P(true);
-  else BLLM_W4P(false);
-#undef BLLM_W4P
-  return true;
-}
-
-template <typename T, typename OT, int VAR, bool AK = false, bool BKC = false>
+template <typename T, typename OT, bool AK = false>
 void launch_v(const void* a, long lda, const void* b, long ldb, void* c, long ldc, long c_split, int M, int N, int K,
               int S, bool accumulate, hipStream_t s) {
-  static const bool attr = hipFuncSetAttribute((const void*)wgrad_gemm_k<T, OT, VAR, AK, BKC>,
+  static const bool attr = hipFuncSetAttribute((const void*)wgrad_gemm_k<T, OT, AK>,
                                                hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES) == hipSuccess;
   (void)attr;
   const dim3 grid((M / BM) * (N / BN), S);
   const bool wide = reinterpret_cast<uintptr_t>(c) % 16 == 0 && (ldc * (long)sizeof(OT)) % 16 == 0 &&
                     (c_split * (long)sizeof(OT)) % 16 == 0;
-  hipLaunchKernelGGL((wgrad_gemm_k<T, OT, VAR, AK, BKC>), grid, dim3(Geo<VAR>::THREADS), LDS_BYTES, s, (const T*)a, lda,
+  hipLaunchKernelGGL((wgrad_gemm_k<T, OT, AK>), grid, dim3(Geo::THREADS), LDS_BYTES, s, (const T*)a, lda,
                      (const T*)b, ldb, (OT*)c, ldc, c_split, M, N, K, (int)accumulate, (int)wide);
 }
 
-constexpr int DEFAULT_VARIANT = 2;
-
-// Default: variant 4 (one wave per SIMD, 128 x 128 per wave) — 1.02-1.06x variant 2 on the
-// Llama-3-8B / Llama-3.2-1B / GPT2-774M weight gradients at 40,960 tokens
-// (profiles/r3/wgrad4_vs_v2.jsonl) — except for deep split-K (S >= 8: GPT2-774M's 1280 x 1280
-// o-projection, 200 workgroups), where variant 2 was 12 % faster.
-int variant(int S) {
-  const char* e = getenv("BLLM_WGRAD_VARIANT");  // per launch (A/B in one process); ~100 ns
-  return e && *e ? atoi(e) : (S >= 8 ? DEFAULT_VARIANT : 4);
-}
-
+// wgrad4_k (1.02-1.06x wgrad_gemm_k on the Llama-3-8B / Llama-3.2-1B / GPT2-774M weight
+// gradients at 40,960 tokens, profiles/r3/wgrad4_vs_v2.jsonl) except for deep split-K (S >= 8:
+// GPT2-774M's 1280 x 1280 o-projection, 200 workgroups), where wgrad_gemm_k was 12 % faster
 template <typename T, typename OT>
 void launch(const void* a, long lda, const void* b, long ldb, void* c, long ldc, long c_split, int M, int N, int K,
             int S, bool accumulate, hipStream_t s) {
-  switch (variant(S)) {
-    case 5:
-      if (launch4p<T, OT>(a, lda, b, ldb, c, ldc, c_split, M, N, K, S, accumulate, s)) break;
-      launch4<T, OT, 1>(a, lda, b, ldb, c, ldc, c_split, M, N, K, S, accumulate, s);
-      break;
-    case 4: {
-      const char* e = getenv("BLLM_WGRAD4_DMA");
-      if (e && *e == '0') launch4<T, OT, 0>(a, lda, b, ldb, c, ldc, c_split, M, N, K, S, accumulate, s);
-      else launch4<T, OT, 1>(a, lda, b, ldb, c, ldc, c_split, M, N, K, S, accumulate, s);
-      break;
-    }
-    case 0: launch_v<T, OT, 0>(a, lda, b, ldb, c, ldc, c_split, M, N, K, S, accumulate, s); break;
-    case 2: launch_v<T, OT, 2>(a, lda, b, ldb, c, ldc, c_split, M, N, K, S, accumulate, s); break;
-    case 3: launch_v<T, OT, 3>(a, lda, b, ldb, c, ldc, c_split, M, N, K, S, accumulate, s); break;
-    default: launch_v<T, OT, 1>(a, lda, b, ldb, c, ldc, c_split, M, N, K, S, accumulate, s); break;
-  }
+  if (S >= 8) launch_v<T, OT>(a, lda, b, ldb, c, ldc, c_split, M, N, K, S, accumulate, s);
+  else launch4<T, OT>(a, lda, b, ldb, c, ldc, c_split, M, N, K, S, accumulate, s);
 }
 
 }  // namespace
@@ -858,17 +535,8 @@ bool gemm_nn_supported(int M, int N, int K) { return M > 0 && N > 0 && M % BM ==
 void gemm_nn(DType dt, DType odt, const void* a, long lda, const void* b, long ldb, void* c, long ldc, int M, int N,
              int K, bool accumulate, hipStream_t s) {
   BLLM_DISPATCH(odt, OT, {
-    if (dt == DType::BF16) launch_v<bf16_t, OT, DEFAULT_VARIANT, true>(a, lda, b, ldb, c, ldc, 0, M, N, K, 1, accumulate, s);
-    else launch_v<f16_t, OT, DEFAULT_VARIANT, true>(a, lda, b, ldb, c, ldc, 0, M, N, K, 1, accumulate, s);
-  });
-}
-
-// both operands K-contiguous: C[M, N] (+)= A[M, K] B[N, K]^T (a Linear's forward y = x W^T)
-void gemm_nt(DType dt, DType odt, const void* a, long lda, const void* b, long ldb, void* c, long ldc, int M, int N,
-             int K, bool accumulate, hipStream_t s) {
-  BLLM_DISPATCH(odt, OT, {
-    if (dt == DType::BF16) launch_v<bf16_t, OT, DEFAULT_VARIANT, true, true>(a, lda, b, ldb, c, ldc, 0, M, N, K, 1, accumulate, s);
-    else launch_v<f16_t, OT, DEFAULT_VARIANT, true, true>(a, lda, b, ldb, c, ldc, 0, M, N, K, 1, accumulate, s);
+    if (dt == DType::BF16) launch_v<bf16_t, OT, true>(a, lda, b, ldb, c, ldc, 0, M, N, K, 1, accumulate, s);
+    else launch_v<f16_t, OT, true>(a, lda, b, ldb, c, ldc, 0, M, N, K, 1, accumulate, s);
   });
 }
 

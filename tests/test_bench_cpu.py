@@ -127,3 +127,17 @@ def test_bench_random_ids_arm():
     """``--data random_ids``: the A/B arm with device-resident random token ids."""
     out = _run(1, ["--data", "random_ids"])
     assert out["data"].startswith("synthetic random token ids") and "data_check" not in out
+
+
+@pytest.mark.parametrize("parallel", ["fsdp", "ddp", "zero1"])
+def test_bench_world2_matches_world1_on_the_global_batch(parallel):
+    """``--data fixed_ids``: world 2 at B=1 per rank trains the same global batches as world 1 at
+    B=2, so the engines' sharded path (real shards, cross-rank reduce-scatter / all-gather, clip
+    norm over ranks) must reproduce the world-1 loss trace."""
+    one = _run(1, ["--parallel", parallel, "--data", "fixed_ids", "--batch_size", "2"])
+    two = _run(2, ["--parallel", parallel, "--data", "fixed_ids", "--batch_size", "1"], spawn=True)
+    assert one["config"]["global_batch"] == two["config"]["global_batch"] == 2
+    a, b = one["loss_trace"], two["loss_trace"]
+    assert len(a) == len(b) == 3
+    assert max(abs(x - y) for x, y in zip(a, b)) < 1e-4, (a, b)
+    assert a[-1] != a[0]                          # the optimizer really moved the weights

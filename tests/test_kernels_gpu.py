@@ -276,18 +276,13 @@ def test_flash_attention_deferred_rescale(dt, hd, step):
     _close(dqkv, dqkv0, dt, 4, name="dqkv")
 
 
-@pytest.mark.parametrize("variant", ["1", "2"])
-@pytest.mark.parametrize("hd", [64, 128])
-@pytest.mark.parametrize("p", [0.0, 0.1])
-def test_flash_attention_fwd_variants(variant, hd, p, monkeypatch):
-    """The 32-key-tile forwards (BLLM_ATTN_FWD_VARIANT 1 / 2; 2 is the default for large hd-64
-    dropout grids) against the oracle, and their keep-mask words equal the oracle's hash."""
-    monkeypatch.setenv("BLLM_ATTN_FWD_VARIANT", variant)
-    for B, T, H, G in ((2, 33, 4, 2), (1, 300, 4, 2), (2, 256, 4, 4)):
-        test_flash_attention(torch.bfloat16, B, T, H, G, hd, p, True)
-        test_flash_attention(torch.bfloat16, B, T, H, G, hd, p, False)
-        if p > 0:
-            test_flash_attention_keep_mask(hd, B, T, H, G, True)
+@pytest.mark.parametrize("causal", [True, False])
+def test_flash_attention_fwd_small_tiles(causal):
+    """hd 64 with dropout on a grid of >= 2048 workgroups (16 x 16 heads x 8 query blocks) takes
+    the 32-key-tile forward at 3 workgroups per CU (csrc/attn_mfma.hip:fwd_small_tiles): against
+    the oracle, and its keep-mask words equal the oracle's hash."""
+    test_flash_attention(torch.bfloat16, 16, 1024, 16, 16, 64, 0.1, causal)
+    test_flash_attention_keep_mask(64, 16, 1024, 16, 16, causal)
 
 
 def test_flash_attention_fp32_is_flash_not_materialised():
@@ -534,13 +529,12 @@ def test_split_k_weight_grad(gdt, accumulate):
 
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("odt", [torch.bfloat16, torch.float32])
-@pytest.mark.parametrize("K,M,N,S", [(128, 256, 256, 1), (384, 512, 768, 1), (2048, 768, 512, 3), (1024, 256, 1024, 2)])
+@pytest.mark.parametrize("K,M,N,S", [(128, 256, 256, 1), (384, 512, 768, 1), (2048, 768, 512, 3), (1024, 256, 1024, 2),
+                                     (1024, 256, 512, 8)])
 @pytest.mark.parametrize("accumulate", [False, True])
-@pytest.mark.parametrize("variant", ["0", "1", "2", "3", "4", "5"])
-def test_wgrad_gemm(dt, odt, K, M, N, S, accumulate, variant, monkeypatch):
-    """Token-major MFMA dW kernel c (+)= a^T b (strided a, split-K) vs an fp32 matmul, every
-    schedule variant (BLLM_WGRAD_VARIANT is read per launch)."""
-    monkeypatch.setenv("BLLM_WGRAD_VARIANT", variant)
+def test_wgrad_gemm(dt, odt, K, M, N, S, accumulate):
+    """Token-major MFMA dW kernel c (+)= a^T b (strided a, split-K) vs an fp32 matmul: the 4-wave
+    schedule (S < 8) and the 8-wave one (deep split-K, S = 8)."""
     a_full = torch.randn(K, M + 64, device=DEV).to(dt)
     a = a_full[:, 32:32 + M]                      # lda = M + 64, 64-B offset
     b = torch.randn(K, N, device=DEV).to(dt)
@@ -549,23 +543,6 @@ def test_wgrad_gemm(dt, odt, K, M, N, S, accumulate, variant, monkeypatch):
     expect = a.float().t() @ b.float() + (c.float() if accumulate else 0)
     ops.wgrad_gemm_(a, b, c, accumulate, S)
     check_close(c, expect, odt, k=3.0, name="wgrad")
-
-
-@pytest.mark.parametrize("odt", [torch.bfloat16, torch.float32])
-@pytest.mark.parametrize("K,M,N,S", [(256, 4096, 4096, 2), (640, 4352, 2048, 1), (1024, 2048, 4096, 4)])
-@pytest.mark.parametrize("accumulate", [False, True])
-def test_wgrad_gemm_persistent_multi_item(odt, K, M, N, S, accumulate, monkeypatch):
-    """Persistent dW kernel (BLLM_WGRAD_VARIANT=5) with more work items (tile x split) than
-    workgroups, uneven items per workgroup, the K-tile stream crossing items of different splits."""
-    monkeypatch.setenv("BLLM_WGRAD_VARIANT", "5")
-    a_full = torch.randn(K, M + 64, device=DEV).to(torch.bfloat16)
-    a = a_full[:, 32:32 + M]
-    b = torch.randn(K, N, device=DEV).to(torch.bfloat16)
-    c = torch.randn(M, N, device=DEV).to(odt)
-    assert ops.wgrad_gemm_ok(a, b, c)
-    expect = a.float().t() @ b.float() + (c.float() if accumulate else 0)
-    ops.wgrad_gemm_(a, b, c, accumulate, S)
-    check_close(c, expect, odt, k=3.0, name="wgrad persistent")
 
 
 def test_wgrad_gemm_in_weight_grad_path():
@@ -600,15 +577,9 @@ def test_wgrad_gemm_unaligned_output(accumulate):
 @pytest.mark.parametrize("odt", [None, torch.float32])
 @pytest.mark.parametrize("M,K,N", [(256, 128, 256), (512, 384, 768), (768, 1024, 512), (1024, 4096, 1536)])
 @pytest.mark.parametrize("accumulate", [False, True])
-@pytest.mark.parametrize("impl", ["gemm_nt", "gemm_nt_pingpong", "gemm_nt_4wave", "gemm_nt_persistent", "wgrad_slots"])
-def test_gemm_nt(dt, odt, M, K, N, accumulate, impl, monkeypatch):
-    """Both-operands-K-contiguous GEMM (c = a . b^T, the forward layout) vs an fp32 matmul,
-    strided rows: the 64-deep-K-tile kernel (csrc/gemm_nt.hip, default), its ping-pong schedule
-    (BLLM_GEMM_NT_SCHED=1), its 4-wave 128 x 128-per-wave schedule (BLLM_GEMM_NT_SCHED=2) and
-    the 32-deep-slot kernel of csrc/gemm_wgrad.hip (BLLM_GEMM_NT_IMPL=1)."""
-    monkeypatch.setenv("BLLM_GEMM_NT_IMPL", "1" if impl == "wgrad_slots" else "2")
-    monkeypatch.setenv("BLLM_GEMM_NT_SCHED",
-                       {"gemm_nt_pingpong": "1", "gemm_nt_4wave": "2", "gemm_nt_persistent": "3"}.get(impl, "0"))
+def test_gemm_nt(dt, odt, M, K, N, accumulate):
+    """Both-operands-K-contiguous GEMM (c = a . b^T, the forward layout) on the persistent kernel
+    of csrc/gemm_nt.hip vs an fp32 matmul, strided rows."""
     a_full = torch.randn(M, K + 64, device=DEV).to(dt)
     a = a_full[:, 32:32 + K]
     b_full = torch.randn(N, K + 32, device=DEV).to(dt)
@@ -622,12 +593,10 @@ def test_gemm_nt(dt, odt, M, K, N, accumulate, impl, monkeypatch):
 @pytest.mark.parametrize("odt", [None, torch.float32])
 @pytest.mark.parametrize("M,K,N", [(8192, 256, 4096), (4352, 128, 4096), (2048, 512, 33 * 256)])
 @pytest.mark.parametrize("accumulate", [False, True])
-def test_gemm_nt_persistent_multi_tile(odt, M, K, N, accumulate, monkeypatch):
-    """Persistent 4-wave schedule (BLLM_GEMM_NT_SCHED=3) with more output tiles than workgroups
-    (each workgroup walks several tiles, the K-tile stream running across tile boundaries; uneven
-    tile counts per workgroup) vs an fp32 matmul, strided A rows."""
-    monkeypatch.setenv("BLLM_GEMM_NT_IMPL", "2")
-    monkeypatch.setenv("BLLM_GEMM_NT_SCHED", "3")
+def test_gemm_nt_persistent_multi_tile(odt, M, K, N, accumulate):
+    """Persistent kernel with more output tiles than workgroups (each workgroup walks several
+    tiles, the K-tile stream running across tile boundaries; uneven tile counts per workgroup) vs
+    an fp32 matmul, strided A rows."""
     dt = torch.bfloat16
     a_full = torch.randn(M, K + 64, device=DEV).to(dt)
     a = a_full[:, 32:32 + K]
@@ -732,7 +701,7 @@ def test_gemm_nt_bias_gelu(dt, M, K, N):
 @pytest.mark.parametrize("M,K,T,H,G", [(512, 256, 256, 4, 2), (2048, 512, 1024, 32, 8), (8192, 128, 1024, 16, 8)])
 def test_gemm_nt_rope(dt, M, K, T, H, G):
     """QKV projection with RoPE in the persistent GEMM's epilogue (K4) against the same GEMM
-    (BLLM_GEMM_NT_SCHED=3) followed by the separate rope_ pass — equal to 1 ulp (same rounding
+    followed by the separate rope_ pass — equal to 1 ulp (same rounding
     points; the fp32 rotation may contract differently) — and against the fp32 oracle."""
     hd = 128
     N = (H + 2 * G) * hd
@@ -742,7 +711,7 @@ def test_gemm_nt_rope(dt, M, K, T, H, G):
     assert ops.gemm_nt_rope_ok(a, w, hd)
     got = ops.gemm_nt_rope(a, w, cos, sin, T, H, G, hd)
     sep = torch.empty(M, N, device=DEV, dtype=dt)
-    ops.gemm_nt_(a, w, sep, False, 3)
+    ops.gemm_nt_(a, w, sep, False)
     ops.rope_(sep, cos, sin, T, H, G, hd)
     ulp = (got.float() - sep.float()).abs() / sep.float().abs().clamp_min(1e-3)
     assert (ulp <= (2 ** -7 if dt == torch.bfloat16 else 2 ** -10)).all(), ulp.max().item()
@@ -753,11 +722,9 @@ def test_gemm_nt_rope(dt, M, K, T, H, G):
 
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("M,K,F", [(256, 128, 128), (512, 512, 768), (1024, 4096, 1792), (4096, 256, 4096)])
-@pytest.mark.parametrize("sched", ["0", "1", "2", "3"])
-def test_gemm_nt_swiglu(dt, M, K, F, sched, monkeypatch):
+def test_gemm_nt_swiglu(dt, M, K, F):
     """Gate/up GEMM with the SwiGLU forward in the epilogue (K10): gu against the fp32 oracle, act
-    bitwise equal to the separate swiglu_fwd kernel applied to that gu; both schedules."""
-    monkeypatch.setenv("BLLM_GEMM_NT_SCHED", sched)
+    bitwise equal to the separate swiglu_fwd kernel applied to that gu."""
     a = torch.randn(M, K, device=DEV).to(dt)
     w = (torch.randn(2 * F, K, device=DEV) / K ** 0.5).to(dt)
     assert ops.gemm_nt_swiglu_ok(a, w)

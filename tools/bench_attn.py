@@ -1,9 +1,7 @@
 #!/usr/bin/env python3
 """Attention kernel micro-benchmark (GPU): fwd / bwd time and effective TFLOP/s at the
 Llama-3-8B (hd 128, GQA 32/8) and GPT-2 (hd 64) training shapes, causal.
-Usage: python tools/bench_attn.py [--iters 20] [--fwd_variants 0,4,5 --rounds 3]
-(``--fwd_variants``: BLLM_ATTN_FWD_VARIANT values A/B'd in this one process, interleaved over
-``--rounds``; each variant's output is checked against the first one's)"""
+Usage: python tools/bench_attn.py [--iters 20] [--shapes llama3-8B-B40,gpt2-774M-B64]"""
 import argparse
 import json
 import os
@@ -36,11 +34,10 @@ def main():
     ap.add_argument("--T", type=int, default=None, help="override the sequence length")
     ap.add_argument("--no_mask", action="store_true",
                     help="dropout shapes: re-hash the keep bits in backward instead of reading the forward's mask")
-    ap.add_argument("--fwd_variants", default="", help="comma-separated forward variants to A/B")
-    ap.add_argument("--rounds", type=int, default=3)
     a = ap.parse_args()
     ops.load_ext(required=True)
     shapes = [("llama3-8B", 4, 1024, 32, 8, 128, 0.0), ("llama3-8B-B24", 24, 1024, 32, 8, 128, 0.0),
+              ("llama3-8B-B40", 40, 1024, 32, 8, 128, 0.0),
               ("llama3.2-1B-B24", 24, 1024, 32, 8, 64, 0.0), ("gpt2-774M", 4, 1024, 20, 20, 64, 0.1),
               ("gpt2-774M-nodrop", 4, 1024, 20, 20, 64, 0.0),
               ("gpt2-774M-B24", 24, 1024, 20, 20, 64, 0.1),
@@ -63,32 +60,6 @@ def main():
         tb = timeit(lambda: ops.flash_attn_bwd(qkv, o, lse, do, B, T, H, G, hd, causal, p, 1, 0, keep_mask=km),
                     a.iters)
         flop = 2 * 2 * B * H * T * T * hd / (2 if causal else 1)  # two matmuls (causal: half the square)
-        if a.fwd_variants:
-            vs = a.fwd_variants.split(",")
-            times = {v: [] for v in vs}
-            outs = {}
-            for _ in range(a.rounds):
-                for v in vs:
-                    os.environ["BLLM_ATTN_FWD_VARIANT"] = v
-                    km2 = None if a.no_mask else ops.attn_keep_mask(qkv, B, T, H, hd, p)
-                    outs[v] = ops.flash_attn_fwd(qkv, B, T, H, G, hd, causal, p, 1, 0, keep_mask=km2)
-                    if km2 is not None:
-                        outs[v] = outs[v] + (km2,)
-                    times[v].append(timeit(lambda: ops.flash_attn_fwd(qkv, B, T, H, G, hd, causal, p, 1, 0,
-                                                                      keep_mask=km2), a.iters))
-            os.environ.pop("BLLM_ATTN_FWD_VARIANT", None)
-            v0 = vs[0]
-            for v in vs:
-                t_med = sorted(times[v])[len(times[v]) // 2]
-                same = all(torch.equal(x, y) for x, y in zip(outs[v][1:], outs[v0][1:]))
-                mask_same = len(outs[v]) < 3 or torch.equal(outs[v][2], outs[v0][2])
-                lse_err = (outs[v][1] - outs[v0][1]).abs().max().item()
-                err = ((outs[v][0].float() - outs[v0][0].float()).norm() / outs[v0][0].float().norm()).item()
-                print(json.dumps(dict(shape=name, fwd_variant=v, fwd_ms_med=round(t_med, 4),
-                                      fwd_ms_all=[round(x, 4) for x in times[v]],
-                                      fwd_tflops=round(flop / t_med / 1e9, 1),
-                                      rel_err_vs_first=err, lse_mask_equal=same, keep_mask_equal=mask_same,
-                                      lse_max_abs_diff=lse_err)))
         res.append(dict(shape=name, B=B, T=T, causal=causal, keep_mask=km is not None, fwd_ms=round(tf, 4), bwd_ms=round(tb, 4),
                         fwd_tflops=round(flop / tf / 1e9, 1), bwd_tflops_5mm=round(2.5 * flop / tb / 1e9, 1)))
     for r in res:

@@ -1,12 +1,12 @@
 #!/usr/bin/env python3
 """Forward-layout GEMM A/B (GPU): y[M, N] = x[M, K] . W[N, K]^T, bf16, random operands.
 
-hipBLASLt (torch.mm), the 64-deep-K-tile kernel csrc/gemm_nt.hip (ops.gemm_nt_ default), its
-ping-pong schedule (BLLM_GEMM_NT_SCHED=1) and the 32-deep-slot kernel of csrc/gemm_wgrad.hip
-(BLLM_GEMM_NT_IMPL=1), interleaved in ONE process over
---rounds, median per shape; each kernel's output checked against hipBLASLt's (relative
-Frobenius).  Shapes: the Llama-3-8B projections at the bench's 40 x 1024 tokens and GPT2-774M's
-at 24 x 1024.  Usage: python tools/bench_gemm_nt.py [--rounds 3 --iters 10 --models llama,gpt2]"""
+hipBLASLt (torch.mm) vs the persistent kernel of csrc/gemm_nt.hip (ops.gemm_nt_), interleaved
+in ONE process over --rounds, median per shape; the kernel's output checked against
+hipBLASLt's (relative Frobenius).  Shapes: the Llama-3-8B projections at the bench's 40 x 1024
+tokens and GPT2-774M's at 24 x 1024.  ``--swiglu``: gate/up + SwiGLU and QKV + RoPE, hipBLASLt +
+the separate pass vs the fused epilogues.
+Usage: python tools/bench_gemm_nt.py [--rounds 3 --iters 10 --models llama,gpt2 --only down]"""
 import argparse
 import json
 import os
@@ -42,18 +42,16 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--models", default="llama,gpt2")
-    ap.add_argument("--nt4_dma", default="0", help="comma list of BLLM_GEMM_NT4_DMA variants of the 4-wave arm")
-    ap.add_argument("--arms", default="hipblaslt,new,pp,4w,old,4p,4g")
+    ap.add_argument("--arms", default="hipblaslt,gemm_nt")
     ap.add_argument("--only", default="", help="comma list of gemm names to run (e.g. gate_up)")
-    ap.add_argument("--nt4p_sv", default="0", help="comma list of BLLM_GEMM_NT4P_SV variants of the persistent arm")
-    ap.add_argument("--nt4p_gm", default="", help="comma list of BLLM_GEMM_NT4P_GM (tile-group depth) arms, SV 0")
     ap.add_argument("--swiglu", action="store_true",
-                    help="gate/up + SwiGLU: hipBLASLt GEMM + separate swiglu_fwd vs the fused kernel (sched 2, 3)")
+                    help="gate/up + SwiGLU and QKV + RoPE: hipBLASLt + separate pass vs the fused kernels")
     a = ap.parse_args()
     ops.load_ext(required=True)
     dt = torch.bfloat16
     if a.swiglu:
-        return bench_swiglu(a)
+        return bench_fused(a)
+    want = a.arms.split(",")
     for model in a.models.split(","):
         tokens, shapes = SHAPES[model]
         for name, (k, n) in shapes.items():
@@ -63,83 +61,28 @@ def main():
             x = torch.rand(m, k, device="cuda", dtype=dt) * 2 - 1
             w = (torch.rand(n, k, device="cuda", dtype=dt) * 2 - 1) * 0.05
             ref = torch.mm(x, w.t())
-            dvs = a.nt4_dma.split(",")
-            svs = a.nt4p_sv.split(",")
-            gms = [g for g in a.nt4p_gm.split(",") if g]
-            outs = {k_: torch.empty(m, n, device="cuda", dtype=dt)
-                    for k_ in ["new", "pp", "old"] + ["w4_" + d for d in dvs] + ["p4_" + v for v in svs]
-                    + ["g4_" + g for g in gms]}
             y = torch.empty(m, n, device="cuda", dtype=dt)
-
-            def new():
-                os.environ.pop("BLLM_GEMM_NT_IMPL", None)
-                os.environ["BLLM_GEMM_NT_SCHED"] = "0"
-                ops.gemm_nt_(x, w, outs["new"])
-
-            def pp():
-                os.environ.pop("BLLM_GEMM_NT_IMPL", None)
-                os.environ["BLLM_GEMM_NT_SCHED"] = "1"
-                ops.gemm_nt_(x, w, outs["pp"])
-
-            def w4(dv):
-                def f():
-                    os.environ.pop("BLLM_GEMM_NT_IMPL", None)
-                    os.environ["BLLM_GEMM_NT_SCHED"] = "2"
-                    os.environ["BLLM_GEMM_NT4_DMA"] = dv
-                    ops.gemm_nt_(x, w, outs["w4_" + dv])
-                return f
-
-            def p4(sv):
-                def f():
-                    os.environ.pop("BLLM_GEMM_NT_IMPL", None)
-                    os.environ["BLLM_GEMM_NT_SCHED"] = "3"
-                    os.environ["BLLM_GEMM_NT4P_SV"] = sv
-                    ops.gemm_nt_(x, w, outs["p4_" + sv])
-                return f
-
-            def old():
-                os.environ["BLLM_GEMM_NT_IMPL"] = "1"
-                ops.gemm_nt_(x, w, outs["old"])
-
-            fns = {"hipblaslt": lambda: torch.mm(x, w.t(), out=y), "gemm_nt_new": new, "gemm_nt_pp": pp,
-                   "gemm_nt_old": old}
-            fns.update({"gemm_nt_4w_" + d: w4(d) for d in dvs})
-            fns.update({"gemm_nt_4p_" + v: p4(v) for v in svs})
-
-            def g4(gm):
-                def f():
-                    os.environ.pop("BLLM_GEMM_NT_IMPL", None)
-                    os.environ["BLLM_GEMM_NT_SCHED"] = "3"
-                    os.environ["BLLM_GEMM_NT4P_SV"] = "0"
-                    os.environ["BLLM_GEMM_NT4P_GM"] = gm
-                    ops.gemm_nt_(x, w, outs["g4_" + gm])
-                    os.environ.pop("BLLM_GEMM_NT4P_GM", None)
-                return f
-            fns.update({"gemm_nt_4g_" + g: g4(g) for g in gms})
-
-            want = a.arms.split(",")
-            fns = {k_: f for k_, f in fns.items()
-                   if k_ == "hipblaslt" and "hipblaslt" in want or k_.startswith("gemm_nt_") and k_.split("_")[2] in want}
+            out = torch.empty(m, n, device="cuda", dtype=dt)
+            fns = {"hipblaslt": lambda: torch.mm(x, w.t(), out=y), "gemm_nt": lambda: ops.gemm_nt_(x, w, out)}
+            fns = {k_: f for k_, f in fns.items() if k_ in want}
             times = {kk: [] for kk in fns}
             for _ in range(a.rounds):
                 for kk, fn in fns.items():
                     times[kk].append(timeit(fn, a.iters))
-            os.environ.pop("BLLM_GEMM_NT_IMPL", None)
             fl = 2.0 * m * n * k
             r = {"model": model, "gemm": name, "M_N_K": [m, n, k]}
             for kk, ts in times.items():
                 med = sorted(ts)[len(ts) // 2]
                 r[kk + "_us"] = round(med * 1e3, 1)
                 r[kk + "_tflops"] = round(fl / med / 1e9, 1)
-            for kk in outs:
-                if any(f.endswith(kk) for f in fns):
-                    r[f"rel_err_{kk}"] = ((outs[kk].float() - ref.float()).norm() / ref.float().norm()).item()
+            if "gemm_nt" in fns:
+                r["rel_err_gemm_nt"] = ((out.float() - ref.float()).norm() / ref.float().norm()).item()
             print(json.dumps(r), flush=True)
-            del x, w, ref, outs, y
+            del x, w, ref, out, y
             torch.cuda.empty_cache()
 
 
-def bench_swiglu(a):
+def bench_fused(a):
     dt = torch.bfloat16
     for model, (tokens, K, F) in {"llama": (40960, 4096, 14336), "llama32_1b": (40960, 2048, 8192)}.items():
         x = torch.rand(tokens, K, device="cuda", dtype=dt) * 2 - 1
@@ -149,13 +92,7 @@ def bench_swiglu(a):
         def sep():
             torch.mm(x, w.t(), out=gu)
             return ops.swiglu_fwd(gu)
-
-        def fused(sc):
-            def f():
-                os.environ["BLLM_GEMM_NT_SCHED"] = sc
-                return ops.gemm_nt_swiglu(x, w)
-            return f
-        fns = {"hipblaslt+swiglu_fwd": sep, "fused_sched2": fused("2"), "fused_sched3": fused("3")}
+        fns = {"hipblaslt+swiglu_fwd": sep, "fused": lambda: ops.gemm_nt_swiglu(x, w)}
         times = {k: [] for k in fns}
         for _ in range(a.rounds):
             for k, fn in fns.items():
@@ -164,9 +101,8 @@ def bench_swiglu(a):
         r = {"model": model, "M_K_F": [tokens, K, F]}
         for k, ts in times.items():
             r[k + "_us"] = round(sorted(ts)[len(ts) // 2] * 1e3, 1)
-        for k in ("fused_sched2", "fused_sched3"):
-            _, act = fns[k]()
-            r["act_equal_" + k] = bool(torch.equal(act, ref))
+        _, act = fns["fused"]()
+        r["act_equal"] = bool(torch.equal(act, ref))
         print(json.dumps(r), flush=True)
         del x, w, gu
         torch.cuda.empty_cache()

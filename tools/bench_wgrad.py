@@ -40,7 +40,6 @@ def main():
     ap.add_argument("--tokens", type=int, default=16384)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--models", default="llama3_8b,gpt2_774m,llama32_1b")
-    ap.add_argument("--variants", default="0,1", help="BLLM_WGRAD_VARIANT values, A/B'd in this process")
     ap.add_argument("--rounds", type=int, default=3, help="interleaved rounds (median reported)")
     a = ap.parse_args()
     ops.load_ext(required=True)
@@ -56,25 +55,18 @@ def main():
             auto = ops.wgrad_splits(out_f, in_f, Nt)
             r["auto_splits"] = auto
             r["preferred"] = ops.wgrad_gemm_preferred(out_f, in_f)
-            variants = [v.strip() for v in a.variants.split(",") if v.strip()]
             times = {}
             for _ in range(a.rounds):  # interleaved rounds in one process (variance correlated)
                 times.setdefault("hipblaslt_us", []).append(
                     timeit(lambda: torch.mm(x.t(), dy, out=g0.t()), a.iters))
-                for v in variants:
-                    os.environ["BLLM_WGRAD_VARIANT"] = v
-                    times.setdefault(f"v{v}_us", []).append(
-                        timeit(lambda: ops.wgrad_gemm_(dy, x, g1, False, auto), a.iters))
+                times.setdefault("mfma_us", []).append(
+                    timeit(lambda: ops.wgrad_gemm_(dy, x, g1, False, auto), a.iters))
             for k, ts in times.items():
                 r[k] = sorted(ts)[len(ts) // 2]
-            err = {}
-            for v in variants:
-                os.environ["BLLM_WGRAD_VARIANT"] = v
-                g1.zero_()
-                ops.wgrad_gemm_(dy, x, g1, False, auto)
-                torch.cuda.synchronize()
-                err[v] = round(((g1.float() - g0.float()).abs().max() / g0.float().abs().max()).item(), 5)
-            r["max_rel_err_vs_hipblaslt"] = err
+            g1.zero_()
+            ops.wgrad_gemm_(dy, x, g1, False, auto)
+            torch.cuda.synchronize()
+            r["max_rel_err_vs_hipblaslt"] = round(((g1.float() - g0.float()).abs().max() / g0.float().abs().max()).item(), 5)
             for k in list(r):
                 if k.endswith("_us"):
                     r[k.replace("_us", "_tflops")] = round(fl / r[k] / 1e6, 1)
