@@ -258,41 +258,69 @@ class FusedLinear:
         self.lora_scale = scales.pop() if len(scales) == 1 else None
 
     def _grouped_lora(self, x: torch.Tensor) -> bool:
+        return self._grouped_lora_dims(x.device, x.dtype, x.shape[1]) and x.dim() == 2 and x.shape[0] >= 1
+
+    def _grouped_lora_dims(self, device, dtype, K: int) -> bool:
         if self.lora_scale is None or len(self.lora_specs) != len(self.specs):
             return False
         if FORCE_GROUPED_LORA:
             return True
-        return ops.lora_kernel_ok(x, self.lora_r, [x.shape[1]] + self.lora_len + self.lora_c0)
+        return ops.lora_kernel_ok_dims(device, dtype, self.lora_r, [K] + self.lora_len + self.lora_c0)
 
-    def _kaug_ok(self, x: torch.Tensor, residual, b) -> bool:
-        """K-augmented LoRA (see forward) for wide frozen groups whose output dwarfs the input
-        (gate/up: out = 8 d): copying x into [x | s t] costs less than the s t B write plus the
-        beta = 1 read of y it replaces.  BLLM_LORA_KAUG=0 turns it off.  Not under a sharding
-        FSDP engine: the persistent [W | Bd^T] copy would keep a full unsharded frozen weight
-        per rank (Llama-3-8B gate/up: ~7.5 GB regardless of world size) and would be rebuilt
-        after every re-gather."""
-        return (residual is None and b is None and self.out_total >= 4 * x.shape[1]
+    def _kaug_base_ok(self) -> bool:
+        """K-augmented LoRA (see forward_kaug) needs a frozen, bias-free base weight that is not
+        sharded: the persistent [W | Bd^T] / [W^T ; Bd] copies would keep a full unsharded frozen
+        weight per rank under a sharding FSDP engine (Llama-3-8B gate/up: ~7.5 GB regardless of
+        world size) and would be rebuilt after every re-gather.  BLLM_LORA_KAUG=0 turns it off."""
+        return (self.has_lora and self.b_params is None
                 and not self.unit.trainable(self.W_params[0])
                 and not self.unit.state.get("sharded", False)
                 and os.environ.get("BLLM_LORA_KAUG", "1") != "0")
 
-    def _waug(self, W: torch.Tensor, K: int) -> torch.Tensor:
-        """[W | Bd^T] [out_total, K + R]: member m's B_m^T in rows c0_m.., columns K + off_m...
-        Kept across calls: the frozen W part is re-copied only when W's storage or version
-        changed (FSDP re-gather, a state-dict load); the B block (trained) every call."""
+    def kaug_input(self, like: torch.Tensor, K: int) -> Optional[torch.Tensor]:
+        """An [N, K + R] buffer for a zero-copy K-augmented forward, or None: the caller's
+        producer (RMSNorm, SwiGLU) writes this projection's input into its first K columns and
+        ``forward_kaug`` adds the s t columns, so neither a copy of x nor a pass over y is paid."""
+        if not (self._kaug_base_ok() and self._grouped_lora_dims(like.device, like.dtype, K)):
+            return None
+        return torch.empty(like.shape[0], K + self.lora_R, dtype=like.dtype, device=like.device)
+
+    def _waug(self, W: torch.Tensor, K: int):
+        """([W | Bd^T] [out, K + R], [W^T ; Bd] [K + R, out]): member m's B_m^T in rows c0_m..,
+        columns K + off_m.. of the first (and transposed in the second, the dX GEMM's
+        K-contiguous operand).  Kept across calls: the frozen W parts are re-copied only when
+        W's storage or version changed (a re-gather, a state-dict load); the B blocks (trained)
+        are rewritten every call, one kernel each."""
         u = self.unit
         key = (W.data_ptr(), W._version, W.shape, W.dtype)
         cached = getattr(self, "_wa_cache", None)
         if cached is not None and cached[0] == key:
-            Wa = cached[1]
+            Wa, WaT = cached[1], cached[2]
         else:
             Wa = torch.empty(W.shape[0], K + self.lora_R, dtype=W.dtype, device=W.device)
             Wa[:, :K].copy_(W)
-            self._wa_cache = (key, Wa)
-        Wa[:, K:].zero_()
-        for s, c0, n, off, r in zip(self.lora_specs, self.lora_c0, self.lora_len, self.lora_off, self.lora_r):
-            Wa[c0:c0 + n, K + off:K + off + r].copy_(u.data(s.lora_B).t())
-        return Wa
+            WaT = torch.empty(K + self.lora_R, W.shape[0], dtype=W.dtype, device=W.device)
+            WaT[:K].copy_(ops.transpose2d(W) if W.is_cuda else W.t())
+            self._wa_cache = (key, Wa, WaT)
+        Bs = [u.data(s.lora_B) for s in self.lora_specs]
+        ops.lora_block_(Wa[:, K:], Bs, self.lora_c0, self.lora_off)
+        ops.lora_block_(WaT[K:].t(), Bs, self.lora_c0, self.lora_off)
+        return Wa, WaT
+
+    def forward_kaug(self, xa: torch.Tensor, residual: Optional[torch.Tensor] = None):
+        """K-augmented forward on ``xa`` = [x | .] (x already written by the producer):
+        s t = s x A_cat goes into the last R columns, then ONE GEMM
+        y (= residual +) [x | s t] . [W | Bd^T]^T — the rank-r update rides in the GEMM's K loop.
+        Backward gets dy Bd = dy B^T from the dX GEMM the same way (``_kaug_lora_backward``)."""
+        u = self.unit
+        R = self.lora_R
+        K = xa.shape[1] - R
+        x, st = xa[:, :K], xa[:, K:]
+        P = ops.lora_pack_t([u.data(s.lora_A) for s in self.lora_specs])          # [R, K]
+        ops.lora_down_into(x, [P], [0], [K], [0], R, self.lora_scale, st)        # s x A_cat
+        Wa, WaT = self._waug(self.W(), K)
+        y = ops.linear_residual(xa, Wa, residual) if residual is not None else mm_nt(xa, Wa)
+        return y, ("kaug", st, P, WaT)
 
     # views are re-fetched every call: FSDP may have re-materialised the storage
     def W(self):
@@ -307,18 +335,13 @@ class FusedLinear:
         b = self.b()
         if residual is not None:
             assert b is None
-        if self.has_lora and self._grouped_lora(x) and self._kaug_ok(x, residual, b):
-            # K-augmented: y = [x | s t] . [W | Bd^T]^T, one GEMM (no s t B pass over y, no
-            # beta = 1 re-read); backward gets dy Bd = dy B^T from the dX GEMM the same way
-            u = self.unit
-            K = x.shape[1]
-            P = ops.lora_pack_t([u.data(s.lora_A) for s in self.lora_specs])          # [R, K]
-            t = ops.lora_down(x, [P], [0], [K], [0], self.lora_R)                     # x A_cat
-            xa = torch.empty(x.shape[0], K + self.lora_R, dtype=x.dtype, device=x.device)
-            xa[:, :K].copy_(x)
-            xa[:, K:].copy_(t * self.lora_scale)
-            Wa = self._waug(W, K)
-            return torch.mm(xa, Wa.t()), ("kaug", t, P, Wa)
+        if (residual is None and self.out_total >= 4 * x.shape[1] and self.has_lora
+                and self._grouped_lora(x) and self._kaug_base_ok()):
+            # an input no producer wrote into a K-augmented buffer (wide output: copying x costs
+            # less than the s t B write plus the beta = 1 re-read of y it replaces)
+            xa = self.kaug_input(x, x.shape[1])
+            xa[:, :x.shape[1]].copy_(x)
+            return self.forward_kaug(xa)
         if self.has_lora and self._grouped_lora(x):
             # y = (residual | bias) + s t B, written by lora_up, then the base GEMM accumulates
             # onto it (beta = 1): the rank-r update costs no read-modify-write pass of y
@@ -449,16 +472,17 @@ class FusedLinear:
         assert not self.has_lora
         return _input_grad(dy, self.W())
 
-    def _kaug_lora_backward(self, dy, x, t, P, Wa, need_dx, dx_acc, accumulate):
+    def _kaug_lora_backward(self, dy, x, st, P, WaT, need_dx, dx_acc, accumulate):
+        """st = s t (the forward's augmented columns), WaT = [W^T ; Bd]."""
         u_ = self.unit
         sc = self.lora_scale
         K = x.shape[1]
         gB = [(u_.grad(s.lora_B), c0, off) for s, c0, off in zip(self.lora_specs, self.lora_c0, self.lora_off)]
         gB = [g for g in gB if g[0] is not None]
-        if gB:
-            ops.lora_wgrad(t, dy, [g for g, _, _ in gB], [o for _, _, o in gB], [c for _, c, _ in gB], sc,
+        if gB:                                                     # dB = s t^T dy = (s t)^T dy
+            ops.lora_wgrad(st, dy, [g for g, _, _ in gB], [o for _, _, o in gB], [c for _, c, _ in gB], 1.0,
                            accumulate)
-        dxa = _input_grad(dy, Wa)                                  # [dy W | dy Bd] = [dx_W | dy B^T]
+        dxa = mm_nt(dy, WaT)                                       # [dy W | dy Bd] = [dx_W | dy B^T]
         ub = dxa[:, K:]
         gA = [(u_.grad(s.lora_A), off) for s, off in zip(self.lora_specs, self.lora_off)]
         gA = [g for g in gA if g[0] is not None]

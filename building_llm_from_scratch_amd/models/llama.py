@@ -157,38 +157,61 @@ class LlamaBlockCompute(UnitCompute):
         eps = cfg.norm_eps
         cos, sin = rc.rope
         x2d = x.reshape(N, d)
-        h1, r1 = ops.rmsnorm_fwd(x2d, u.data(b.norm1.weight), eps)
-        qkv = self.qkv.forward_rope(h1, cos, sin, T, H, G, hd)   # K4: RoPE in the GEMM epilogue
-        if qkv is not None:
-            xa_qkv = None
-        else:
-            qkv, xa_qkv = self.qkv.forward(h1)
+        keep = rc.block_mode(self.index) == "none" or recompute  # the recompute's outputs live one block
+        # LoRA with a frozen base: the norms / SwiGLU write straight into the K-augmented
+        # [x | s t] operand of the next projection (FusedLinear.kaug_input / forward_kaug)
+        xq = self.qkv.kaug_input(x2d, d)
+        if xq is not None:
+            h1, r1 = ops.rmsnorm_fwd_into(x2d, u.data(b.norm1.weight), eps, xq[:, :d])
+            qkv, xa_qkv = self.qkv.forward_kaug(xq)
             ops.rope_(qkv, cos, sin, T, H, G, hd)
+        else:
+            h1, r1 = ops.rmsnorm_fwd(x2d, u.data(b.norm1.weight), eps)
+            qkv = self.qkv.forward_rope(h1, cos, sin, T, H, G, hd)   # K4: RoPE in the GEMM epilogue
+            if qkv is not None:
+                xa_qkv = None
+            else:
+                qkv, xa_qkv = self.qkv.forward(h1)
+                ops.rope_(qkv, cos, sin, T, H, G, hd)
         o, lse = ops.flash_attn_fwd(qkv, B, T, H, G, hd, causal=True)
         x2, xa_o = self.o.forward(o, residual=x2d)
-        h2, r2 = ops.rmsnorm_fwd(x2, u.data(b.norm2.weight), eps)
+        xg = self.gu.kaug_input(x2, d)
         fused = None
-        if not (recompute and not self.down.has_lora and RECOMPUTE_FUSED):
-            fused = self.gu.forward_swiglu(h2)     # gate/up GEMM with the SwiGLU epilogue
-        if fused is not None:
-            (gu, act), xa_gu = fused, None
+        if xg is not None:
+            h2, r2 = ops.rmsnorm_fwd_into(x2, u.data(b.norm2.weight), eps, xg[:, :d])
+            gu, xa_gu = self.gu.forward_kaug(xg)
         else:
-            gu, xa_gu = self.gu.forward(h2)
+            h2, r2 = ops.rmsnorm_fwd(x2, u.data(b.norm2.weight), eps)
+            if not (recompute and not self.down.has_lora and RECOMPUTE_FUSED):
+                fused = self.gu.forward_swiglu(h2)     # gate/up GEMM with the SwiGLU epilogue
+            if fused is not None:
+                (gu, act), xa_gu = fused, None
+            else:
+                gu, xa_gu = self.gu.forward(h2)
         if recompute and not self.down.has_lora and RECOMPUTE_FUSED:
             # backward rebuilds act inside the SwiGLU backward kernel (swiglu_bwd_act)
             act, x3, xa_dn = None, None, None
         else:
-            if fused is None:
-                act = ops.swiglu_fwd(gu)
-            if recompute:
-                x3, xa_dn = None, self.down.lora_state(act)
+            F = gu.shape[1] // 2
+            xd = None if (fused is not None or recompute) else self.down.kaug_input(gu, F)
+            if xd is not None:
+                act = ops.swiglu_fwd_into(gu, xd[:, :F])
+                x3, xa_dn = self.down.forward_kaug(xd, residual=x2)
             else:
-                x3, xa_dn = self.down.forward(act, residual=x2)
+                if fused is None:
+                    act = ops.swiglu_fwd(gu)
+                if recompute:
+                    x3, xa_dn = None, self.down.lora_state(act)
+                else:
+                    x3, xa_dn = self.down.forward(act, residual=x2)
         saved = None
         if save:
+            if not keep:
+                # h1 / h2 are dropped (rebuilt in backward): keep only the s t columns of their
+                # K-augmented buffers, not the whole [x | s t]
+                xa_qkv, xa_gu = (_compact_kaug(v) for v in (xa_qkv, xa_gu))
             saved = dict(x=x2d, r1=r1, qkv=qkv, o=o, lse=lse, x2=x2, r2=r2, gu=gu,
                          xa=(xa_qkv, xa_o, xa_gu, xa_dn))
-            keep = rc.block_mode(self.index) == "none" or recompute  # the recompute's outputs live one block
             # selective: act is rebuilt by the SwiGLU backward (swiglu_bwd_act), h1/h2 by rmsnorm
             if act is not None and (keep or self.down.has_lora or not RECOMPUTE_FUSED):
                 saved["act"] = act
@@ -265,6 +288,13 @@ class LlamaBlockCompute(UnitCompute):
         del dqkv, h1
         dx, _ = ops.rmsnorm_bwd(dh1, s["x"], w1, s["r1"], dx2, u.grad(b.norm1.weight), acc)
         return dx.view(B, T, d)
+
+
+def _compact_kaug(xa):
+    """A saved ("kaug", s t view, P, WaT) with the s t columns copied out of their buffer."""
+    if isinstance(xa, tuple) and xa[0] == "kaug":
+        return (xa[0], xa[1].contiguous(), xa[2], xa[3])
+    return xa
 
 
 # BLLM_RECOMPUTE_FUSED=0: the checkpoint recompute runs its SwiGLU forward as a separate pass (A/B)

@@ -24,7 +24,8 @@ __all__ = [
     "rope_", "rope_tables", "flash_attn_fwd", "flash_attn_bwd", "swiglu_fwd", "swiglu_bwd", "swiglu_bwd_act",
     "gelu_fwd", "gelu_bwd", "gelu_bwd_bias", "gelu_bwd_act", "dropout_bwd_bias", "ce_fwd", "ce_bwd_", "embedding_fwd", "embedding_bwd",
     "sq_norm_multi", "adamw_step_", "attn_decode", "bias_grad_", "ext_available", "load_ext", "attention_backend",
-    "lora_down", "lora_up_", "lora_wgrad", "lora_pack_t", "lora_kernel_ok", "sum_partials_",
+    "lora_down", "lora_up_", "lora_wgrad", "lora_pack_t", "lora_kernel_ok", "lora_kernel_ok_dims",
+    "lora_down_into", "lora_block_", "rmsnorm_fwd_into", "swiglu_fwd_into", "sum_partials_",
     "wgrad_gemm_", "wgrad_gemm_ok", "wgrad_gemm_enabled", "wgrad_gemm_preferred", "wgrad_splits",
     "gemm_nn_", "gemm_nt_", "gemm_nn_ok", "dgrad_gemm_enabled", "transpose2d", "dgrad_wt_enabled", "attn_keep_mask",
 ]
@@ -71,6 +72,16 @@ def rmsnorm_fwd(x, w, eps: float):
     if _hip(x):
         return _k().rmsnorm_fwd(x, w, eps)
     return ref.rmsnorm_fwd(x, w, eps)
+
+
+def rmsnorm_fwd_into(x, w, eps: float, y):
+    """rmsnorm_fwd written into ``y``, a row-strided [N, d] view (the x part of a K-augmented
+    LoRA operand) -> (y, rstd)."""
+    if _hip(x):
+        return y, _k().rmsnorm_fwd_into_(x, w, eps, y)
+    out, rstd = ref.rmsnorm_fwd(x, w, eps)
+    y.copy_(out)
+    return y, rstd
 
 
 def _vec_into(out, g32, accumulate):
@@ -488,6 +499,15 @@ def swiglu_fwd(gu):
     return ref.swiglu_fwd(gu)
 
 
+def swiglu_fwd_into(gu, act):
+    """swiglu_fwd written into ``act``, a row-strided [N, F] view -> act."""
+    if _hip(gu):
+        _k().swiglu_fwd_into_(gu, act)
+        return act
+    act.copy_(ref.swiglu_fwd(gu))
+    return act
+
+
 def swiglu_bwd(gu, dact):
     if _hip(gu):
         return _k().swiglu_bwd(gu, dact)
@@ -550,9 +570,13 @@ def lora_kernel_ok(x: torch.Tensor, ranks, widths) -> bool:
     token count (row tails are bounds-checked: variable-length instruction batches), every rank
     a multiple of 16 (<= 64) and every column width (input and member outputs) a multiple of 32.
     Otherwise the caller uses the hipBLASLt GEMM path."""
-    if x.device.type != "cuda" or x.dtype not in (torch.bfloat16, torch.float16):
+    if x.dim() != 2 or x.shape[0] < 1:
         return False
-    if x.dim() != 2 or x.shape[0] < 1 or x.shape[1] % 32:
+    return lora_kernel_ok_dims(x.device, x.dtype, ranks, widths) and x.shape[1] % 32 == 0
+
+
+def lora_kernel_ok_dims(device, dtype, ranks, widths) -> bool:
+    if torch.device(device).type != "cuda" or dtype not in (torch.bfloat16, torch.float16):
         return False
     return all(r % 16 == 0 and 0 < r <= 64 for r in ranks) and all(w % 32 == 0 for w in widths)
 
@@ -562,6 +586,27 @@ def lora_down(x, ws, c0, lens, ocol, R: int, scale: float = 1.0):
     if _hip(x):
         return _k().lora_down(x, list(ws), list(c0), list(lens), list(ocol), int(R), float(scale))
     return ref.lora_down(x, ws, c0, lens, ocol, R, scale)
+
+
+def lora_down_into(x, ws, c0, lens, ocol, R: int, scale: float, out):
+    """lora_down written into ``out``, a row-strided [N, R] view (the s t columns of [x | s t])."""
+    if _hip(x):
+        _k().lora_down_into_(x, list(ws), list(c0), list(lens), list(ocol), int(R), float(scale), out)
+        return out
+    out.copy_(ref.lora_down(x, ws, c0, lens, ocol, R, scale))
+    return out
+
+
+def lora_block_(dst, Bs, c0, off):
+    """dst [rows, R]: B_i^T at rows c0_i.., columns off_i.., zeros elsewhere (the B block of a
+    K-augmented weight; ``dst`` may be a transposed view)."""
+    if _hip(dst):
+        _k().lora_block_(dst, list(Bs), list(c0), list(off))
+        return dst
+    dst.zero_()
+    for b, c, o in zip(Bs, c0, off):
+        dst[c:c + b.shape[1], o:o + b.shape[0]].copy_(b.t())
+    return dst
 
 
 def lora_up_(y, t, us, c0, toff, scale: float, base=None, bias=None):

@@ -10,7 +10,8 @@ namespace bllm {
 // norms.hip
 int norm_bwd_num_wg(int N, int d);
 int norm_max_dim(DType dt);
-void rmsnorm_fwd(DType dt, const void* x, const void* w, void* y, float* rstd, int N, int d, float eps, hipStream_t s);
+void rmsnorm_fwd(DType dt, const void* x, const void* w, void* y, float* rstd, int N, int d, float eps, long ldy,
+                 hipStream_t s);
 void layernorm_fwd(DType dt, const void* x, const void* w, const void* b, void* y, float* mean, float* rstd, int N,
                    int d, float eps, hipStream_t s);
 // dW / dB land in `dw` / `db` of dtype `odt` (written, or added when `accumulate`)
@@ -24,7 +25,7 @@ void col_reduce(const float* part, DType odt, void* out, int P, int d, bool accu
 // elementwise.hip
 // out[C, R] = in[R, C]^T, 16-bit elements, R % 8 == 0 and C % 8 == 0
 void transpose16(const void* in, void* out, long R, long C, hipStream_t s);
-void swiglu_fwd(DType dt, const void* gu, void* act, long N, int F, hipStream_t s);
+void swiglu_fwd(DType dt, const void* gu, void* act, long N, int F, long lda, hipStream_t s);
 // act (nullable, may alias dact): also write silu(g) * u there -- the activation-checkpoint
 // recompute then needs no separate SwiGLU forward pass for the down projection's dW
 void swiglu_bwd(DType dt, const void* gu, const void* dact, void* dgu, void* act, long N, int F, hipStream_t s);
@@ -146,7 +147,15 @@ struct LoraPackArgs {  // out[off_m + j][k] = a_m[k][j]
   int off[LORA_MAX], r[LORA_MAX];
   const void* a[LORA_MAX];
 };
+struct LoraBlockArgs {  // dst[row * s_row + j * s_j] = B_m[j - off_m][row - c0_m] inside member m's block, else 0
+  void* dst; long s_row, s_j;
+  int rows, R;
+  int n;
+  int c0[LORA_MAX], len[LORA_MAX], off[LORA_MAX], r[LORA_MAX];
+  const void* b[LORA_MAX]; long ldb[LORA_MAX];
+};
 void lora_down(DType dt, const LoraDownArgs& a, int N, hipStream_t s);
+void lora_block(DType dt, const LoraBlockArgs& a, hipStream_t s);
 void lora_up(DType dt, const LoraUpArgs& a, int N, int max_len, hipStream_t s);
 int lora_wgrad_splits(int blocks, int N);
 void lora_wgrad(DType dt, DType odt, const LoraWgradArgs& a, int N, int S, hipStream_t s);

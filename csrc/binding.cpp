@@ -57,8 +57,26 @@ std::tuple<Tensor, Tensor> rmsnorm_fwd(const Tensor& x, const Tensor& w, double 
   auto y = at::empty_like(x);
   auto rstd = at::empty({N}, x.options().dtype(at::kFloat));
   bllm::rmsnorm_fwd(dt_of(x), x.data_ptr(), w.data_ptr(), y.data_ptr(), rstd.data_ptr<float>(), N, d, (float)eps,
-                    stream());
+                    (long)d, stream());
   return {y, rstd};
+}
+
+// y: a [N, d] row-strided view (stride(0) >= d, 16-B aligned rows), e.g. the x part of a
+// K-augmented LoRA operand [x | s t]; returns rstd
+Tensor rmsnorm_fwd_into_(const Tensor& x, const Tensor& w, double eps, Tensor& y) {
+  check_gpu(x, "x"); check_gpu(w, "w"); check_gpu(y, "y");
+  c10::DeviceGuard g(x.device());
+  check_rows(x, 16 / x.element_size());
+  const int64_t N = x.size(0), d = x.size(1);
+  TORCH_CHECK(d <= bllm::norm_max_dim(dt_of(x)) && w.numel() == d && w.scalar_type() == x.scalar_type());
+  TORCH_CHECK(y.dim() == 2 && y.size(0) == N && y.size(1) == d && y.stride(1) == 1 && y.stride(0) >= d &&
+                  y.scalar_type() == x.scalar_type() && (y.stride(0) * y.element_size()) % 16 == 0 &&
+                  reinterpret_cast<uintptr_t>(y.data_ptr()) % 16 == 0,
+              "rmsnorm_fwd_into_: y must be a 16-B aligned [N, d] row-strided view");
+  auto rstd = at::empty({N}, x.options().dtype(at::kFloat));
+  bllm::rmsnorm_fwd(dt_of(x), x.data_ptr(), w.data_ptr(), y.data_ptr(), rstd.data_ptr<float>(), N, d, (float)eps,
+                    (long)y.stride(0), stream());
+  return rstd;
 }
 
 // dW goes to `dw_out` (any float dtype, written or accumulated) when given, else a new fp32 [d]
@@ -178,8 +196,20 @@ Tensor swiglu_fwd(const Tensor& gu) {
   TORCH_CHECK(gu.dim() == 2 && gu.size(1) % 2 == 0);
   const int64_t N = gu.size(0), F = gu.size(1) / 2;
   auto act = at::empty({N, F}, gu.options());
-  bllm::swiglu_fwd(dt_of(gu), gu.data_ptr(), act.data_ptr(), N, F, stream());
+  bllm::swiglu_fwd(dt_of(gu), gu.data_ptr(), act.data_ptr(), N, F, (long)F, stream());
   return act;
+}
+
+// act: a [N, F] row-strided view (the act part of a K-augmented [act | s t] operand)
+void swiglu_fwd_into_(const Tensor& gu, Tensor& act) {
+  check_gpu(gu, "gu"); check_gpu(act, "act");
+  c10::DeviceGuard g(gu.device());
+  TORCH_CHECK(gu.dim() == 2 && gu.size(1) % 2 == 0 && gu.is_contiguous());
+  const int64_t N = gu.size(0), F = gu.size(1) / 2;
+  TORCH_CHECK(act.dim() == 2 && act.size(0) == N && act.size(1) == F && act.stride(1) == 1 && act.stride(0) >= F &&
+                  act.scalar_type() == gu.scalar_type(),
+              "swiglu_fwd_into_: act must be an [N, F] row-strided view");
+  bllm::swiglu_fwd(dt_of(gu), gu.data_ptr(), act.data_ptr(), N, F, (long)act.stride(0), stream());
 }
 
 Tensor swiglu_bwd(const Tensor& gu, const Tensor& dact) {
@@ -615,17 +645,18 @@ static void check_lora_mat(const Tensor& t, const char* name) {
 }
 
 // out[:, ocol_i : ocol_i + r_i] = scale * x[:, c0_i : c0_i + len_i] . w_i^T ;  w_i [r_i, >= len_i]
-Tensor lora_down(const Tensor& x, at::TensorList ws, at::IntArrayRef c0, at::IntArrayRef lens,
-                 at::IntArrayRef ocol, int64_t R, double scale) {
+static void lora_down_impl(const Tensor& x, at::TensorList ws, at::IntArrayRef c0, at::IntArrayRef lens,
+                           at::IntArrayRef ocol, int64_t R, double scale, Tensor& out) {
   check_lora_mat(x, "x");
   c10::DeviceGuard g(x.device());
   TORCH_CHECK(x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kHalf, "lora_down: bf16/fp16 only");
   const int64_t N = x.size(0);
   TORCH_CHECK(N > 0 && R % 16 == 0 && R > 0, "lora_down: N > 0 and R a multiple of 16 required");
   TORCH_CHECK(ws.size() == c0.size() && ws.size() == lens.size() && ws.size() == ocol.size());
-  auto out = at::empty({N, R}, x.options());
+  TORCH_CHECK(out.is_cuda() && out.dim() == 2 && out.size(0) == N && out.size(1) == R && out.stride(1) == 1 &&
+                  out.scalar_type() == x.scalar_type(), "lora_down: out must be an [N, R] row-strided view");
   bllm::LoraDownArgs a{};
-  a.x = x.data_ptr(); a.ldx = x.stride(0); a.out = out.data_ptr(); a.ldo = R; a.scale = (float)scale;
+  a.x = x.data_ptr(); a.ldx = x.stride(0); a.out = out.data_ptr(); a.ldo = out.stride(0); a.scale = (float)scale;
   for (size_t i = 0; i < ws.size(); ++i) {
     const Tensor& w = ws[i];
     check_lora_mat(w, "w");
@@ -644,7 +675,40 @@ Tensor lora_down(const Tensor& x, at::TensorList ws, at::IntArrayRef c0, at::Int
     }
   }
   bllm::lora_down(dt_of(x), a, (int)N, stream());
+}
+
+Tensor lora_down(const Tensor& x, at::TensorList ws, at::IntArrayRef c0, at::IntArrayRef lens,
+                 at::IntArrayRef ocol, int64_t R, double scale) {
+  auto out = at::empty({x.size(0), R}, x.options());
+  lora_down_impl(x, ws, c0, lens, ocol, R, scale, out);
   return out;
+}
+
+// dst [rows, R] (any strides, one of them 1): member i's B_i^T [len_i, r_i] at rows c0_i.., columns
+// off_i.., zeros elsewhere -- the B block of a K-augmented LoRA weight, one launch per group
+void lora_block_(Tensor& dst, at::TensorList bs, at::IntArrayRef c0, at::IntArrayRef off) {
+  TORCH_CHECK(dst.is_cuda() && dst.dim() == 2 && (dst.stride(0) == 1 || dst.stride(1) == 1) &&
+                  (dst.scalar_type() == at::kBFloat16 || dst.scalar_type() == at::kHalf), "lora_block_: dst");
+  c10::DeviceGuard g(dst.device());
+  TORCH_CHECK(bs.size() == c0.size() && bs.size() == off.size() && (int64_t)bs.size() <= bllm::LORA_MAX);
+  bllm::LoraBlockArgs a{};
+  a.dst = dst.data_ptr(); a.s_row = dst.stride(0); a.s_j = dst.stride(1);
+  a.rows = (int)dst.size(0); a.R = (int)dst.size(1); a.n = (int)bs.size();
+  for (size_t i = 0; i < bs.size(); ++i) {
+    const Tensor& b = bs[i];
+    TORCH_CHECK(b.is_cuda() && b.dim() == 2 && b.stride(1) == 1 && b.scalar_type() == dst.scalar_type(),
+                "lora_block_: B must be a row-major [r, len] GPU tensor of dst's dtype");
+    TORCH_CHECK(c0[i] + b.size(1) <= dst.size(0) && off[i] + b.size(0) <= dst.size(1), "lora_block_: block out of range");
+    a.c0[i] = (int)c0[i]; a.len[i] = (int)b.size(1); a.off[i] = (int)off[i]; a.r[i] = (int)b.size(0);
+    a.b[i] = b.data_ptr(); a.ldb[i] = b.stride(0);
+  }
+  bllm::lora_block(dt_of(dst), a, stream());
+}
+
+// writes into a row-strided view, e.g. the s t columns of a K-augmented [x | s t] operand
+void lora_down_into_(const Tensor& x, at::TensorList ws, at::IntArrayRef c0, at::IntArrayRef lens,
+                     at::IntArrayRef ocol, int64_t R, double scale, Tensor& out) {
+  lora_down_impl(x, ws, c0, lens, ocol, R, scale, out);
 }
 
 // y[:, c0_i : c0_i + len_i] = base + bias + scale * t[:, toff_i : toff_i + r_i] . u_i ;  u_i [r_i, len_i], any
@@ -934,6 +998,7 @@ TORCH_LIBRARY(bllm, m) {
   m.def("debug_error() -> int", &debug_error);
   m.def("kernel_debug_build() -> bool", &kernel_debug_build);
   m.def("rmsnorm_fwd(Tensor x, Tensor w, float eps) -> (Tensor, Tensor)");
+  m.def("rmsnorm_fwd_into_(Tensor x, Tensor w, float eps, Tensor(a!) y) -> Tensor");
   m.def("rmsnorm_bwd(Tensor dy, Tensor x, Tensor w, Tensor rstd, Tensor? dx_acc, Tensor(a!)? dw_out, bool accumulate) -> (Tensor, Tensor)");
   m.def("layernorm_fwd(Tensor x, Tensor w, Tensor b, float eps) -> (Tensor, Tensor, Tensor)");
   m.def("layernorm_bwd(Tensor dy, Tensor x, Tensor w, Tensor mean, Tensor rstd, Tensor? dx_acc, Tensor(a!)? dw_out, Tensor(b!)? db_out, bool accumulate) -> (Tensor, Tensor, Tensor)");
@@ -943,6 +1008,7 @@ TORCH_LIBRARY(bllm, m) {
   m.def("transpose2d(Tensor a) -> Tensor");
   m.def("linear_residual(Tensor x, Tensor W, Tensor C) -> Tensor");
   m.def("swiglu_fwd(Tensor gu) -> Tensor");
+  m.def("swiglu_fwd_into_(Tensor gu, Tensor(a!) act) -> ()");
   m.def("swiglu_bwd(Tensor gu, Tensor dact) -> Tensor");
   m.def("swiglu_bwd_act(Tensor gu, Tensor(a!) dact) -> Tensor");
   m.def("gelu_fwd(Tensor f) -> Tensor");
@@ -966,6 +1032,8 @@ TORCH_LIBRARY(bllm, m) {
   m.def("embedding_fwd(Tensor idx, Tensor wte, Tensor? wpe, int T, float p, int seed, int offset) -> Tensor");
   m.def("embedding_bwd(Tensor idx, Tensor dx, Tensor(a!)? grad_wte, Tensor(b!)? grad_wpe, int T, bool accumulate) -> ()");
   m.def("lora_down(Tensor x, Tensor[] ws, int[] c0, int[] lens, int[] ocol, int R, float scale) -> Tensor");
+  m.def("lora_block_(Tensor(a!) dst, Tensor[] bs, int[] c0, int[] off) -> ()");
+  m.def("lora_down_into_(Tensor x, Tensor[] ws, int[] c0, int[] lens, int[] ocol, int R, float scale, Tensor(a!) out) -> ()");
   m.def("lora_up_(Tensor(a!) y, Tensor t, Tensor[] us, int[] c0, int[] toff, float scale, Tensor? base, Tensor? bias) -> ()");
   m.def("lora_wgrad(Tensor p, Tensor q, Tensor(a!)[] gs, int[] pa, int[] qb, float scale, bool accumulate) -> ()");
   m.def("lora_pack_t(Tensor[] a) -> Tensor");
@@ -975,6 +1043,7 @@ TORCH_LIBRARY(bllm, m) {
 
 TORCH_LIBRARY_IMPL(bllm, CUDA, m) {
   m.impl("rmsnorm_fwd", &rmsnorm_fwd);
+  m.impl("rmsnorm_fwd_into_", &rmsnorm_fwd_into_);
   m.impl("rmsnorm_bwd", &rmsnorm_bwd);
   m.impl("layernorm_fwd", &layernorm_fwd);
   m.impl("layernorm_bwd", &layernorm_bwd);
@@ -984,6 +1053,7 @@ TORCH_LIBRARY_IMPL(bllm, CUDA, m) {
   m.impl("transpose2d", &transpose2d);
   m.impl("linear_residual", &linear_residual);
   m.impl("swiglu_fwd", &swiglu_fwd);
+  m.impl("swiglu_fwd_into_", &swiglu_fwd_into_);
   m.impl("swiglu_bwd", &swiglu_bwd);
   m.impl("swiglu_bwd_act", &swiglu_bwd_act);
   m.impl("gelu_fwd", &gelu_fwd);
@@ -1007,6 +1077,8 @@ TORCH_LIBRARY_IMPL(bllm, CUDA, m) {
   m.impl("embedding_fwd", &embedding_fwd);
   m.impl("embedding_bwd", &embedding_bwd);
   m.impl("lora_down", &lora_down);
+  m.impl("lora_down_into_", &lora_down_into_);
+  m.impl("lora_block_", &lora_block_);
   m.impl("lora_up_", &lora_up_);
   m.impl("lora_wgrad", &lora_wgrad);
   m.impl("lora_pack_t", &lora_pack_t);

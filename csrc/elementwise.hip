@@ -18,7 +18,8 @@ static inline int ew_grid(long nvec) {
 // ---------------------------------------------------------------- SwiGLU
 // gu: [N, 2F] = [gate | up] per row (fused [fc1; fc2] GEMM output); act: [N, F]
 template <typename T, int VEC>
-__global__ __launch_bounds__(256) void swiglu_fwd_k(const T* __restrict__ gu, T* __restrict__ act, long N, int F) {
+__global__ __launch_bounds__(256) void swiglu_fwd_k(const T* __restrict__ gu, T* __restrict__ act, long N, int F,
+                                                    long lda) {
   const int fv = F / VEC;
   const long total = N * fv;
   for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
@@ -30,7 +31,7 @@ __global__ __launch_bounds__(256) void swiglu_fwd_k(const T* __restrict__ gu, T*
       const float a = to_f(g.v[j]);
       o.v[j] = from_f<T>(a / (1.f + __expf(-a)) * to_f(u.v[j]));
     }
-    stv<T, VEC>(act + r * F + c, o);
+    stv<T, VEC>(act + r * lda + c, o);
   }
 }
 
@@ -62,11 +63,12 @@ __global__ __launch_bounds__(256) void swiglu_bwd_k(const T* __restrict__ gu, co
 // division, U independent 16-B load pairs in flight per lane before any math (the grid-stride loop
 // above serialises load -> compute per vector).  One workgroup per token row; N rows >> 256 CUs.
 template <typename T, int VEC, int U>
-__global__ __launch_bounds__(256) void swiglu_fwd_rows_k(const T* __restrict__ gu, T* __restrict__ act, int F) {
+__global__ __launch_bounds__(256) void swiglu_fwd_rows_k(const T* __restrict__ gu, T* __restrict__ act, int F,
+                                                         long lda) {
   const int fv = F / VEC;
   const T* g0 = gu + (long)blockIdx.x * 2 * F;
   const T* u0 = g0 + F;
-  T* o0 = act + (long)blockIdx.x * F;
+  T* o0 = act + (long)blockIdx.x * lda;
   for (int base = threadIdx.x; base < fv; base += 256 * U) {
     VecN<T, VEC> g[U], u[U];
 #pragma unroll
@@ -419,15 +421,16 @@ void bias_grad(DType dt, DType odt, const void* dy, float* part, void* out, int 
 
 // row-per-workgroup kernels (4 16-B load groups in flight per lane) for the wide rows of the
 // Llama MLPs; the grid-stride kernels otherwise (narrow / odd rows, debug shapes)
-void swiglu_fwd(DType dt, const void* gu, void* act, long N, int F, hipStream_t s) {
+// act rows lda apart (lda > F: the act part of a K-augmented [act | s t] row)
+void swiglu_fwd(DType dt, const void* gu, void* act, long N, int F, long lda, hipStream_t s) {
   BLLM_DISPATCH(dt, T, {
-    EW_VEC(T, F % (16 / sizeof(T)) == 0, {
+    EW_VEC(T, F % (16 / sizeof(T)) == 0 && lda % (16 / sizeof(T)) == 0, {
       if (F / VEC >= 512 && N <= 0x7fffffffL)
         hipLaunchKernelGGL((swiglu_fwd_rows_k<T, VEC, 4>), dim3((unsigned)N), dim3(256), 0, s, (const T*)gu,
-                           (T*)act, F);
+                           (T*)act, F, lda);
       else
         hipLaunchKernelGGL((swiglu_fwd_k<T, VEC>), dim3(ew_grid(N * F / VEC)), dim3(256), 0, s, (const T*)gu,
-                           (T*)act, N, F);
+                           (T*)act, N, F, lda);
     });
   });
 }

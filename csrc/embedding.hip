@@ -44,36 +44,76 @@ __global__ __launch_bounds__(256) void emb_fwd_k(const int64_t* __restrict__ idx
   }
 }
 
-// one workgroup per sorted position; only run heads do work
+// One wave per (sorted position, 64*VEC-column slice); only the waves on a run head work.  A run
+// is summed in sorted order (fixed -> reproducible), four rows per trip with their loads in
+// flight together; row indices come 16 per vector load (broadcast by v_readlane) and the run's
+// end 64 ids per ballot probe.  With a byte-level vocabulary (the offline tokenizer) a run is
+// hundreds of rows long: the previous one-workgroup-per-run walk, one dependent scalar load per
+// row, was latency bound.
+__device__ __forceinline__ long lane_i64(long v, int src) {
+  const int lo = __builtin_amdgcn_readlane((int)(unsigned)(v & 0xffffffff), src);
+  const int hi = __builtin_amdgcn_readlane((int)(v >> 32), src);
+  return (long)(((unsigned long)(unsigned)hi << 32) | (unsigned)lo);
+}
+
 template <typename T, int VEC>
 __global__ __launch_bounds__(256) void emb_bwd_tok_k(const int64_t* __restrict__ sorted,
                                                      const int64_t* __restrict__ perm, const T* __restrict__ dx,
                                                      T* __restrict__ grad, long N, int d, bool accumulate) {
-  const long i = blockIdx.x;
+  const long i = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= N) return;
   const int64_t id = sorted[i];
   if (i > 0 && sorted[i - 1] == id) return;
+  const int lane = threadIdx.x & 63;
+  const int c = (blockIdx.y * 64 + lane) * VEC;
+  const bool live = c < d;
+  // run end: 64 sorted ids per probe, first mismatch by ballot
   long e = i + 1;
-  while (e < N && sorted[e] == id) ++e;
-  for (int c = threadIdx.x * VEC; c < d; c += 256 * VEC) {
-    float acc[VEC];
+  for (;;) {
+    const long k = e + lane;
+    const uint64_t m = __builtin_amdgcn_ballot_w64(k >= N || sorted[k] != id);
+    if (m) {
+      e += __builtin_ctzll(m);
+      break;
+    }
+    e += 64;
+  }
+  float acc[VEC];
 #pragma unroll
-    for (int j = 0; j < VEC; ++j) acc[j] = 0.f;
-    for (long k = i; k < e; ++k) {
-      VecN<T, VEC> v = ldv<T, VEC>(dx + perm[k] * d + c);
+  for (int j = 0; j < VEC; ++j) acc[j] = 0.f;
+  for (long k0 = i; k0 < e; k0 += 16) {
+    // 16 row indices in one vector load, broadcast by v_readlane; 4 row loads in flight
+    const long pk = k0 + (lane & 15) < e ? (long)perm[k0 + (lane & 15)] : 0;
+    const int n = e - k0 < 16 ? (int)(e - k0) : 16;
+    int u = 0;
+    for (; u + 4 <= n; u += 4) {
+      VecN<T, VEC> v[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (live) v[q] = ldv<T, VEC>(dx + lane_i64(pk, u + q) * d + c);
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) acc[j] += live ? to_f(v[q].v[j]) : 0.f;
+    }
+    for (; u < n; ++u) {
+      if (!live) continue;
+      VecN<T, VEC> v = ldv<T, VEC>(dx + lane_i64(pk, u) * d + c);
 #pragma unroll
       for (int j = 0; j < VEC; ++j) acc[j] += to_f(v.v[j]);
     }
-    T* g = grad + id * d + c;
-    VecN<T, VEC> o;
-    if (accumulate) {
-      VecN<T, VEC> old = ldv<T, VEC>(g);
-#pragma unroll
-      for (int j = 0; j < VEC; ++j) acc[j] += to_f(old.v[j]);
-    }
-#pragma unroll
-    for (int j = 0; j < VEC; ++j) o.v[j] = from_f<T>(acc[j]);
-    stv<T, VEC>(g, o);
   }
+  if (!live) return;
+  T* g = grad + id * d + c;
+  VecN<T, VEC> o;
+  if (accumulate) {
+    VecN<T, VEC> old = ldv<T, VEC>(g);
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) acc[j] += to_f(old.v[j]);
+  }
+#pragma unroll
+  for (int j = 0; j < VEC; ++j) o.v[j] = from_f<T>(acc[j]);
+  stv<T, VEC>(g, o);
 }
 
 template <typename T, int VEC>
@@ -130,7 +170,8 @@ void embedding_bwd_tok(DType dt, const int64_t* sorted, const int64_t* perm, con
                        int d, bool accumulate, hipStream_t s) {
   BLLM_DISPATCH(dt, T, {
     EMB_VEC(T, d, {
-      hipLaunchKernelGGL((emb_bwd_tok_k<T, VEC>), dim3(N), dim3(256), 0, s, sorted, perm, (const T*)dx, (T*)grad,
+      const dim3 grid((unsigned)((N + 3) / 4), (unsigned)ceil_div(d, 64 * VEC));
+      hipLaunchKernelGGL((emb_bwd_tok_k<T, VEC>), grid, dim3(256), 0, s, sorted, perm, (const T*)dx, (T*)grad,
                          N, d, accumulate);
     });
   });

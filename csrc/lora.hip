@@ -331,9 +331,36 @@ __global__ __launch_bounds__(256) void lora_pack_t_k(LoraPackArgs a, int K) {
   }
 }
 
+// The B block of a K-augmented weight: [W | Bd^T] (forward, dst row-major [out, K + R] at column K)
+// or [W^T ; Bd] (the dX GEMM's transposed operand, at row K).  Every (row, j) of the [out, R]
+// block is written -- B_m^T inside member m's rows x rank columns, 0 elsewhere -- the unit-stride
+// index fastest.
+template <typename T>
+__global__ __launch_bounds__(256) void lora_block_k(LoraBlockArgs a) {
+  const long total = (long)a.rows * a.R;
+  const bool row_fast = a.s_row == 1;
+  for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < total; e += (long)gridDim.x * 256) {
+    const int row = row_fast ? (int)(e % a.rows) : (int)(e / a.R);
+    const int j = row_fast ? (int)(e / a.rows) : (int)(e % a.R);
+    T v = from_f<T>(0.f);
+    for (int m = 0; m < a.n; ++m) {
+      const int rr = row - a.c0[m], jj = j - a.off[m];
+      if (rr >= 0 && rr < a.len[m] && jj >= 0 && jj < a.r[m]) v = ((const T*)a.b[m])[(long)jj * a.ldb[m] + rr];
+    }
+    ((T*)a.dst)[(long)row * a.s_row + (long)j * a.s_j] = v;
+  }
+}
+
 }  // namespace
 
 // ----------------------------------------------------------------------------- launchers
+void lora_block(DType dt, const LoraBlockArgs& a, hipStream_t s) {
+  const long total = (long)a.rows * a.R;
+  const int g = (int)((total + 255) / 256 < 1024 ? (total + 255) / 256 : 1024);
+  if (dt == DType::BF16) hipLaunchKernelGGL(lora_block_k<bf16_t>, dim3(g), dim3(256), 0, s, a);
+  else hipLaunchKernelGGL(lora_block_k<f16_t>, dim3(g), dim3(256), 0, s, a);
+}
+
 void lora_down(DType dt, const LoraDownArgs& a, int N, hipStream_t s) {
   dim3 grid(ceil_div(N, 16), a.n);
   if (dt == DType::BF16) hipLaunchKernelGGL(lora_down_k<bf16_t>, grid, dim3(512), 0, s, a, N);

@@ -22,7 +22,7 @@ template <typename T, int NV, bool LN>
 __global__ __launch_bounds__(256) void norm_fwd_k(const T* __restrict__ x, const T* __restrict__ w,
                                                   const T* __restrict__ b, T* __restrict__ y,
                                                   float* __restrict__ mean_out, float* __restrict__ rstd_out,
-                                                  int N, int d, float eps) {
+                                                  int N, int d, float eps, long ldy) {
   constexpr int VEC = 16 / sizeof(T);
   const int row = blockIdx.x * ROWS_PER_WG + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
@@ -58,7 +58,7 @@ __global__ __launch_bounds__(256) void norm_fwd_k(const T* __restrict__ x, const
   } else {
     rs = rsqrtf(s1 / d + eps);
   }
-  T* yr = y + (size_t)row * d;
+  T* yr = y + (size_t)row * ldy;  // ldy > d: written into the x part of a K-augmented [x | s t] row
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
     const int c = lane + 64 * i;
@@ -232,13 +232,13 @@ void col_reduce(const float* part, DType odt, void* out, int P, int d, bool accu
 // ----------------------------------------------------------------------------- launchers
 template <typename T, bool LN>
 static void fwd_dispatch(const void* x, const void* w, const void* b, void* y, float* mean, float* rstd,
-                         int N, int d, float eps, hipStream_t s) {
+                         int N, int d, float eps, long ldy, hipStream_t s) {
   constexpr int VEC = 16 / sizeof(T);
   const int nvec = d / VEC;
   const int nv = (nvec + 63) / 64;
   dim3 grid(ceil_div(N, ROWS_PER_WG)), block(256);
 #define L(NVV) hipLaunchKernelGGL((norm_fwd_k<T, NVV, LN>), grid, block, 0, s, (const T*)x, (const T*)w, \
-                                  (const T*)b, (T*)y, mean, rstd, N, d, eps)
+                                  (const T*)b, (T*)y, mean, rstd, N, d, eps, ldy)
   if (nv <= 1) L(1); else if (nv <= 2) L(2); else if (nv <= 4) L(4); else if (nv <= 8) L(8); else L(16);
 #undef L
 }
@@ -270,13 +270,13 @@ int norm_bwd_num_wg(int N, int d) {
 // max supported row length per dtype (NV <= 16): 8192 (bf16/f16), 4096 (f32)
 int norm_max_dim(DType dt) { return dt == DType::F32 ? 4096 : 8192; }
 
-void rmsnorm_fwd(DType dt, const void* x, const void* w, void* y, float* rstd, int N, int d, float eps,
+void rmsnorm_fwd(DType dt, const void* x, const void* w, void* y, float* rstd, int N, int d, float eps, long ldy,
                  hipStream_t s) {
-  BLLM_DISPATCH(dt, T, (fwd_dispatch<T, false>(x, w, nullptr, y, nullptr, rstd, N, d, eps, s)));
+  BLLM_DISPATCH(dt, T, (fwd_dispatch<T, false>(x, w, nullptr, y, nullptr, rstd, N, d, eps, ldy, s)));
 }
 void layernorm_fwd(DType dt, const void* x, const void* w, const void* b, void* y, float* mean, float* rstd,
                    int N, int d, float eps, hipStream_t s) {
-  BLLM_DISPATCH(dt, T, (fwd_dispatch<T, true>(x, w, b, y, mean, rstd, N, d, eps, s)));
+  BLLM_DISPATCH(dt, T, (fwd_dispatch<T, true>(x, w, b, y, mean, rstd, N, d, eps, (long)d, s)));
 }
 void rmsnorm_bwd(DType dt, const void* dy, const void* x, const void* w, const float* rstd, const void* dx_acc,
                  void* dx, float* part, DType odt, void* dw, bool accumulate, int N, int d, int nwg, hipStream_t s) {

@@ -178,6 +178,26 @@ def test_embedding(dt, pos):
         _close(gp, gp0, dt, 4, name="pos dW")
 
 
+@pytest.mark.parametrize("dt", DTYPES)
+@pytest.mark.parametrize("d", [1280, 4096])
+def test_embedding_bwd_long_runs(dt, d):
+    """Byte-level vocabularies give runs of hundreds of equal ids: runs longer than one 64-id
+    ballot probe and not a multiple of the 16-row index batch, a 1-row run, a partial last
+    column slice (1280 = 2.5 x 512), and accumulate=True onto an existing gradient."""
+    V, N = 50, 2053
+    g_ = torch.Generator().manual_seed(5)
+    idx = torch.randint(3, 10, (N,), generator=g_)
+    idx[17] = 40                                  # a run of one
+    idx = idx.to(DEV)
+    dx = torch.randn(N, d, device=DEV).to(dt)
+    base = torch.randn(V, d, device=DEV).to(dt)
+    g = base.clone()
+    ops.embedding_bwd(idx, dx, g, None, N, accumulate=True)
+    g0 = torch.zeros(V, d)
+    ref.embedding_bwd(idx.cpu(), dx.cpu().float(), g0, None, N)
+    _close(g, g0 + base.cpu().float(), dt, 4, name="emb dW (long runs, accumulate)")
+
+
 @pytest.mark.parametrize("pdt", [torch.bfloat16, torch.float32])
 def test_adamw_and_norm(pdt):
     n = 4099
@@ -475,6 +495,44 @@ def test_lora_kernels(dt, r, N):
     dx = torch.empty(N, K, device=DEV, dtype=dt)
     ops.lora_up_(dx, u, [P], [0], [0], s, base=dx_acc)
     _close(dx, dx0, dt, 2, name="up bwd (rank > 64 in LDS passes)" if R > 64 else "up bwd")
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("N", [1000, 4096])
+def test_kaug_producers_and_blocks(dt, N):
+    """Zero-copy K-augmentation pieces: RMSNorm / SwiGLU written into the x part of an
+    [N, K + R] buffer (bitwise their contiguous outputs), lora_down into its last R columns,
+    and the [out, R] B block of [W | Bd^T] and of the transposed [W^T ; Bd]."""
+    K, F, r = 512, 1024, 16
+    outs, c0 = [512, 128, 128], [0, 512, 640]
+    R = 3 * r
+    x = torch.randn(N, K, device=DEV).to(dt)
+    w = (1 + 0.1 * torch.randn(K, device=DEV)).to(dt)
+    xa = torch.full((N, K + R), float("nan"), device=DEV, dtype=dt)
+    y, rstd = ops.rmsnorm_fwd_into(x, w, 1e-5, xa[:, :K])
+    y0, rstd0 = ops.rmsnorm_fwd(x, w, 1e-5)
+    assert torch.equal(xa[:, :K], y0) and torch.equal(rstd, rstd0) and y.data_ptr() == xa.data_ptr()
+    assert torch.isnan(xa[:, K:].float()).all()                        # nothing past the view written
+    As = [(0.1 * torch.randn(K, r, device=DEV)).to(dt) for _ in outs]
+    P = ops.lora_pack_t(As)
+    ops.lora_down_into(xa[:, :K], [P], [0], [K], [0], R, 0.5, xa[:, K:])
+    assert torch.equal(xa[:, K:], ops.lora_down(y0, [P], [0], [K], [0], R, 0.5))
+    gu = torch.randn(N, 2 * F, device=DEV).to(dt)
+    xd = torch.full((N, F + R), float("nan"), device=DEV, dtype=dt)
+    ops.swiglu_fwd_into(gu, xd[:, :F])
+    assert torch.equal(xd[:, :F], ops.swiglu_fwd(gu)) and torch.isnan(xd[:, F:].float()).all()
+    Bs = [torch.randn(r, o, device=DEV).to(dt) for o in outs]
+    offs = [0, r, 2 * r]
+    M = sum(outs)
+    ref_blk = torch.zeros(M, R, device=DEV, dtype=dt)
+    for b, c, o in zip(Bs, c0, offs):
+        ref_blk[c:c + b.shape[1], o:o + r] = b.t()
+    Wa = torch.full((M, K + R), float("nan"), device=DEV, dtype=dt)
+    ops.lora_block_(Wa[:, K:], Bs, c0, offs)
+    WaT = torch.full((K + R, M), float("nan"), device=DEV, dtype=dt)
+    ops.lora_block_(WaT[K:].t(), Bs, c0, offs)
+    assert torch.equal(Wa[:, K:], ref_blk) and torch.equal(WaT[K:], ref_blk.t())
+    assert torch.isnan(Wa[:, :K].float()).all() and torch.isnan(WaT[:K].float()).all()
 
 
 def test_lora_model_uses_kernels_and_matches_gemm_path(monkeypatch):

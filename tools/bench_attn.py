@@ -42,7 +42,7 @@ def main():
               ("gpt2-774M-nodrop", 4, 1024, 20, 20, 64, 0.0),
               ("gpt2-774M-B24", 24, 1024, 20, 20, 64, 0.1),
               ("gpt2-774M-B24-nodrop", 24, 1024, 20, 20, 64, 0.0),
-              ("gpt2-774M-B64", 64, 1024, 20, 20, 64, 0.1),
+              ("gpt2-774M-B64", 64, 1024, 20, 20, 64, 0.1), ("gpt2-774M-B64-nodrop", 64, 1024, 20, 20, 64, 0.0),
               ("gpt2-124M", 4, 1024, 12, 12, 64, 0.0)]
     if a.shapes:
         keep = a.shapes.split(",")
