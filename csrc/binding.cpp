@@ -64,7 +64,8 @@ std::tuple<Tensor, Tensor> rmsnorm_fwd(const Tensor& x, const Tensor& w, double 
 // y: a [N, d] row-strided view (stride(0) >= d, 16-B aligned rows), e.g. the x part of a
 // K-augmented LoRA operand [x | s t]; returns rstd
 Tensor rmsnorm_fwd_into_(const Tensor& x, const Tensor& w, double eps, Tensor& y) {
-  check_gpu(x, "x"); check_gpu(w, "w"); check_gpu(y, "y");
+  check_gpu(x, "x"); check_gpu(w, "w");
+  TORCH_CHECK(y.is_cuda() && y.device() == x.device(), "rmsnorm_fwd_into_: y must be on x's GPU");
   c10::DeviceGuard g(x.device());
   check_rows(x, 16 / x.element_size());
   const int64_t N = x.size(0), d = x.size(1);
@@ -202,7 +203,8 @@ Tensor swiglu_fwd(const Tensor& gu) {
 
 // act: a [N, F] row-strided view (the act part of a K-augmented [act | s t] operand)
 void swiglu_fwd_into_(const Tensor& gu, Tensor& act) {
-  check_gpu(gu, "gu"); check_gpu(act, "act");
+  check_gpu(gu, "gu");
+  TORCH_CHECK(act.is_cuda() && act.device() == gu.device(), "swiglu_fwd_into_: act must be on gu's GPU");
   c10::DeviceGuard g(gu.device());
   TORCH_CHECK(gu.dim() == 2 && gu.size(1) % 2 == 0 && gu.is_contiguous());
   const int64_t N = gu.size(0), F = gu.size(1) / 2;

@@ -40,24 +40,15 @@ template <> struct MfA<f16_t> {
 };
 __device__ __forceinline__ void mfma_drain() { asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory"); }
 
-// DV (BLLM_GEMM_NT4_DMA, read per launch for A/B): how a piece is issued.
-//   0  global_load_lds_dwordx4, saddr = the tile's base pointer (glds16s: m0 saved / restored)
-//   1  buffer_load_dwordx4 ... offen lds on a loop-invariant descriptor of the wave's 64 rows, the
-//      tile advance in soffset, m0 written without save / restore (nothing else in the kernel
-//      uses m0)
-//   2  as 1 with sc0 sc1 (the cache policy of gfx950's hipBLASLt MT256x256x64 DTL kernels)
-//   3  as 1 with nt
+// One LDS-DMA piece: buffer_load_dwordx4 ... offen lds on a loop-invariant descriptor of the
+// wave's rows, the tile advance in soffset, m0 written without save / restore (nothing else in the
+// kernel uses m0).  The alternatives measured in round 3 (global_load_lds with saddr, sc0 sc1 and nt
+// cache policies) were no faster and were removed.
 template <int DV>
 __device__ __forceinline__ void bdma16(const i32x4& rsrc, uint32_t voff, uint32_t soff, uint32_t lds_dst) {
-  if constexpr (DV == 2)
-    asm volatile("s_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, %2 offen sc0 sc1 lds"
-                 ::"v"(voff), "s"(rsrc), "s"(soff), "s"(lds_dst) : "memory");
-  else if constexpr (DV == 3)
-    asm volatile("s_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, %2 offen nt lds"
-                 ::"v"(voff), "s"(rsrc), "s"(soff), "s"(lds_dst) : "memory");
-  else
-    asm volatile("s_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, %2 offen lds"
-                 ::"v"(voff), "s"(rsrc), "s"(soff), "s"(lds_dst) : "memory");
+  static_assert(DV == 1, "only the offen descriptor form is kept");
+  asm volatile("s_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, %2 offen lds"
+               ::"v"(voff), "s"(rsrc), "s"(soff), "s"(lds_dst) : "memory");
 }
 // raw buffer descriptor (stride 0, no bounds limit) of a wave-uniform base pointer
 __device__ __forceinline__ i32x4 make_rsrc(const void* p) {

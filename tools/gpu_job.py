@@ -44,7 +44,9 @@ def recipes(p):
         "prof": [("prof", 600, f"rocprofv3 --kernel-trace --stats -d gpurun_out/{p['tag']}/rocprof -o run -- "
                   + _bench(extra, int(p.get("steps", 3)), 2)),
                  ("breakdown", 120, f"{PY} tools/step_breakdown.py \"$(find gpurun_out/{p['tag']}/rocprof -name "
-                  f"'*.db' -print -quit)\" --marker {p.get('marker', 'emb_fwd')}")],
+                  f"'*.db' -print -quit)\" --marker {p.get('marker', 'emb_fwd')}"),
+                 # the trace database is tens of MiB: drop it so gpurun_out/ stays under the copy-back cap
+                 ("cleanup", 60, f"rm -rf gpurun_out/{p['tag']}/rocprof")],
         "cmd": [("cmd", int(p.get("timeout", 600)), p.get("cmd", "true"))],
     }
 
