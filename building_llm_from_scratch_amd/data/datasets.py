@@ -113,6 +113,34 @@ class InstructionDataset(Dataset):
         return len(self.data)
 
 
+def format_input_phi(entry: dict) -> str:
+    """Phi-style prompt (reference datautils/dataset_instruction_finetune.py:28-42):
+    ``<|user|>\n{instruction}`` plus ``\n{input}`` when there is one."""
+    return f"<|user|>\n{entry['instruction']}" + (f"\n{entry['input']}" if entry.get("input") else "")
+
+
+class InstructionDatasetPhi(Dataset):
+    """Phi-format instruction data (reference dataset_instruction_finetune.py:79-99): prompt +
+    ``\n<|assistant|>:\n{output}``.  The reference's items are bare token lists, which its own
+    collate cannot take (it unpacks (prompt length, ids) pairs); here an item is
+    ``(prompt length, ids)`` like ``InstructionDataset``, so ``custom_collate_fn`` masks the prompt."""
+
+    def __init__(self, data: Sequence[dict], tokenizer):
+        self.data = data
+        self.encoded_texts: List[List[int]] = []
+        self.instruction_lengths: List[int] = []
+        for entry in data:
+            prompt = format_input_phi(entry)
+            self.encoded_texts.append(tokenizer.encode(prompt + f"\n<|assistant|>:\n{entry['output']}"))
+            self.instruction_lengths.append(len(tokenizer.encode(prompt)))
+
+    def __getitem__(self, index):
+        return self.instruction_lengths[index], self.encoded_texts[index]
+
+    def __len__(self):
+        return len(self.data)
+
+
 def custom_collate_fn(batch, pad_token_id: int = 50256, ignore_index: int = -100,
                       allowed_max_length: Optional[int] = None):
     batch_max_length = max(len(item) + 1 for _, item in batch)

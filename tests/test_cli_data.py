@@ -118,6 +118,23 @@ def test_collate_survey_example():
     assert x[0].tolist() == [5, 8, 9, 50256, 50256]
 
 
+def test_phi_format_dataset():
+    """Phi-format formatter and dataset (reference dataset_instruction_finetune.py:28-99); items
+    carry the prompt length so the reference collate masks the prompt."""
+    from building_llm_from_scratch_amd.data.datasets import InstructionDatasetPhi, format_input_phi
+    e1 = {"instruction": "Add.", "input": "1 2", "output": "3"}
+    e2 = {"instruction": "Greet.", "input": "", "output": "hi"}
+    assert format_input_phi(e1) == "<|user|>\nAdd.\n1 2"
+    assert format_input_phi(e2) == "<|user|>\nGreet."
+    tok = ByteTokenizer()
+    ds = InstructionDatasetPhi([e1, e2], tok)
+    n, ids = ds[0]
+    assert tok.decode(ids) == "<|user|>\nAdd.\n1 2\n<|assistant|>:\n3"
+    assert n == len(tok.encode(format_input_phi(e1))) and len(ds) == 2
+    x, y = custom_collate_fn([ds[0], ds[1]], pad_token_id=0)
+    assert (y[0, :n - 1] == -100).all() and y[0, n - 1] != -100
+
+
 # ---------------------------------------------------------------------------- prep
 def test_prepare_gutenberg(tmp_path):
     src = tmp_path / "txt"
