@@ -106,8 +106,9 @@ unsigned int debug_take_attn_decode();
 unsigned int debug_take_elementwise();
 void embedding_fwd(DType dt, const int64_t* idx, const void* wte, const void* wpe, void* out, long N, int d, int T,
                    float p, uint64_t seed, uint64_t offset, long vocab, hipStream_t s);
-void embedding_bwd_tok(DType dt, const int64_t* sorted, const int64_t* perm, const void* dx, void* grad, long N, int d,
-                       bool accumulate, hipStream_t s);
+long embedding_bwd_part_floats(long N, int d);  // fp32 scratch the token backward needs
+void embedding_bwd_tok(DType dt, const int64_t* sorted, const int64_t* perm, const void* dx, void* grad, float* part,
+                       long N, int d, bool accumulate, hipStream_t s);
 void embedding_bwd_pos(DType dt, const void* dx, void* grad, int B, int T, int d, bool accumulate, hipStream_t s);
 
 // lora.hip — see the file header for the operand conventions

@@ -624,10 +624,12 @@ void embedding_bwd(const Tensor& idx, const Tensor& dx, const optional<Tensor>& 
     check_gpu(gw, "grad_wte");
     TORCH_CHECK(gw.size(1) == d && gw.scalar_type() == dx.scalar_type());
     if (!accumulate) gw.zero_();
-    auto sorted = at::sort(idx.reshape({-1}));
+    // stable: equal ids keep their token order, so the fp32 sums run in a fixed order
+    auto sorted = at::sort(idx.reshape({-1}), /*stable=*/true, 0, false);
     Tensor sid = std::get<0>(sorted).contiguous(), perm = std::get<1>(sorted).contiguous();
+    auto part = at::empty({bllm::embedding_bwd_part_floats(N, (int)d)}, dx.options().dtype(at::kFloat));
     bllm::embedding_bwd_tok(dt_of(dx), sid.data_ptr<int64_t>(), perm.data_ptr<int64_t>(), dx.data_ptr(),
-                            gw.data_ptr(), N, (int)d, accumulate, stream());
+                            gw.data_ptr(), part.data_ptr<float>(), N, (int)d, accumulate, stream());
   }
   if (grad_wpe.has_value()) {
     Tensor gp = *grad_wpe;

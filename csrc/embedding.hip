@@ -44,12 +44,21 @@ __global__ __launch_bounds__(256) void emb_fwd_k(const int64_t* __restrict__ idx
   }
 }
 
-// One wave per (sorted position, 64*VEC-column slice); only the waves on a run head work.  A run
-// is summed in sorted order (fixed -> reproducible), four rows per trip with their loads in
-// flight together; row indices come 16 per vector load (broadcast by v_readlane) and the run's
-// end 64 ids per ballot probe.  With a byte-level vocabulary (the offline tokenizer) a run is
-// hundreds of rows long: the previous one-workgroup-per-run walk, one dependent scalar load per
-// row, was latency bound.
+// Token-embedding backward, deterministic and independent of how skewed the ids are.  The
+// sorted positions are cut into blocks of EMB_BLK; one wave per (block, 64*VEC-column slice)
+// walks its block in sorted order (rows fetched 4 at a time, their indices 64 per vector load
+// and broadcast by v_readlane) and cuts it into segments of equal id:
+//   * a segment that is a whole run (it does not touch a neighbouring block's run) writes the
+//     table row directly;
+//   * the block's first segment, when its run started in an earlier block, goes to part[blk][0];
+//     its last segment, when its run continues into the next block (and did not start earlier),
+//     to part[blk][1] -- fp32 partial rows.
+// A second pass finishes every run that crosses blocks from the block where it ends, adding the
+// partials block by block backwards (fixed order: bitwise reproducible).  Byte-level ids (the
+// offline tokenizer) make runs of thousands of rows -- the space character alone is ~15 % of
+// the text -- which one wave per run walked in ~5 ms per step.
+constexpr int EMB_BLK = 128;
+
 __device__ __forceinline__ long lane_i64(long v, int src) {
   const int lo = __builtin_amdgcn_readlane((int)(unsigned)(v & 0xffffffff), src);
   const int hi = __builtin_amdgcn_readlane((int)(v >> 32), src);
@@ -57,63 +66,103 @@ __device__ __forceinline__ long lane_i64(long v, int src) {
 }
 
 template <typename T, int VEC>
-__global__ __launch_bounds__(256) void emb_bwd_tok_k(const int64_t* __restrict__ sorted,
-                                                     const int64_t* __restrict__ perm, const T* __restrict__ dx,
-                                                     T* __restrict__ grad, long N, int d, bool accumulate) {
-  const long i = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (i >= N) return;
-  const int64_t id = sorted[i];
-  if (i > 0 && sorted[i - 1] == id) return;
-  const int lane = threadIdx.x & 63;
-  const int c = (blockIdx.y * 64 + lane) * VEC;
-  const bool live = c < d;
-  // run end: 64 sorted ids per probe, first mismatch by ballot
-  long e = i + 1;
-  for (;;) {
-    const long k = e + lane;
-    const uint64_t m = __builtin_amdgcn_ballot_w64(k >= N || sorted[k] != id);
-    if (m) {
-      e += __builtin_ctzll(m);
-      break;
-    }
-    e += 64;
-  }
-  float acc[VEC];
-#pragma unroll
-  for (int j = 0; j < VEC; ++j) acc[j] = 0.f;
-  for (long k0 = i; k0 < e; k0 += 16) {
-    // 16 row indices in one vector load, broadcast by v_readlane; 4 row loads in flight
-    const long pk = k0 + (lane & 15) < e ? (long)perm[k0 + (lane & 15)] : 0;
-    const int n = e - k0 < 16 ? (int)(e - k0) : 16;
-    int u = 0;
-    for (; u + 4 <= n; u += 4) {
-      VecN<T, VEC> v[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-        if (live) v[q] = ldv<T, VEC>(dx + lane_i64(pk, u + q) * d + c);
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-#pragma unroll
-        for (int j = 0; j < VEC; ++j) acc[j] += live ? to_f(v[q].v[j]) : 0.f;
-    }
-    for (; u < n; ++u) {
-      if (!live) continue;
-      VecN<T, VEC> v = ldv<T, VEC>(dx + lane_i64(pk, u) * d + c);
-#pragma unroll
-      for (int j = 0; j < VEC; ++j) acc[j] += to_f(v.v[j]);
-    }
-  }
-  if (!live) return;
+__device__ __forceinline__ void emb_store_row(T* grad, long id, int d, int c, const float (&acc)[VEC], bool accumulate) {
   T* g = grad + id * d + c;
-  VecN<T, VEC> o;
+  float v[VEC];
+#pragma unroll
+  for (int j = 0; j < VEC; ++j) v[j] = acc[j];
   if (accumulate) {
     VecN<T, VEC> old = ldv<T, VEC>(g);
 #pragma unroll
-    for (int j = 0; j < VEC; ++j) acc[j] += to_f(old.v[j]);
+    for (int j = 0; j < VEC; ++j) v[j] += to_f(old.v[j]);
   }
+  VecN<T, VEC> o;
 #pragma unroll
-  for (int j = 0; j < VEC; ++j) o.v[j] = from_f<T>(acc[j]);
+  for (int j = 0; j < VEC; ++j) o.v[j] = from_f<T>(v[j]);
   stv<T, VEC>(g, o);
+}
+
+template <typename T, int VEC>
+__global__ __launch_bounds__(64) void emb_bwd_tok_k(const int64_t* __restrict__ sorted,
+                                                    const int64_t* __restrict__ perm, const T* __restrict__ dx,
+                                                    T* __restrict__ grad, float* __restrict__ part, long N, int d,
+                                                    bool accumulate) {
+  const int lane = threadIdx.x;
+  const long k = blockIdx.x, b0 = k * EMB_BLK, b1 = b0 + EMB_BLK < N ? b0 + EMB_BLK : N;
+  const int c = (blockIdx.y * 64 + lane) * VEC;
+  const bool live = c < d;
+  float acc[VEC];
+#pragma unroll
+  for (int j = 0; j < VEC; ++j) acc[j] = 0.f;
+  long cur = sorted[b0], s0 = b0;
+  auto flush = [&](long s1) {  // segment [s0, s1) of id cur
+    const bool before = s0 == b0 && b0 > 0 && sorted[b0 - 1] == cur;
+    const bool after = s1 == b1 && b1 < N && sorted[b1] == cur;
+    if (live) {
+      if (!before && !after) {
+        emb_store_row<T, VEC>(grad, cur, d, c, acc, accumulate);
+      } else {
+        float* pr = part + ((k * 2 + (before ? 0 : 1)) * (long)d + c);
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) pr[j] = acc[j];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) acc[j] = 0.f;
+  };
+  for (long p0 = b0; p0 < b1; p0 += 64) {
+    const int n = b1 - p0 < 64 ? (int)(b1 - p0) : 64;
+    const long myid = lane < n ? (long)sorted[p0 + lane] : -1;
+    const long myrow = lane < n ? (long)perm[p0 + lane] : 0;
+    for (int u = 0; u < n; u += 4) {
+      VecN<T, VEC> v[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (live && u + q < n) v[q] = ldv<T, VEC>(dx + lane_i64(myrow, u + q) * d + c);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if (u + q >= n) break;
+        const long id = lane_i64(myid, u + q);
+        if (id != cur) {
+          flush(p0 + u + q);
+          cur = id;
+          s0 = p0 + u + q;
+        }
+        if (live) {
+#pragma unroll
+          for (int j = 0; j < VEC; ++j) acc[j] += to_f(v[q].v[j]);
+        }
+      }
+    }
+  }
+  flush(b1);
+}
+
+// runs that cross blocks, finished in the block where they end
+template <typename T, int VEC>
+__global__ __launch_bounds__(64) void emb_bwd_tok_fix_k(const int64_t* __restrict__ sorted,
+                                                        T* __restrict__ grad, const float* __restrict__ part, long N,
+                                                        int d, bool accumulate) {
+  const long k = blockIdx.x, b0 = k * EMB_BLK, b1 = b0 + EMB_BLK < N ? b0 + EMB_BLK : N;
+  if (k == 0) return;
+  const long id = sorted[b0];
+  if (sorted[b0 - 1] != id) return;                                        // no run enters the block
+  if (sorted[b1 - 1] == id && b1 < N && sorted[b1] == id) return;          // it continues past it
+  const int c = (blockIdx.y * 64 + threadIdx.x) * VEC;
+  if (c >= d) return;
+  float acc[VEC];
+  const float* pr = part + (k * 2 + 0) * (long)d + c;
+#pragma unroll
+  for (int j = 0; j < VEC; ++j) acc[j] = pr[j];
+  for (long b = k - 1;; --b) {
+    const long bs = b * EMB_BLK;
+    const bool start = sorted[bs] != id || bs == 0 || sorted[bs - 1] != id;  // the run starts in block b
+    const float* q = part + (b * 2 + (start ? 1 : 0)) * (long)d + c;
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) acc[j] += q[j];
+    if (start) break;
+  }
+  emb_store_row<T, VEC>(grad, id, d, c, acc, accumulate);
 }
 
 template <typename T, int VEC>
@@ -166,13 +215,18 @@ void embedding_fwd(DType dt, const int64_t* idx, const void* wte, const void* wp
   });
 }
 
-void embedding_bwd_tok(DType dt, const int64_t* sorted, const int64_t* perm, const void* dx, void* grad, long N,
-                       int d, bool accumulate, hipStream_t s) {
+long embedding_bwd_part_floats(long N, int d) { return (long)ceil_div(N, EMB_BLK) * 2 * d; }
+
+void embedding_bwd_tok(DType dt, const int64_t* sorted, const int64_t* perm, const void* dx, void* grad, float* part,
+                       long N, int d, bool accumulate, hipStream_t s) {
+  if (N <= 0) return;
   BLLM_DISPATCH(dt, T, {
     EMB_VEC(T, d, {
-      const dim3 grid((unsigned)((N + 3) / 4), (unsigned)ceil_div(d, 64 * VEC));
-      hipLaunchKernelGGL((emb_bwd_tok_k<T, VEC>), grid, dim3(256), 0, s, sorted, perm, (const T*)dx, (T*)grad,
+      const dim3 grid((unsigned)ceil_div(N, EMB_BLK), (unsigned)ceil_div(d, 64 * VEC));
+      hipLaunchKernelGGL((emb_bwd_tok_k<T, VEC>), grid, dim3(64), 0, s, sorted, perm, (const T*)dx, (T*)grad, part,
                          N, d, accumulate);
+      hipLaunchKernelGGL((emb_bwd_tok_fix_k<T, VEC>), grid, dim3(64), 0, s, sorted, (T*)grad, (const float*)part, N,
+                         d, accumulate);
     });
   });
 }

@@ -184,11 +184,14 @@ def test_embedding_bwd_long_runs(dt, d):
     """Byte-level vocabularies give runs of hundreds of equal ids: runs longer than one 64-id
     ballot probe and not a multiple of the 16-row index batch, a 1-row run, a partial last
     column slice (1280 = 2.5 x 512), and accumulate=True onto an existing gradient."""
-    V, N = 50, 2053
+    V = 50
     g_ = torch.Generator().manual_seed(5)
-    idx = torch.randint(3, 10, (N,), generator=g_)
-    idx[17] = 40                                  # a run of one
-    idx = idx.to(DEV)
+    # sorted runs that start / end exactly on the 128-position block boundaries of the kernel,
+    # span several blocks, or are one row long; then shuffled into token order
+    counts = torch.tensor([128, 256, 1, 127, 129, 300, 1, 1, 383, 64, 640])
+    idx = torch.repeat_interleave(torch.arange(3, 3 + len(counts)), counts)
+    idx = idx[torch.randperm(idx.numel(), generator=g_)].to(DEV)
+    N = idx.numel()
     dx = torch.randn(N, d, device=DEV).to(dt)
     base = torch.randn(V, d, device=DEV).to(dt)
     g = base.clone()

@@ -45,6 +45,8 @@ def recipes(p):
                   + _bench(extra, int(p.get("steps", 3)), 2)),
                  ("breakdown", 120, f"{PY} tools/step_breakdown.py \"$(find gpurun_out/{p['tag']}/rocprof -name "
                   f"'*.db' -print -quit)\" --marker {p.get('marker', 'emb_fwd')}"),
+                 ("kstats", 120, f"{PY} tools/kstats.py \"$(find gpurun_out/{p['tag']}/rocprof -name "
+                  f"'*.db' -print -quit)\" --grep '{p.get('kgrep', '')}'"),
                  # the trace database is tens of MiB: drop it so gpurun_out/ stays under the copy-back cap
                  ("cleanup", 60, f"rm -rf gpurun_out/{p['tag']}/rocprof")],
         "cmd": [("cmd", int(p.get("timeout", 600)), p.get("cmd", "true"))],
