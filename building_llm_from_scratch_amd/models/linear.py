@@ -283,7 +283,13 @@ class FusedLinear:
         ``forward_kaug`` adds the s t columns, so neither a copy of x nor a pass over y is paid."""
         if not (self._kaug_base_ok() and self._grouped_lora_dims(like.device, like.dtype, K)):
             return None
-        return torch.empty(like.shape[0], K + self.lora_R, dtype=like.dtype, device=like.device)
+        return torch.empty(like.shape[0], K + self._kaug_pad(K), dtype=like.dtype, device=like.device)
+
+    def _kaug_pad(self, K: int) -> int:
+        """Columns after x: the R of s t, rounded up so that a row is a whole number of 128-byte
+        lines (K + R = 2096 split every 64-column read of x over two lines: the dA pass ran 1.6x
+        slower on it); the pad columns are zero in both operands."""
+        return -(-(K + self.lora_R) // 64) * 64 - K
 
     def _waug(self, W: torch.Tensor, K: int):
         """([W | Bd^T] [out, K + R], [W^T ; Bd] [K + R, out]): member m's B_m^T in rows c0_m..,
@@ -292,14 +298,15 @@ class FusedLinear:
         W's storage or version changed (a re-gather, a state-dict load); the B blocks (trained)
         are rewritten every call, one kernel each."""
         u = self.unit
+        Rp = self._kaug_pad(K)
         key = (W.data_ptr(), W._version, W.shape, W.dtype)
         cached = getattr(self, "_wa_cache", None)
         if cached is not None and cached[0] == key:
             Wa, WaT = cached[1], cached[2]
         else:
-            Wa = torch.empty(W.shape[0], K + self.lora_R, dtype=W.dtype, device=W.device)
+            Wa = torch.empty(W.shape[0], K + Rp, dtype=W.dtype, device=W.device)
             Wa[:, :K].copy_(W)
-            WaT = torch.empty(K + self.lora_R, W.shape[0], dtype=W.dtype, device=W.device)
+            WaT = torch.empty(K + Rp, W.shape[0], dtype=W.dtype, device=W.device)
             WaT[:K].copy_(ops.transpose2d(W) if W.is_cuda else W.t())
             self._wa_cache = (key, Wa, WaT)
         Bs = [u.data(s.lora_B) for s in self.lora_specs]
@@ -307,20 +314,19 @@ class FusedLinear:
         ops.lora_block_(WaT[K:].t(), Bs, self.lora_c0, self.lora_off)
         return Wa, WaT
 
-    def forward_kaug(self, xa: torch.Tensor, residual: Optional[torch.Tensor] = None):
+    def forward_kaug(self, xa: torch.Tensor, K: int, residual: Optional[torch.Tensor] = None):
         """K-augmented forward on ``xa`` = [x | .] (x already written by the producer):
         s t = s x A_cat goes into the last R columns, then ONE GEMM
         y (= residual +) [x | s t] . [W | Bd^T]^T — the rank-r update rides in the GEMM's K loop.
         Backward gets dy Bd = dy B^T from the dX GEMM the same way (``_kaug_lora_backward``)."""
         u = self.unit
         R = self.lora_R
-        K = xa.shape[1] - R
-        x, st = xa[:, :K], xa[:, K:]
+        x = xa[:, :K]
         P = ops.lora_pack_t([u.data(s.lora_A) for s in self.lora_specs])          # [R, K]
-        ops.lora_down_into(x, [P], [0], [K], [0], R, self.lora_scale, st)        # s x A_cat
+        ops.lora_down_into(x, [P], [0], [K], [0], R, self.lora_scale, xa[:, K:])  # [s x A_cat | 0]
         Wa, WaT = self._waug(self.W(), K)
         y = ops.linear_residual(xa, Wa, residual) if residual is not None else mm_nt(xa, Wa)
-        return y, ("kaug", st, P, WaT)
+        return y, ("kaug", xa[:, K:K + R], P, WaT)
 
     # views are re-fetched every call: FSDP may have re-materialised the storage
     def W(self):
@@ -341,7 +347,7 @@ class FusedLinear:
             # less than the s t B write plus the beta = 1 re-read of y it replaces)
             xa = self.kaug_input(x, x.shape[1])
             xa[:, :x.shape[1]].copy_(x)
-            return self.forward_kaug(xa)
+            return self.forward_kaug(xa, x.shape[1])
         if self.has_lora and self._grouped_lora(x):
             # y = (residual | bias) + s t B, written by lora_up, then the base GEMM accumulates
             # onto it (beta = 1): the rank-r update costs no read-modify-write pass of y
@@ -482,8 +488,8 @@ class FusedLinear:
         if gB:                                                     # dB = s t^T dy = (s t)^T dy
             ops.lora_wgrad(st, dy, [g for g, _, _ in gB], [o for _, _, o in gB], [c for _, c, _ in gB], 1.0,
                            accumulate)
-        dxa = mm_nt(dy, WaT)                                       # [dy W | dy Bd] = [dx_W | dy B^T]
-        ub = dxa[:, K:]
+        dxa = mm_nt(dy, WaT)                                       # [dy W | dy Bd | 0] = [dx_W | dy B^T | 0]
+        ub = dxa[:, K:K + self.lora_R]
         gA = [(u_.grad(s.lora_A), off) for s, off in zip(self.lora_specs, self.lora_off)]
         gA = [g for g in gA if g[0] is not None]
         if gA:

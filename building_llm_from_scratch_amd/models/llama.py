@@ -163,7 +163,7 @@ class LlamaBlockCompute(UnitCompute):
         xq = self.qkv.kaug_input(x2d, d)
         if xq is not None:
             h1, r1 = ops.rmsnorm_fwd_into(x2d, u.data(b.norm1.weight), eps, xq[:, :d])
-            qkv, xa_qkv = self.qkv.forward_kaug(xq)
+            qkv, xa_qkv = self.qkv.forward_kaug(xq, d)
             ops.rope_(qkv, cos, sin, T, H, G, hd)
         else:
             h1, r1 = ops.rmsnorm_fwd(x2d, u.data(b.norm1.weight), eps)
@@ -179,7 +179,7 @@ class LlamaBlockCompute(UnitCompute):
         fused = None
         if xg is not None:
             h2, r2 = ops.rmsnorm_fwd_into(x2, u.data(b.norm2.weight), eps, xg[:, :d])
-            gu, xa_gu = self.gu.forward_kaug(xg)
+            gu, xa_gu = self.gu.forward_kaug(xg, d)
         else:
             h2, r2 = ops.rmsnorm_fwd(x2, u.data(b.norm2.weight), eps)
             if not (recompute and not self.down.has_lora and RECOMPUTE_FUSED):
@@ -196,7 +196,7 @@ class LlamaBlockCompute(UnitCompute):
             xd = None if (fused is not None or recompute) else self.down.kaug_input(gu, F)
             if xd is not None:
                 act = ops.swiglu_fwd_into(gu, xd[:, :F])
-                x3, xa_dn = self.down.forward_kaug(xd, residual=x2)
+                x3, xa_dn = self.down.forward_kaug(xd, F, residual=x2)
             else:
                 if fused is None:
                     act = ops.swiglu_fwd(gu)

@@ -589,11 +589,13 @@ def lora_down(x, ws, c0, lens, ocol, R: int, scale: float = 1.0):
 
 
 def lora_down_into(x, ws, c0, lens, ocol, R: int, scale: float, out):
-    """lora_down written into ``out``, a row-strided [N, R] view (the s t columns of [x | s t])."""
+    """lora_down written into ``out``, a row-strided [N, >= R] view (the s t columns of
+    [x | s t | 0]); columns past R are zeroed (the row-alignment pad)."""
     if _hip(x):
         _k().lora_down_into_(x, list(ws), list(c0), list(lens), list(ocol), int(R), float(scale), out)
         return out
-    out.copy_(ref.lora_down(x, ws, c0, lens, ocol, R, scale))
+    out[:, :R].copy_(ref.lora_down(x, ws, c0, lens, ocol, R, scale))
+    out[:, R:].zero_()
     return out
 
 

@@ -116,6 +116,7 @@ constexpr int LORA_MAX = 8;
 struct LoraDownArgs {  // chunk c: out[:, ocol_c : +16*nt_c] = x[:, c0_c : +len_c] . W_c^T
   const void* x; long ldx;
   void* out; long ldo;
+  int R, zpad;                 // out columns [R, R + zpad) are written with zeros
   float scale;
   int n;
   int c0[LORA_MAX], len[LORA_MAX], ocol[LORA_MAX], nt[LORA_MAX];
@@ -139,8 +140,8 @@ struct LoraWgradArgs {  // member m: G_m[a*sa + b*sb] (+)= scale . sum_n p[n][pa
   int n;
   int pa[LORA_MAX], qb[LORA_MAX], r[LORA_MAX], len[LORA_MAX], nblk[LORA_MAX];
   long sa[LORA_MAX], sb[LORA_MAX];
-  void* g[LORA_MAX];
-  float* part; long part_ld; long part_off[LORA_MAX];  // S > 1: part[s][part_off_m + e], row length part_ld
+  void* gt[LORA_MAX][4];       // output of member m's 16-column tile t (element [0][0] of that tile)
+  float* part; long part_ld; long part_off[LORA_MAX];  // S > 1: part[s][part_off_m + a * len_m + b]
 };
 struct LoraPackArgs {  // out[off_m + j][k] = a_m[k][j]
   void* out;

@@ -657,10 +657,11 @@ static void lora_down_impl(const Tensor& x, at::TensorList ws, at::IntArrayRef c
   const int64_t N = x.size(0);
   TORCH_CHECK(N > 0 && R % 16 == 0 && R > 0, "lora_down: N > 0 and R a multiple of 16 required");
   TORCH_CHECK(ws.size() == c0.size() && ws.size() == lens.size() && ws.size() == ocol.size());
-  TORCH_CHECK(out.is_cuda() && out.dim() == 2 && out.size(0) == N && out.size(1) == R && out.stride(1) == 1 &&
-                  out.scalar_type() == x.scalar_type(), "lora_down: out must be an [N, R] row-strided view");
+  TORCH_CHECK(out.is_cuda() && out.dim() == 2 && out.size(0) == N && out.size(1) >= R && out.stride(1) == 1 &&
+                  out.scalar_type() == x.scalar_type(), "lora_down: out must be an [N, >= R] row-strided view");
   bllm::LoraDownArgs a{};
   a.x = x.data_ptr(); a.ldx = x.stride(0); a.out = out.data_ptr(); a.ldo = out.stride(0); a.scale = (float)scale;
+  a.R = (int)R; a.zpad = (int)(out.size(1) - R);  // columns past R: zeros (alignment pad)
   for (size_t i = 0; i < ws.size(); ++i) {
     const Tensor& w = ws[i];
     check_lora_mat(w, "w");
@@ -766,6 +767,7 @@ void lora_wgrad(const Tensor& p, const Tensor& q, at::TensorList gs, at::IntArra
   a.p = p.data_ptr(); a.ldp = p.stride(0); a.q = q.data_ptr(); a.ldq = q.stride(0);
   a.scale = (float)scale; a.accumulate = accumulate;
   const DType odt = dt_of(gs[0]);
+  const int64_t esz = gs[0].element_size();
   int blocks = 0;
   for (size_t i = 0; i < gs.size(); ++i) {
     const Tensor& gm = gs[i];
@@ -774,12 +776,24 @@ void lora_wgrad(const Tensor& p, const Tensor& q, at::TensorList gs, at::IntArra
     const int64_t r = gm.size(0), len = gm.size(1);
     TORCH_CHECK(r % 16 == 0 && r <= 64 && len % 8 == 0 && pa[i] % 8 == 0 && qb[i] % 8 == 0, "lora_wgrad: alignment");
     TORCH_CHECK(pa[i] + r <= p.size(1) && qb[i] + len <= q.size(1), "lora_wgrad: window out of range");
+    // merge into the previous member when both read the same Q window, their P windows are
+    // adjacent, their output strides agree and the merged rank stays <= 64 (dA of a group)
+    if (a.n > 0) {
+      const int j = a.n - 1;
+      if (a.qb[j] == (int)qb[i] && a.len[j] == (int)len && a.pa[j] + a.r[j] == (int)pa[i] && a.r[j] + r <= 64 &&
+          a.sa[j] == gm.stride(0) && a.sb[j] == gm.stride(1)) {
+        for (int64_t t = 0; t < r / 16; ++t)
+          a.gt[j][a.r[j] / 16 + t] = (char*)gm.data_ptr() + 16 * t * gm.stride(0) * esz;
+        a.r[j] += (int)r;
+        continue;
+      }
+    }
     a.pa[a.n] = (int)pa[i]; a.qb[a.n] = (int)qb[i]; a.r[a.n] = (int)r; a.len[a.n] = (int)len;
     a.nblk[a.n] = bllm::ceil_div(len, 64); a.sa[a.n] = gm.stride(0); a.sb[a.n] = gm.stride(1);
-    a.g[a.n] = gm.data_ptr();
-    blocks += a.nblk[a.n];
+    for (int64_t t = 0; t < r / 16; ++t) a.gt[a.n][t] = (char*)gm.data_ptr() + 16 * t * gm.stride(0) * esz;
     ++a.n;
   }
+  for (int i = 0; i < a.n; ++i) blocks += a.nblk[i];
   const int S = bllm::lora_wgrad_splits(blocks, (int)N);
   Tensor part;
   if (S > 1) {

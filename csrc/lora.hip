@@ -13,7 +13,10 @@
 //               fwd: y += s t B  (U = B);  bwd: dx += s u A^T (U = A^T)
 //   lora_wgrad  G_m = s . P[:, a-window]^T . Q[:, b-window]   (reduction over the N tokens)
 //               dB = s t^T dy,  dA = s x^T u — written (or accumulated) straight into the
-//               unit's flat gradient in its dtype; deterministic (fixed-order split-N partials)
+//               unit's flat gradient in its dtype; deterministic (fixed-order split-N partials).
+//               Members that read the same Q window (every dA of a group: all read x) are
+//               merged by the binding into one of rank sum r_m <= 64, so x is streamed once;
+//               its 16-column tiles carry their own output pointers (gt).
 //
 // All three are HBM-bound (the rank is 8-64): x / dy / y are streamed exactly once per kernel
 // with 16-byte lane accesses; the small operands (A, B, t, u) stay L2-resident.
@@ -53,8 +56,8 @@ template <typename T> __device__ __forceinline__ float from_bits(short b) {
 
 // --------------------------------------------------------------------------- lora_down
 // Block = 8 waves on 16 rows; the K loop is split over the waves (wave w takes k-steps
-// w, w+8, ...; four per trip so four 16-B x loads are in flight per lane) and the eight
-// partial 16 x (16*NT) tiles are summed through LDS.
+// w, w+8, ...; eight, then four, per trip: that many 16-B x loads in flight per lane) and the
+// eight partial 16 x (16*NT) tiles are summed through LDS.
 // MFMA: A = X rows (lane: X[row l&15][k 8(l>>4)..+8], one 16-B load), B[k][col] = W[col][k]
 // (W rows are k-contiguous -> one 16-B load per column tile).
 template <typename T>
@@ -75,6 +78,18 @@ __global__ __launch_bounds__(512) void lora_down_k(LoraDownArgs a, int N) {
   for (int t = 0; t < 4; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int nks = a.len[ch] >> 5;
   int ks = wave;
+  for (; ks + 7 * NW < nks; ks += 8 * NW) {  // eight 16-B x loads in flight per lane
+    s16x8 xa[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) xa[u] = ld8(x + (ks + u * NW) * 32);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      if (t < nt) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) acc[t] = MF16<T>::mma(xa[u], ld8(w + t * wstep + (ks + u * NW) * 32), acc[t]);
+      }
+    }
+  }
   for (; ks + 3 * NW < nks; ks += 4 * NW) {
     s16x8 xa[4];
 #pragma unroll
@@ -109,6 +124,13 @@ __global__ __launch_bounds__(512) void lora_down_k(LoraDownArgs a, int N) {
 #pragma unroll
     for (int q = 0; q < NW; ++q) v += red[q][r][c];
     out[(long)r * a.ldo + c] = from_f<T>(v * a.scale);
+  }
+  if (ch == 0 && a.zpad > 0) {  // zero columns [R, R + zpad): the alignment pad of a K-augmented row
+    T* pad = (T*)a.out + row0 * a.ldo + a.R;
+    for (int e = threadIdx.x; e < 16 * a.zpad; e += NW * 64) {
+      const int r = e / a.zpad, c = e - r * a.zpad;
+      if (row0 + r < N) pad[(long)r * a.ldo + c] = from_f<T>(0.f);
+    }
   }
 }
 
@@ -163,6 +185,18 @@ __global__ __launch_bounds__(256) void lora_up_k(LoraUpArgs a, int rows, int N) 
     for (int rt = 0; rt < rows / 64; ++rt) {
       const long row0 = (long)blockIdx.x * rows + rt * 64 + wave * 16;
       if (row0 >= N) break;  // wave-uniform: this wave's remaining tiles are past the tokens
+      // the tile's base (or, for a later rank pass, y) rows are loaded first, so their HBM
+      // latency runs under the MFMAs and the LDS re-layout instead of in front of the stores
+      VecN<T, 8> bs[4];
+      const T* bsrc = j0 ? (const T*)a.y : (const T*)a.base;
+      const long bld = j0 ? a.ldy : a.ldb;
+      if (bsrc && col_ok) {
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+          const int row = (lane >> 4) + 4 * p;
+          if (row0 + row < N) bs[p] = ldv<T, 8>(bsrc + (row0 + row) * bld + a.c0[m] + cb + c8);
+        }
+      }
       const long tr = row0 + (lane & 15) < N ? row0 + (lane & 15) : N - 1;
       const T* t = (const T*)a.t + tr * a.ldt + a.toff[m] + j0;
       f32x4 acc[8];
@@ -192,15 +226,11 @@ __global__ __launch_bounds__(256) void lora_up_k(LoraUpArgs a, int rows, int N) 
         const f32x4 v0 = *reinterpret_cast<const f32x4*>(&ep[row * EP + c8]);
         const f32x4 v1 = *reinterpret_cast<const f32x4*>(&ep[row * EP + c8 + 4]);
         const float v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
-        VecN<T, 8> bs, o;
-        if (a.base) bs = ldv<T, 8>((const T*)a.base + (row0 + row) * a.ldb + a.c0[m] + cb + c8);
-        if (j0) {  // later rank pass: accumulate onto what the first pass wrote
-          bs = ldv<T, 8>((const T*)a.y + g);
-        }
+        VecN<T, 8> o;
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
           float z = a.scale * v[i];
-          if (a.base || j0) z += to_f(bs.v[i]);
+          if (bsrc) z += to_f(bs[p].v[i]);
           if (bias && !j0) z += to_f(bb.v[i]);
           o.v[i] = from_f<T>(z);
         }
@@ -282,22 +312,23 @@ __global__ __launch_bounds__(256) void lora_wgrad_k(LoraWgradArgs a, int N) {
         if (t < nt) acc[t] = MF16<T>::mma(qa, tr_frag(&ps[n * NP + t * 16 + 4 * tp], NP), acc[t]);
     }
   }
-  // lane holds G[b = b0 + 16*wave + 4(l>>4) + i][a = 16t + (l&15)]
+  // lane holds G[b = b0 + 16*wave + 4(l>>4) + i][a = 16t + (l&15)]; column tile t of member m
+  // goes to gt[m][t] (a merged member spans several output matrices, 16 columns each at least)
   const long sa = a.sa[m], sb = a.sb[m];
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
     if (t >= nt) continue;
+    OT* gtile = (OT*)a.gt[m][t];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int b = b0 + wave * 16 + 4 * (lane >> 4) + i, aa = t * 16 + (lane & 15);
+      const int b = b0 + wave * 16 + 4 * (lane >> 4) + i, ac = lane & 15;
       if (b >= len) continue;
-      const long o = (long)aa * sa + (long)b * sb;
       const float v = acc[t][i] * a.scale;
-      if (S > 1) {
-        a.part[(long)split * a.part_ld + a.part_off[m] + o] = v;
+      if (S > 1) {  // dense [r][len] partial
+        a.part[(long)split * a.part_ld + a.part_off[m] + (long)(t * 16 + ac) * len + b] = v;
       } else {
-        OT* g = (OT*)a.g[m];
-        g[o] = from_f<OT>(a.accumulate ? to_f(g[o]) + v : v);
+        const long o = (long)ac * sa + (long)b * sb;
+        gtile[o] = from_f<OT>(a.accumulate ? to_f(gtile[o]) + v : v);
       }
     }
   }
@@ -310,10 +341,12 @@ __global__ __launch_bounds__(256) void lora_reduce_k(LoraWgradArgs a, int S, lon
     int m = 0;
     while (m + 1 < a.n && e >= a.part_off[m + 1]) ++m;
     const long o = e - a.part_off[m];
+    const int aa = (int)(o / a.len[m]);
+    const long b = o - (long)aa * a.len[m];
     float v = 0.f;
     for (int s = 0; s < S; ++s) v += a.part[(long)s * a.part_ld + e];
-    OT* g = (OT*)a.g[m];
-    g[o] = from_f<OT>(a.accumulate ? to_f(g[o]) + v : v);
+    OT* g = (OT*)a.gt[m][aa >> 4] + (long)(aa & 15) * a.sa[m] + b * a.sb[m];
+    *g = from_f<OT>(a.accumulate ? to_f(*g) + v : v);
   }
 }
 

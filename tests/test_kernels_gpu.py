@@ -520,6 +520,9 @@ def test_kaug_producers_and_blocks(dt, N):
     P = ops.lora_pack_t(As)
     ops.lora_down_into(xa[:, :K], [P], [0], [K], [0], R, 0.5, xa[:, K:])
     assert torch.equal(xa[:, K:], ops.lora_down(y0, [P], [0], [K], [0], R, 0.5))
+    xp = torch.full((N, K + 64), float("nan"), device=DEV, dtype=dt)      # row padded to 128 B lines
+    ops.lora_down_into(y0, [P], [0], [K], [0], R, 0.5, xp[:, K:])
+    assert torch.equal(xp[:, K:K + R], xa[:, K:]) and (xp[:, K + R:] == 0).all()
     gu = torch.randn(N, 2 * F, device=DEV).to(dt)
     xd = torch.full((N, F + R), float("nan"), device=DEV, dtype=dt)
     ops.swiglu_fwd_into(gu, xd[:, :F])

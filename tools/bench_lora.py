@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """LoRA kernel micro-benchmark (GPU): csrc/lora.hip ops at the Llama-3.2-1B LoRA shapes
-(N = 4096 tokens, rank 16) with their HBM-roofline time, so each kernel's efficiency is read
+(N = 38,400 tokens, rank 16) with their HBM-roofline time, so each kernel's efficiency is read
 off directly.  Usage: python tools/bench_lora.py [--tokens 4096] [--rank 16] [--iters 50]"""
 import argparse
 import json
@@ -30,7 +30,7 @@ def timeit(fn, iters):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--tokens", type=int, default=4096)
+    ap.add_argument("--tokens", type=int, default=38400, help="default: the LoRA preset's ~38k tokens per step")
     ap.add_argument("--rank", type=int, default=16)
     ap.add_argument("--iters", type=int, default=50)
     a = ap.parse_args()
@@ -54,12 +54,18 @@ def main():
         dx = torch.empty(N, K, device="cuda", dtype=dt)
         gB = [torch.empty(r, o, device="cuda", dtype=dt) for o in outs]
         gA = [torch.empty(K, r, device="cuda", dtype=dt) for _ in outs]
+        Rp = -(-(K + R) // 64) * 64 - K                        # rows padded to 128-B lines (FusedLinear._kaug_pad)
+        xa = torch.randn(N, K + Rp, device="cuda", dtype=dt)    # K-augmented [x | s t | 0] / [dx_W | u | 0]
         res = {"group": name, "N_K_M": [N, K, M]}
         cases = {
             "down_fwd": (lambda: ops.lora_down(x, [P], [0], [K], [0], R), N * K * 2),
             "down_bwd": (lambda: ops.lora_down(dy, Bs, c0, outs, offs, R), N * M * 2),
             "up_fwd": (lambda: ops.lora_up_(y, t, Bs, c0, offs, 2.0), N * M * 2),
             "up_bwd": (lambda: ops.lora_up_(dx, u, [P], [0], [0], 2.0), N * K * 2),
+            "down_fwd_kaug": (lambda: ops.lora_down_into(xa[:, :K], [P], [0], [K], [0], R, 2.0, xa[:, K:]), N * K * 2),
+            "up_bwd_kaug": (lambda: ops.lora_up_(dx, xa[:, K:K + R], [P], [0], [0], 2.0, base=xa[:, :K]), 2 * N * K * 2),
+            "wgrad_A_kaug": (lambda: ops.lora_wgrad(xa[:, K:K + R], xa[:, :K], [g.t() for g in gA], offs, [0] * len(outs),
+                                                    2.0), N * K * 2),
             "wgrad_B": (lambda: ops.lora_wgrad(t, dy, gB, offs, c0, 2.0), N * M * 2),
             "wgrad_A": (lambda: ops.lora_wgrad(u, x, [g.t() for g in gA], offs, [0] * len(outs), 2.0), N * K * 2),
         }
@@ -68,7 +74,7 @@ def main():
             res[k] = {"us": round(us, 1), "roofline_us": round(nbytes / HBM * 1e6, 1),
                       "TB/s": round(nbytes / us / 1e6, 2)}
         print(json.dumps(res), flush=True)
-        del x, dy, y, dx, t, u
+        del x, dy, y, dx, t, u, xa
         torch.cuda.empty_cache()
 
 

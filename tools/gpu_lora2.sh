@@ -1,0 +1,13 @@
+# LoRA kernels after the aligned K-augmentation + merged dA: tests, micro-bench, preset A/B, breakdown.
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"; export TMPDIR=/tmp; mkdir -p gpurun_out/l2
+timeout -k 10 400 python -u -m pytest tests/test_kernels_gpu.py tests/test_model_gpu.py -x -q --timeout 200 --timeout-method thread -p no:cacheprovider -k "kaug or lora" > gpurun_out/l2/tests.log 2>&1 || { echo "tests rc=$?"; tail -30 gpurun_out/l2/tests.log; exit 3; }
+tail -2 gpurun_out/l2/tests.log
+timeout -k 10 200 python tools/bench_lora.py --iters 20 > gpurun_out/l2/bench_lora.jsonl 2>&1 || exit 4
+for i in 1 2; do
+timeout -k 10 300 python -u bench.py --preset llama32_1b_lora_alpaca --steps 10 --warmup 3 > gpurun_out/l2/lora_kaug_$i.log 2>&1 || exit 5
+BLLM_LORA_KAUG=0 timeout -k 10 300 python -u bench.py --preset llama32_1b_lora_alpaca --steps 10 --warmup 3 > gpurun_out/l2/lora_nokaug_$i.log 2>&1 || exit 6
+done
+grep -o '"value": [0-9.]*' gpurun_out/l2/lora_*.log
+python tools/gpu_job.py prof --set preset=llama32_1b_lora_alpaca --set kgrep=lora --tag l2_prof > /dev/null 2>&1 || exit 7
+cat gpurun_out/l2_prof/kstats.log; head -20 gpurun_out/l2_prof/breakdown.log
