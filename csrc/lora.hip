@@ -185,18 +185,6 @@ __global__ __launch_bounds__(256) void lora_up_k(LoraUpArgs a, int rows, int N) 
     for (int rt = 0; rt < rows / 64; ++rt) {
       const long row0 = (long)blockIdx.x * rows + rt * 64 + wave * 16;
       if (row0 >= N) break;  // wave-uniform: this wave's remaining tiles are past the tokens
-      // the tile's base (or, for a later rank pass, y) rows are loaded first, so their HBM
-      // latency runs under the MFMAs and the LDS re-layout instead of in front of the stores
-      VecN<T, 8> bs[4];
-      const T* bsrc = j0 ? (const T*)a.y : (const T*)a.base;
-      const long bld = j0 ? a.ldy : a.ldb;
-      if (bsrc && col_ok) {
-#pragma unroll
-        for (int p = 0; p < 4; ++p) {
-          const int row = (lane >> 4) + 4 * p;
-          if (row0 + row < N) bs[p] = ldv<T, 8>(bsrc + (row0 + row) * bld + a.c0[m] + cb + c8);
-        }
-      }
       const long tr = row0 + (lane & 15) < N ? row0 + (lane & 15) : N - 1;
       const T* t = (const T*)a.t + tr * a.ldt + a.toff[m] + j0;
       f32x4 acc[8];
@@ -226,11 +214,15 @@ __global__ __launch_bounds__(256) void lora_up_k(LoraUpArgs a, int rows, int N) 
         const f32x4 v0 = *reinterpret_cast<const f32x4*>(&ep[row * EP + c8]);
         const f32x4 v1 = *reinterpret_cast<const f32x4*>(&ep[row * EP + c8 + 4]);
         const float v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
-        VecN<T, 8> o;
+        VecN<T, 8> bs, o;
+        if (a.base) bs = ldv<T, 8>((const T*)a.base + (row0 + row) * a.ldb + a.c0[m] + cb + c8);
+        if (j0) {  // later rank pass: accumulate onto what the first pass wrote
+          bs = ldv<T, 8>((const T*)a.y + g);
+        }
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
           float z = a.scale * v[i];
-          if (bsrc) z += to_f(bs[p].v[i]);
+          if (a.base || j0) z += to_f(bs.v[i]);
           if (bias && !j0) z += to_f(bb.v[i]);
           o.v[i] = from_f<T>(z);
         }
