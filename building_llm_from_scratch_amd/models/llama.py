@@ -347,32 +347,56 @@ class HeadComputeMixin:
     def _fused_ok(self, h) -> bool:
         return not self.head.has_lora and self.head.b_params is None
 
+    def _head_padded(self, W: torch.Tensor):
+        """W with its rows padded to a multiple of 256 (zero rows), or W itself when V already is
+        one.  GPT-2's V = 50,257 gives odd-leading-dimension logits, on which hipBLASLt falls back
+        to slower non-K-contiguous kernels (2.2-2.6 ms per 16k-token chunk, 0.8-1 PF); the padded
+        vocabulary keeps every head GEMM on the tile-aligned kernels and our dW kernel.  The buffer
+        is kept across steps (its pad rows are zeroed once); the V real rows are re-copied per
+        call: the optimizer moves them."""
+        V, d = W.shape
+        Vp = -(-V // 256) * 256
+        if Vp == V or not W.is_cuda:
+            return W
+        buf = getattr(self, "_wpad_buf", None)
+        if buf is None or buf.shape != (Vp, d) or buf.dtype != W.dtype or buf.device != W.device:
+            buf = self._wpad_buf = torch.zeros(Vp, d, dtype=W.dtype, device=W.device)
+        buf[:V].copy_(W)
+        return buf
+
     def _fused_loss(self, x2d, h, ns, targets, nvalid):
         W = self.head.W()                                          # [V, d]
         N, V = h.shape[0], W.shape[0]
-        rows = max(MIN_CHUNK_ROWS, LOGIT_CHUNK_BYTES // (V * h.element_size()) // MIN_CHUNK_ROWS * MIN_CHUNK_ROWS)
-        gW = None
+        Wp = self._head_padded(W)                                  # [Vp, d], rows >= V zero
+        Vp = Wp.shape[0]
+        rows = max(MIN_CHUNK_ROWS, LOGIT_CHUNK_BYTES // (Vp * h.element_size()) // MIN_CHUNK_ROWS * MIN_CHUNK_ROWS)
+        gW = gWp = None
         if self.head.unit.trainable(self.head.W_params[0]):
             gW = torch.empty(W.shape, dtype=self.head.unit.train.grad.dtype, device=W.device)
+            gWp = gW if Vp == V else torch.empty(Wp.shape, dtype=gW.dtype, device=W.device)
         dh = torch.empty_like(h)
-        Wd = W
-        if _dgrad_wt_ok(h[:rows], W):   # one K-contiguous copy of W for every chunk's dX GEMM
-            Wd = ops.transpose2d(W).t()
+        Wd = Wp
+        if _dgrad_wt_ok(h[:rows], Wp):   # one K-contiguous copy of W for every chunk's dX GEMM
+            Wd = ops.transpose2d(Wp).t()
         scale = (self.rctx.loss_scale / nvalid).reshape(1)
         total = torch.zeros(1, dtype=torch.float32, device=h.device)
         for s0 in range(0, N, rows):
             hc, tc = h[s0:s0 + rows], targets[s0:s0 + rows]
-            logits = mm_nt(hc, W)
-            lrow, lse = ops.ce_fwd(logits, tc, self.ignore_index)
+            logits = mm_nt(hc, Wp)                                 # [rows, Vp]; columns >= V are 0
+            lv = logits[:, :V]
+            lrow, lse = ops.ce_fwd(lv, tc, self.ignore_index)
             total += lrow.sum()
-            dl = ops.ce_bwd_(logits, tc, lse, scale, self.ignore_index)   # in place
-            if Wd is not W:
+            ops.ce_bwd_(lv, tc, lse, scale, self.ignore_index)    # in place; the zero pad stays
+            dl = logits
+            if Wd is not Wp:
                 mm_nt(dl, Wd.t(), out=dh[s0:s0 + rows])                   # dh = dl . W (W^T copy)
             else:
                 torch.mm(dl, Wd, out=dh[s0:s0 + rows])
-            if gW is not None:
-                _weight_grad(dl, hc, gW, accumulate=s0 > 0)
-            del logits, dl
+            if gWp is not None:
+                _weight_grad(dl, hc, gWp, accumulate=s0 > 0)
+            del logits, dl, lv
+        if gWp is not None and gWp is not gW:
+            gW.copy_(gWp[:V])
         return total[0] / nvalid, (x2d, ns, dh, gW, [], self.rctx.loss_scale, "fused")
 
     def _fused_lora_ok(self) -> bool:

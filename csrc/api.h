@@ -93,9 +93,9 @@ void attn_decode(DType dt, const void* q, const void* kc, const void* vc, void* 
                  int Tmax, int L, hipStream_t s);
 
 // loss.hip
-void ce_fwd(DType dt, const void* logits, const int64_t* tgt, float* loss, float* lse, long N, long V,
+void ce_fwd(DType dt, const void* logits, const int64_t* tgt, float* loss, float* lse, long N, long V, long ld,
             long ignore_index, hipStream_t s);
-void ce_bwd(DType dt, void* logits, const int64_t* tgt, const float* lse, const float* scale, long N, long V,
+void ce_bwd(DType dt, void* logits, const int64_t* tgt, const float* lse, const float* scale, long N, long V, long ld,
             long ignore_index, hipStream_t s);
 
 // embedding.hip

@@ -573,26 +573,33 @@ Tensor flash_attn_bwd(const Tensor& qkv, const Tensor& o, const Tensor& lse, con
 }
 
 // ------------------------------------------------------------------ loss
+// logits may be a row-strided view (unit stride within a row): the vocabulary padded to whole
+// GEMM tiles in the fused head, CE over the first V columns
+static void check_logits(const Tensor& logits) {
+  TORCH_CHECK(logits.is_cuda() && logits.dim() == 2 && logits.stride(1) == 1 && logits.stride(0) >= logits.size(1),
+              "bllm ce: logits must be a 2-D GPU tensor with unit-stride rows");
+}
+
 std::tuple<Tensor, Tensor> ce_fwd(const Tensor& logits, const Tensor& targets, int64_t ignore_index) {
-  check_gpu(logits, "logits"); check_gpu(targets, "targets");
+  check_logits(logits); check_gpu(targets, "targets");
   c10::DeviceGuard g(logits.device());
-  TORCH_CHECK(logits.dim() == 2 && targets.dim() == 1 && targets.size(0) == logits.size(0));
+  TORCH_CHECK(targets.dim() == 1 && targets.size(0) == logits.size(0));
   TORCH_CHECK(targets.scalar_type() == at::kLong);
   const int64_t N = logits.size(0), V = logits.size(1);
   auto loss = at::empty({N}, logits.options().dtype(at::kFloat));
   auto lse = at::empty({N}, logits.options().dtype(at::kFloat));
   bllm::ce_fwd(dt_of(logits), logits.data_ptr(), targets.data_ptr<int64_t>(), loss.data_ptr<float>(),
-               lse.data_ptr<float>(), N, V, ignore_index, stream());
+               lse.data_ptr<float>(), N, V, logits.stride(0), ignore_index, stream());
   return {loss, lse};
 }
 
 void ce_bwd_(Tensor& logits, const Tensor& targets, const Tensor& lse, const Tensor& scale, int64_t ignore_index) {
-  check_gpu(logits, "logits"); check_gpu(targets, "targets"); check_gpu(lse, "lse"); check_gpu(scale, "scale");
+  check_logits(logits); check_gpu(targets, "targets"); check_gpu(lse, "lse"); check_gpu(scale, "scale");
   c10::DeviceGuard g(logits.device());
   TORCH_CHECK(scale.scalar_type() == at::kFloat && scale.numel() >= 1);
   const int64_t N = logits.size(0), V = logits.size(1);
   bllm::ce_bwd(dt_of(logits), logits.data_ptr(), targets.data_ptr<int64_t>(), lse.data_ptr<float>(),
-               scale.data_ptr<float>(), N, V, ignore_index, stream());
+               scale.data_ptr<float>(), N, V, logits.stride(0), ignore_index, stream());
 }
 
 // ------------------------------------------------------------------ embedding

@@ -26,11 +26,11 @@ __device__ __forceinline__ void online_add(float x, float& m, float& s) {
 template <typename T>
 __global__ __launch_bounds__(256) void ce_fwd_k(const T* __restrict__ logits, const int64_t* __restrict__ tgt,
                                                 float* __restrict__ loss, float* __restrict__ lse_out, long V,
-                                                long ignore_index) {
+                                                long ld, long ignore_index) {
   constexpr int VEC = 16 / sizeof(T);
   __shared__ float sm[4], ss[4];
   const long row = blockIdx.x;
-  const T* p = logits + row * V;
+  const T* p = logits + row * ld;
   const int mis = (int)(((uintptr_t)p / sizeof(T)) % VEC);
   const long head = mis ? (long)(VEC - mis) < V ? (VEC - mis) : V : 0;
   const long nv = (V - head) / VEC;
@@ -81,10 +81,10 @@ __global__ __launch_bounds__(256) void ce_fwd_k(const T* __restrict__ logits, co
 template <typename T>
 __global__ __launch_bounds__(256) void ce_bwd_k(T* __restrict__ logits, const int64_t* __restrict__ tgt,
                                                 const float* __restrict__ lse, const float* __restrict__ scale_p,
-                                                long V, long ignore_index) {
+                                                long V, long ld, long ignore_index) {
   constexpr int VEC = 16 / sizeof(T);
   const long row = blockIdx.x;
-  T* p = logits + row * V;
+  T* p = logits + row * ld;
   const long t = tgt[row];
   const bool valid = t != ignore_index;
   const float sc = valid ? scale_p[0] : 0.f;
@@ -109,16 +109,17 @@ __global__ __launch_bounds__(256) void ce_bwd_k(T* __restrict__ logits, const in
   for (long i = tail0 + threadIdx.x; i < V; i += 256) p[i] = from_f<T>(__expf(to_f(p[i]) - l) * sc - (i == t ? sc : 0.f));
 }
 
-void ce_fwd(DType dt, const void* logits, const int64_t* tgt, float* loss, float* lse, long N, long V,
+// rows ld elements apart (ld > V: the vocabulary padded to whole GEMM tiles, pad columns untouched)
+void ce_fwd(DType dt, const void* logits, const int64_t* tgt, float* loss, float* lse, long N, long V, long ld,
             long ignore_index, hipStream_t s) {
   BLLM_DISPATCH(dt, T, {
-    hipLaunchKernelGGL(ce_fwd_k<T>, dim3(N), dim3(256), 0, s, (const T*)logits, tgt, loss, lse, V, ignore_index);
+    hipLaunchKernelGGL(ce_fwd_k<T>, dim3(N), dim3(256), 0, s, (const T*)logits, tgt, loss, lse, V, ld, ignore_index);
   });
 }
-void ce_bwd(DType dt, void* logits, const int64_t* tgt, const float* lse, const float* scale, long N, long V,
+void ce_bwd(DType dt, void* logits, const int64_t* tgt, const float* lse, const float* scale, long N, long V, long ld,
             long ignore_index, hipStream_t s) {
   BLLM_DISPATCH(dt, T, {
-    hipLaunchKernelGGL(ce_bwd_k<T>, dim3(N), dim3(256), 0, s, (T*)logits, tgt, lse, scale, V, ignore_index);
+    hipLaunchKernelGGL(ce_bwd_k<T>, dim3(N), dim3(256), 0, s, (T*)logits, tgt, lse, scale, V, ld, ignore_index);
   });
 }
 
