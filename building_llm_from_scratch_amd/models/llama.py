@@ -399,76 +399,91 @@ class HeadComputeMixin:
             gW.copy_(gWp[:V])
         return total[0] / nvalid, (x2d, ns, dh, gW, [], self.rctx.loss_scale, "fused")
 
-    def _fused_lora_ok(self) -> bool:
+    def _fused_lora_ok(self, h) -> bool:
         hd = self.head
-        return (hd.has_lora and len(hd.specs) == 1 and hd.b_params is None
-                and not hd.unit.trainable(hd.W_params[0]))
+        if not (hd.has_lora and len(hd.specs) == 1 and hd.b_params is None
+                and not hd.unit.trainable(hd.W_params[0])):
+            return False
+        # on the GPU the rank-r parts run on csrc/lora.hip (rank % 16 <= 64, widths % 32)
+        spec = hd.specs[0]
+        return not h.is_cuda or ops.lora_kernel_ok_dims(h.device, h.dtype, [spec.lora_A.shape[1]],
+                                                        [h.shape[1], spec.out_features])
 
-    def _waug(self, W, Bm):
-        """[W | B^T] ([V, d + r]) in a buffer kept across steps; both parts re-copied per call
-        (FSDP may re-materialise W, the optimizer moves B): ~0.2 ms for the Llama-3.2-1B head."""
+    def _waug(self, W, Bm, rp: int):
+        """[W | B^T | 0] ([V, d + rp], rp >= r pads a row to whole 128-byte lines) in a buffer kept
+        across steps; W and B^T re-copied per call (FSDP may re-materialise W, the optimizer moves
+        B), the pad columns zeroed once."""
         V, d = W.shape
         r = Bm.shape[0]
         buf = getattr(self, "_waug_buf", None)
-        if buf is None or buf.shape != (V, d + r) or buf.dtype != W.dtype or buf.device != W.device:
-            buf = self._waug_buf = torch.empty(V, d + r, dtype=W.dtype, device=W.device)
+        if buf is None or buf.shape != (V, d + rp) or buf.dtype != W.dtype or buf.device != W.device:
+            buf = self._waug_buf = torch.zeros(V, d + rp, dtype=W.dtype, device=W.device)
         buf[:, :d].copy_(W)
-        buf[:, d:].copy_(Bm.t())
+        buf[:, d:d + r].copy_(Bm.t())
         return buf
 
     def _fused_lora_loss(self, x2d, h, ns, targets, nvalid):
         """LoRA head (the reference's replace_linear_with_lora also wraps the output head; its
         base weight is frozen) on the same chunked head + CE, with the rank-r path folded into
         the head GEMMs by augmenting K (t = h A, s = alpha / r):
-            logits         = [h | s t] . [W | B^T]^T
-            [dh_W | dl B^T] = dl . [W | B^T]
+            logits              = [h | s t | 0] . [W | B^T | 0]^T
+            [dh_W | dl B^T | 0] = dl . [W | B^T | 0]
         one GEMM each per chunk instead of a separate s t B pass over the [N, V] logits plus a
-        beta = 1 GEMM, and a separate dl B^T pass over dlogits (Llama-3.2-1B Alpaca: ~2 ms of
-        a 75 ms step)."""
+        beta = 1 GEMM, and a separate dl B^T pass over dlogits.  The rows are padded to whole
+        128-byte lines; s t, dB = (s t)^T dl, dA = s h^T (dl B^T) and dh += s (dl B^T) A^T run on
+        the LoRA kernels (csrc/lora.hip), dB straight from each chunk's dlogits."""
         hd, u = self.head, self.head.unit
         spec = hd.specs[0]
         A, Bm, sc = u.data(spec.lora_A), u.data(spec.lora_B), float(spec.scaling)   # [d, r], [r, V]
         W = hd.W()
         N, d = h.shape
         V, r = W.shape[0], A.shape[1]
-        Wa = self._waug(W, Bm)
-        t = torch.mm(h, A)                                                  # [N, r]
-        ha = torch.empty(N, d + r, dtype=h.dtype, device=h.device)
+        rp = -(-(d + r) // 64) * 64 - d
+        Wa = self._waug(W, Bm, rp)
+        P = ops.lora_pack_t([A])                                            # A^T [r, d]
+        ha = torch.empty(N, d + rp, dtype=h.dtype, device=h.device)
         ha[:, :d].copy_(h)
-        ha[:, d:].copy_(t * sc)
+        ops.lora_down_into(h, [P], [0], [d], [0], r, sc, ha[:, d:])         # [s h A | 0]
+        st = ha[:, d:d + r]
         rows = max(MIN_CHUNK_ROWS, LOGIT_CHUNK_BYTES // (V * h.element_size()) // MIN_CHUNK_ROWS * MIN_CHUNK_ROWS)
         Wd = Wa
         if _dgrad_wt_ok(ha[:rows], Wa):
             Wd = ops.transpose2d(Wa).t()
         dha = torch.empty_like(ha)
         # (grad views only exist in backward: FSDP allocates the full gradient in pre_backward)
-        gB = torch.zeros(r, V, dtype=torch.float32, device=h.device) if u.trainable(spec.lora_B) else None
+        gB = torch.empty(r, V, dtype=torch.float32, device=h.device) if u.trainable(spec.lora_B) else None
         scale = (self.rctx.loss_scale / nvalid).reshape(1)
         total = torch.zeros(1, dtype=torch.float32, device=h.device)
         for s0 in range(0, N, rows):
             hc, tc = ha[s0:s0 + rows], targets[s0:s0 + rows]
-            logits = torch.mm(hc, Wa.t())
+            logits = mm_nt(hc, Wa)
             lrow, lse = ops.ce_fwd(logits, tc, self.ignore_index)
             total += lrow.sum()
             dl = ops.ce_bwd_(logits, tc, lse, scale, self.ignore_index)   # in place
-            torch.mm(dl, Wd, out=dha[s0:s0 + rows])
-            if gB is not None:                                            # dB = s t^T dl
-                gB += torch.mm(t[s0:s0 + rows].t(), dl).float().mul_(sc)
+            if Wd is not Wa:
+                mm_nt(dl, Wd.t(), out=dha[s0:s0 + rows])
+            else:
+                torch.mm(dl, Wd, out=dha[s0:s0 + rows])
+            if gB is not None:                                            # dB = (s t)^T dl
+                ops.lora_wgrad(st[s0:s0 + rows], dl, [gB], [0], [0], 1.0, accumulate=s0 > 0)
             del logits, dl
-        ub = dha[:, d:]                                                   # dl B^T
-        dh = torch.addmm(dha[:, :d], ub, A.t(), alpha=sc)                 # + s (dl B^T) A^T
+        ub = dha[:, d:d + r]                                              # dl B^T
+        dh = torch.empty_like(h)
+        ops.lora_up_(dh, ub, [P], [0], [0], sc, base=dha[:, :d])          # dh_W + s (dl B^T) A^T
         lora = []
         if gB is not None:
             lora.append((spec.lora_B, gB))
         if u.trainable(spec.lora_A):                                      # dA = s h^T (dl B^T)
-            lora.append((spec.lora_A, torch.mm(h.t(), ub).float().mul_(sc)))
+            gA = torch.empty(d, r, dtype=torch.float32, device=h.device)
+            ops.lora_wgrad(ub, h, [gA.t()], [0], [0], sc)
+            lora.append((spec.lora_A, gA))
         del dha, ha
         return total[0] / nvalid, (x2d, ns, dh, None, lora, self.rctx.loss_scale, "fused")
 
     def forward_loss(self, x, targets, save):
         x2d = x.reshape(-1, x.shape[-1])
         h, ns = self._norm_fwd(x2d)
-        if save and (self._fused_ok(h) or self._fused_lora_ok()):
+        if save and (self._fused_ok(h) or self._fused_lora_ok(h)):
             nvalid = (targets != self.ignore_index).sum().to(torch.float32).clamp_(min=1.0)
             if not self._fused_ok(h):
                 return self._fused_lora_loss(x2d, h, ns, targets, nvalid)

@@ -165,7 +165,7 @@ def test_fused_chunked_lora_head(family, monkeypatch):
             torch.nn.init.normal_(mod.B, std=0.05)
     m.flatten()
     head = m.computes[-1]
-    assert head._fused_lora_ok()
+    assert head._fused_lora_ok(torch.empty(1, cfg.emb_dim))
     idx = torch.randint(0, cfg.vocab_size, (3, 13))
     tgt = torch.randint(0, cfg.vocab_size, (3, 13))
     tgt[1, :5] = -100
