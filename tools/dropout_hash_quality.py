@@ -1,0 +1,32 @@
+#!/usr/bin/env python3
+"""Statistical check of candidate dropout hashes over the attention index pattern (keep
+fraction, keep correlation along keys and rows, 16-bit value histogram): the shipped 2-multiply
+lowbias32 vs a 1-multiply round.  CPU only; run: python tools/dropout_hash_quality.py"""
+import numpy as np
+M=0xFFFFFFFF
+def lowbias32(x):
+    x = x & M; x ^= x >> 16; x = (x * 0x7FEB352D) & M; x ^= x >> 15; x = (x * 0x846CA68B) & M; x ^= x >> 16; return x
+def one_round(x):
+    x = x & M; x ^= x >> 16; x = (x * 0x7FEB352D) & M; x ^= x >> 15; return x
+def seedmix(seed, hi): return lowbias32(np.uint64(seed) + np.uint64((hi * 0x9E3779B9) & M))
+thr = int(round(0.1*65536))
+T=1024
+for name,f in (("lowbias32",lowbias32),("1-round",one_round)):
+    seed=1234567
+    s = np.uint64(seedmix(seed, 0))
+    # a [rows x T] causal-ish block of elements: element e = row*T + k, pair e>>1
+    rows=512
+    e = (np.arange(rows, dtype=np.uint64)[:,None]*np.uint64(T) + np.arange(T, dtype=np.uint64)[None,:]) + np.uint64(7*T*T)
+    pair = e >> np.uint64(1)
+    h = f((pair & np.uint64(M)) ^ s)
+    bits = np.where((e & np.uint64(1)) == 1, h >> np.uint64(16), h & np.uint64(0xFFFF))
+    keep = (bits >= thr).astype(np.float64)
+    p = 1 - keep.mean()
+    kc = keep - keep.mean()
+    def corr(a,b): return float((a*b).mean()/np.sqrt((a*a).mean()*(b*b).mean()))
+    lags = [corr(kc[:, :-L], kc[:, L:]) for L in (1,2,3,4,8,16,64)]
+    rowc = [corr(kc[:-L], kc[L:]) for L in (1,2,4)]
+    # chi-square of 16-bit value histogram in 256 bins
+    hist = np.bincount((bits >> np.uint64(8)).astype(np.int64).ravel(), minlength=256)
+    exp = bits.size/256; chi = float(((hist-exp)**2/exp).sum())
+    print(f"{name}: drop frac {p:.5f} (target {thr/65536:.5f}), key-lag corr {[round(x,4) for x in lags]}, row-lag corr {[round(x,4) for x in rowc]}, chi2(255 dof) {chi:.0f}")
