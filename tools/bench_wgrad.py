@@ -18,7 +18,8 @@ SHAPES = {
     "llama3_8b": [("qkv", 6144, 4096), ("o", 4096, 4096), ("gate_up", 28672, 4096), ("down", 4096, 14336),
                   ("head", 128256, 4096)],
     "llama32_1b": [("qkv", 3072, 2048), ("o", 2048, 2048), ("gate_up", 16384, 2048), ("down", 2048, 8192)],
-    "gpt2_774m": [("qkv", 3840, 1280), ("o", 1280, 1280), ("fc1", 5120, 1280), ("fc2", 1280, 5120)],
+    "gpt2_774m": [("qkv", 3840, 1280), ("o", 1280, 1280), ("fc1", 5120, 1280), ("fc2", 1280, 5120),
+                  ("head_padded", 50432, 1280)],
 }
 
 
