@@ -425,16 +425,16 @@ class HeadComputeMixin:
     def _fused_lora_loss(self, x2d, h, ns, targets, nvalid):
         """LoRA head (the reference's replace_linear_with_lora also wraps the output head; its
         base weight is frozen) on the same chunked head + CE, with the rank-r path folded into
-        the head GEMMs by augmenting K (t = h A, s = alpha / r):
-            logits              = [h | s t | 0] . [W | B^T | 0]^T
-            [dh_W | dl B^T | 0] = dl . [W | B^T | 0]
-        one GEMM each per chunk instead of a separate s t B pass over the [N, V] logits plus a
-        beta = 1 GEMM, and a separate dl B^T pass over dlogits.  The rows are padded to whole
-        128-byte lines; s t, dB = (s t)^T dl, dA = s h^T (dl B^T) and dh += s (dl B^T) A^T run on
-        the LoRA kernels (csrc/lora.hip), dB straight from each chunk's dlogits."""
-        hd, u = self.head, self.head.unit
+        the logits GEMM by augmenting K (t = h A, s = alpha / r):
+            logits = [h | s t | 0] . [W | B^T | 0]^T          (rows padded to 128-byte lines)
+        one GEMM per chunk instead of a separate s t B pass over the [N, V] logits plus a beta = 1
+        GEMM.  The dX GEMM stays at the base width, dh_W = dl . W on the cached K-contiguous W^T
+        (an augmented [N, d + r] output made hipBLASLt fall back from 1.64 to 0.66-0.75 PF at
+        V = 128k, tools/bench_head_k.py); u = dl B^T and dB = (s t)^T dl run on the LoRA kernels
+        over each dlogits chunk, then dh = dh_W + s u A^T and dA = s h^T u."""
+        hd, u_ = self.head, self.head.unit
         spec = hd.specs[0]
-        A, Bm, sc = u.data(spec.lora_A), u.data(spec.lora_B), float(spec.scaling)   # [d, r], [r, V]
+        A, Bm, sc = u_.data(spec.lora_A), u_.data(spec.lora_B), float(spec.scaling)   # [d, r], [r, V]
         W = hd.W()
         N, d = h.shape
         V, r = W.shape[0], A.shape[1]
@@ -446,12 +446,17 @@ class HeadComputeMixin:
         ops.lora_down_into(h, [P], [0], [d], [0], r, sc, ha[:, d:])         # [s h A | 0]
         st = ha[:, d:d + r]
         rows = max(MIN_CHUNK_ROWS, LOGIT_CHUNK_BYTES // (V * h.element_size()) // MIN_CHUNK_ROWS * MIN_CHUNK_ROWS)
-        Wd = Wa
-        if _dgrad_wt_ok(ha[:rows], Wa):
-            Wd = ops.transpose2d(Wa).t()
-        dha = torch.empty_like(ha)
+        Wd = W
+        if _dgrad_wt_ok(h[:rows], W):    # frozen: the K-contiguous W^T copy is kept across steps
+            key = (W.data_ptr(), W._version, W.shape, W.dtype)
+            cached = getattr(self, "_wt_cache", None)
+            if cached is None or cached[0] != key:
+                cached = self._wt_cache = (key, ops.transpose2d(W))
+            Wd = cached[1].t()
+        dh = torch.empty_like(h)
+        ub = torch.empty(N, r, dtype=h.dtype, device=h.device)
         # (grad views only exist in backward: FSDP allocates the full gradient in pre_backward)
-        gB = torch.empty(r, V, dtype=torch.float32, device=h.device) if u.trainable(spec.lora_B) else None
+        gB = torch.empty(r, V, dtype=torch.float32, device=h.device) if u_.trainable(spec.lora_B) else None
         scale = (self.rctx.loss_scale / nvalid).reshape(1)
         total = torch.zeros(1, dtype=torch.float32, device=h.device)
         for s0 in range(0, N, rows):
@@ -460,24 +465,23 @@ class HeadComputeMixin:
             lrow, lse = ops.ce_fwd(logits, tc, self.ignore_index)
             total += lrow.sum()
             dl = ops.ce_bwd_(logits, tc, lse, scale, self.ignore_index)   # in place
-            if Wd is not Wa:
-                mm_nt(dl, Wd.t(), out=dha[s0:s0 + rows])
+            if Wd is not W:
+                mm_nt(dl, Wd.t(), out=dh[s0:s0 + rows])                   # dh_W = dl . W
             else:
-                torch.mm(dl, Wd, out=dha[s0:s0 + rows])
+                torch.mm(dl, Wd, out=dh[s0:s0 + rows])
+            ops.lora_down_into(dl, [Bm], [0], [V], [0], r, 1.0, ub[s0:s0 + rows])   # u = dl B^T
             if gB is not None:                                            # dB = (s t)^T dl
                 ops.lora_wgrad(st[s0:s0 + rows], dl, [gB], [0], [0], 1.0, accumulate=s0 > 0)
             del logits, dl
-        ub = dha[:, d:d + r]                                              # dl B^T
-        dh = torch.empty_like(h)
-        ops.lora_up_(dh, ub, [P], [0], [0], sc, base=dha[:, :d])          # dh_W + s (dl B^T) A^T
+        ops.lora_up_(dh, ub, [P], [0], [0], sc, base=dh)                  # dh_W + s u A^T
         lora = []
         if gB is not None:
             lora.append((spec.lora_B, gB))
-        if u.trainable(spec.lora_A):                                      # dA = s h^T (dl B^T)
+        if u_.trainable(spec.lora_A):                                     # dA = s h^T u
             gA = torch.empty(d, r, dtype=torch.float32, device=h.device)
             ops.lora_wgrad(ub, h, [gA.t()], [0], [0], sc)
             lora.append((spec.lora_A, gA))
-        del dha, ha
+        del ha
         return total[0] / nvalid, (x2d, ns, dh, None, lora, self.rctx.loss_scale, "fused")
 
     def forward_loss(self, x, targets, save):
