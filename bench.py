@@ -75,7 +75,8 @@ PEAK_BF16 = 2.5e15
 # the frozen GEMMs need the larger M); Llama-3-8B's 40 is the planner-checked headline batch.
 PRESETS = {
     "llama3_8b_fsdp": dict(model="llama3", num_params="8B", parallel="fsdp", actv_ckpt="auto", batch_size=40,
-                           data="pretrain", mixed_precision=None, lora_rank=0),
+                           data="pretrain", mixed_precision=None, lora_rank=0,
+                           tunableop="configs/tunableop_llama3_8b_b40_mi355x.csv"),
     "gpt2_774m_ddp": dict(model="GPT2", num_params="774M", parallel="ddp", actv_ckpt="none", batch_size=64,
                           data="pretrain", mixed_precision=None, lora_rank=0),
     "llama32_1b_lora_alpaca": dict(model="llama3_2", num_params="1B", parallel="ddp", actv_ckpt="none",
@@ -136,8 +137,9 @@ def parse(argv=None):
                          "the results CSV here (a tuning run, not a measurement)")
     ap.add_argument("--tunableop", default=None,
                     help="PyTorch TunableOp results CSV (every hipBLASLt + rocBLAS solution timed per GEMM "
-                         "shape), e.g. configs/tunableop_llama3_8b_b40_mi355x.csv: +0.6 %% on the headline "
-                         "(profiles/r2_tunableop_*.log); read-only, shapes not in the file keep the heuristic")
+                         "shape); the headline preset uses configs/tunableop_llama3_8b_b40_mi355x.csv (+0.3 %% "
+                         "same box, profiles/r4/lora_kaug_ab/hl_*.log); read-only: shapes not in the file, "
+                         "or a file whose library versions do not match, keep hipBLASLt's heuristic; 'none' = off")
     a = ap.parse_args(argv)
     for k, v in PRESETS[a.preset].items():
         if getattr(a, k, None) is None:
@@ -322,6 +324,12 @@ def main(argv=None):
     if a.tunableop_tune:
         os.environ.update(PYTORCH_TUNABLEOP_ENABLED="1", PYTORCH_TUNABLEOP_TUNING="1",
                           PYTORCH_TUNABLEOP_FILENAME=os.path.abspath(a.tunableop_tune).replace(".csv", "%d.csv"))
+    if a.tunableop in ("none", ""):
+        a.tunableop = None
+    if a.tunableop and not os.path.isabs(a.tunableop):
+        a.tunableop = os.path.join(os.path.dirname(os.path.abspath(__file__)), a.tunableop)
+    if a.tunableop and (a.device != "cuda" or not os.path.exists(a.tunableop)):
+        a.tunableop = None
     if a.tunableop:  # must be set before the first GEMM; TunableOp reads <name><device ordinal>.csv
         import tempfile
         d = tempfile.mkdtemp(prefix="bllm_tunableop_")
@@ -544,6 +552,8 @@ def main(argv=None):
                 "mixed_precision": a.mixed_precision,
                 "lora": {"rank": a.lora_rank, "alpha": a.lora_alpha} if a.lora_rank else None,
                 "optimizer": "AdamW fp32 master, wd 0.1, clip 1.0",
+                "gemm_tuning": (os.path.relpath(a.tunableop, os.path.dirname(os.path.abspath(__file__)))
+                                if a.tunableop else None),
             },
             "mfu": round(mfu, 4),
             "hfu": round(mfu * recompute, 4),

@@ -9,12 +9,17 @@ Backward writes ``dW`` / ``db`` / ``dA`` / ``dB`` directly into the unit's flat 
 buffer (``out=`` GEMMs; ``addmm_`` when accumulating micro-batches).
 
 LoRA on the GPU runs on the fused kernels of csrc/lora.hip (reference lora.py:24-26,45-46),
-a fixed number of launches per group however many members it has:
-  fwd  P = [A_1^T; A_2^T; ...] (pack), t = x P^T (lora_down), y[:, cols_m] += s t_m B_m (lora_up)
-  bwd  u_m = dy[:, cols_m] B_m^T (lora_down), dB_m = s t_m^T dy[:, cols_m] and
-       dA_m = s x^T u_m (lora_wgrad, into the flat gradient), dx += s u P (lora_up)
-Groups the kernels cannot take (fp32, ranks not a multiple of 16, odd widths, token counts not
-a multiple of 64 such as single-token decode) use per-member hipBLASLt GEMMs.
+a fixed number of launches per group however many members it has.  Two forms:
+  * K-augmented (frozen, bias-free, unsharded base; ``kaug_input`` / ``forward_kaug``): the
+    producer of x (RMSNorm, SwiGLU) writes it into [x | s t | 0], lora_down adds s t, and ONE
+    GEMM computes y (+ residual) = [x | s t] . [W | Bd^T]^T; the dX GEMM on the cached
+    [W^T ; Bd] returns [dx_W | dy B^T]; dB / dA by lora_wgrad, dx += s u P by lora_up;
+  * grouped (everything else the kernels take):
+      fwd  P = [A_1^T; A_2^T; ...] (pack), t = x P^T (lora_down), y[:, cols_m] += s t_m B_m (lora_up)
+      bwd  u_m = dy[:, cols_m] B_m^T (lora_down), dB_m = s t_m^T dy[:, cols_m] and
+           dA_m = s x^T u_m (lora_wgrad, into the flat gradient), dx += s u P (lora_up)
+Groups the kernels cannot take (fp32, ranks not a multiple of 16, odd widths) use per-member
+hipBLASLt GEMMs.
 """
 from __future__ import annotations
 

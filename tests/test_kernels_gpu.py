@@ -542,8 +542,8 @@ def test_kaug_producers_and_blocks(dt, N):
 
 
 def test_lora_model_uses_kernels_and_matches_gemm_path(monkeypatch):
-    """A LoRA Llama step on the fused kernels gives the same loss / LoRA grads as the
-    per-member hipBLASLt path."""
+    """A LoRA Llama step on the fused kernels (K-augmented QKV / gate-up / down, grouped o, the
+    fused LoRA head: V = 512) gives the same loss / LoRA grads as the per-member hipBLASLt path."""
     from building_llm_from_scratch_amd.config import get_config
     from building_llm_from_scratch_amd.models import build_model, replace_linear_with_lora
     from building_llm_from_scratch_amd.models import linear
@@ -564,6 +564,8 @@ def test_lora_model_uses_kernels_and_matches_gemm_path(monkeypatch):
                 torch.nn.init.normal_(mod.B, std=0.05)
         m.flatten(device=DEV)
         monkeypatch.setattr(ops, "lora_kernel_ok", (lambda *a: True) if use_kernels else (lambda *a: False))
+        if not use_kernels:   # also the zero-copy K-augmented groups and the fused LoRA head
+            monkeypatch.setattr(ops, "lora_kernel_ok_dims", lambda *a: False)
         idx = torch.randint(0, cfg.vocab_size, (2, 128), device=DEV, generator=torch.Generator(DEV).manual_seed(1))
         loss = m(idx, idx)
         loss.backward()
