@@ -78,7 +78,8 @@ PRESETS = {
                            data="pretrain", mixed_precision=None, lora_rank=0,
                            tunableop="configs/tunableop_llama3_8b_b40_mi355x.csv"),
     "gpt2_774m_ddp": dict(model="GPT2", num_params="774M", parallel="ddp", actv_ckpt="none", batch_size=64,
-                          data="pretrain", mixed_precision=None, lora_rank=0),
+                          data="pretrain", mixed_precision=None, lora_rank=0,
+                          tunableop="configs/tunableop_gpt2_774m_b64_mi355x.csv"),
     "llama32_1b_lora_alpaca": dict(model="llama3_2", num_params="1B", parallel="ddp", actv_ckpt="none",
                                    batch_size=96, data="alpaca", mixed_precision=None, lora_rank=16),
     "llama2_7b_fsdp_mp": dict(model="llama2", num_params="7B", parallel="fsdp", actv_ckpt="none", batch_size=24,
@@ -137,8 +138,9 @@ def parse(argv=None):
                          "the results CSV here (a tuning run, not a measurement)")
     ap.add_argument("--tunableop", default=None,
                     help="PyTorch TunableOp results CSV (every hipBLASLt + rocBLAS solution timed per GEMM "
-                         "shape); the headline preset uses configs/tunableop_llama3_8b_b40_mi355x.csv (+0.3 %% "
-                         "same box, profiles/r4/lora_kaug_ab/hl_*.log); read-only: shapes not in the file, "
+                         "shape); the headline and GPT-2 presets use configs/tunableop_*_mi355x.csv (+0.35 %% / "
+                         "+1.25 %% same box, profiles/r4/tunableop_default/, profiles/r4/tunableop_gpt2/); "
+                         "read-only: shapes not in the file, "
                          "or a file whose library versions do not match, keep hipBLASLt's heuristic; 'none' = off")
     a = ap.parse_args(argv)
     for k, v in PRESETS[a.preset].items():
@@ -587,8 +589,8 @@ def main(argv=None):
         if prof is not None:
             out["profile_ms"] = prof
         print(json.dumps(out), flush=True)
-    if a.tunableop_tune and cuda:
-        torch.cuda.tunable.write_file()
+    if a.tunableop_tune and cuda and hasattr(torch.cuda.tunable, "write_file"):
+        torch.cuda.tunable.write_file()     # (newer PyTorch writes the results file at exit itself)
     dist.destroy_process_group()
 
 
