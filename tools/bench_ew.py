@@ -55,7 +55,19 @@ def main():
     ):
         us = _time(fn)
         res[name] = {"us": round(us, 1), "GBps": round(nbytes / us / 1e3, 1)}
-    del f64, dg64, dm64
+    x64 = torch.randn(N64, 1280, device=dev).to(dt)
+    w1 = torch.randn(1280, device=dev).to(dt)
+    b1 = torch.randn(1280, device=dev).to(dt)
+    _, m64, r64 = ops.layernorm_fwd(x64, w1, b1, 1e-5)
+    dw1 = torch.zeros(1280, device=dev, dtype=dt)
+    for name, fn, nbytes in (
+        ("gpt2_b64_layernorm_bwd_1280", lambda: ops.layernorm_bwd(dm64, x64, w1, m64, r64, dm64, dw1, db1, True),
+         4 * N64 * 1280 * 2),
+        ("gpt2_b64_layernorm_fwd_1280", lambda: ops.layernorm_fwd(x64, w1, b1, 1e-5), 2 * N64 * 1280 * 2),
+    ):
+        us = _time(fn)
+        res[name] = {"us": round(us, 1), "GBps": round(nbytes / us / 1e3, 1)}
+    del f64, dg64, dm64, x64
     for name, fn, nbytes in (
         ("swiglu_fwd", lambda: ops.swiglu_fwd(gu), 3 * N * F * 2),
         ("swiglu_bwd", lambda: ops.swiglu_bwd(gu, da), 5 * N * F * 2),
