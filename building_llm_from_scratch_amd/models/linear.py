@@ -436,8 +436,11 @@ class FusedLinear:
         return self.unit.fused_grad(self.b_params) if self.b_params is not None else None
 
     def backward(self, dy: torch.Tensor, x: torch.Tensor, xa, need_dx: bool = True,
-                 accumulate: bool = False, dx_acc: Optional[torch.Tensor] = None, bias_done: bool = False):
-        """Returns dx (plus ``dx_acc`` if given) and writes parameter grads into the flat."""
+                 accumulate: bool = False, dx_acc: Optional[torch.Tensor] = None, bias_done: bool = False,
+                 lowrank_dx: bool = False):
+        """Returns dx (plus ``dx_acc`` if given) and writes parameter grads into the flat.
+        ``lowrank_dx``: a K-augmented group may instead return ("lowrank", base, u, P, s) with
+        dx = base + s u P left for the consumer to form (ops.swiglu_bwd_lowrank)."""
         u = self.unit
         gW = u.fused_grad(self.W_params)
         if gW is not None:
@@ -447,7 +450,7 @@ class FusedLinear:
             if gb is not None:
                 ops.bias_grad_(dy, gb, accumulate)
         if self.has_lora and isinstance(xa, tuple) and xa[0] == "kaug":
-            return self._kaug_lora_backward(dy, x, xa[1], xa[2], xa[3], need_dx, dx_acc, accumulate)
+            return self._kaug_lora_backward(dy, x, xa[1], xa[2], xa[3], need_dx, dx_acc, accumulate, lowrank_dx)
         if self.has_lora and isinstance(xa, tuple) and xa[0] == "grouped":
             return self._grouped_lora_backward(dy, x, xa[1], xa[2], need_dx, dx_acc, accumulate)
         dx = None
@@ -483,7 +486,7 @@ class FusedLinear:
         assert not self.has_lora
         return _input_grad(dy, self.W())
 
-    def _kaug_lora_backward(self, dy, x, st, P, WaT, need_dx, dx_acc, accumulate):
+    def _kaug_lora_backward(self, dy, x, st, P, WaT, need_dx, dx_acc, accumulate, lowrank_dx=False):
         """st = s t (the forward's augmented columns), WaT = [W^T ; Bd]."""
         u_ = self.unit
         sc = self.lora_scale
@@ -501,6 +504,8 @@ class FusedLinear:
             ops.lora_wgrad(ub, x, [g.t() for g, _ in gA], [o for _, o in gA], [0] * len(gA), sc, accumulate)
         if not need_dx:
             return None
+        if lowrank_dx and dx_acc is None and ops.swiglu_bwd_lowrank_ok(self.lora_R, K):
+            return ("lowrank", dxa[:, :K], ub, P, sc)             # the consumer adds s u P
         dx = torch.empty(x.shape, dtype=x.dtype, device=x.device)
         ops.lora_up_(dx, ub, [P], [0], [0], sc, base=dxa[:, :K])  # dx_W + s (dy B^T) A_cat^T
         if dx_acc is not None:

@@ -262,9 +262,12 @@ class LlamaBlockCompute(UnitCompute):
         # ---- MLP
         if "act" in s or self.down.has_lora:
             act = s["act"] if "act" in s else ops.swiglu_fwd(s["gu"])
-            d_act = self.down.backward(dy2, act, xa_dn, accumulate=acc)
+            d_act = self.down.backward(dy2, act, xa_dn, accumulate=acc, lowrank_dx=True)
             del act
-            d_gu = ops.swiglu_bwd(s["gu"], d_act)
+            if isinstance(d_act, tuple):   # K-augmented LoRA: dact = base + s u P inside the kernel
+                d_gu = ops.swiglu_bwd_lowrank(s["gu"], *d_act[1:])
+            else:
+                d_gu = ops.swiglu_bwd(s["gu"], d_act)
             del d_act
         else:
             # recompute without act: dX GEMM first, then one SwiGLU backward pass that also

@@ -514,6 +514,19 @@ def swiglu_bwd(gu, dact):
     return ref.swiglu_bwd(gu, dact)
 
 
+def swiglu_bwd_lowrank_ok(r: int, F: int) -> bool:
+    return r == 16 and F % 8 == 0
+
+
+def swiglu_bwd_lowrank(gu, base, u, P, scale: float):
+    """swiglu_bwd(gu, dact) with dact = base + scale * u @ P formed inside the kernel (the down
+    projection's K-augmented LoRA dX: base = dy W, u = dy B^T [N, r], P = A^T [r, F])."""
+    if _hip(gu):
+        return _k().swiglu_bwd_lowrank(gu, base, u, P, float(scale))
+    dact = (base.float() + scale * (u.float() @ P.float())).to(gu.dtype)
+    return ref.swiglu_bwd(gu, dact)
+
+
 def swiglu_bwd_act(gu, dact):
     """``swiglu_bwd`` that also overwrites ``dact`` in place with act = silu(g) * u (what
     ``swiglu_fwd`` returns): the checkpoint recompute skips its SwiGLU forward pass."""

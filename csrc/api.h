@@ -26,6 +26,10 @@ void col_reduce(const float* part, DType odt, void* out, int P, int d, bool accu
 // out[C, R] = in[R, C]^T, 16-bit elements, R % 8 == 0 and C % 8 == 0
 void transpose16(const void* in, void* out, long R, long C, hipStream_t s);
 void swiglu_fwd(DType dt, const void* gu, void* act, long N, int F, long lda, hipStream_t s);
+// SwiGLU backward with dact = base + scale . u P formed on the fly (down-projection LoRA dX)
+bool swiglu_bwd_lr_ok(int r, int F);
+void swiglu_bwd_lr(DType dt, const void* gu, const void* base, long ldb, const void* u, long ldu, const void* P, int r,
+                   float scale, void* dgu, long N, int F, hipStream_t s);
 // act (nullable, may alias dact): also write silu(g) * u there -- the activation-checkpoint
 // recompute then needs no separate SwiGLU forward pass for the down projection's dW
 void swiglu_bwd(DType dt, const void* gu, const void* dact, void* dgu, void* act, long N, int F, hipStream_t s);

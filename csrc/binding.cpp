@@ -224,6 +224,23 @@ Tensor swiglu_bwd(const Tensor& gu, const Tensor& dact) {
   return dgu;
 }
 
+// swiglu_bwd with dact = base + scale . u P (base [N, F] and u [N, r] row-strided views, P [r, F])
+Tensor swiglu_bwd_lowrank(const Tensor& gu, const Tensor& base, const Tensor& u, const Tensor& P, double scale) {
+  check_gpu(gu, "gu"); check_gpu(P, "P");
+  c10::DeviceGuard g(gu.device());
+  const int64_t N = gu.size(0), F = gu.size(1) / 2, r = P.size(0);
+  TORCH_CHECK(bllm::swiglu_bwd_lr_ok((int)r, (int)F) && P.size(1) == F, "swiglu_bwd_lowrank: rank 16, F % 8");
+  TORCH_CHECK(base.is_cuda() && base.dim() == 2 && base.size(0) == N && base.size(1) == F && base.stride(1) == 1 &&
+                  base.stride(0) % 8 == 0 && (uintptr_t)base.data_ptr() % 16 == 0, "swiglu_bwd_lowrank: base");
+  TORCH_CHECK(u.is_cuda() && u.dim() == 2 && u.size(0) == N && u.size(1) == r && u.stride(1) == 1, "swiglu_bwd_lowrank: u");
+  TORCH_CHECK(base.scalar_type() == gu.scalar_type() && u.scalar_type() == gu.scalar_type() &&
+                  P.scalar_type() == gu.scalar_type(), "swiglu_bwd_lowrank: dtypes");
+  auto dgu = at::empty_like(gu);
+  bllm::swiglu_bwd_lr(dt_of(gu), gu.data_ptr(), base.data_ptr(), base.stride(0), u.data_ptr(), u.stride(0),
+                      P.data_ptr(), (int)r, (float)scale, dgu.data_ptr(), N, (int)F, stream());
+  return dgu;
+}
+
 // dgu as swiglu_bwd, and dact is overwritten in place by act = silu(g) * u
 Tensor swiglu_bwd_act(const Tensor& gu, Tensor& dact) {
   check_gpu(gu, "gu"); check_gpu(dact, "dact");
@@ -1034,6 +1051,7 @@ TORCH_LIBRARY(bllm, m) {
   m.def("linear_residual(Tensor x, Tensor W, Tensor C) -> Tensor");
   m.def("swiglu_fwd(Tensor gu) -> Tensor");
   m.def("swiglu_fwd_into_(Tensor gu, Tensor(a!) act) -> ()");
+  m.def("swiglu_bwd_lowrank(Tensor gu, Tensor base, Tensor u, Tensor P, float scale) -> Tensor");
   m.def("swiglu_bwd(Tensor gu, Tensor dact) -> Tensor");
   m.def("swiglu_bwd_act(Tensor gu, Tensor(a!) dact) -> Tensor");
   m.def("gelu_fwd(Tensor f) -> Tensor");
@@ -1079,6 +1097,7 @@ TORCH_LIBRARY_IMPL(bllm, CUDA, m) {
   m.impl("linear_residual", &linear_residual);
   m.impl("swiglu_fwd", &swiglu_fwd);
   m.impl("swiglu_fwd_into_", &swiglu_fwd_into_);
+  m.impl("swiglu_bwd_lowrank", &swiglu_bwd_lowrank);
   m.impl("swiglu_bwd", &swiglu_bwd);
   m.impl("swiglu_bwd_act", &swiglu_bwd_act);
   m.impl("gelu_fwd", &gelu_fwd);

@@ -59,6 +59,65 @@ __global__ __launch_bounds__(256) void swiglu_bwd_k(const T* __restrict__ gu, co
   }
 }
 
+// SwiGLU backward whose incoming gradient is the down projection's K-augmented LoRA dX:
+//   dact = base + s . u P      (base = dy W from the dX GEMM, u = dy B^T [N, r], P = A^T [r, F])
+// is formed on the fly instead of by a read-modify-write pass over [N, F] (lora_up).  A workgroup
+// owns LR_ROWS rows: their u rows sit in LDS, and each thread keeps the r x 8 slice of P for its
+// column vector in registers across the rows, so P is read once per workgroup, not per row.
+constexpr int LR_ROWS = 16;
+template <typename T, int R>
+__global__ __launch_bounds__(256) void swiglu_bwd_lr_k(const T* __restrict__ gu, const T* __restrict__ base,
+                                                       long ldb, const T* __restrict__ u, long ldu,
+                                                       const T* __restrict__ P, float s, T* __restrict__ dgu,
+                                                       long N, int F) {
+  constexpr int VEC = 8;
+  __shared__ float us[LR_ROWS][R];
+  const long r0 = (long)blockIdx.x * LR_ROWS;
+  for (int e = threadIdx.x; e < LR_ROWS * R; e += 256) {
+    const int rr = e / R, j = e - rr * R;
+    us[rr][j] = r0 + rr < N ? to_f(u[(r0 + rr) * ldu + j]) : 0.f;
+  }
+  __syncthreads();
+  const int fv = F / VEC;
+  for (int cv = threadIdx.x; cv < fv; cv += 256) {
+    const int c = cv * VEC;
+    float pr[R][VEC];
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      const VecN<T, VEC> pv = ldv<T, VEC>(P + (long)j * F + c);
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) pr[j][e] = to_f(pv.v[e]);
+    }
+    for (int rr = 0; rr < LR_ROWS; ++rr) {
+      const long r = r0 + rr;
+      if (r >= N) break;
+      const VecN<T, VEC> g = ldv<T, VEC>(gu + r * 2 * F + c), up = ldv<T, VEC>(gu + r * 2 * F + F + c);
+      const VecN<T, VEC> bs = ldv<T, VEC>(base + r * ldb + c);
+      float corr[VEC];
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) corr[e] = 0.f;
+#pragma unroll
+      for (int j = 0; j < R; ++j) {
+        const float uj = us[rr][j];
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) corr[e] = fmaf(uj, pr[j][e], corr[e]);
+      }
+      VecN<T, VEC> dg, du;
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) {
+        // rounded to T like the lora_up output it replaces
+        const float dd = to_f(from_f<T>(to_f(bs.v[e]) + s * corr[e]));
+        const float a = to_f(g.v[e]), b = to_f(up.v[e]);
+        const float sg = 1.f / (1.f + __expf(-a));
+        dg.v[e] = from_f<T>(dd * b * sg * (1.f + a * (1.f - sg)));
+        du.v[e] = from_f<T>(dd * a * sg);
+      }
+      stv<T, VEC>(dgu + r * 2 * F + c, dg);
+      stv<T, VEC>(dgu + r * 2 * F + F + c, du);
+    }
+  }
+}
+
 // Row-per-workgroup variants for wide FFNs (F/VEC >= 512, e.g. Llama F=14336): no 64-bit index
 // division, U independent 16-B load pairs in flight per lane before any math (the grid-stride loop
 // above serialises load -> compute per vector).  One workgroup per token row; N rows >> 256 CUs.
@@ -433,6 +492,17 @@ void swiglu_fwd(DType dt, const void* gu, void* act, long N, int F, long lda, hi
                            (T*)act, N, F, lda);
     });
   });
+}
+bool swiglu_bwd_lr_ok(int r, int F) { return r == 16 && F % 8 == 0; }  // P slice: 128 VGPRs at r = 16
+void swiglu_bwd_lr(DType dt, const void* gu, const void* base, long ldb, const void* u, long ldu, const void* P, int r,
+                   float scale, void* dgu, long N, int F, hipStream_t s) {
+  const dim3 grid((unsigned)((N + LR_ROWS - 1) / LR_ROWS));
+#define LR_L(TT, RR) hipLaunchKernelGGL((swiglu_bwd_lr_k<TT, RR>), grid, dim3(256), 0, s, (const TT*)gu, (const TT*)base, \
+                                        ldb, (const TT*)u, ldu, (const TT*)P, scale, (TT*)dgu, N, F)
+  (void)r;
+  if (dt == DType::BF16) LR_L(bf16_t, 16);
+  else LR_L(f16_t, 16);
+#undef LR_L
 }
 void swiglu_bwd(DType dt, const void* gu, const void* dact, void* dgu, void* act, long N, int F, hipStream_t s) {
   BLLM_DISPATCH(dt, T, {

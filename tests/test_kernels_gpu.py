@@ -541,6 +541,25 @@ def test_kaug_producers_and_blocks(dt, N):
     assert torch.isnan(Wa[:, :K].float()).all() and torch.isnan(WaT[:K].float()).all()
 
 
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("N", [1000, 4096])
+def test_swiglu_bwd_lowrank(dt, N):
+    """SwiGLU backward with dact = base + s u P formed in the kernel (base / u: column slices of
+    one K-augmented [dx_W | u | 0] buffer) vs the separate lora_up + swiglu_bwd passes."""
+    F, r, Rp = 1024, 16, 64
+    gu = torch.randn(N, 2 * F, device=DEV).to(dt)
+    dxa = torch.randn(N, F + Rp, device=DEV).to(dt)
+    P = (0.1 * torch.randn(r, F, device=DEV)).to(dt)
+    base, u = dxa[:, :F], dxa[:, F:F + r]
+    got = ops.swiglu_bwd_lowrank(gu, base, u, P, 0.5)
+    dact = torch.empty(N, F, device=DEV, dtype=dt)
+    ops.lora_up_(dact, u, [P], [0], [0], 0.5, base=base)
+    want = ops.swiglu_bwd(gu, dact)
+    _close(got, want, dt, 2, name="swiglu_bwd_lowrank")
+    ref_dact = (base.float() + 0.5 * u.float() @ P.float()).to(dt)
+    _close(got, ops.swiglu_bwd(gu, ref_dact), dt, 2, name="swiglu_bwd_lowrank vs fp32 dact")
+
+
 def test_lora_model_uses_kernels_and_matches_gemm_path(monkeypatch):
     """A LoRA Llama step on the fused kernels (K-augmented QKV / gate-up / down, grouped o, the
     fused LoRA head: V = 512) gives the same loss / LoRA grads as the per-member hipBLASLt path."""
