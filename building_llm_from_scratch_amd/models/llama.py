@@ -433,8 +433,9 @@ class HeadComputeMixin:
         one GEMM per chunk instead of a separate s t B pass over the [N, V] logits plus a beta = 1
         GEMM.  The dX GEMM stays at the base width, dh_W = dl . W on the cached K-contiguous W^T
         (an augmented [N, d + r] output made hipBLASLt fall back from 1.64 to 0.66-0.75 PF at
-        V = 128k, tools/bench_head_k.py); u = dl B^T and dB = (s t)^T dl run on the LoRA kernels
-        over each dlogits chunk, then dh = dh_W + s u A^T and dA = s h^T u."""
+        V = 128k, tools/bench_head_k.py); u = dl B^T is a skinny hipBLASLt GEMM over each dlogits
+        chunk (355 us vs 610 us for lora_down, tools/bench_head_u.py), dB = (s t)^T dl runs on
+        lora_wgrad, then dh = dh_W + s u A^T and dA = s h^T u on the LoRA kernels."""
         hd, u_ = self.head, self.head.unit
         spec = hd.specs[0]
         A, Bm, sc = u_.data(spec.lora_A), u_.data(spec.lora_B), float(spec.scaling)   # [d, r], [r, V]
@@ -472,7 +473,7 @@ class HeadComputeMixin:
                 mm_nt(dl, Wd.t(), out=dh[s0:s0 + rows])                   # dh_W = dl . W
             else:
                 torch.mm(dl, Wd, out=dh[s0:s0 + rows])
-            ops.lora_down_into(dl, [Bm], [0], [V], [0], r, 1.0, ub[s0:s0 + rows])   # u = dl B^T
+            torch.mm(dl, Bm.t(), out=ub[s0:s0 + rows])            # u = dl B^T (hipBLASLt: 5.9 TB/s here)
             if gB is not None:                                            # dB = (s t)^T dl
                 ops.lora_wgrad(st[s0:s0 + rows], dl, [gB], [0], [0], 1.0, accumulate=s0 > 0)
             del logits, dl

@@ -1,0 +1,21 @@
+#!/usr/bin/env python3
+"""u = dl B^T over one LoRA-head dlogits chunk (8192 x 128,256): lora_down vs a hipBLASLt mm."""
+import torch, json
+def timeit(fn, iters=20):
+    for _ in range(3): fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters): fn()
+    e.record(); torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters * 1e3
+import sys; sys.path.insert(0, '.')
+from building_llm_from_scratch_amd import ops
+ops.load_ext(required=True)
+rows, V, r = 8192, 128256, 16
+dl = (torch.rand(rows, V, device='cuda')*2-1).to(torch.bfloat16)
+B = (torch.rand(r, V, device='cuda')*2-1).to(torch.bfloat16)
+ub = torch.empty(rows, r, device='cuda', dtype=torch.bfloat16)
+t1 = timeit(lambda: ops.lora_down_into(dl, [B], [0], [V], [0], r, 1.0, ub))
+t2 = timeit(lambda: torch.mm(dl, B.t(), out=ub))
+print(json.dumps({"lora_down_us": round(t1,1), "hipblaslt_mm_us": round(t2,1), "GB": rows*V*2/1e9}))
