@@ -324,6 +324,8 @@ def launch(argv=None):
 def main(argv=None):
     a = parse(argv)
     if a.tunableop_tune:
+        # a tuning run writes its own file; a preset's read-only table would switch tuning off
+        a.tunableop = None
         os.environ.update(PYTORCH_TUNABLEOP_ENABLED="1", PYTORCH_TUNABLEOP_TUNING="1",
                           PYTORCH_TUNABLEOP_FILENAME=os.path.abspath(a.tunableop_tune).replace(".csv", "%d.csv"))
     if a.tunableop in ("none", ""):
@@ -333,10 +335,12 @@ def main(argv=None):
     if a.tunableop and (a.device != "cuda" or not os.path.exists(a.tunableop)):
         a.tunableop = None
     if a.tunableop:  # must be set before the first GEMM; TunableOp reads <name><device ordinal>.csv
+        import shutil
         import tempfile
         d = tempfile.mkdtemp(prefix="bllm_tunableop_")
         local = int(os.environ.get("LOCAL_RANK", "0"))
-        os.symlink(os.path.abspath(a.tunableop), os.path.join(d, f"results{local}.csv"))
+        # a copy, not a symlink: whatever TunableOp writes back can never reach the shipped table
+        shutil.copyfile(os.path.abspath(a.tunableop), os.path.join(d, f"results{local}.csv"))
         os.environ.update(PYTORCH_TUNABLEOP_ENABLED="1", PYTORCH_TUNABLEOP_TUNING="0",
                           PYTORCH_TUNABLEOP_FILENAME=os.path.join(d, "results%d.csv"))
     import torch
@@ -452,6 +456,10 @@ def main(argv=None):
     if comm is not None:
         comm.reset(enabled=True)     # exposed collective waits of the timed steps only
     tokens = 0
+    from building_llm_from_scratch_amd.utils.telemetry import GpuTelemetry, library_versions, tunableop_status
+    telem = GpuTelemetry(int(os.environ.get("LOCAL_RANK", "0"))) if cuda else None
+    if telem is not None:
+        telem.start()
     t0 = time.perf_counter()
     for i in range(a.steps):
         loss = step(a.warmup + i)
@@ -459,6 +467,7 @@ def main(argv=None):
     dist.barrier()
     sync()
     elapsed = time.perf_counter() - t0
+    telemetry = telem.stop() if telem is not None else {"source": None, "samples": 0}
     comm_by_kind = comm.summary() if comm is not None else {}
     if comm is not None:
         comm.enabled = False
@@ -498,6 +507,8 @@ def main(argv=None):
                       or per * world > n_windows}
     comm_kinds = [None] * world
     dist.all_gather_object(comm_kinds, comm_by_kind)
+    telem_all = [None] * world
+    dist.all_gather_object(telem_all, telemetry)
     prof = profile_phases(model, opt, next_batch, dev) if (a.profile and rank == 0 and cuda) else None
     if rank == 0:
         headline = a.preset == "llama3_8b_fsdp" and cuda and not a.layers and not a.one_device
@@ -578,6 +589,12 @@ def main(argv=None):
                      "bucket_mib": getattr(engine, "bucket_mb", None),
                      "deferred_init": bool(getattr(engine, "deferred_init", False))},
         }
+        # what the box did during the timed steps (clocks, power, temperature, throttle residency)
+        # and whether the GEMM tuning table was taken: box-to-box differences become readable
+        out["telemetry"] = {"rank0": telem_all[0],
+                            "sclk_mhz_avg_per_rank": [t.get("sclk_mhz_avg") for t in telem_all]}
+        out["versions"] = library_versions() if cuda else {"torch": torch.__version__, "hip": torch.version.hip}
+        out["tunableop"] = tunableop_status(a.tunableop) if cuda else None
         if data_check is not None:
             out["data_check"] = data_check
         if loss_trace is not None:

@@ -61,10 +61,39 @@ def engine_kind(args) -> str:
     return "ddp"
 
 
+def plan_checkpointing(config, args, device, world: int = 1):
+    """``--actv_ckpt_mode auto``: the per-block plan of train/memplan.py for this rank's engine,
+    batch and device capacity (bench.py's headline policy)."""
+    from .train import memplan
+    total = None
+    if device is not None and torch.device(device).type == "cuda":
+        total = torch.cuda.get_device_properties(torch.device(device)).total_memory
+    budget = args.ckpt_budget_gib * memplan.GIB if getattr(args, "ckpt_budget_gib", None) else None
+    trainable = 1.0
+    if args.use_lora:   # frozen base: no fp32 master / moments / grads for it (LoRA params are tiny)
+        trainable = 0.0
+    elt = torch.empty((), dtype=config.dtype).element_size()
+    return memplan.plan_ckpt(config, args.batch_size, config.context_length, world=world, engine=engine_kind(args),
+                             budget=budget, device_total=total, elt=elt,
+                             prefetch=max(1, getattr(args, "fsdp_prefetch", 0) or 2), trainable_frac=trainable)
+
+
 def build_model(config, rank, device, args):
     misc.start_memory_tracking()
     ckpt = getattr(args, "actv_ckpt_mode", None) or ("full" if args.use_actv_ckpt else "none")
+    plan = None
+    if ckpt == "auto":
+        plan = plan_checkpointing(config, args, device, getattr(args, "world_size", 1))
+        ckpt = "selective"
     model = _build_model(config, use_actv_ckpt=ckpt, device=device)
+    if plan is not None:
+        model.set_block_modes(plan.modes)
+        model.ckpt_plan = plan    # the trainer re-plans after the first step's measured peak
+        if rank == 0:
+            s = plan.summary()
+            logger.info(f"Activation checkpointing (auto): {s['full']} blocks fully recomputed, "
+                        f"{s['selective']} selective; estimated peak {s['est_peak_gib']} GiB of "
+                        f"{s['budget_gib']} GiB budget")
     if getattr(args, "actv_ckpt_segments", None):
         model.set_actv_ckpt(ckpt, args.actv_ckpt_segments)
     if rank == 0:

@@ -79,8 +79,13 @@ def build_parser() -> argparse.ArgumentParser:
     # ---- extensions (defaults = reference behaviour)
     x = p.add_argument_group("extensions")
     x.add_argument("--context_length", type=int, default=1024, help="Llama ctx clamp (reference: fixed 1024)")
-    x.add_argument("--actv_ckpt_mode", choices=["none", "selective", "full"], default=None,
-                   help="granularity; --use_actv_ckpt alone = full (reference semantics)")
+    x.add_argument("--actv_ckpt_mode", choices=["none", "selective", "full", "auto"], default=None,
+                   help="granularity; --use_actv_ckpt alone = full (reference semantics); auto = the HBM "
+                        "memory planner (train/memplan.py: every block selective plus the fewest fully "
+                        "recomputed blocks under --ckpt_budget_gib, re-planned after the first step's "
+                        "measured peak) -- the headline bench's policy")
+    x.add_argument("--ckpt_budget_gib", type=float, default=None,
+                   help="auto mode: per-rank peak-memory ceiling (default 250 GiB, capped at device - 18 GiB)")
     x.add_argument("--actv_ckpt_segments", type=int, default=None,
                    help="full mode: checkpoint_sequential segments (default n_layers = reference); "
                         "fewer segments recompute fewer blocks for more memory")

@@ -106,6 +106,7 @@ class Trainer:
             a, b = (int(v) for v in str(profile_steps).split(":"))
             self.profile_steps = (a, b)
         self._prof = None
+        self._probed = False
 
     # ------------------------------------------------------------------ helpers
     def _dist(self) -> bool:
@@ -181,7 +182,33 @@ class Trainer:
             self.optimizer.clip_grad_norm_(self.max_grad_norm)
             self.optimizer.step()
         self.tokens_seen += input_batch.numel() * self.world_size
+        if not self._probed:
+            self._probed = True
+            self._probe_ckpt_plan()
         return loss
+
+    def _probe_ckpt_plan(self):
+        """``--actv_ckpt_mode auto``: check the planner's estimate against the first step's measured
+        peak (max over ranks) and add fully recomputed blocks if it was over budget, exactly as
+        bench.py does for the headline."""
+        plan = getattr(self.model, "ckpt_plan", None)
+        if plan is None or torch.device(self.device).type != "cuda":
+            return
+        from . import memplan
+        torch.cuda.synchronize()
+        pk = torch.tensor([float(torch.cuda.max_memory_allocated(self.device))], device=self.device)
+        if self._dist():
+            dist.all_reduce(pk, op=dist.ReduceOp.MAX)
+        elt = torch.empty((), dtype=self.config.dtype).element_size()
+        new = memplan.replan_after_probe(plan, self.config, self.loaderObj.batch_size,
+                                         self.config.context_length, pk.item(), elt=elt)
+        if new is not plan:
+            self.model.set_block_modes(new.modes)
+            self.model.ckpt_plan = new
+            torch.cuda.reset_peak_memory_stats(self.device)
+        if self.rank == 0:
+            logger.info(f"Activation checkpointing (auto): first-step peak {pk.item() / memplan.GIB:.1f} GiB; "
+                        + ("plan kept" if new is plan else f"re-planned: {new.summary()}"))
 
     def train_epoch(self, epoch_no, train_loader, val_loader, start_context="Every effort moves you",
                     file_index: int = 0, skip_batches: int = 0):
@@ -200,11 +227,15 @@ class Trainer:
                 self.train_losses.append(train_loss)
                 self.val_losses.append(val_loss)
                 self.track_tokens_seen.append(self.tokens_seen)
+                # training throughput since the last eval point, measured up to the loss read
+                # above (a device sync) and restarted after eval / sample / checkpoint: those
+                # phases never count against tok/s
                 now = time.perf_counter()
                 tps = None
                 if self._t_last is not None:
                     tps = (self.tokens_seen - self._tok_last) / max(now - self._t_last, 1e-9)
-                self._t_last, self._tok_last = now, self.tokens_seen
+                self._tok_last = self.tokens_seen
+                self._t_last = None
                 if self.rank == 0:
                     logger.info(f"Epoch {epoch_no + 1} | Step {self.global_step} "
                                 f"| Train Loss: {train_loss:.3f} | Val Loss: {val_loss:.3f}"
@@ -218,6 +249,11 @@ class Trainer:
                 self.generate_and_print_sample(start_context)
             if self.save_ckpt_freq and self.global_step % self.save_ckpt_freq == 0:
                 self.save_checkpoint(f"model_pg_{self.global_step}.pth")
+            if self._t_last is None:   # (re)start the throughput clock after the eval-step phases
+                if torch.cuda.is_available() and torch.device(self.device).type == "cuda":
+                    torch.cuda.synchronize()
+                self._t_last = time.perf_counter()
+                self._tok_last = self.tokens_seen
             if self.max_steps is not None and self.global_step + 1 >= self.max_steps:
                 self.stop = True
                 return

@@ -45,6 +45,12 @@ def _run(n, extra, timeout=600, spawn=False):
     assert out["per_rank"]["ms_per_step_max"] == out["ms_per_step"]
     assert out["launcher"] == ("spawn" if spawn and n > 1 else ("single" if n == 1 else "torchrun"))
     assert "INVALID" in out["config"]["model"]  # a CPU run can never pass for a measurement
+    # box telemetry fields are always present; on CPU they are empty / null
+    tel = out["telemetry"]
+    assert tel["rank0"]["source"] is None and tel["rank0"]["samples"] == 0
+    assert len(tel["sclk_mhz_avg_per_rank"]) == n and all(v is None for v in tel["sclk_mhz_avg_per_rank"])
+    assert "torch" in out["versions"] and "hip" in out["versions"]
+    assert out["tunableop"] is None
     return out
 
 
@@ -141,3 +147,27 @@ def test_bench_world2_matches_world1_on_the_global_batch(parallel):
     assert len(a) == len(b) == 3
     assert max(abs(x - y) for x, y in zip(a, b)) < 1e-4, (a, b)
     assert a[-1] != a[0]                          # the optimizer really moved the weights
+
+
+def test_telemetry_summary_math():
+    """GpuTelemetry's reductions on canned SMU samples (no GPU): averages, residency fractions
+    from accumulator deltas, N/A sentinels ignored."""
+    from building_llm_from_scratch_amd.utils.telemetry import GpuTelemetry, tunableop_status
+    t = GpuTelemetry.__new__(GpuTelemetry)
+    t.smi, t.h, t.interval = None, None, 0.25
+    t.samples = [{"sclk": 2000.0, "mclk": 1900.0, "power": 1300.0, "hotspot": 80.0, "hbm": 70.0, "throttle": 0,
+                  "indep": 0},
+                 {"sclk": 1800.0, "mclk": 1900.0, "power": 1400.0, "hotspot": 90.0, "hbm": 72.0, "throttle": 4,
+                  "indep": 0}]
+    t._m0 = {"accumulation_counter": 100, "ppt_residency_acc": 10, "socket_thm_residency_acc": 0,
+             "xgmi_read_data_acc": [0, 5, 0xFFFFFFFFFFFFFFFF]}
+    t._m1 = {"accumulation_counter": 300, "ppt_residency_acc": 110, "socket_thm_residency_acc": 0,
+             "xgmi_read_data_acc": [7, 9, 0xFFFFFFFFFFFFFFFF]}
+    s = t.summary()
+    assert s["sclk_mhz_avg"] == 1900.0 and s["sclk_mhz_min"] == 1800.0 and s["power_w_max"] == 1400.0
+    assert s["throttle_status_nonzero_frac"] == 0.5
+    assert s["limit_residency"] == {"ppt": 0.5, "socket_thm": 0.0}
+    assert s["xgmi"]["xgmi_read_kb"] == 11
+    assert tunableop_status(None) is None
+    st = tunableop_status(os.path.join(ROOT, "configs", "tunableop_llama3_8b_b40_mi355x.csv"))
+    assert st["file_rows"] >= 5    # validators compared on a GPU box only

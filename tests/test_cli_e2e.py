@@ -71,3 +71,27 @@ def test_multi_process_spawn_gloo(tmp_path, mode):
         os.environ.pop("MASTER_PORT", None)
     sd = torch.load(out / "model_pg_final.pth", weights_only=True)
     assert "trf_blocks.0.norm1.weight" in sd and sd["trf_blocks.0.norm1.weight"].dtype == torch.float32
+
+
+@pytest.mark.parametrize("budget,full", [(None, 0), ("0.000001", 2)])
+def test_actv_ckpt_auto_planner(tmp_path, budget, full):
+    """``--actv_ckpt_mode auto`` (bench.py's headline policy) through the CLI: the memory planner
+    picks per-block modes for this engine and batch; a tiny budget forces every block to full
+    recompute.  Runs under FSDP on 2 gloo ranks."""
+    out = tmp_path / "ckpt"
+    os.environ["MASTER_PORT"] = str(_free_port())
+    extra = ["--ckpt_budget_gib", budget] if budget else []
+    try:
+        r = _run(["--model", "llama3_2", "--num_params", "1B", "--debug", "--run_type", "multi_gpu", "--backend",
+                  "gloo", "--nprocs", "2", "--device", "cpu", "--use_fsdp", "--use_actv_ckpt", "--actv_ckpt_mode",
+                  "auto", "--data_dir", str(tmp_path / "data"), "--synthetic_data", "--output_dir", str(out),
+                  "--n_epochs", "1", "--max_steps", "5", "--eval_freq", "2", "--save_ckpt_freq", "100",
+                  "--print_sample_iter", "100", "--batch_size", "2", "--no_plot", "--sample_tokens", "2",
+                  "--metrics_file", str(tmp_path / "m.jsonl")] + extra, tmp_path)
+    finally:
+        os.environ.pop("MASTER_PORT", None)
+    log = r.stdout + r.stderr
+    assert f"Activation checkpointing (auto): {full} blocks fully recomputed, {2 - full} selective" in log, log[-3000:]
+    rows = [json.loads(line) for line in open(tmp_path / "m.jsonl")]
+    # throughput is reported from the second eval point on, eval / sample / checkpoint excluded
+    assert rows[0]["tokens_per_s"] is None and all(r["tokens_per_s"] > 0 for r in rows[1:])
