@@ -111,6 +111,9 @@ def parse(argv=None):
     ap.add_argument("--lora_rank", type=int, default=None)
     ap.add_argument("--lora_alpha", type=int, default=32)
     ap.add_argument("--reshard_after_forward", type=int, default=1)
+    ap.add_argument("--bucket_mb", type=float, default=256.0,
+                    help="DDP / ZeRO-1 gradient bucket size (MiB); DDP grows it in warm-up while its "
+                         "all-reduce wait shows in the step")
     ap.add_argument("--fsdp_prefetch", type=int, default=0,
                     help="FSDP units all-gathered ahead (0 = auto: gather time over xGMI vs unit compute)")
     ap.add_argument("--layers", type=int, default=None, help="(debug only) override n_layers; invalidates the metric")
@@ -168,6 +171,9 @@ def init_dist(a):
         dev = torch.device("cpu")
     kw = dict(timeout=timedelta(minutes=a.pg_timeout_min))
     rccl = dev.type == "cuda" and not a.one_device
+    # per-collective start / end events on RCCL's stream (Work._get_duration: the bandwidth
+    # account of parallel/commstats.py); read by ProcessGroupNCCL at construction
+    os.environ.setdefault("TORCH_NCCL_ENABLE_TIMING", "1")
     if rccl:
         from building_llm_from_scratch_amd.parallel import nccl_pg_options
         kw["device_id"] = dev
@@ -381,7 +387,7 @@ def main(argv=None):
             p.requires_grad = False
         replace_linear_with_lora(model, rank=a.lora_rank, alpha=a.lora_alpha)
     reduce = get_policy(a.mixed_precision).reduce_dtype if a.mixed_precision else None
-    engine = setup_engine(model, a.parallel, device=dev, reduce_dtype=reduce,
+    engine = setup_engine(model, a.parallel, device=dev, reduce_dtype=reduce, bucket_mb=a.bucket_mb,
                           reshard_after_forward=bool(a.reshard_after_forward), prefetch=a.fsdp_prefetch)
     opt = FusedAdamW(model, lr=3e-4, weight_decay=0.1, engine=engine, overlap=a.overlap_optimizer)
 
@@ -435,7 +441,13 @@ def main(argv=None):
         return loss
 
     probe_peak = None
+    comm = getattr(engine, "comm", None)
+    adapt_hist = []
     for i in range(a.warmup):
+        if comm is not None:
+            comm.reset(enabled=True)      # this warm-up step's exposed waits (adaptation input)
+        sync()
+        tw = time.perf_counter()
         loss = step(i)
         if i == 0 and plan is not None and cuda:
             # memory probe: the first step's measured peak (max over ranks) checks the plan
@@ -449,7 +461,13 @@ def main(argv=None):
                 plan = new
                 model.set_block_modes(plan.modes)
                 torch.cuda.reset_peak_memory_stats(dev)
-    comm = getattr(engine, "comm", None)
+        # warm-up adaptation (after the cold first step): FSDP prefetch depth / DDP bucket
+        # size grown while a collective wait shows in the step (MAX over ranks, parallel/)
+        if i >= 1 and hasattr(engine, "adapt"):
+            sync()
+            rec = engine.adapt(1e3 * (time.perf_counter() - tw))
+            if rec is not None:
+                adapt_hist.append(rec)
     sync()
     dist.barrier()
     sync()
@@ -469,6 +487,7 @@ def main(argv=None):
     elapsed = time.perf_counter() - t0
     telemetry = telem.stop() if telem is not None else {"source": None, "samples": 0}
     comm_by_kind = comm.summary() if comm is not None else {}
+    comm_bw = comm.bandwidth() if comm is not None else {}
     if comm is not None:
         comm.enabled = False
     comm_ms = sum(v["ms"] for v in comm_by_kind.values()) / a.steps
@@ -509,6 +528,9 @@ def main(argv=None):
     dist.all_gather_object(comm_kinds, comm_by_kind)
     telem_all = [None] * world
     dist.all_gather_object(telem_all, telemetry)
+    # the adapted comm parameters of every rank (must agree: they fix the collective order)
+    knobs_all = [None] * world
+    dist.all_gather_object(knobs_all, (getattr(engine, "prefetch", None), getattr(engine, "bucket_mb", None)))
     prof = profile_phases(model, opt, next_batch, dev) if (a.profile and rank == 0 and cuda) else None
     if rank == 0:
         headline = a.preset == "llama3_8b_fsdp" and cuda and not a.layers and not a.one_device
@@ -585,8 +607,14 @@ def main(argv=None):
             # commstats.py); max over ranks.  0 at world 1 (no-shard engines issue none)
             "comm_exposed_ms": round(max(r[3] for r in per_rank), 3),
             "comm": {"by_kind_rank0": comm_kinds[0],
+                     # achieved bandwidth of every collective of the timed steps (rank 0):
+                     # RCCL's own issue-to-complete time per collective; busbw is per link
+                     "gbps_by_kind": comm_bw,
                      "fsdp_prefetch": getattr(engine, "prefetch", None) if a.parallel == "fsdp" else None,
                      "bucket_mib": getattr(engine, "bucket_mb", None),
+                     "adapted": adapt_hist,
+                     "per_rank_fsdp_prefetch": [k[0] for k in knobs_all] if a.parallel == "fsdp" else None,
+                     "per_rank_bucket_mib": [k[1] for k in knobs_all],
                      "deferred_init": bool(getattr(engine, "deferred_init", False))},
         }
         # what the box did during the timed steps (clocks, power, temperature, throttle residency)

@@ -114,6 +114,9 @@ def build_parser() -> argparse.ArgumentParser:
     x.add_argument("--bucket_mb", type=float, default=256.0, help="DDP all-reduce bucket size")
     x.add_argument("--fsdp_prefetch", type=int, default=0,
                    help="FSDP: units all-gathered ahead of the computing one (0 = auto from gather vs compute time)")
+    x.add_argument("--comm_adapt_steps", type=int, default=3,
+                   help="first N steps: grow the FSDP prefetch depth / DDP bucket size while an exposed "
+                        "collective wait exceeds 2%% of the step (MAX over ranks)")
     x.add_argument("--no_reshard_after_forward", action="store_true",
                    help="FSDP: keep gathered params from forward to backward (ZeRO-2 style)")
     x.add_argument("--no_plot", action="store_true")
@@ -144,6 +147,7 @@ def ddp_setup(rank: int, world_size: int, args):
     device = _device_for(args, int(os.environ.get("LOCAL_RANK", rank)))
     backend = args.backend or ("nccl" if device.type == "cuda" else "gloo")
     timeout = timedelta(minutes=getattr(args, "pg_timeout_min", 30.0))
+    os.environ.setdefault("TORCH_NCCL_ENABLE_TIMING", "1")   # per-collective bandwidth account
     if backend == "nccl":
         from .parallel import nccl_pg_options
         dist.init_process_group("nccl", rank=rank, world_size=world_size, device_id=device, timeout=timeout,
@@ -219,7 +223,7 @@ def main(rank: int, args):
                       loss_scaler=DynamicLossScaler() if config.dtype == torch.float16 else None,
                       max_steps=args.max_steps, sample_tokens=args.sample_tokens,
                       save_resume=args.save_resume_state, world_size=world, profile_steps=args.profile_steps,
-                      num_workers=args.num_workers, seed=args.seed)
+                      num_workers=args.num_workers, seed=args.seed, comm_adapt_steps=args.comm_adapt_steps)
     trainer.generate_and_print_sample("Every effort moves you", temperature=1.0, top_k=5, memory_check=True)
     if args.resume:
         # after the start-up sample: the restored host RNG state is the one saved at the checkpoint

@@ -396,14 +396,19 @@ class BaseLM(nn.Module):
         every rank computes the same values for the units it shards."""
         seed = self.init_seed if seed is None else seed
         ids = {id(p) for fb in unit.buffers() for p in fb.params}
-        torch.manual_seed(unit_seed(seed, unit.index))
-        for mod in self.modules():
-            own = [p for p in mod.parameters(recurse=False) if id(p) in ids]
-            if not own:
-                continue
-            if not hasattr(mod, "reset_parameters"):
-                raise TypeError(f"{type(mod).__name__} has no reset_parameters: cannot initialise a meta-built model")
-            mod.reset_parameters()
+        # the unit seed must not leak into the caller's streams (dropout, sampling, shuffling
+        # continue from where they were): fork the CPU RNG and the device's own
+        devs = [p.device for fb in unit.buffers() for p in fb.params if p.device.type == "cuda"][:1]
+        with torch.random.fork_rng(devices=devs, device_type="cuda"):
+            torch.manual_seed(unit_seed(seed, unit.index))
+            for mod in self.modules():
+                own = [p for p in mod.parameters(recurse=False) if id(p) in ids]
+                if not own:
+                    continue
+                if not hasattr(mod, "reset_parameters"):
+                    raise TypeError(f"{type(mod).__name__} has no reset_parameters: cannot initialise a "
+                                    "meta-built model")
+                mod.reset_parameters()
 
     def _ensure_flat(self):
         if self._comps is None:

@@ -126,56 +126,18 @@ def _dgrad_wt_ok(dy: torch.Tensor, W: torch.Tensor) -> bool:
 
 
 # The forward-layout GEMMs (y = x W^T, dX on the transposed weight copy, the fused head's logits
-# and dh).  BLLM_GEMM_NT: 0 = hipBLASLt (default: it measures faster on these shapes,
-# profiles/r4/kernel_experiments.md); 1 = csrc/gemm_nt.hip's persistent kernel wherever its shape
-# rules hold; auto = per shape, whichever of the two timed faster on this device (measured once
-# per shape and process, like TunableOp; rank 0's pick is broadcast when a process group is up,
-# so every rank runs the same kernel; never inside a graph capture)
-GEMM_NT_MODE = os.environ.get("BLLM_GEMM_NT", "0")
-GEMM_NT = GEMM_NT_MODE not in ("0", "")
-_NT_PICK: dict = {}
-
-
-def _time_nt(a, b, out) -> bool:
-    """True when csrc/gemm_nt.hip ran this shape faster than hipBLASLt (median of 3 x 3)."""
-    c = torch.empty(a.shape[0], b.shape[0], dtype=out.dtype if out is not None else a.dtype, device=a.device)
-    arms = {False: lambda: torch.mm(a, b.t(), out=c) if c.dtype == a.dtype else c.copy_(torch.mm(a, b.t())),
-            True: lambda: ops.gemm_nt_(a, b, c, False)}
-    times = {k: [] for k in arms}
-    for fn in arms.values():
-        fn()
-    for _ in range(3):
-        for k, fn in arms.items():
-            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            s.record()
-            for _ in range(3):
-                fn()
-            e.record()
-            e.synchronize()
-            times[k].append(s.elapsed_time(e))
-    pick = sorted(times[True])[1] < sorted(times[False])[1]
-    import torch.distributed as dist
-    if dist.is_available() and dist.is_initialized():   # one decision for every rank
-        t = torch.tensor([int(pick)], device=a.device if dist.get_backend() == "nccl" else "cpu")
-        dist.broadcast(t, src=0)
-        pick = bool(t.item())
-    return pick
+# and dh).  BLLM_GEMM_NT: 0 = hipBLASLt / rocBLAS (default), 1 = csrc/gemm_nt.hip's persistent
+# kernel wherever its shape rules hold (an A/B switch).  Round 5 measured the library GEMMs
+# (TunableOp-picked per shape) 3-12 % faster on every Llama-3-8B and GPT-2 projection, and the
+# epilogue fusions built on this kernel lost end to end (profiles/r5/fused_epilogues_ab.md).  A
+# per-shape timed pick ("auto") was removed: a lazily timed pick differs between ranks whose
+# batch shapes differ, and settling it needed a collective inside a cache miss.
+GEMM_NT = os.environ.get("BLLM_GEMM_NT", "0") == "1"
 
 
 def nt_choice(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None) -> bool:
     """Whether mm_nt runs this call on csrc/gemm_nt.hip (else hipBLASLt)."""
-    if not GEMM_NT or not ops.gemm_nt_ok(a, b, out):
-        return False
-    if GEMM_NT_MODE != "auto":
-        return True
-    key = (tuple(a.shape), a.stride(0), tuple(b.shape), b.stride(0), a.dtype,
-           None if out is None else (out.dtype, out.stride(0)), a.device)
-    pick = _NT_PICK.get(key)
-    if pick is None:
-        if torch.cuda.is_current_stream_capturing():
-            return False
-        pick = _NT_PICK[key] = _time_nt(a, b, out)
-    return pick
+    return GEMM_NT and ops.gemm_nt_ok(a, b, out)
 
 
 def mm_nt(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:

@@ -74,12 +74,20 @@ def step_plan(engine) -> List[Dict]:
             return plan
         ar = engine.arena
         zero = isinstance(engine, ZeroEngine)
-        # buckets complete in reverse unit order during backward
-        order = sorted(range(len(ar.buckets)), key=lambda b: -max(ar.buckets[b]))
-        for b in order:
-            g = ar.bucket_grad(b)
-            rd = engine.reduce_dtype or g.dtype
-            plan.append(_op("reduce_scatter" if zero else "all_reduce", "backward", g.numel(), rd, f"bucket{b}", W))
+        if zero:
+            # buckets complete in reverse unit order during backward
+            order = sorted(range(len(ar.buckets)), key=lambda b: -max(ar.buckets[b]))
+            for b in order:
+                g = ar.bucket_grad(b)
+                rd = engine.reduce_dtype or g.dtype
+                plan.append(_op("reduce_scatter", "backward", g.numel(), rd, f"bucket{b}", W))
+        else:
+            # DDP all-reduces launch groups (runs of buckets, merged by the warm-up adaptation)
+            order = sorted(range(len(engine.groups)), key=lambda gi: -max(engine.groups[gi]))
+            for gi in order:
+                g = engine._group_grad(gi)
+                rd = engine.reduce_dtype or g.dtype
+                plan.append(_op("all_reduce", "backward", g.numel(), rd, f"group{gi}", W))
         if zero:
             plan.append(_op("all_reduce", "clip", 1, torch.float32, "grad_sq_norm", W))
             for b in range(len(ar.buckets)):

@@ -35,7 +35,11 @@ class DDPEngine(LocalEngine):
         self.arena = Arena(model, device, dtype, self.world_size, bucket_mb * 2 ** 20)
         self.bucket_mb = bucket_mb
         from .commstats import CommStats
-        self.comm = CommStats(device)
+        self.comm = CommStats(device, self.world_size)
+        self.adapt_log: List[dict] = []
+        # launch groups: runs of consecutive arena buckets all-reduced as ONE collective over
+        # their contiguous range (the arena keeps its buckets; the warm-up adaptation merges them)
+        self._set_groups(bucket_mb)
         self.reduce_dtype = reduce_dtype if reduce_dtype not in (None, dtype) else None
         # a single rank has nothing to average with: no broadcast, no all-reduce (same hooks)
         from . import force_comm
@@ -55,42 +59,88 @@ class DDPEngine(LocalEngine):
             if u.frozen is not None:
                 dist.broadcast(u.frozen.data, src=0, group=self.pg)
 
+    def _set_groups(self, group_mb: float):
+        """Group consecutive buckets (in backward completion order: last bucket first) until a
+        group holds >= group_mb of gradient."""
+        ar = self.arena
+        elt = ar.grad.element_size()
+        groups, cur, sz = [], [], 0
+        for b in reversed(range(len(ar.buckets))):
+            cur.insert(0, b)
+            s, e = ar.ranges[b]
+            sz += (e - s) * elt
+            if sz >= group_mb * 2 ** 20:
+                groups.append(cur)
+                cur, sz = [], 0
+        if cur:
+            groups.append(cur)
+        self.groups = groups[::-1]
+        self.group_of = {b: gi for gi, g in enumerate(self.groups) for b in g}
+        self.bucket_mb = group_mb
+
     # ------------------------------------------------------------------ hooks
     def pre_backward(self, unit):
         if not self._started:
             self._started = True
-            self._pending = [len(b) for b in self.arena.buckets]
+            self._pending = [sum(len(self.arena.buckets[b]) for b in g) for g in self.groups]
             self._works = []
 
     def post_backward(self, unit):
         if self.no_comm or not self.sync_grads or unit.index not in self.arena.bucket_of:
             return
-        b = self.arena.bucket_of[unit.index]
-        self._pending[b] -= 1
-        if self._pending[b] == 0:
-            self._launch(b)
+        gi = self.group_of[self.arena.bucket_of[unit.index]]
+        self._pending[gi] -= 1
+        if self._pending[gi] == 0:
+            self._launch(gi)
 
-    def _launch(self, b):
-        g = self.arena.bucket_grad(b)
+    def _group_grad(self, gi):
+        bs = self.groups[gi]
+        return self.arena.grad[self.arena.ranges[bs[0]][0]:self.arena.ranges[bs[-1]][1]]
+
+    def _launch(self, gi):
+        g = self._group_grad(gi)
         if self.reduce_dtype is not None:
             tmp = g.to(self.reduce_dtype)
             w = dist.all_reduce(tmp, group=self.pg, async_op=True)
+            self.comm.issued("all_reduce", w, tmp.numel() * tmp.element_size())
             self._works.append((w, tmp, g))
         else:
-            self._works.append((dist.all_reduce(g, group=self.pg, async_op=True), None, None))
+            w = dist.all_reduce(g, group=self.pg, async_op=True)
+            self.comm.issued("all_reduce", w, g.numel() * g.element_size())
+            self._works.append((w, None, None))
 
     def finish_backward(self):
         if self.sync_grads and not self.no_comm:
-            for b, n in enumerate(self._pending):
+            for gi, n in enumerate(self._pending):
                 if n > 0:  # units that saw no backward this step (e.g. frozen paths)
-                    self._launch(b)
+                    self._launch(gi)
             for w, tmp, g in self._works:
                 with self.comm.waiting("all_reduce"):
                     w.wait()
+                self.comm.completed(w)
                 if tmp is not None:
                     g.copy_(tmp)
         self._works = []
         self._started = False
+
+    def adapt(self, step_ms: float) -> Optional[dict]:
+        """Warm-up adaptation: if the exposed all-reduce wait (MAX over ranks) exceeds
+        ``ADAPT_FRAC`` of the step, double the launch-group size (fewer, larger all-reduces:
+        per-collective latency amortised over more bytes on the point-to-point xGMI links).
+        The same MAX on every rank keeps the collective order identical."""
+        if self.no_comm:
+            return None
+        from .commstats import ADAPT_FRAC, max_over_ranks
+        s = self.comm.summary()
+        ar, step = max_over_ranks([s.get("all_reduce", {}).get("ms", 0.0), step_ms], self.pg,
+                                  self.arena.grad.device)
+        rec = {"exposed_all_reduce_ms": round(ar, 3), "step_ms": round(step, 2), "bucket_mib": self.bucket_mb}
+        total_mb = self.arena.grad.numel() * self.arena.grad.element_size() / 2 ** 20
+        if ar > ADAPT_FRAC * step and len(self.groups) > 1 and self.bucket_mb < total_mb:
+            self._set_groups(self.bucket_mb * 2)
+            rec["bucket_mib_new"] = self.bucket_mb
+        self.adapt_log.append(rec)
+        return rec
 
     @torch.no_grad()
     def load_full_state_dict(self, sd, strict: bool = True):

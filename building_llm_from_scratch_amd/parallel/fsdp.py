@@ -72,7 +72,8 @@ class FSDPEngine(LocalEngine):
         self.grad_prescale = 1.0 / self.world_size
         self.is_cuda = self.device.type == "cuda"
         from .commstats import CommStats
-        self.comm = CommStats(self.device)
+        self.comm = CommStats(self.device, self.world_size)
+        self.adapt_log: List[Dict] = []
         from . import force_comm
         self.no_shard = self.world_size == 1 and not force_comm()
         dtype = next(model.parameters()).dtype
@@ -143,7 +144,9 @@ class FSDPEngine(LocalEngine):
         self.model.rctx.wait_param_ready(u.index)  # its shard may still be in the optimizer stream
         for fb in st["bufs"]:
             _alloc(fb.data, fb.nbytes)
-            works.append(dist.all_gather_into_tensor(fb.data, fb.shard, group=self.pg, async_op=async_op))
+            w = dist.all_gather_into_tensor(fb.data, fb.shard, group=self.pg, async_op=async_op)
+            self.comm.issued("all_gather", w, fb.nbytes)
+            works.append(w)
         if async_op:
             st["gather_work"] = works
         else:
@@ -155,6 +158,7 @@ class FSDPEngine(LocalEngine):
             with self.comm.waiting("all_gather"):
                 for w in st["gather_work"]:
                     w.wait()
+                    self.comm.completed(w)
             st["gather_work"] = None
             st["gathered"] = True
         if not st["gathered"]:
@@ -197,6 +201,28 @@ class FSDPEngine(LocalEngine):
         nbytes = sum(fb.numel * fb.data.element_size() for fb in big.state["bufs"])
         self.prefetch = fsdp_prefetch_depth(nbytes, numel, tokens, self.world_size)
 
+    # ------------------------------------------------------------------ warm-up adaptation
+    MAX_PREFETCH = 4
+
+    def adapt(self, step_ms: float) -> Optional[Dict]:
+        """Called after a warm-up step with the comm stats of that step: if the exposed
+        all-gather wait (MAX over ranks) exceeds ``ADAPT_FRAC`` of the step, gather one more
+        unit ahead (each costs one gathered unit of HBM).  Every rank takes the same decision
+        from the same MAX, so all ranks keep issuing the same collective order.  Replaces the
+        link / FLOP-rate constants of ``commplan.fsdp_prefetch_depth`` with what the links did."""
+        if self.no_shard:
+            return None
+        from .commstats import ADAPT_FRAC, max_over_ranks
+        s = self.comm.summary()
+        ag, step = max_over_ranks([s.get("all_gather", {}).get("ms", 0.0), step_ms], self.pg, self.device)
+        rec = {"exposed_all_gather_ms": round(ag, 3), "step_ms": round(step, 2), "prefetch": self.prefetch}
+        if ag > ADAPT_FRAC * step and self.prefetch < self.MAX_PREFETCH:
+            self.prefetch += 1
+            self.prefetch_auto = False   # measured, no longer sized from constants
+            rec["prefetch_new"] = self.prefetch
+        self.adapt_log.append(rec)
+        return rec
+
     # ------------------------------------------------------------------ hooks
     def pre_forward(self, unit):
         if self.prefetch_auto and unit.index == 0 and self._prefetch_tokens is None:
@@ -238,9 +264,11 @@ class FSDPEngine(LocalEngine):
                 full = fb.grad.to(self.reduce_dtype)
                 part = torch.empty(fb.grad_shard.numel(), dtype=self.reduce_dtype, device=full.device)
                 w = dist.reduce_scatter_tensor(part, full, group=self.pg, async_op=True)
+                self.comm.issued("reduce_scatter", w, full.numel() * full.element_size())
                 self._rs_works.append((w, fb, full, part))
             else:
                 w = dist.reduce_scatter_tensor(fb.grad_shard, fb.grad, group=self.pg, async_op=True)
+                self.comm.issued("reduce_scatter", w, fb.grad.numel() * fb.grad.element_size())
                 self._rs_works.append((w, fb, None, None))
             # the full gradient is released only after the reduce-scatter completed: freeing it
             # now would hand the block back to the compute stream's allocator pool while RCCL
@@ -255,6 +283,7 @@ class FSDPEngine(LocalEngine):
             w, fb, full, part = self._rs_works.pop(0)
             with self.comm.waiting("reduce_scatter"):
                 w.wait()
+            self.comm.completed(w)
             if part is not None:
                 fb.grad_shard.copy_(part)
             _free(fb.grad)

@@ -37,7 +37,7 @@ class ZeroEngine(LocalEngine):
         self.arena = Arena(model, device, dtype, self.world_size, bucket_mb * 2 ** 20)
         self.bucket_mb = bucket_mb
         from .commstats import CommStats
-        self.comm = CommStats(device)
+        self.comm = CommStats(device, self.world_size)
         from . import force_comm
         self.no_comm = self.world_size == 1 and not force_comm()  # one rank: its shard is the whole bucket
         if not self.no_comm and not self.deferred_init:
@@ -85,9 +85,11 @@ class ZeroEngine(LocalEngine):
             full = g.to(self.reduce_dtype)
             part = torch.empty(self.grad_shards[b].numel(), dtype=self.reduce_dtype, device=g.device)
             w = dist.reduce_scatter_tensor(part, full, group=self.pg, async_op=True)
+            self.comm.issued("reduce_scatter", w, full.numel() * full.element_size())
             self._works.append((w, b, full, part))
         else:
             w = dist.reduce_scatter_tensor(self.grad_shards[b], g, group=self.pg, async_op=True)
+            self.comm.issued("reduce_scatter", w, g.numel() * g.element_size())
             self._works.append((w, b, None, None))
 
     def finish_backward(self):
@@ -97,6 +99,7 @@ class ZeroEngine(LocalEngine):
         for w, b, full, part in self._works:
             with self.comm.waiting("reduce_scatter"):
                 w.wait()
+            self.comm.completed(w)
             if part is not None:
                 self.grad_shards[b].copy_(part)
         self._works = []
@@ -122,12 +125,15 @@ class ZeroEngine(LocalEngine):
         shard = self._shard(full)
         inp = shard if full.device.type == "cuda" else shard.clone()  # RCCL all-gathers in place
         self._ag_works[b] = dist.all_gather_into_tensor(full, inp, group=self.pg, async_op=True)
+        self.comm.issued("all_gather", self._ag_works[b], full.numel() * full.element_size())
 
     def pre_forward(self, unit):
         b = self.arena.bucket_of.get(unit.index)
         if b is not None and b in self._ag_works:
             with self.comm.waiting("all_gather"):
-                self._ag_works.pop(b).wait()
+                w = self._ag_works.pop(b)
+                w.wait()
+            self.comm.completed(w)
 
     def sync(self):
         for w in self._ag_works.values():

@@ -72,6 +72,15 @@ def static_bytes(cfg, world: int = 1, engine: str = "fsdp", elt: int = 2, prefet
     P = cfg.num_params()
     Pt = P * trainable_frac
     opt = 12 * Pt                                       # fp32 master, m, v
+    # LoRA on a frozen, unsharded base (models/linear.py ``_waug``): every augmented block group
+    # keeps [W | B^T] and its transpose [W^T ; B] across steps -- two more copies of the block
+    # weights (the head and embedding are not augmented this way)
+    kaug = 0.0
+    if trainable_frac < 1.0 and not (engine == "fsdp" and world > 1):
+        d, F = cfg.emb_dim, cfg.hidden_dim
+        kv = cfg.n_kv_groups * cfg.head_dim if cfg.is_llama else d
+        per_block = d * (d + 2 * kv) + d * d + (3 if cfg.is_llama else 2) * d * F
+        kaug = 2 * per_block * cfg.n_layers * elt
     if engine == "fsdp" and world > 1:
         d, F, V = cfg.emb_dim, cfg.hidden_dim, cfg.vocab_size
         kv = cfg.n_kv_groups * cfg.head_dim
@@ -82,8 +91,8 @@ def static_bytes(cfg, world: int = 1, engine: str = "fsdp", elt: int = 2, prefet
         gathered = (prefetch + 1) * max(unit, head) + 3 * unit + head
         return (P * elt + Pt * elt + opt) / world + gathered
     if engine == "zero1" and world > 1:
-        return P * elt + Pt * elt + opt / world
-    return P * elt + Pt * elt + opt
+        return P * elt + Pt * elt + opt / world + kaug
+    return P * elt + Pt * elt + opt + kaug
 
 
 def estimate_peak(cfg, batch: int, seq: int, modes: List[str], world: int = 1, engine: str = "fsdp",

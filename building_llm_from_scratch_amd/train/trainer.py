@@ -61,7 +61,8 @@ class Trainer:
                  print_sample_iter=1, eval_iter=1, engine=None, max_grad_norm=1.0, metrics_file=None,
                  loss_scaler: Optional[DynamicLossScaler] = None, max_steps: Optional[int] = None,
                  sample_tokens: int = 200, save_resume: bool = False, world_size: int = 1,
-                 profile_steps: Optional[str] = None, num_workers: int = 0, seed: int = 123):
+                 profile_steps: Optional[str] = None, num_workers: int = 0, seed: int = 123,
+                 comm_adapt_steps: int = 3):
         self.config = config
         self.model = model
         self.optimizer = optimizer
@@ -107,8 +108,14 @@ class Trainer:
             self.profile_steps = (a, b)
         self._prof = None
         self._probed = False
+        # steps 1..comm_adapt_steps feed the engine's warm-up adaptation (parallel/ fsdp, ddp)
+        self.comm_adapt_steps = comm_adapt_steps
 
     # ------------------------------------------------------------------ helpers
+    def _sync(self):
+        if torch.cuda.is_available() and torch.device(self.device).type == "cuda":
+            torch.cuda.synchronize()
+
     def _dist(self) -> bool:
         return self.world_size > 1 and dist.is_available() and dist.is_initialized()
 
@@ -157,6 +164,12 @@ class Trainer:
     def train_batch(self, input_batch, target_batch):
         self.optimizer.zero_grad()
         self.global_step += 1
+        adapting = (self.engine is not None and hasattr(self.engine, "adapt")
+                    and 1 <= self.global_step <= self.comm_adapt_steps)
+        if adapting:   # the engine grows its prefetch / bucket size while a collective wait shows
+            self._sync()
+            self.engine.comm.reset(enabled=True)
+            t_step = time.perf_counter()
         self._profiler_tick()
         lr = self.lr_at(self.global_step)
         for g in self.optimizer.param_groups:
@@ -182,6 +195,12 @@ class Trainer:
             self.optimizer.clip_grad_norm_(self.max_grad_norm)
             self.optimizer.step()
         self.tokens_seen += input_batch.numel() * self.world_size
+        if adapting:
+            self._sync()
+            rec = self.engine.adapt(1e3 * (time.perf_counter() - t_step))
+            self.engine.comm.enabled = False
+            if rec is not None and self.rank == 0 and any(k.endswith("_new") for k in rec):
+                logger.info(f"comm adaptation at step {self.global_step}: {rec}")
         if not self._probed:
             self._probed = True
             self._probe_ckpt_plan()

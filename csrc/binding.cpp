@@ -235,6 +235,8 @@ Tensor swiglu_bwd_lowrank(const Tensor& gu, const Tensor& base, const Tensor& u,
   TORCH_CHECK(u.is_cuda() && u.dim() == 2 && u.size(0) == N && u.size(1) == r && u.stride(1) == 1, "swiglu_bwd_lowrank: u");
   TORCH_CHECK(base.scalar_type() == gu.scalar_type() && u.scalar_type() == gu.scalar_type() &&
                   P.scalar_type() == gu.scalar_type(), "swiglu_bwd_lowrank: dtypes");
+  TORCH_CHECK(gu.scalar_type() == at::kBFloat16 || gu.scalar_type() == at::kHalf, "swiglu_bwd_lowrank: bf16 / fp16");
+  TORCH_CHECK(gu.is_contiguous() && P.is_contiguous(), "swiglu_bwd_lowrank: contiguous gu and P");
   auto dgu = at::empty_like(gu);
   bllm::swiglu_bwd_lr(dt_of(gu), gu.data_ptr(), base.data_ptr(), base.stride(0), u.data_ptr(), u.stride(0),
                       P.data_ptr(), (int)r, (float)scale, dgu.data_ptr(), N, (int)F, stream());

@@ -39,7 +39,8 @@ def _run(n, extra, timeout=600, spawn=False):
     for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
               "scaling", "vs_baseline", "dtype", "data", "config"):
         assert k in out, k
-    assert out["n_gpus"] == n and out["steps"] == 2 and out["warmup"] == 1 and out["value"] > 0
+    warm = int(extra[extra.index("--warmup") + 1]) if "--warmup" in extra else 1
+    assert out["n_gpus"] == n and out["steps"] == 2 and out["warmup"] == warm and out["value"] > 0
     assert out["rccl_world"] == n                # the process group really had N ranks
     assert len(out["per_rank"]["ms_per_step"]) == n
     assert out["per_rank"]["ms_per_step_max"] == out["ms_per_step"]
@@ -171,3 +172,28 @@ def test_telemetry_summary_math():
     assert tunableop_status(None) is None
     st = tunableop_status(os.path.join(ROOT, "configs", "tunableop_llama3_8b_b40_mi355x.csv"))
     assert st["file_rows"] >= 5    # validators compared on a GPU box only
+
+
+@pytest.mark.parametrize("parallel", ["fsdp", "ddp"])
+def test_bench_warmup_comm_adaptation_world4(parallel, monkeypatch):
+    """A slow link on rank 1 only (injected wait, BLLM_COMM_DELAY_MS) makes the exposed
+    collective wait exceed 2 % of the step; the warm-up adaptation then grows the FSDP prefetch
+    depth / the DDP bucket size.  The decision uses the MAX over ranks, so every rank ends on
+    the same value (same collective order), and the JSON carries the achieved bandwidth."""
+    monkeypatch.setenv("BLLM_COMM_DELAY_MS", "40")
+    monkeypatch.setenv("BLLM_COMM_DELAY_RANKS", "1")
+    extra = ["--parallel", parallel, "--warmup", "4"] + (["--fsdp_prefetch", "1"] if parallel == "fsdp" else [])
+    if parallel == "ddp":
+        extra += ["--bucket_mb", "0.02", "--actv_ckpt", "none"]
+    # (--warmup given twice: argparse keeps the last)
+    out = _run(4, extra)
+    c = out["comm"]
+    assert len(c["adapted"]) == 3                      # warm-up steps 1..3 (step 0 is cold)
+    if parallel == "fsdp":
+        assert c["fsdp_prefetch"] > 1 and any("prefetch_new" in r for r in c["adapted"])
+        assert len(set(c["per_rank_fsdp_prefetch"])) == 1 and c["per_rank_fsdp_prefetch"][0] == c["fsdp_prefetch"]
+        assert c["gbps_by_kind"]["all_gather"]["count"] > 0 and c["gbps_by_kind"]["all_gather"]["algbw_gbps"] > 0
+    else:
+        assert c["bucket_mib"] > 0.02 and any("bucket_mib_new" in r for r in c["adapted"])
+        assert len(set(c["per_rank_bucket_mib"])) == 1
+        assert c["gbps_by_kind"]["all_reduce"]["busbw_gbps"] > 0

@@ -128,3 +128,14 @@ def test_meta_built_lora_init():
     assert a.abs().max() > 0
     assert torch.count_nonzero(sd["trf_blocks.0.att.W_query.lora.B"]) == 0
     assert sd["trf_blocks.0.att.W_query.linear.weight"].abs().max() > 0
+
+
+def test_meta_init_leaves_caller_rng_untouched():
+    """Per-unit seeded initialisation runs under a forked RNG: the caller's stream continues
+    exactly where it was (dropout, sampling and shuffling are not re-seeded by the build)."""
+    torch.manual_seed(4242)
+    expect = torch.rand(5)
+    torch.manual_seed(4242)
+    m = _meta_model()
+    setup_engine(m, "local", device=torch.device("cpu"))
+    assert torch.equal(torch.rand(5), expect)

@@ -78,6 +78,11 @@ def test_bench_headline_path_world2_one_gpu_matches_world1():
     assert len(set(a)) == len(a)                         # four different batches, weights moving
     assert two["comm_exposed_ms"] > 0 and forced["comm_exposed_ms"] > 0, (two["comm"], forced["comm"])
     assert set(forced["comm"]["by_kind_rank0"]) >= {"all_gather", "reduce_scatter"}, forced["comm"]
+    # achieved bandwidth per collective kind from RCCL's own start / end events
+    bw = forced["comm"]["gbps_by_kind"]
+    for kind in ("all_gather", "reduce_scatter"):
+        assert bw[kind]["count"] > 0 and bw[kind]["algbw_gbps"] > 0, bw
+        assert bw[kind]["timing"] == "rccl events", bw
     os.makedirs("gpurun_out", exist_ok=True)
     with open(os.path.join("gpurun_out", "bench_world2_one_gpu.json"), "w") as f:
         json.dump({"world1": one, "world2_one_gpu": two, "world1_forced_comm": forced}, f, indent=1)

@@ -93,3 +93,19 @@ def test_block_modes_drive_the_model():
     assert [m.rctx.block_mode(i) for i in range(4)] == ["full", "selective", "selective", "none"]
     m.set_actv_ckpt("full")
     assert m.ckpt_summary()["full"] == 3
+
+
+def test_lora_kaug_copies_counted():
+    """A frozen base under LoRA keeps two augmented copies of the block weights per rank
+    (models/linear.py _waug) unless FSDP shards the base: memplan counts them."""
+    from building_llm_from_scratch_amd.config import get_config
+    from building_llm_from_scratch_amd.train import memplan
+    cfg = get_config("llama3", "8B")
+    full = memplan.static_bytes(cfg, world=8, engine="ddp", elt=2, trainable_frac=1.0)
+    lora = memplan.static_bytes(cfg, world=8, engine="ddp", elt=2, trainable_frac=0.0)
+    blocks = cfg.n_layers * 218.11e6        # SURVEY §2.5 per-block params
+    # full: params + grads + 12 B/param optimizer; lora: params + 2 block copies
+    assert abs(lora - (cfg.num_params() * 2 + 2 * blocks * 2)) / lora < 0.01
+    assert full > lora
+    sharded = memplan.static_bytes(cfg, world=8, engine="fsdp", elt=2, trainable_frac=0.0)
+    assert sharded < lora / 4    # no augmented copies under FSDP sharding

@@ -307,19 +307,15 @@ def test_fused_bias_gelu_epilogue_in_model(ckpt, monkeypatch):
         assert _rel(g1[k], g0[k]) < 2e-2, (k, _rel(g1[k], g0[k]))
 
 
-@pytest.mark.parametrize("mode", ["on", "auto"])
-def test_gemm_nt_kernel_in_model(mode, monkeypatch):
-    """BLLM_GEMM_NT: the forward-layout GEMMs (projections, the dX GEMMs on the transposed weight
-    copy, the fused head's logits and dh) on csrc/gemm_nt.hip (always, or per-shape timed
-    selection) give hipBLASLt's loss and gradients to rounding (B*T = 512 tokens: every GEMM
-    takes the kernel)."""
+def test_gemm_nt_kernel_in_model(monkeypatch):
+    """BLLM_GEMM_NT=1: the forward-layout GEMMs (projections, the dX GEMMs on the transposed
+    weight copy, the fused head's logits and dh) on csrc/gemm_nt.hip give hipBLASLt's loss and
+    gradients to rounding (B*T = 512 tokens: every GEMM takes the kernel)."""
     from building_llm_from_scratch_amd.models import linear
     ops.load_ext(required=True)
     cfg = _cfgs()["llama_hd64"].replace(dtype=torch.bfloat16, vocab_size=1024)
     idx = torch.randint(0, cfg.vocab_size, (2, 257), device="cuda")
     monkeypatch.setattr(linear, "DGRAD_WT_MIN_TOKENS", 256)
-    monkeypatch.setattr(linear, "GEMM_NT_MODE", "auto" if mode == "auto" else "1")
-    monkeypatch.setattr(linear, "_NT_PICK", {})
     calls = []
     orig = ops.gemm_nt_
     monkeypatch.setattr(ops, "gemm_nt_", lambda *a: (calls.append(1), orig(*a))[1])
@@ -333,8 +329,6 @@ def test_gemm_nt_kernel_in_model(mode, monkeypatch):
         loss.backward()
         res[on] = (loss.item(), {k: p.grad.float().clone() for k, p in m.named_parameters()})
     assert len(calls) >= 10, len(calls)
-    if mode == "auto":
-        assert linear._NT_PICK and set(linear._NT_PICK.values()) <= {False, True}, linear._NT_PICK
     (l0, g0), (l1, g1) = res[False], res[True]
     assert abs(l0 - l1) < 1e-2 * abs(l0)
     for k in g0:
