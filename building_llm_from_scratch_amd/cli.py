@@ -120,6 +120,8 @@ def build_parser() -> argparse.ArgumentParser:
     x.add_argument("--no_reshard_after_forward", action="store_true",
                    help="FSDP: keep gathered params from forward to backward (ZeRO-2 style)")
     x.add_argument("--no_plot", action="store_true")
+    x.add_argument("--skip_final_save", action="store_true",
+                   help="do not write model_pg_final.pth (throughput runs of multi-GB models)")
     x.add_argument("--profile_steps", type=str, default=None,
                    help="torch.profiler window 'first:last' (global steps) -> chrome trace in --output_dir")
     return p
@@ -246,7 +248,8 @@ def main(rank: int, args):
         logger.info("Training complete. Final model saved.")
         if device.type == "cuda":
             logger.info(f"Maximum GPU memory used: {torch.cuda.max_memory_allocated() / 1e9:.2f} GB")
-    trainer.save_checkpoint("model_pg_final.pth")
+    if not args.skip_final_save:
+        trainer.save_checkpoint("model_pg_final.pth")
     if args.run_type == "multi_gpu":
         dist.barrier()
         dist.destroy_process_group()

@@ -108,6 +108,7 @@ class Trainer:
             self.profile_steps = (a, b)
         self._prof = None
         self._probed = False
+        self._data_wait = 0.0
         # steps 1..comm_adapt_steps feed the engine's warm-up adaptation (parallel/ fsdp, ddp)
         self.comm_adapt_steps = comm_adapt_steps
 
@@ -235,7 +236,15 @@ class Trainer:
         it = iter(train_loader)
         if skip_batches:
             it = itertools.islice(it, skip_batches, None)
-        for bi, (input_batch, target_batch) in enumerate(it, start=skip_batches):
+        bi = skip_batches - 1
+        while True:
+            t_wait = time.perf_counter()
+            try:
+                input_batch, target_batch = next(it)
+            except StopIteration:
+                break
+            self._data_wait += time.perf_counter() - t_wait   # host time blocked on the loader
+            bi += 1
             self.pos = (epoch_no, file_index, bi + 1)
             loss = self.train_batch(input_batch, target_batch)
             if self.global_step % self.eval_freq == 0:
@@ -259,11 +268,18 @@ class Trainer:
                     logger.info(f"Epoch {epoch_no + 1} | Step {self.global_step} "
                                 f"| Train Loss: {train_loss:.3f} | Val Loss: {val_loss:.3f}"
                                 + (f" | {tps:,.0f} tok/s" if tps else ""))
+                    cuda = torch.cuda.is_available()
                     self.metrics.write(step=self.global_step, epoch=epoch_no, train_loss=train_loss,
                                        val_loss=val_loss, lr=self.track_lrs[-1], tokens_seen=self.tokens_seen,
                                        tokens_per_s=tps, batch_loss=lv,
-                                       max_mem_gb=(torch.cuda.max_memory_allocated() / 1e9
-                                                   if torch.cuda.is_available() else None))
+                                       # host seconds blocked on the data loader since the last
+                                       # eval point, and the caching allocator's cumulative
+                                       # free-and-retry count (each one a device sync)
+                                       data_wait_s=round(self._data_wait, 4),
+                                       alloc_retries=(torch.cuda.memory_stats().get("num_alloc_retries", 0)
+                                                      if cuda else None),
+                                       max_mem_gb=(torch.cuda.max_memory_allocated() / 1e9 if cuda else None))
+                self._data_wait = 0.0
             if self.print_sample_iter and self.global_step % self.print_sample_iter == 0:
                 self.generate_and_print_sample(start_context)
             if self.save_ckpt_freq and self.global_step % self.save_ckpt_freq == 0:

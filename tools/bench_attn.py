@@ -32,6 +32,9 @@ def main():
     ap.add_argument("--shapes", default="", help="comma-separated shape names (default: all)")
     ap.add_argument("--noncausal", action="store_true", help="full (non-causal) attention")
     ap.add_argument("--T", type=int, default=None, help="override the sequence length")
+    ap.add_argument("--env_ab", default="",
+                    help="NAME: time the forward with env NAME=0 and NAME=1 in this process (A/B of a "
+                         "kernel variant read per launch) and report the outputs' max difference")
     ap.add_argument("--no_mask", action="store_true",
                     help="dropout shapes: re-hash the keep bits in backward instead of reading the forward's mask")
     a = ap.parse_args()
@@ -60,6 +63,22 @@ def main():
         tb = timeit(lambda: ops.flash_attn_bwd(qkv, o, lse, do, B, T, H, G, hd, causal, p, 1, 0, keep_mask=km),
                     a.iters)
         flop = 2 * 2 * B * H * T * T * hd / (2 if causal else 1)  # two matmuls (causal: half the square)
+        if a.env_ab:
+            ab = {}
+            outs = {}
+            for rnd in range(3):
+                for v in ("0", "1"):
+                    os.environ[a.env_ab] = v
+                    t = timeit(lambda: ops.flash_attn_fwd(qkv, B, T, H, G, hd, causal, p, 1, 0, keep_mask=km), a.iters)
+                    ab.setdefault(v, []).append(t)
+                    outs[v] = ops.flash_attn_fwd(qkv, B, T, H, G, hd, causal, p, 1, 0, keep_mask=km)
+            os.environ.pop(a.env_ab)
+            med = {v: sorted(ts)[1] for v, ts in ab.items()}
+            (o0, l0), (o1, l1) = outs["0"], outs["1"]
+            print(json.dumps(dict(shape=name, ab=a.env_ab, fwd_ms_0=round(med["0"], 4), fwd_ms_1=round(med["1"], 4),
+                                  tflops_0=round(flop / med["0"] / 1e9, 1), tflops_1=round(flop / med["1"] / 1e9, 1),
+                                  max_abs_o=float((o0.float() - o1.float()).abs().max()),
+                                  max_abs_lse=float((l0 - l1).abs().max()))), flush=True)
         res.append(dict(shape=name, B=B, T=T, causal=causal, keep_mask=km is not None, fwd_ms=round(tf, 4), bwd_ms=round(tb, 4),
                         fwd_tflops=round(flop / tf / 1e9, 1), bwd_tflops_5mm=round(2.5 * flop / tb / 1e9, 1)))
     for r in res:
