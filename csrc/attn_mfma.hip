@@ -83,7 +83,7 @@ template <typename T> __device__ __forceinline__ uint32_t pack2(float a, float b
 // per-lane offsets, 2x(LD) saddr DMA issues with precomputed per-lane source offsets, and
 // ~130 VALU of online softmax (scale folded into the exp2 FMA; the O rescale is skipped when
 // no lane's running max moved, which is the common case after the first tiles).
-template <typename T, int HD, bool DROP, int FWD_BK, int NBUF, int OCC, bool PIPE = false>
+template <typename T, int HD, bool DROP, int FWD_BK, int NBUF, int OCC>
 __global__ __launch_bounds__(256, OCC) void attn_fwd_mfma_k(const T* __restrict__ qkv, T* __restrict__ out,
                                                           float* __restrict__ lse, int T_, int H, int G, int B_,
                                                           bool causal, uint32_t thr, float inv_keep, uint64_t seed,
@@ -398,118 +398,6 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd_mfma_k(const T* __restrict_
         }
       }
   };
-  // ---- pipelined body of a full 64-key tile (NKT == 2, no dropout): the two 32-key sub-tiles
-  // are software-pipelined inside the wave so that its own VALU work rides under its own MFMAs
-  //   A: S0 = K0 Q^T            (K1 fragments read under it)
-  //   B: S1 = K1 Q^T            || softmax of S0 (max, rescale decision, exp, pack); V0 reads
-  //   C: O += V0^T P0           || softmax of S1; V1 reads
-  //   D: O += V1^T P1
-  // Program order is pinned per MFMA slot with sched_barrier(0) (the VALU chunk of a slot is
-  // issued between two MFMAs of the wave, where the matrix pipe is busy anyway).  The online
-  // softmax runs per 32-key sub-tile (the running max may move twice per tile); the deferred
-  // rescale of O is applied between phases, after the MFMAs that still accumulate against the
-  // old max (rare, wave-uniform branch).
-  auto body_pipe = [&](auto edge_c, int k0, const char* kb, const char* vb) {
-    constexpr bool EDGE = decltype(edge_c)::value;
-    f32x16 sa = f32x16{}, sb = f32x16{};
-    v8 kf0[KK], kf1[KK], vf0[2 * DT], vf1[2 * DT];
-    v8 pa[2], pb[2];
-    float mxa = -INFINITY, mxb = -INFINITY, lsa = 0.f, lsb = 0.f, al_a = 1.f, al_b = 1.f;
-    bool ra = false, rb = false;
-    auto kread = [&](int kt, int kk) -> v8 { return *reinterpret_cast<const v8*>(kb + kt * 32 * ROWB + koff[kk]); };
-    auto vread = [&](int kt, int f) -> v8 {   // fragment f = s2 * DT + dt of sub-tile kt
-      const int s2 = f / DT, dt = f % DT;
-      const int off = voff[dt] + (kt * 32 + s2 * 16) * ROWB;
-      const s16x4 r1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(vb + off));
-      const s16x4 r2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(vb + off + 8 * ROWB));
-      return __builtin_bit_cast(v8, __builtin_shufflevector(r1, r2, 0, 1, 2, 3, 4, 5, 6, 7));
-    };
-    // softmax of sub-tile kt in 8 steps: 0-1 masked max (8 elements each), 2 max exchange +
-    // rescale decision, 3-6 exp + row sum (4 elements each), 7 pack P into 2 MFMA operands
-    auto sm_step = [&](f32x16& s, int kt, int st, float& mx, float& ls, float& al, bool& resc, v8 (&pf)[2]) {
-      if (st <= 1) {
-        if constexpr (EDGE) {
-          const int lim = (causal ? min(qi[0], T_ - 1) : T_ - 1) - (k0 + 4 * hh);
-#pragma unroll
-          for (int r = 8 * st; r < 8 * st + 8; ++r)
-            if (kt * 32 + (r & 3) + 8 * (r >> 2) > lim) s[r] = -INFINITY;
-        }
-#pragma unroll
-        for (int r = 8 * st; r < 8 * st + 8; ++r) mx = fmaxf(mx, s[r]);
-      } else if (st == 2) {
-        const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
-        const float ms = fmaxf(mx, fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]))) * c;
-        resc = __builtin_amdgcn_ballot_w64(ms > m[0] + kRescaleThr) != 0;
-        const float mn = resc ? fmaxf(m[0], ms) : m[0];
-        al = resc ? __builtin_amdgcn_exp2f(m[0] - mn) : 1.f;
-        m[0] = mn;
-        l[0] *= al;
-      } else if (st <= 6) {
-#pragma unroll
-        for (int r = 4 * (st - 3); r < 4 * (st - 3) + 4; ++r) {
-          const float pv = __builtin_amdgcn_exp2f(fmaf(s[r], c, -m[0]));
-          ls += pv;
-          s[r] = pv;
-        }
-        // anchor: keeps this step's exps in its MFMA slot (LLVM otherwise sinks them to their
-        // first use, the PV MFMAs, past the rescale branch)
-        asm volatile("" : "+v"(s), "+v"(ls));
-      } else {
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) {
-          uint32_t uu[4];
-#pragma unroll
-          for (int j = 0; j < 4; ++j) uu[j] = pack2<T>(s[8 * s2 + 2 * j], s[8 * s2 + 2 * j + 1]);
-          __builtin_memcpy(&pf[s2], uu, 16);
-        }
-        l[0] += ls;
-        asm volatile("" : "+v"(pf[0]), "+v"(pf[1]));
-      }
-    };
-    // ---- A: S0 (K1 fragments read under it)
-#pragma unroll
-    for (int kk = 0; kk < KK; ++kk) kf0[kk] = kread(0, kk);
-#pragma unroll
-    for (int kk = 0; kk < KK; ++kk) {
-      sa = MF<T>::mma(kf0[kk], qf[0][kk], sa);
-      kf1[kk] = kread(1, kk);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    // ---- B: S1 || softmax(S0); V0 fragments read
-#pragma unroll
-    for (int kk = 0; kk < KK; ++kk) {
-      sb = MF<T>::mma(kf1[kk], qf[0][kk], sb);
-#pragma unroll
-      for (int st = kk * 8 / KK; st < (kk + 1) * 8 / KK; ++st) sm_step(sa, 0, st, mxa, lsa, al_a, ra, pa);
-#pragma unroll
-      for (int f = kk * 2 * DT / KK; f < (kk + 1) * 2 * DT / KK; ++f) vf0[f] = vread(0, f);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    if (ra) {   // S0 moved the max: O (all earlier tiles) to the new reference, before P0 V0
-#pragma unroll
-      for (int i = 0; i < DT; ++i) o[0][i] *= al_a;
-    }
-    // ---- C: O += V0^T P0 || softmax(S1); V1 fragments read
-#pragma unroll
-    for (int f = 0; f < 2 * DT; ++f) {
-      const int s2 = f / DT, dt = f % DT;
-      o[0][dt] = MF<T>::mma(vf0[f], pa[s2], o[0][dt]);
-#pragma unroll
-      for (int st = f * 8 / (2 * DT); st < (f + 1) * 8 / (2 * DT); ++st) sm_step(sb, 1, st, mxb, lsb, al_b, rb, pb);
-      vf1[f] = vread(1, f);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    if (rb) {   // S1 moved the max: rescale O (including P0 V0) before P1 V1
-#pragma unroll
-      for (int i = 0; i < DT; ++i) o[0][i] *= al_b;
-    }
-    // ---- D: O += V1^T P1
-#pragma unroll
-    for (int f = 0; f < 2 * DT; ++f) {
-      const int s2 = f / DT, dt = f % DT;
-      o[0][dt] = MF<T>::mma(vf1[f], pb[s2], o[0][dt]);
-    }
-  };
   using Ic1 = std::integral_constant<int, 1>;
   using IcN = std::integral_constant<int, NKT>;
   using Yes = std::true_type;
@@ -524,8 +412,7 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd_mfma_k(const T* __restrict_
     if (t + NBUF - 1 < ntiles) issue(t + NBUF - 1, buf == 0 ? NBUF - 1 : buf - 1);
     kw_t = t;
     const char* kb = smem + buf * 2 * TILE_B;
-    if constexpr (PIPE && !DROP && NKT == 2 && QB == 1) body_pipe(No{}, t * FWD_BK, kb, kb + TILE_B);
-    else body(IcN{}, No{}, t * FWD_BK, kb, kb + TILE_B);
+    body(IcN{}, No{}, t * FWD_BK, kb, kb + TILE_B);
     ring_wait(t);  // the DMA of tile t+1 has landed (asm-issued, so drained by hand)
     buf = buf == NBUF - 1 ? 0 : buf + 1;
   }
@@ -537,12 +424,8 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd_mfma_k(const T* __restrict_
     kw_t = t;
     const char* kb = smem + buf * 2 * TILE_B;
     const int kvis = min(causal ? wq_hi : T_ - 1, T_ - 1) - k0;  // >= 0 for an active tile
-    if (NKT == 1 || kvis >= 32) {
-      if constexpr (PIPE && !DROP && NKT == 2 && QB == 1) body_pipe(Yes{}, k0, kb, kb + TILE_B);
-      else body(IcN{}, Yes{}, k0, kb, kb + TILE_B);
-    } else {
-      body(Ic1{}, Yes{}, k0, kb, kb + TILE_B);
-    }
+    if (NKT == 1 || kvis >= 32) body(IcN{}, Yes{}, k0, kb, kb + TILE_B);
+    else body(Ic1{}, Yes{}, k0, kb, kb + TILE_B);
     ring_wait(t);
     buf = buf == NBUF - 1 ? 0 : buf + 1;
   }
@@ -588,10 +471,6 @@ void attn_fwd_mfma(DType dt, const void* qkv, void* o, float* lse, int B, int T_
   const uint32_t thr = drop_threshold16(p);
   const float ik = drop_inv_keep(p);
   const bool small = fwd_small_tiles(hd, p, (long)((T_ + FWD_BQ - 1) / FWD_BQ) * H * B);
-  // BLLM_ATTN_PIPE=1: the sub-tile-pipelined body (A/B; read per launch so one process can
-  // time both)
-  const char* pe = getenv("BLLM_ATTN_PIPE");
-  const bool pipe = pe != nullptr && atoi(pe) != 0;
 #define LAUNCH_V(TT, HDD, BK, NB, OC)                                                                      \
   do {                                                                                                        \
     const int lds = NB * 2 * BK * HDD * 2;                                                                    \
@@ -599,9 +478,6 @@ void attn_fwd_mfma(DType dt, const void* qkv, void* o, float* lse, int B, int T_
     if (p > 0.f)                                                                                              \
       hipLaunchKernelGGL((attn_fwd_mfma_k<TT, HDD, true, BK, NB, OC>), grid, block, lds, s,          \
                          (const TT*)qkv, (TT*)o, lse, T_, H, G, B, causal, thr, ik, seed, offset, keep_mask); \
-    else if (pipe)                                                                                            \
-      hipLaunchKernelGGL((attn_fwd_mfma_k<TT, HDD, false, BK, NB, OC, true>), grid, block, lds, s,   \
-                         (const TT*)qkv, (TT*)o, lse, T_, H, G, B, causal, thr, ik, seed, offset, nullptr); \
     else                                                                                                      \
       hipLaunchKernelGGL((attn_fwd_mfma_k<TT, HDD, false, BK, NB, OC>), grid, block, lds, s,         \
                          (const TT*)qkv, (TT*)o, lse, T_, H, G, B, causal, thr, ik, seed, offset, nullptr); \

@@ -41,7 +41,6 @@ constexpr int ROWB = TK * 2;             // 128 B per LDS row (one K-tile of one
 constexpr int IMGB = TM * ROWB;          // 32 KiB per operand image
 constexpr int BUFB = 2 * IMGB;           // A + B
 constexpr int LDS_BYTES = 2 * BUFB;      // double buffer, 128 KiB
-constexpr int LDS_PF = LDS_BYTES + 4 * 256;   // + the prefetch scratch slots (PFD > 0)
 constexpr int GROUP_M = 4;               // tile-group depth (4 measured best of 1-32, profiles/r3)
 
 using g4::EPI_NONE;
@@ -75,11 +74,7 @@ struct Sched4 {
 //   0  XCD-contiguous: XCD x walks a contiguous range of the grouped tile order (its own M-band)
 //   1  plain: tile order dealt round-robin over the XCDs (what an XCD-unaware launch does)
 //   2  XCD-contiguous over the TRANSPOSED grid: each XCD owns an N-band (B private, A shared)
-// PFD > 0: besides the 2-deep LDS ring, one dword per staged row of K-tile t + PFD is loaded
-// (LDS-DMA into a scratch slot) right after each RAW barrier, so the lines are in L2 / MALL before
-// the ring's own pieces ask for them (an L2 prefetch ahead of the LDS prefetch).
-constexpr int PF_SLOT = LDS_BYTES;         // 256-B scratch per wave behind the ring
-template <typename T, typename OT, bool ACC, int EPI = EPI_NONE, int PFD = 0>
+template <typename T, typename OT, bool ACC, int EPI = EPI_NONE>
 __global__ __launch_bounds__(THREADS4, 1) void gemm_nt4p_k(const T* __restrict__ A, long lda,
                                                            const T* __restrict__ B, long ldb, OT* __restrict__ C,
                                                            long ldc, int M, int N, int K, OT* __restrict__ act = nullptr,
@@ -175,27 +170,6 @@ __global__ __launch_bounds__(THREADS4, 1) void gemm_nt4p_k(const T* __restrict__
     dsel(t);
     dmap(buf, k);
   };
-  // L2 prefetch of K-tile t of the stream: one dword of each of this wave's 64 A rows and 64 B rows
-  // (EPI_NONE row map), into the wave's scratch LDS slot; always exactly 2 VMEM ops so the RAW
-  // barrier's vmcnt stays a constant
-  const uint32_t pfo_a = (uint32_t)lane * ldab, pfo_b = (uint32_t)lane * ldbb;
-  auto l2pf = [&](int t) {
-    const bool nx = t >= nt;
-    const int tt = !nx ? t : (tid_n < nblk ? t - nt : nt - 1);
-    const i32x4 a = nx ? srAn : srAc, b = nx ? srBn : srBc;
-    i32x4 ra, rb;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      ra[e] = __builtin_amdgcn_readfirstlane(a[e]);
-      rb[e] = __builtin_amdgcn_readfirstlane(b[e]);
-    }
-    const uint32_t so = __builtin_amdgcn_readfirstlane((uint32_t)(tt < nt ? tt : nt - 1) * TKB);
-    const uint32_t d = lds0 + PF_SLOT + 256u * wave;
-    asm volatile("s_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dword %0, %1, %2 offen lds\n\t"
-                 "buffer_load_dword %4, %5, %2 offen lds"
-                 ::"v"(pfo_a), "s"(ra), "s"(so), "s"(d), "v"(pfo_b), "s"(rb) : "memory");
-  };
-
   const int xo0 = ((0 + (lane >> 4)) ^ ((lane >> 1) & 7)) << 4;
   const int xo1 = ((4 + (lane >> 4)) ^ ((lane >> 1) & 7)) << 4;
   const char* pA0 = smem + (128 * wm + (lane & 15)) * ROWB + xo0;
@@ -220,8 +194,7 @@ __global__ __launch_bounds__(THREADS4, 1) void gemm_nt4p_k(const T* __restrict__
   for (int k = 0; k < 16; ++k) dma(0, 0, k);
 #pragma unroll
   for (int k = 0; k < 16; ++k) dma(1, 1, k);
-  if constexpr (PFD > 0) l2pf(PFD);   // (keeps the RAW barriers' vmcnt count uniform)
-  wait_vm<(PFD > 0 ? 18 : 16)>();
+  wait_vm<16>();
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
 #pragma unroll
@@ -255,10 +228,9 @@ __global__ __launch_bounds__(THREADS4, 1) void gemm_nt4p_k(const T* __restrict__
       const int i = n >> 3, j = n & 7;
       if (SC::piece(64 + n) >= 0) dmap(cur, SC::piece(64 + n));
       if (64 + n == SC::RAW) {
-        wait_vm<(PFD > 0 ? 18 : 16)>();
+        wait_vm<16>();
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
-        if constexpr (PFD > 0) l2pf(t + PFD);
       }
       if (64 + n >= SC::RAW && (64 + n - SC::RAW) * SC::RPM < 16) {
 #pragma unroll
@@ -429,21 +401,20 @@ inline int grid_of(int M, int N) {
   return nblk < ncu ? nblk : ncu;
 }
 
-template <typename T, typename OT, bool ACC, int EPI, int PFD = 0>
+template <typename T, typename OT, bool ACC, int EPI>
 void set_lds_attr() {
-  static const bool at = hipFuncSetAttribute((const void*)gemm_nt4p_k<T, OT, ACC, EPI, PFD>,
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, LDS_PF) == hipSuccess;
+  static const bool at = hipFuncSetAttribute((const void*)gemm_nt4p_k<T, OT, ACC, EPI>,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES) == hipSuccess;
   (void)at;
 }
 
-// experiment knobs (read once): BLLM_NT_MAP (tile map, see the kernel), BLLM_NT_GM (group depth),
-// BLLM_NT_PF (L2 prefetch distance in K-tiles: 0, 3, 4 or 6)
+// experiment knobs (read once): BLLM_NT_MAP (tile map, see the kernel), BLLM_NT_GM (group
+// depth) -- the round-5 placement A/B (profiles/r5/kernel_experiments.md); defaults ship
 struct NtKnobs {
-  int map = 0, gm = GROUP_M, pf = 0;
+  int map = 0, gm = GROUP_M;
   NtKnobs() {
     if (const char* e = getenv("BLLM_NT_MAP")) map = atoi(e);
     if (const char* e = getenv("BLLM_NT_GM")) gm = atoi(e) > 0 ? atoi(e) : GROUP_M;
-    if (const char* e = getenv("BLLM_NT_PF")) pf = atoi(e);
   }
 };
 static const NtKnobs& knobs() {
@@ -451,39 +422,21 @@ static const NtKnobs& knobs() {
   return k;
 }
 
-template <int PFD>
-void launch_pf(const bf16_t* a, long lda, const bf16_t* b, long ldb, bf16_t* c, long ldc, int M, int N, int K,
-               hipStream_t s) {
-  set_lds_attr<bf16_t, bf16_t, false, EPI_NONE, PFD>();
-  hipLaunchKernelGGL((gemm_nt4p_k<bf16_t, bf16_t, false, EPI_NONE, PFD>), dim3(grid_of(M, N)), dim3(THREADS4), LDS_PF,
-                     s, a, lda, b, ldb, c, ldc, M, N, K, nullptr, 0, nullptr, nullptr, 1, 0, knobs().gm, nullptr,
-                     knobs().map);
-}
-
 template <typename T, typename OT>
 void launch(const void* a, long lda, const void* b, long ldb, void* c, long ldc, int M, int N, int K, bool accumulate,
             hipStream_t s) {
   const int grid = grid_of(M, N);
-  if constexpr (std::is_same<T, bf16_t>::value && std::is_same<OT, bf16_t>::value) {
-    const NtKnobs& kb = knobs();
-    if (!accumulate && (kb.pf || kb.map || kb.gm != GROUP_M)) {
-      const auto* A_ = (const bf16_t*)a;
-      const auto* B_ = (const bf16_t*)b;
-      auto* C_ = (bf16_t*)c;
-      if (kb.pf == 3) return launch_pf<3>(A_, lda, B_, ldb, C_, ldc, M, N, K, s);
-      if (kb.pf == 4) return launch_pf<4>(A_, lda, B_, ldb, C_, ldc, M, N, K, s);
-      if (kb.pf == 6) return launch_pf<6>(A_, lda, B_, ldb, C_, ldc, M, N, K, s);
-      return launch_pf<0>(A_, lda, B_, ldb, C_, ldc, M, N, K, s);
-    }
-  }
+  const NtKnobs& kb = knobs();
   if (accumulate) {
     set_lds_attr<T, OT, true, EPI_NONE>();
     hipLaunchKernelGGL((gemm_nt4p_k<T, OT, true>), dim3(grid), dim3(THREADS4), LDS_BYTES, s, (const T*)a, lda,
-                       (const T*)b, ldb, (OT*)c, ldc, M, N, K);
+                       (const T*)b, ldb, (OT*)c, ldc, M, N, K, nullptr, 0, nullptr, nullptr, 1, 0, kb.gm, nullptr,
+                       kb.map);
   } else {
     set_lds_attr<T, OT, false, EPI_NONE>();
     hipLaunchKernelGGL((gemm_nt4p_k<T, OT, false>), dim3(grid), dim3(THREADS4), LDS_BYTES, s, (const T*)a, lda,
-                       (const T*)b, ldb, (OT*)c, ldc, M, N, K);
+                       (const T*)b, ldb, (OT*)c, ldc, M, N, K, nullptr, 0, nullptr, nullptr, 1, 0, kb.gm, nullptr,
+                       kb.map);
   }
 }
 

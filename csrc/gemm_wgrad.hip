@@ -368,24 +368,31 @@ __global__ __launch_bounds__(Geo::THREADS) void wgrad_gemm_k(const T* __restrict
 //     t+1), then the reads of a0/b0 of tile t+1 over the last 16 MFMAs.
 // The body is branch-free for every tile (past the end the pieces re-load the last tile into a
 // buffer nothing reads again).  Pieces are buffer_load ... lds on a per-K-tile descriptor.
+// tile maps (``map``, experiment knob BLLM_WG_MAP): 0 = XCD-contiguous over GROUP_M-deep column-major
+// groups (each XCD an M-band), 1 = plain bid order, 2 = the same over the transposed grid (each XCD
+// an N-band); ``group_m`` = group depth (BLLM_WG_GM)
 template <typename T, typename OT>
 __global__ __launch_bounds__(g4::THREADS4, 1) void wgrad4_k(const T* __restrict__ A, long lda,
                                                             const T* __restrict__ B, long ldb, OT* __restrict__ C,
                                                             long ldc, long c_split, int M, int N, int K,
-                                                            int accumulate, int wide) {
+                                                            int accumulate, int wide, int map = 0,
+                                                            int group_m = GROUP_M) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int wm = wave >> 1, wn = wave & 1;
 
   const int nbm = M / BM, nbn = N / BN, nblk = nbm * nbn;
   const int bid = blockIdx.x, xcd = bid & 7, q8 = nblk >> 3, r8 = nblk & 7;
-  const int wid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
-  const int per_group = GROUP_M * nbn;
+  const int wid = map == 1 ? bid : (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const bool trg = map == 2;
+  const int gmaj = trg ? nbn : nbm, gmin = trg ? nbm : nbn;
+  const int per_group = group_m * gmin;
   const int grp = wid / per_group;
-  const int first_m = grp * GROUP_M;
-  const int gm = nbm - first_m < GROUP_M ? nbm - first_m : GROUP_M;
+  const int first_m = grp * group_m;
+  const int gm = gmaj - first_m < group_m ? gmaj - first_m : group_m;
   const int in_g = wid - grp * per_group;
-  const int tm = first_m + in_g % gm, tn = in_g / gm;
+  const int ta = first_m + in_g % gm, tb = in_g / gm;
+  const int tm = trg ? tb : ta, tn = trg ? ta : tb;
   const long m0 = (long)tm * BM, n0 = (long)tn * BN;
 
   const int S = gridDim.y, sp = blockIdx.y, nch = K / KCH;
@@ -501,8 +508,12 @@ void launch4(const void* a, long lda, const void* b, long ldb, void* c, long ldc
   const dim3 grid((M / BM) * (N / BN), S);
   const bool wide = reinterpret_cast<uintptr_t>(c) % 16 == 0 && (ldc * (long)sizeof(OT)) % 16 == 0 &&
                     (c_split * (long)sizeof(OT)) % 16 == 0;
+  // experiment knobs, read per launch (A/B in one process): tile map and group depth
+  const char* em = getenv("BLLM_WG_MAP");
+  const char* eg = getenv("BLLM_WG_GM");
+  const int map = em ? atoi(em) : 0, gm = eg && atoi(eg) > 0 ? atoi(eg) : GROUP_M;
   hipLaunchKernelGGL((wgrad4_k<T, OT>), grid, dim3(g4::THREADS4), LDS_BYTES, s, (const T*)a, lda, (const T*)b, ldb,
-                     (OT*)c, ldc, c_split, M, N, K, (int)accumulate, (int)wide);
+                     (OT*)c, ldc, c_split, M, N, K, (int)accumulate, (int)wide, map, gm);
 }
 
 template <typename T, typename OT, bool AK = false>

@@ -299,21 +299,6 @@ def test_flash_attention_deferred_rescale(dt, hd, step):
     _close(dqkv, dqkv0, dt, 4, name="dqkv")
 
 
-@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
-@pytest.mark.parametrize("B,T,H,G,hd", [(2, 64, 4, 4, 64), (1, 200, 8, 2, 128), (2, 33, 4, 2, 64),
-                                         (1, 512, 8, 2, 128), (1, 300, 2, 2, 128), (2, 1024, 4, 1, 128)])
-@pytest.mark.parametrize("causal", [True, False])
-def test_flash_attention_pipelined_fwd(dt, B, T, H, G, hd, causal, monkeypatch):
-    """BLLM_ATTN_PIPE=1: the sub-tile-pipelined forward body (softmax of one 32-key sub-tile under
-    the MFMAs of the other, per-sub-tile online max) against the fp32 oracle, and the backward on
-    its LSE; plus the deferred-rescale sequences that move the max mid-tile."""
-    monkeypatch.setenv("BLLM_ATTN_PIPE", "1")
-    test_flash_attention(dt, B, T, H, G, hd, 0.0, causal)
-    if (B, T) == (1, 512):
-        for hd_, step in ((128, 0.35), (128, 0.6), (64, 0.5)):
-            test_flash_attention_deferred_rescale(dt, hd_, step)
-
-
 @pytest.mark.parametrize("causal", [True, False])
 def test_flash_attention_fwd_small_tiles(causal):
     """hd 64 with dropout on a grid of >= 2048 workgroups (16 x 16 heads x 8 query blocks) takes

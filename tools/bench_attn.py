@@ -35,6 +35,9 @@ def main():
     ap.add_argument("--env_ab", default="",
                     help="NAME: time the forward with env NAME=0 and NAME=1 in this process (A/B of a "
                          "kernel variant read per launch) and report the outputs' max difference")
+    ap.add_argument("--variants", default="",
+                    help="forward A/B arms 'name:VAR=v+VAR2=v;name2:...' (kernel knobs read per launch), "
+                         "timed interleaved with the default; outputs compared with the default's")
     ap.add_argument("--no_mask", action="store_true",
                     help="dropout shapes: re-hash the keep bits in backward instead of reading the forward's mask")
     a = ap.parse_args()
@@ -63,6 +66,22 @@ def main():
         tb = timeit(lambda: ops.flash_attn_bwd(qkv, o, lse, do, B, T, H, G, hd, causal, p, 1, 0, keep_mask=km),
                     a.iters)
         flop = 2 * 2 * B * H * T * T * hd / (2 if causal else 1)  # two matmuls (causal: half the square)
+        if a.variants:
+            arms = [("default", {})] + [(vd.split(":", 1)[0], dict(e.split("=", 1) for e in vd.split(":", 1)[1].split("+") if e))
+                                        for vd in a.variants.split(";") if vd]
+            tt, outs = {}, {}
+            for rnd in range(3):
+                for an, env in arms:
+                    os.environ.update(env)
+                    tt.setdefault(an, []).append(
+                        timeit(lambda: ops.flash_attn_fwd(qkv, B, T, H, G, hd, causal, p, 1, 0, keep_mask=km), a.iters))
+                    outs[an] = ops.flash_attn_fwd(qkv, B, T, H, G, hd, causal, p, 1, 0, keep_mask=km)
+                    for k_ in env:
+                        os.environ.pop(k_)
+            o_ref = outs["default"][0].float()
+            print(json.dumps(dict(shape=name, fwd_tflops={an: round(flop / sorted(v)[1] / 1e9, 1) for an, v in tt.items()},
+                                  max_abs_o={an: float((o[0].float() - o_ref).abs().max()) for an, o in outs.items()})),
+                  flush=True)
         if a.env_ab:
             ab = {}
             outs = {}

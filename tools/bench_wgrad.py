@@ -42,6 +42,9 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--models", default="llama3_8b,gpt2_774m,llama32_1b")
     ap.add_argument("--rounds", type=int, default=3, help="interleaved rounds (median reported)")
+    ap.add_argument("--variants", default="",
+                    help="extra MFMA arms 'name:VAR=v,VAR2=v;name2:...' timed interleaved with the default "
+                         "(kernel knobs read per launch)")
     a = ap.parse_args()
     ops.load_ext(required=True)
     Nt = a.tokens
@@ -62,6 +65,14 @@ def main():
                     timeit(lambda: torch.mm(x.t(), dy, out=g0.t()), a.iters))
                 times.setdefault("mfma_us", []).append(
                     timeit(lambda: ops.wgrad_gemm_(dy, x, g1, False, auto), a.iters))
+                for vd in filter(None, a.variants.split(";")):
+                    vname, kv = vd.split(":", 1)
+                    env = dict(e.split("=") for e in kv.split(",") if e)
+                    os.environ.update(env)
+                    times.setdefault(f"{vname}_us", []).append(
+                        timeit(lambda: ops.wgrad_gemm_(dy, x, g1, False, auto), a.iters))
+                    for k_ in env:
+                        os.environ.pop(k_)
             for k, ts in times.items():
                 r[k] = sorted(ts)[len(ts) // 2]
             g1.zero_()
