@@ -249,16 +249,16 @@ class Trainer:
             loss = self.train_batch(input_batch, target_batch)
             if self.global_step % self.eval_freq == 0:
                 lv = float(loss.item())
+                # training throughput since the last eval point, measured up to this loss read
+                # (a device sync) and restarted after eval / sample / checkpoint: those phases
+                # never count against tok/s
+                now = time.perf_counter()
                 if not math.isfinite(lv):
                     raise FloatingPointError(f"non-finite training loss at step {self.global_step}")
                 train_loss, val_loss = self.evaluate_model(train_loader, val_loader, self.eval_iter)
                 self.train_losses.append(train_loss)
                 self.val_losses.append(val_loss)
                 self.track_tokens_seen.append(self.tokens_seen)
-                # training throughput since the last eval point, measured up to the loss read
-                # above (a device sync) and restarted after eval / sample / checkpoint: those
-                # phases never count against tok/s
-                now = time.perf_counter()
                 tps = None
                 if self._t_last is not None:
                     tps = (self.tokens_seen - self._tok_last) / max(now - self._t_last, 1e-9)

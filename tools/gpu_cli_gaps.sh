@@ -12,3 +12,5 @@ timeout -k 10 600 rocprofv3 --kernel-trace -d gpurun_out/cligaps/bench -o run --
 timeout -k 10 120 python tools/gaps.py "$(find gpurun_out/cligaps/bench -name '*.db' -print -quit)" --top 25 > gpurun_out/cligaps/bench_gaps.txt 2>&1
 cat gpurun_out/cligaps/bench_gaps.txt
 rm -rf gpurun_out/cligaps/cli gpurun_out/cligaps/bench
+timeout -k 10 300 python -u -c 'import __graft_entry__ as g; g.smoke()' > gpurun_out/cligaps/smoke.log 2>&1 || { tail -20 gpurun_out/cligaps/smoke.log; exit 5; }
+grep "smoke ok" gpurun_out/cligaps/smoke.log
