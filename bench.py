@@ -334,21 +334,10 @@ def main(argv=None):
         a.tunableop = None
         os.environ.update(PYTORCH_TUNABLEOP_ENABLED="1", PYTORCH_TUNABLEOP_TUNING="1",
                           PYTORCH_TUNABLEOP_FILENAME=os.path.abspath(a.tunableop_tune).replace(".csv", "%d.csv"))
-    if a.tunableop in ("none", ""):
-        a.tunableop = None
-    if a.tunableop and not os.path.isabs(a.tunableop):
-        a.tunableop = os.path.join(os.path.dirname(os.path.abspath(__file__)), a.tunableop)
-    if a.tunableop and (a.device != "cuda" or not os.path.exists(a.tunableop)):
-        a.tunableop = None
-    if a.tunableop:  # must be set before the first GEMM; TunableOp reads <name><device ordinal>.csv
-        import shutil
-        import tempfile
-        d = tempfile.mkdtemp(prefix="bllm_tunableop_")
-        local = int(os.environ.get("LOCAL_RANK", "0"))
-        # a copy, not a symlink: whatever TunableOp writes back can never reach the shipped table
-        shutil.copyfile(os.path.abspath(a.tunableop), os.path.join(d, f"results{local}.csv"))
-        os.environ.update(PYTORCH_TUNABLEOP_ENABLED="1", PYTORCH_TUNABLEOP_TUNING="0",
-                          PYTORCH_TUNABLEOP_FILENAME=os.path.join(d, "results%d.csv"))
+    from building_llm_from_scratch_amd.utils.gemm_tuning import install_table, resolve_table
+    a.tunableop = resolve_table(a.tunableop) if a.device == "cuda" else None
+    # must be set before the first GEMM
+    install_table(a.tunableop, int(os.environ.get("LOCAL_RANK", "0")))
     import torch
     from building_llm_from_scratch_amd import ops
     from building_llm_from_scratch_amd.models import build_model, replace_linear_with_lora
@@ -636,6 +625,9 @@ def main(argv=None):
         print(json.dumps(out), flush=True)
     if a.tunableop_tune and cuda and hasattr(torch.cuda.tunable, "write_file"):
         torch.cuda.tunable.write_file()     # (newer PyTorch writes the results file at exit itself)
+    # leave together: a rank tearing its gloo pairs down while rank 0 still assembles the line
+    # aborted one rank of eight (SIGABRT at exit) under a loaded CPU test run
+    dist.barrier()
     dist.destroy_process_group()
 
 

@@ -119,6 +119,9 @@ def build_parser() -> argparse.ArgumentParser:
                         "collective wait exceeds 2%% of the step (MAX over ranks)")
     x.add_argument("--no_reshard_after_forward", action="store_true",
                    help="FSDP: keep gathered params from forward to backward (ZeRO-2 style)")
+    x.add_argument("--tunableop", type=str, default="auto",
+                   help="TunableOp GEMM table (read-only): a CSV path, 'auto' = the shipped MI355X table of "
+                        "--model/--num_params if there is one (configs/tunableop_*), or 'none'")
     x.add_argument("--no_plot", action="store_true")
     x.add_argument("--skip_final_save", action="store_true",
                    help="do not write model_pg_final.pth (throughput runs of multi-GB models)")
@@ -181,7 +184,13 @@ def main(rank: int, args):
     from .train.checkpoint import load_resume_state, rank_state_path, resume_state_path
     from .train.trainer import DynamicLossScaler, Trainer
 
+    from .utils.gemm_tuning import install_table, resolve_table
     world = getattr(args, "world_size", 1)
+    if torch.cuda.is_available() and args.device != "cpu":   # before the first GEMM
+        table = resolve_table(args.tunableop, args.model, args.num_params)
+        install_table(table, int(os.environ.get("LOCAL_RANK", rank)))
+        if rank == 0 and table:
+            logger.info(f"GEMM selection table (TunableOp, read-only): {os.path.relpath(table)}")
     if args.run_type == "multi_gpu":
         device = ddp_setup(rank, world, args)
     else:

@@ -44,6 +44,29 @@ def _make_loader(owner, ds, shuffle, drop_last, num_workers, generator):
                       generator=generator if shuffle else None, **workers)
 
 
+def first_batches(loader, n):
+    """The first ``n`` batches ``iter(loader)`` yields, read in this process.
+
+    Evaluation reads ``eval_iter`` (5) batches of each loader every ``eval_freq`` steps.  For a
+    loader with worker processes, ``iter(loader)`` forks its workers each time: ~2 s of GPU idle
+    per loader per evaluation on an MI355X box under a 240 GiB Llama-3-8B run (rocprofv3 gaps,
+    profiles/r5/cli2/gaps.txt).  The batch sampler gives the same batch indices, and five batches
+    of memory-mapped windows collate in milliseconds in the main process.
+    """
+    if n <= 0:
+        return
+    if getattr(loader, "num_workers", 0) == 0 or getattr(loader, "batch_sampler", None) is None:
+        for i, batch in enumerate(loader):
+            if i >= n:
+                break
+            yield batch
+        return
+    for i, idx in enumerate(loader.batch_sampler):
+        if i >= n:
+            break
+        yield loader.collate_fn([loader.dataset[j] for j in idx])
+
+
 class DataloaderPT:
     def __init__(self, tokenizer, batch_size, max_length, stride, eos_text="<|endoftext|>",
                  dataset_name="gutenberg", run_type="single_gpu", train_ratio=0.90,

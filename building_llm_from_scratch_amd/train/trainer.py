@@ -27,6 +27,7 @@ import torch.distributed as dist
 
 from ..logger import MetricsWriter, setup_logger
 from ..utils.misc import read_json_file, read_text_file, text_to_token_ids, token_ids_to_text
+from ..data.loaders import first_batches
 from .checkpoint import resume_state_path, save_model, save_resume_state
 from .generate import generate_cached
 
@@ -402,9 +403,7 @@ class Trainer:
             return float("nan")
         num_batches = min(num_batches or len(data_loader), len(data_loader))
         total = 0.0
-        for i, (inp, tgt) in enumerate(data_loader):
-            if i >= num_batches:
-                break
+        for inp, tgt in first_batches(data_loader, num_batches):
             total += float(self.calc_loss_batch(inp, tgt).item())
         return self._allreduce_mean(total / num_batches)
 

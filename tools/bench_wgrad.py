@@ -42,6 +42,8 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--models", default="llama3_8b,gpt2_774m,llama32_1b")
     ap.add_argument("--rounds", type=int, default=3, help="interleaved rounds (median reported)")
+    ap.add_argument("--only", default="", help="comma list of gemm names to run")
+    ap.add_argument("--no_hipblaslt", action="store_true", help="time only our kernel (profiling runs)")
     ap.add_argument("--variants", default="",
                     help="extra MFMA arms 'name:VAR=v,VAR2=v;name2:...' timed interleaved with the default "
                          "(kernel knobs read per launch)")
@@ -50,6 +52,8 @@ def main():
     Nt = a.tokens
     for model in a.models.split(","):
         for name, out_f, in_f in SHAPES[model]:
+            if a.only and name not in a.only.split(","):
+                continue
             dy = (torch.rand(Nt, out_f, device="cuda") * 2 - 1).to(torch.bfloat16)
             x = (torch.rand(Nt, in_f, device="cuda") * 2 - 1).to(torch.bfloat16)
             g0 = torch.empty(out_f, in_f, device="cuda", dtype=torch.bfloat16)
@@ -61,8 +65,9 @@ def main():
             r["preferred"] = ops.wgrad_gemm_preferred(out_f, in_f)
             times = {}
             for _ in range(a.rounds):  # interleaved rounds in one process (variance correlated)
-                times.setdefault("hipblaslt_us", []).append(
-                    timeit(lambda: torch.mm(x.t(), dy, out=g0.t()), a.iters))
+                if not a.no_hipblaslt:
+                    times.setdefault("hipblaslt_us", []).append(
+                        timeit(lambda: torch.mm(x.t(), dy, out=g0.t()), a.iters))
                 times.setdefault("mfma_us", []).append(
                     timeit(lambda: ops.wgrad_gemm_(dy, x, g1, False, auto), a.iters))
                 for vd in filter(None, a.variants.split(";")):
@@ -78,7 +83,9 @@ def main():
             g1.zero_()
             ops.wgrad_gemm_(dy, x, g1, False, auto)
             torch.cuda.synchronize()
-            r["max_rel_err_vs_hipblaslt"] = round(((g1.float() - g0.float()).abs().max() / g0.float().abs().max()).item(), 5)
+            if not a.no_hipblaslt:
+                r["max_rel_err_vs_hipblaslt"] = round(((g1.float() - g0.float()).abs().max()
+                                                       / g0.float().abs().max()).item(), 5)
             for k in list(r):
                 if k.endswith("_us"):
                     r[k.replace("_us", "_tflops")] = round(fl / r[k] / 1e6, 1)
