@@ -115,6 +115,9 @@ def _ln_bwd(unit, norm, dy, x, mean, rstd, dx_acc, acc):
 FUSED_BIAS = True
 # BLLM_RECOMPUTE_FUSED=0: the checkpoint recompute runs its GELU forward as a separate pass (A/B)
 RECOMPUTE_FUSED = os.environ.get("BLLM_RECOMPUTE_FUSED", "1") != "0"
+# the attention residual's dropout-add and norm2 as one row pass (ops.dropout_add_layernorm, bitwise
+# the two kernels); BLLM_FUSED_LN_DROPOUT=0: separate passes (A/B, profiles/r5/ln_dropout/)
+FUSED_LN_DROPOUT = os.environ.get("BLLM_FUSED_LN_DROPOUT", "1") != "0"
 
 
 def _drop_bwd_bias(lin, dy, p, seed, offset, acc):
@@ -196,9 +199,14 @@ class GPTBlockCompute(UnitCompute):
         km = ops.attn_keep_mask(qkv, B, T, H, hd, p) if save else None
         o, lse = ops.flash_attn_fwd(qkv, B, T, H, H, hd, True, p, rc.seed, offs[0], keep_mask=km)
         a, xa_o = self.o.forward(o)
-        x2 = ops.dropout_add(x2d, a, p, rc.seed, offs[1])
+        if FUSED_LN_DROPOUT:
+            u = self.unit
+            x2, h2, m2, r2 = ops.dropout_add_layernorm(x2d, a, u.data(b.norm2.weight), u.data(b.norm2.bias), 1e-5,
+                                                       p, rc.seed, offs[1])
+        else:
+            x2 = ops.dropout_add(x2d, a, p, rc.seed, offs[1])
+            h2, m2, r2 = self._ln(x2, b.norm2)
         del a
-        h2, m2, r2 = self._ln(x2, b.norm2)
         rebuild_g = recompute and not self.proj.has_lora and RECOMPUTE_FUSED
         fused = None if rebuild_g else self.fc.forward_bias_gelu(h2)   # K9: bias + GELU in the epilogue
         if fused is not None:

@@ -399,10 +399,12 @@ class FusedLinear:
 
     def backward(self, dy: torch.Tensor, x: torch.Tensor, xa, need_dx: bool = True,
                  accumulate: bool = False, dx_acc: Optional[torch.Tensor] = None, bias_done: bool = False,
-                 lowrank_dx: bool = False):
+                 lowrank_dx: bool = False, defer_lora_A: bool = False, lora_B_done: bool = False):
         """Returns dx (plus ``dx_acc`` if given) and writes parameter grads into the flat.
-        ``lowrank_dx``: a K-augmented group may instead return ("lowrank", base, u, P, s) with
-        dx = base + s u P left for the consumer to form (ops.swiglu_bwd_lowrank)."""
+        ``lowrank_dx``: a K-augmented group may instead return ("lowrank", base, u, P, s, A_deferred)
+        with dx = base + s u P left for the consumer to form (ops.swiglu_bwd_lowrank); with
+        ``defer_lora_A`` that consumer also sums dA = s x^T u (A_deferred True: ops.swiglu_bwd_lowrank_wgrad).
+        ``lora_B_done``: the caller already summed the K-augmented group's dB (same kernel)."""
         u = self.unit
         gW = u.fused_grad(self.W_params)
         if gW is not None:
@@ -412,7 +414,8 @@ class FusedLinear:
             if gb is not None:
                 ops.bias_grad_(dy, gb, accumulate)
         if self.has_lora and isinstance(xa, tuple) and xa[0] == "kaug":
-            return self._kaug_lora_backward(dy, x, xa[1], xa[2], xa[3], need_dx, dx_acc, accumulate, lowrank_dx)
+            return self._kaug_lora_backward(dy, x, xa[1], xa[2], xa[3], need_dx, dx_acc, accumulate, lowrank_dx,
+                                            defer_lora_A, lora_B_done)
         if self.has_lora and isinstance(xa, tuple) and xa[0] == "grouped":
             return self._grouped_lora_backward(dy, x, xa[1], xa[2], need_dx, dx_acc, accumulate)
         dx = None
@@ -448,26 +451,29 @@ class FusedLinear:
         assert not self.has_lora
         return _input_grad(dy, self.W())
 
-    def _kaug_lora_backward(self, dy, x, st, P, WaT, need_dx, dx_acc, accumulate, lowrank_dx=False):
+    def _kaug_lora_backward(self, dy, x, st, P, WaT, need_dx, dx_acc, accumulate, lowrank_dx=False,
+                            defer_A=False, B_done=False):
         """st = s t (the forward's augmented columns), WaT = [W^T ; Bd]."""
         u_ = self.unit
         sc = self.lora_scale
         K = x.shape[1]
         gB = [(u_.grad(s.lora_B), c0, off) for s, c0, off in zip(self.lora_specs, self.lora_c0, self.lora_off)]
         gB = [g for g in gB if g[0] is not None]
-        if gB:                                                     # dB = s t^T dy = (s t)^T dy
+        if gB and not B_done:                                      # dB = s t^T dy = (s t)^T dy
             ops.lora_wgrad(st, dy, [g for g, _, _ in gB], [o for _, _, o in gB], [c for _, c, _ in gB], 1.0,
                            accumulate)
         dxa = mm_nt(dy, WaT)                                       # [dy W | dy Bd | 0] = [dx_W | dy B^T | 0]
         ub = dxa[:, K:K + self.lora_R]
+        lowrank = need_dx and lowrank_dx and dx_acc is None and ops.swiglu_bwd_lowrank_ok(self.lora_R, K)
+        defer = lowrank and defer_A
         gA = [(u_.grad(s.lora_A), off) for s, off in zip(self.lora_specs, self.lora_off)]
         gA = [g for g in gA if g[0] is not None]
-        if gA:
+        if gA and not defer:
             ops.lora_wgrad(ub, x, [g.t() for g, _ in gA], [o for _, o in gA], [0] * len(gA), sc, accumulate)
         if not need_dx:
             return None
-        if lowrank_dx and dx_acc is None and ops.swiglu_bwd_lowrank_ok(self.lora_R, K):
-            return ("lowrank", dxa[:, :K], ub, P, sc)             # the consumer adds s u P
+        if lowrank:
+            return ("lowrank", dxa[:, :K], ub, P, sc, defer)      # the consumer adds s u P (and dA)
         dx = torch.empty(x.shape, dtype=x.dtype, device=x.device)
         ops.lora_up_(dx, ub, [P], [0], [0], sc, base=dxa[:, :K])  # dx_W + s (dy B^T) A_cat^T
         if dx_acc is not None:

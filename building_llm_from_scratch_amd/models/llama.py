@@ -249,6 +249,26 @@ class LlamaBlockCompute(UnitCompute):
         x3, _ = self.down.forward(ops.swiglu_fwd(gu), residual=x2)
         return x3
 
+    def _lora_swiglu_wgrad(self, xa_dn, xa_gu, F):
+        """(gB_gate, gB_up, gA_down^T) when the MLP's LoRA gradients can be summed inside the
+        SwiGLU backward (ops.swiglu_bwd_lowrank_wgrad: both groups K-augmented, rank 16 per
+        member, the down projection's low-rank dX formed by that kernel, all three trainable),
+        else None."""
+        dn, gu = self.down, self.gu
+        if not (LORA_SWIGLU_WGRAD and dn.has_lora and gu.has_lora):
+            return None
+        kaug = lambda xa: isinstance(xa, tuple) and xa[0] == "kaug"  # noqa: E731
+        if not (kaug(xa_dn) and kaug(xa_gu) and dn.lora_R == 16 and gu.lora_r == [16, 16]
+                and gu.lora_c0 == [0, F] and gu.lora_len == [F, F] and gu.lora_off == [0, 16]
+                and ops.swiglu_bwd_lowrank_ok(16, F) and ops.swiglu_bwd_lowrank_wgrad_ok(16, F)):
+            return None
+        u = self.unit
+        gBg, gBu = (u.grad(sp.lora_B) for sp in gu.lora_specs)
+        gAd = u.grad(dn.lora_specs[0].lora_A)
+        if gBg is None or gBu is None or gAd is None or not (gBg.dtype == gBu.dtype == gAd.dtype):
+            return None
+        return gBg, gBu, gAd.t()
+
     def backward(self, dy, s):
         rc, cfg, u, b = self.rctx, self.rctx.cfg, self.unit, self.block
         B, T = rc.B, rc.T
@@ -260,12 +280,22 @@ class LlamaBlockCompute(UnitCompute):
         dy2 = dy.reshape(N, d)
         w1, w2 = u.data(b.norm1.weight), u.data(b.norm2.weight)
         # ---- MLP
+        gu_B_done = False
         if "act" in s or self.down.has_lora:
-            act = s["act"] if "act" in s else ops.swiglu_fwd(s["gu"])
-            d_act = self.down.backward(dy2, act, xa_dn, accumulate=acc, lowrank_dx=True)
+            fuse = self._lora_swiglu_wgrad(xa_dn, xa_gu, s["gu"].shape[1] // 2)
+            # the fused kernel rebuilds act itself: no SwiGLU forward for the down dA
+            act = s["act"] if "act" in s else (s["gu"][:, :s["gu"].shape[1] // 2] if fuse
+                                               else ops.swiglu_fwd(s["gu"]))
+            d_act = self.down.backward(dy2, act, xa_dn, accumulate=acc, lowrank_dx=True, defer_lora_A=fuse is not None)
             del act
-            if isinstance(d_act, tuple):   # K-augmented LoRA: dact = base + s u P inside the kernel
-                d_gu = ops.swiglu_bwd_lowrank(s["gu"], *d_act[1:])
+            assert fuse is None or (isinstance(d_act, tuple) and d_act[5]), "fused LoRA SwiGLU path not taken"
+            if isinstance(d_act, tuple) and d_act[5]:
+                # K-augmented LoRA MLP: dact = base + s u P, the gate/up dB and the down dA summed in
+                # the same pass over the rows (ops.swiglu_bwd_lowrank_wgrad)
+                d_gu = ops.swiglu_bwd_lowrank_wgrad(s["gu"], *d_act[1:5], xa_gu[1], *fuse, accumulate=acc)
+                gu_B_done = True
+            elif isinstance(d_act, tuple):   # K-augmented LoRA: dact = base + s u P inside the kernel
+                d_gu = ops.swiglu_bwd_lowrank(s["gu"], *d_act[1:5])
             else:
                 d_gu = ops.swiglu_bwd(s["gu"], d_act)
             del d_act
@@ -277,7 +307,7 @@ class LlamaBlockCompute(UnitCompute):
             self.down.backward(dy2, act, None, need_dx=False, accumulate=acc)
             del act
         h2 = s["h2"] if "h2" in s else ops.rmsnorm_fwd(s["x2"], w2, eps)[0]
-        dh2 = self.gu.backward(d_gu, h2, xa_gu, accumulate=acc)
+        dh2 = self.gu.backward(d_gu, h2, xa_gu, accumulate=acc, lora_B_done=gu_B_done)
         del d_gu, h2
         dx2, _ = ops.rmsnorm_bwd(dh2, s["x2"], w2, s["r2"], dy2, u.grad(b.norm2.weight), acc)
         del dh2
@@ -291,6 +321,10 @@ class LlamaBlockCompute(UnitCompute):
         del dqkv, h1
         dx, _ = ops.rmsnorm_bwd(dh1, s["x"], w1, s["r1"], dx2, u.grad(b.norm1.weight), acc)
         return dx.view(B, T, d)
+
+
+# BLLM_LORA_SWIGLU_WGRAD=0: the gate/up dB and down dA of a LoRA MLP as separate lora_wgrad passes (A/B)
+LORA_SWIGLU_WGRAD = os.environ.get("BLLM_LORA_SWIGLU_WGRAD", "1") != "0"
 
 
 def _compact_kaug(xa):

@@ -21,7 +21,9 @@ from ._ext import ext_available, kernel_debug, load_ext
 
 __all__ = [
     "rmsnorm_fwd", "rmsnorm_bwd", "layernorm_fwd", "layernorm_bwd", "dropout_add", "dropout_bwd",
+    "dropout_add_layernorm",
     "rope_", "rope_tables", "flash_attn_fwd", "flash_attn_bwd", "swiglu_fwd", "swiglu_bwd", "swiglu_bwd_act",
+    "swiglu_bwd_lowrank_wgrad", "swiglu_bwd_lowrank_wgrad_ok",
     "gelu_fwd", "gelu_bwd", "gelu_bwd_bias", "gelu_bwd_act", "dropout_bwd_bias", "ce_fwd", "ce_bwd_", "embedding_fwd", "embedding_bwd",
     "sq_norm_multi", "adamw_step_", "attn_decode", "bias_grad_", "ext_available", "load_ext", "attention_backend",
     "lora_down", "lora_up_", "lora_wgrad", "lora_pack_t", "lora_kernel_ok", "lora_kernel_ok_dims",
@@ -126,6 +128,15 @@ def dropout_add(x, a, p: float, seed: int, offset: int):
     if _hip(x):
         return _k().dropout_add(x, a, float(p), int(seed), int(offset))
     return ref.dropout_add(x, a, p, seed, offset)
+
+
+def dropout_add_layernorm(x, a, w, b, eps: float, p: float, seed: int, offset: int):
+    """x2 = x + dropout(a) and (y, mean, rstd) = layernorm_fwd(x2) in one pass over the rows ->
+    (x2, y, mean, rstd); bitwise ``dropout_add`` followed by ``layernorm_fwd``."""
+    if _hip(x):
+        return _k().dropout_add_layernorm(x, a, w, b, float(eps), float(p), int(seed), int(offset))
+    x2 = ref.dropout_add(x, a, p, seed, offset)
+    return (x2,) + tuple(ref.layernorm_fwd(x2, w, b, eps))
 
 
 def dropout_bwd(dy, p: float, seed: int, offset: int):
@@ -525,6 +536,27 @@ def swiglu_bwd_lowrank(gu, base, u, P, scale: float):
         return _k().swiglu_bwd_lowrank(gu, base, u, P, float(scale))
     dact = (base.float() + scale * (u.float() @ P.float())).to(gu.dtype)
     return ref.swiglu_bwd(gu, dact)
+
+
+def swiglu_bwd_lowrank_wgrad_ok(r: int, F: int) -> bool:
+    return r == 16 and F % 64 == 0
+
+
+def swiglu_bwd_lowrank_wgrad(gu, base, u, P, scale: float, st, gB_gate, gB_up, gA_down_t, accumulate: bool = False):
+    """``swiglu_bwd_lowrank`` that also sums, over the same rows, the LoRA gradients that read them:
+    gB_gate (+)= st[:, :16]^T dg, gB_up (+)= st[:, 16:32]^T du (the K-augmented gate/up group's dB;
+    st = s t) and gA_down_t (+)= scale u^T act (the down projection's dA^T, act = swiglu_fwd(gu),
+    u = dy B^T of the down LoRA)."""
+    if _hip(gu):
+        return _k().swiglu_bwd_lowrank_wgrad(gu, base, u, P, float(scale), st, gB_gate, gB_up, gA_down_t,
+                                             bool(accumulate))
+    dgu = swiglu_bwd_lowrank(gu, base, u, P, scale)
+    F = gu.shape[1] // 2
+    act = ref.swiglu_fwd(gu)
+    for g, L, R, sc in ((gB_gate, st[:, :16], dgu[:, :F], 1.0), (gB_up, st[:, 16:32], dgu[:, F:], 1.0),
+                        (gA_down_t, u[:, :16], act, scale)):
+        _vec_into(g, sc * (L.float().t() @ R.float()), accumulate)
+    return dgu
 
 
 def swiglu_bwd_act(gu, dact):

@@ -20,6 +20,10 @@ void rmsnorm_bwd(DType dt, const void* dy, const void* x, const void* w, const f
 void layernorm_bwd(DType dt, const void* dy, const void* x, const void* w, const float* mean, const float* rstd,
                    const void* dx_acc, void* dx, float* part_w, float* part_b, DType odt, void* dw, void* db,
                    bool accumulate, int N, int d, int nwg, hipStream_t s);
+// x2 = x + dropout(a) (stored) and y = LayerNorm(x2) in one pass (GPT-2 attention residual + norm2)
+void dropout_add_layernorm_fwd(DType dt, const void* x, const void* a, void* xs, const void* w, const void* b, void* y,
+                               float* mean, float* rstd, int N, int d, float eps, float p, uint64_t seed,
+                               uint64_t offset, hipStream_t s);
 void col_reduce(const float* part, DType odt, void* out, int P, int d, bool accumulate, hipStream_t s);
 
 // elementwise.hip
@@ -28,6 +32,13 @@ void transpose16(const void* in, void* out, long R, long C, hipStream_t s);
 void swiglu_fwd(DType dt, const void* gu, void* act, long N, int F, long lda, hipStream_t s);
 // SwiGLU backward with dact = base + scale . u P formed on the fly (down-projection LoRA dX)
 bool swiglu_bwd_lr_ok(int r, int F);
+// swiglu_bwd_lr plus the gate / up dB and down dA^T reductions over the same rows: fp32 partials
+// part [S][3][16][F] (sum them with lora_reduce); u = dy B^T of the down LoRA, st = s t of gate|up
+bool swiglu_bwd_lr_wgrad_ok(int r, int F);
+int swiglu_bwd_lr_wgrad_splits(long N, int F);
+void swiglu_bwd_lr_wgrad(DType dt, const void* gu, const void* base, long ldb, const void* u, long ldu, const void* P,
+                         const void* st, long ldst, float scale, void* dgu, float* part, long N, int F, int S,
+                         hipStream_t s);
 void swiglu_bwd_lr(DType dt, const void* gu, const void* base, long ldb, const void* u, long ldu, const void* P, int r,
                    float scale, void* dgu, long N, int F, hipStream_t s);
 // act (nullable, may alias dact): also write silu(g) * u there -- the activation-checkpoint
@@ -165,6 +176,8 @@ void lora_block(DType dt, const LoraBlockArgs& a, hipStream_t s);
 void lora_up(DType dt, const LoraUpArgs& a, int N, int max_len, hipStream_t s);
 int lora_wgrad_splits(int blocks, int N);
 void lora_wgrad(DType dt, DType odt, const LoraWgradArgs& a, int N, int S, hipStream_t s);
+// g_m (+)= sum_s part[s][part_off_m + a * len_m + b] (a.part, a.part_ld, a.part_off set; scale not applied)
+void lora_reduce(DType odt, const LoraWgradArgs& a, int S, hipStream_t s);
 void lora_pack_t(DType dt, const LoraPackArgs& a, int K, int max_r, hipStream_t s);
 
 // gemm_wgrad.hip — C[M, N] (+)= A^T B with A [K, M], B [K, N] row-major (dW = dY^T X).

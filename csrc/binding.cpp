@@ -160,6 +160,28 @@ std::tuple<Tensor, Tensor, Tensor> layernorm_bwd(const Tensor& dy, const Tensor&
   return {dx, dw, db};
 }
 
+// x2 = x + dropout(a), (y, mean, rstd) = LayerNorm(x2): one pass (GPT-2's attention residual + norm2)
+std::tuple<Tensor, Tensor, Tensor, Tensor> dropout_add_layernorm(const Tensor& x, const Tensor& a, const Tensor& w,
+                                                                 const Tensor& b, double eps, double p, int64_t seed,
+                                                                 int64_t offset) {
+  check_gpu(x, "x"); check_gpu(a, "a"); check_gpu(w, "w"); check_gpu(b, "b");
+  c10::DeviceGuard g(x.device());
+  check_rows(x, 16 / x.element_size());
+  TORCH_CHECK(a.sizes() == x.sizes() && a.scalar_type() == x.scalar_type() && a.is_contiguous(),
+              "dropout_add_layernorm: a must be a contiguous tensor of x's shape and dtype");
+  const int64_t N = x.size(0), d = x.size(1);
+  TORCH_CHECK(d <= bllm::norm_max_dim(dt_of(x)) && w.numel() == d && b.numel() == d &&
+              w.scalar_type() == x.scalar_type() && b.scalar_type() == x.scalar_type());
+  auto x2 = at::empty_like(x);
+  auto y = at::empty_like(x);
+  auto mean = at::empty({N}, x.options().dtype(at::kFloat));
+  auto rstd = at::empty({N}, x.options().dtype(at::kFloat));
+  bllm::dropout_add_layernorm_fwd(dt_of(x), x.data_ptr(), a.data_ptr(), x2.data_ptr(), w.data_ptr(), b.data_ptr(),
+                                  y.data_ptr(), mean.data_ptr<float>(), rstd.data_ptr<float>(), N, d, (float)eps,
+                                  (float)p, (uint64_t)seed, (uint64_t)offset, stream());
+  return {x2, y, mean, rstd};
+}
+
 // ------------------------------------------------------------------ elementwise
 Tensor dropout_add(const Tensor& x, const Tensor& a, double p, int64_t seed, int64_t offset) {
   check_gpu(x, "x"); check_gpu(a, "a");
@@ -240,6 +262,52 @@ Tensor swiglu_bwd_lowrank(const Tensor& gu, const Tensor& base, const Tensor& u,
   auto dgu = at::empty_like(gu);
   bllm::swiglu_bwd_lr(dt_of(gu), gu.data_ptr(), base.data_ptr(), base.stride(0), u.data_ptr(), u.stride(0),
                       P.data_ptr(), (int)r, (float)scale, dgu.data_ptr(), N, (int)F, stream());
+  return dgu;
+}
+
+// swiglu_bwd_lowrank that also accumulates the LoRA gradients reading the same rows:
+// gB_gate (+)= st[:, :16]^T dg, gB_up (+)= st[:, 16:32]^T du (the gate/up group's dB, st = s t), and
+// gA_down_t (+)= scale u^T act (the down projection's dA, a [16, F] view of its [F, 16] gradient)
+Tensor swiglu_bwd_lowrank_wgrad(const Tensor& gu, const Tensor& base, const Tensor& u, const Tensor& P, double scale,
+                                const Tensor& st, Tensor& gB_gate, Tensor& gB_up, Tensor& gA_down_t, bool accumulate) {
+  check_gpu(gu, "gu"); check_gpu(P, "P");
+  c10::DeviceGuard g(gu.device());
+  const int64_t N = gu.size(0), F = gu.size(1) / 2, r = P.size(0);
+  TORCH_CHECK(bllm::swiglu_bwd_lr_wgrad_ok((int)r, (int)F) && P.size(1) == F, "swiglu_bwd_lowrank_wgrad: rank 16, F % 64");
+  TORCH_CHECK(gu.scalar_type() == at::kBFloat16 || gu.scalar_type() == at::kHalf, "swiglu_bwd_lowrank_wgrad: bf16 / fp16");
+  TORCH_CHECK(gu.is_contiguous() && P.is_contiguous(), "swiglu_bwd_lowrank_wgrad: contiguous gu and P");
+  auto rows16 = [&](const Tensor& t, int64_t cols, const char* name) {
+    TORCH_CHECK(t.is_cuda() && t.dim() == 2 && t.size(0) == N && t.size(1) >= cols && t.stride(1) == 1 &&
+                    (t.stride(0) * t.element_size()) % 16 == 0 && (uintptr_t)t.data_ptr() % 16 == 0 &&
+                    t.scalar_type() == gu.scalar_type(),
+                "swiglu_bwd_lowrank_wgrad: ", name, " must be a 16-B aligned row-strided [N, >=", cols, "] view");
+  };
+  rows16(base, F, "base");
+  TORCH_CHECK(base.size(1) == F, "swiglu_bwd_lowrank_wgrad: base is [N, F]");
+  rows16(u, 16, "u");
+  rows16(st, 32, "st");
+  const DType odt = dt_of(gB_gate);
+  const Tensor* gs[3] = {&gB_gate, &gB_up, &gA_down_t};
+  for (const Tensor* t : gs)
+    TORCH_CHECK(t->is_cuda() && t->dim() == 2 && t->size(0) == 16 && t->size(1) == F && dt_of(*t) == odt &&
+                    (t->is_contiguous() || t->t().is_contiguous()),
+                "swiglu_bwd_lowrank_wgrad: gradients are [16, F] (transposed) contiguous blocks of one dtype");
+  auto dgu = at::empty_like(gu);
+  const int S = bllm::swiglu_bwd_lr_wgrad_splits(N, (int)F);
+  auto part = at::empty({S, 3 * 16 * F}, gu.options().dtype(at::kFloat));
+  bllm::swiglu_bwd_lr_wgrad(dt_of(gu), gu.data_ptr(), base.data_ptr(), base.stride(0), u.data_ptr(), u.stride(0),
+                            P.data_ptr(), st.data_ptr(), st.stride(0), (float)scale, dgu.data_ptr(),
+                            part.data_ptr<float>(), N, (int)F, S, stream());
+  bllm::LoraWgradArgs a{};
+  a.accumulate = accumulate;
+  a.n = 3;
+  for (int m = 0; m < 3; ++m) {
+    a.r[m] = 16; a.len[m] = (int)F; a.sa[m] = gs[m]->stride(0); a.sb[m] = gs[m]->stride(1);
+    a.gt[m][0] = gs[m]->data_ptr();
+    a.part_off[m] = (int64_t)m * 16 * F;
+  }
+  a.part = part.data_ptr<float>(); a.part_ld = 3 * 16 * F;
+  bllm::lora_reduce(odt, a, S, stream());
   return dgu;
 }
 
@@ -1047,6 +1115,7 @@ TORCH_LIBRARY(bllm, m) {
   m.def("layernorm_fwd(Tensor x, Tensor w, Tensor b, float eps) -> (Tensor, Tensor, Tensor)");
   m.def("layernorm_bwd(Tensor dy, Tensor x, Tensor w, Tensor mean, Tensor rstd, Tensor? dx_acc, Tensor(a!)? dw_out, Tensor(b!)? db_out, bool accumulate) -> (Tensor, Tensor, Tensor)");
   m.def("dropout_add(Tensor x, Tensor a, float p, int seed, int offset) -> Tensor");
+  m.def("dropout_add_layernorm(Tensor x, Tensor a, Tensor w, Tensor b, float eps, float p, int seed, int offset) -> (Tensor, Tensor, Tensor, Tensor)");
   m.def("dropout_bwd(Tensor dy, float p, int seed, int offset) -> Tensor");
   m.def("bwd_bias_grad_(Tensor(a!) src, Tensor? aux, Tensor(b!)? db, bool accumulate, int op, float p, int seed, int offset, bool act_inplace=False) -> Tensor");
   m.def("transpose2d(Tensor a) -> Tensor");
@@ -1054,6 +1123,7 @@ TORCH_LIBRARY(bllm, m) {
   m.def("swiglu_fwd(Tensor gu) -> Tensor");
   m.def("swiglu_fwd_into_(Tensor gu, Tensor(a!) act) -> ()");
   m.def("swiglu_bwd_lowrank(Tensor gu, Tensor base, Tensor u, Tensor P, float scale) -> Tensor");
+  m.def("swiglu_bwd_lowrank_wgrad(Tensor gu, Tensor base, Tensor u, Tensor P, float scale, Tensor st, Tensor(a!) gB_gate, Tensor(b!) gB_up, Tensor(c!) gA_down_t, bool accumulate) -> Tensor");
   m.def("swiglu_bwd(Tensor gu, Tensor dact) -> Tensor");
   m.def("swiglu_bwd_act(Tensor gu, Tensor(a!) dact) -> Tensor");
   m.def("gelu_fwd(Tensor f) -> Tensor");
@@ -1093,6 +1163,7 @@ TORCH_LIBRARY_IMPL(bllm, CUDA, m) {
   m.impl("layernorm_fwd", &layernorm_fwd);
   m.impl("layernorm_bwd", &layernorm_bwd);
   m.impl("dropout_add", &dropout_add);
+  m.impl("dropout_add_layernorm", &dropout_add_layernorm);
   m.impl("dropout_bwd", &dropout_bwd);
   m.impl("bwd_bias_grad_", &bwd_bias_grad_);
   m.impl("transpose2d", &transpose2d);
@@ -1100,6 +1171,7 @@ TORCH_LIBRARY_IMPL(bllm, CUDA, m) {
   m.impl("swiglu_fwd", &swiglu_fwd);
   m.impl("swiglu_fwd_into_", &swiglu_fwd_into_);
   m.impl("swiglu_bwd_lowrank", &swiglu_bwd_lowrank);
+  m.impl("swiglu_bwd_lowrank_wgrad", &swiglu_bwd_lowrank_wgrad);
   m.impl("swiglu_bwd", &swiglu_bwd);
   m.impl("swiglu_bwd_act", &swiglu_bwd_act);
   m.impl("gelu_fwd", &gelu_fwd);

@@ -118,6 +118,148 @@ __global__ __launch_bounds__(256) void swiglu_bwd_lr_k(const T* __restrict__ gu,
   }
 }
 
+// SwiGLU backward of a LoRA MLP (K-augmented gate/up group + down projection, r = 16) with the
+// three rank-16 weight-gradient reductions that read these rows fused into the same pass:
+//   dact = base + s . u P;  (dg, du) = swiglu_bwd(gu, dact)                 (as swiglu_bwd_lr_k)
+//   G0[j][c] = sum_n st[n][j]      . dg[n][c]      dB of the gate LoRA   (st = s t, gate | up)
+//   G1[j][c] = sum_n st[n][16 + j] . du[n][c]      dB of the up LoRA
+//   G2[j][c] = s sum_n u[n][j]     . act[n][c]     dA^T of the down LoRA (act = silu(g) up)
+// -- the separate lora_wgrad passes re-read dgu ([N, 2F]) and act ([N, F]) from HBM.  Column-slab
+// mapping: a workgroup owns LRW_COLS columns of F and one of S contiguous row ranges, walked in
+// LRW_CH-row chunks; thread (row rr, vector cv) computes 8 columns of one row as swiglu_bwd_lr_k
+// (the P slice in registers), the chunk's dg / du / act (rounded as stored) and its st / u rows
+// go through LDS, and the four waves run the reductions as 16x16x32 MFMAs (wave w: columns
+// 16w .. 16w+15; both operands read with ds_read_b64_tr_b16, k = the chunk's rows).  fp32
+// partials per row range [S][3][16][F] are summed by lora_reduce (fixed order: deterministic).
+constexpr int LRW_COLS = 64, LRW_CH = 32;
+constexpr int LRW_RS = LRW_COLS * 2 + 16;  // bytes per row of a dg / du / act tile (padded)
+constexpr int LRW_LS = 32;                 // bytes per row of an st / u tile (16 x 16-bit)
+
+typedef short lrw_s16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) lrw_s16x4 lrw_lds_s16x4;
+typedef float lrw_f32x4 __attribute__((ext_vector_type(4)));
+
+template <typename T> struct LrwMfma;
+template <> struct LrwMfma<bf16_t> {
+  typedef __bf16 v8 __attribute__((ext_vector_type(8)));
+  static __device__ __forceinline__ lrw_f32x4 run(v8 a, v8 b, lrw_f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+  }
+};
+template <> struct LrwMfma<f16_t> {
+  typedef _Float16 v8 __attribute__((ext_vector_type(8)));
+  static __device__ __forceinline__ lrw_f32x4 run(v8 a, v8 b, lrw_f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+  }
+};
+// 8 k-values (rows 8g .. 8g+7 of a tile) of one column for this lane: two transposed reads
+template <typename v8>
+__device__ __forceinline__ v8 lrw_frag(const char* tile, int stride, int col_byte, int lane) {
+  const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+  const char* a = tile + (8 * g + q) * stride + col_byte + 8 * p;
+  const lrw_s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lrw_lds_s16x4*)(a));
+  const lrw_s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lrw_lds_s16x4*)(a + 4 * stride));
+  return __builtin_bit_cast(v8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void swiglu_bwd_lr_wg_k(const T* __restrict__ gu, const T* __restrict__ base,
+                                                          long ldb, const T* __restrict__ u, long ldu,
+                                                          const T* __restrict__ P, const T* __restrict__ st,
+                                                          long ldst, float s, T* __restrict__ dgu,
+                                                          float* __restrict__ part, long N, int F, long rows_per) {
+  constexpr int R = 16, VEC = 8;
+  typedef typename LrwMfma<T>::v8 v8;
+  __shared__ __attribute__((aligned(16))) char Lt[2][3][LRW_CH * LRW_LS];  // st gate, st up, u
+  __shared__ __attribute__((aligned(16))) char Rt[2][3][LRW_CH * LRW_RS];  // dg, du, act
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int rr = tid >> 3, cv = tid & 7;
+  const int c = blockIdx.x * LRW_COLS + cv * VEC;
+  const long r0 = (long)blockIdx.y * rows_per;
+  const long r1 = r0 + rows_per < N ? r0 + rows_per : N;
+
+  float pr[R][VEC];
+#pragma unroll
+  for (int j = 0; j < R; ++j) {
+    const Vec16<T> pv = ld16(P + (long)j * F + c);
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) pr[j][e] = to_f(pv.v[e]);
+  }
+  // st / u staging: thread t < 192 moves 16 B = half a 16-wide row of tile lq
+  const int lq = tid >> 6, lrow = (tid & 63) >> 1, lh = tid & 1;
+  const T* lsrc = lq == 0 ? st + 8 * lh : lq == 1 ? st + 16 + 8 * lh : u + 8 * lh;
+  const long lld = lq == 2 ? ldu : ldst;
+
+  Vec16<T> g, up, bs;
+  uint4 lreg = make_uint4(0, 0, 0, 0);
+  auto load = [&](long row) {
+    if (row + rr < r1) {
+      const long rw = row + rr;
+      g = ld16(gu + rw * 2 * F + c);
+      up = ld16(gu + rw * 2 * F + F + c);
+      bs = ld16(base + rw * ldb + c);
+    }
+    lreg = make_uint4(0, 0, 0, 0);
+    if (lq < 3 && row + lrow < r1) lreg = *reinterpret_cast<const uint4*>(lsrc + (row + lrow) * lld);
+  };
+  lrw_f32x4 acc[3];
+#pragma unroll
+  for (int q = 0; q < 3; ++q) acc[q] = lrw_f32x4{0.f, 0.f, 0.f, 0.f};
+  if (r0 < r1) load(r0);
+  int par = 0;
+  for (long row = r0; row < r1; row += LRW_CH, par ^= 1) {
+    if (lq < 3) *reinterpret_cast<uint4*>(Lt[par][lq] + lrow * LRW_LS + lh * 16) = lreg;
+    __syncthreads();  // st / u rows of this chunk visible (and the chunk before last's tiles free)
+    const bool valid = row + rr < r1;
+    const Vec16<T> cg = g, cu = up, cb = bs;
+    if (row + LRW_CH < r1) load(row + LRW_CH);  // next chunk's loads in flight under the math
+    float uj[R];
+    {
+      const Vec16<T> u0 = ld16(reinterpret_cast<const T*>(Lt[par][2] + rr * LRW_LS));
+      const Vec16<T> u1 = ld16(reinterpret_cast<const T*>(Lt[par][2] + rr * LRW_LS + 16));
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) uj[e] = to_f(u0.v[e]), uj[VEC + e] = to_f(u1.v[e]);
+    }
+    Vec16<T> dg, du, act;
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) {
+      float corr = 0.f;
+#pragma unroll
+      for (int j = 0; j < R; ++j) corr = fmaf(uj[j], pr[j][e], corr);
+      // rounded to T like the lora_up output it replaces (as swiglu_bwd_lr_k)
+      const float dd = to_f(from_f<T>(to_f(cb.v[e]) + s * corr));
+      const float a = to_f(cg.v[e]), b = to_f(cu.v[e]);
+      const float sg = 1.f / (1.f + __expf(-a));
+      dg.v[e] = valid ? from_f<T>(dd * b * sg * (1.f + a * (1.f - sg))) : from_f<T>(0.f);
+      du.v[e] = valid ? from_f<T>(dd * a * sg) : from_f<T>(0.f);
+      act.v[e] = valid ? from_f<T>(a / (1.f + __expf(-a)) * b) : from_f<T>(0.f);  // bitwise as swiglu_fwd
+    }
+    if (valid) {
+      st16(dgu + (row + rr) * 2 * F + c, dg);
+      st16(dgu + (row + rr) * 2 * F + F + c, du);
+    }
+    st16(reinterpret_cast<T*>(Rt[par][0] + rr * LRW_RS + cv * 16), dg);
+    st16(reinterpret_cast<T*>(Rt[par][1] + rr * LRW_RS + cv * 16), du);
+    st16(reinterpret_cast<T*>(Rt[par][2] + rr * LRW_RS + cv * 16), act);
+    __syncthreads();  // the chunk's dg / du / act tiles visible
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      const v8 a = lrw_frag<v8>(Lt[par][q], LRW_LS, 0, lane);
+      const v8 b = lrw_frag<v8>(Rt[par][q], LRW_RS, 32 * w, lane);
+      acc[q] = LrwMfma<T>::run(a, b, acc[q]);
+    }
+  }
+  // C map of 16x16x32: column = lane & 15, rows 4 (lane >> 4) + i  ->  G_q[j][col]
+  const int col = blockIdx.x * LRW_COLS + 16 * w + (lane & 15);
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    float* o = part + ((long)blockIdx.y * 3 + q) * R * F + col;
+    const float sc = q == 2 ? s : 1.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) o[(long)(4 * (lane >> 4) + i) * F] = sc * acc[q][i];
+  }
+}
+
 // Row-per-workgroup variants for wide FFNs (F/VEC >= 512, e.g. Llama F=14336): no 64-bit index
 // division, U independent 16-B load pairs in flight per lane before any math (the grid-stride loop
 // above serialises load -> compute per vector).  One workgroup per token row; N rows >> 256 CUs.
@@ -503,6 +645,27 @@ void swiglu_bwd_lr(DType dt, const void* gu, const void* base, long ldb, const v
   if (dt == DType::BF16) LR_L(bf16_t, 16);
   else LR_L(f16_t, 16);
 #undef LR_L
+}
+bool swiglu_bwd_lr_wgrad_ok(int r, int F) { return r == 16 && F % LRW_COLS == 0; }
+int swiglu_bwd_lr_wgrad_splits(long N, int F) {
+  // ~512 workgroups (two per CU at the kernel's register use), each row range >= 4 chunks
+  const int slabs = F / LRW_COLS;
+  int S = (512 + slabs - 1) / slabs;
+  const long max_s = (N + 4 * LRW_CH - 1) / (4 * LRW_CH);
+  if (S > max_s) S = (int)max_s;
+  return S < 1 ? 1 : (S > 64 ? 64 : S);
+}
+void swiglu_bwd_lr_wgrad(DType dt, const void* gu, const void* base, long ldb, const void* u, long ldu, const void* P,
+                         const void* st, long ldst, float scale, void* dgu, float* part, long N, int F, int S,
+                         hipStream_t s) {
+  const long rows_per = (N + S - 1) / S;
+  const dim3 grid((unsigned)(F / LRW_COLS), (unsigned)S);
+#define LRW_L(TT) hipLaunchKernelGGL((swiglu_bwd_lr_wg_k<TT>), grid, dim3(256), 0, s, (const TT*)gu, (const TT*)base, ldb, \
+                                     (const TT*)u, ldu, (const TT*)P, (const TT*)st, ldst, scale, (TT*)dgu, part, N, F,   \
+                                     rows_per)
+  if (dt == DType::BF16) LRW_L(bf16_t);
+  else LRW_L(f16_t);
+#undef LRW_L
 }
 void swiglu_bwd(DType dt, const void* gu, const void* dact, void* dgu, void* act, long N, int F, hipStream_t s) {
   BLLM_DISPATCH(dt, T, {

@@ -426,6 +426,14 @@ void lora_wgrad(DType dt, DType odt, const LoraWgradArgs& a, int N, int S, hipSt
   });
 }
 
+void lora_reduce(DType odt, const LoraWgradArgs& a, int S, hipStream_t s) {
+  BLLM_DISPATCH(odt, OT, {
+    const long total = a.part_ld;
+    const int g = (int)((total + 255) / 256 < 2048 ? (total + 255) / 256 : 2048);
+    hipLaunchKernelGGL(lora_reduce_k<OT>, dim3(g), dim3(256), 0, s, a, S, total);
+  });
+}
+
 void lora_pack_t(DType dt, const LoraPackArgs& a, int K, int max_r, hipStream_t s) {
   dim3 grid(ceil_div((long)K * max_r, 256) < 256 ? ceil_div((long)K * max_r, 256) : 256, a.n);
   if (dt == DType::BF16) hipLaunchKernelGGL(lora_pack_t_k<bf16_t>, grid, dim3(256), 0, s, a, K);

@@ -18,11 +18,25 @@ constexpr int ROWS_PER_WG = 4;  // 4 waves x 1 row
 // d=4096), which col_reduce_k streams once
 constexpr int MAX_BWD_WG = 1024;
 
-template <typename T, int NV, bool LN>
+// Residual-dropout prologue (ADD, GPT-2's attention residual + norm2 in one pass):
+//   xs = x + dropout(a) is stored (rounded to T) and normalised, bitwise dropout_add_k then
+//   norm_fwd_k (same keep bits at element index row * d + column, same lane -> column map).
+struct AddDrop {
+  const void* a = nullptr;
+  void* xs = nullptr;
+  uint64_t seed = 0, offset = 0;
+  uint32_t thr = 0;
+  float inv_keep = 1.f;
+};
+
+template <typename T, int NV, bool LN, bool ADD = false>
 __global__ __launch_bounds__(256) void norm_fwd_k(const T* __restrict__ x, const T* __restrict__ w,
                                                   const T* __restrict__ b, T* __restrict__ y,
                                                   float* __restrict__ mean_out, float* __restrict__ rstd_out,
-                                                  int N, int d, float eps, long ldy) {
+                                                  int N, int d, float eps, long ldy, AddDrop ad = AddDrop{}) {
+  // no FMA contraction: every instantiation (ADD or not) rounds identically, so the fused
+  // residual + norm pass is bitwise the two separate kernels
+#pragma clang fp contract(off)
   constexpr int VEC = 16 / sizeof(T);
   const int row = blockIdx.x * ROWS_PER_WG + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
@@ -36,6 +50,18 @@ __global__ __launch_bounds__(256) void norm_fwd_k(const T* __restrict__ x, const
     const int c = lane + 64 * i;
     if (c < nvec) {
       Vec16<T> r = ld16(xr + c * VEC);
+      if constexpr (ADD) {
+        const Vec16<T> av = ld16(static_cast<const T*>(ad.a) + (size_t)row * d + c * VEC);
+        uint32_t bits[VEC];
+        drop_bits_run<VEC>(ad.seed, ad.offset + (uint64_t)row * d + c * VEC, bits);
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) {
+          float t = bits[j] >= ad.thr ? to_f(av.v[j]) * ad.inv_keep : 0.f;
+          t += to_f(r.v[j]);
+          r.v[j] = from_f<T>(t);
+        }
+        st16(static_cast<T*>(ad.xs) + (size_t)row * d + c * VEC, r);
+      }
 #pragma unroll
       for (int j = 0; j < VEC; ++j) { v[i][j] = to_f(r.v[j]); s1 += LN ? v[i][j] : v[i][j] * v[i][j]; }
     }
@@ -230,15 +256,15 @@ void col_reduce(const float* part, DType odt, void* out, int P, int d, bool accu
 }
 
 // ----------------------------------------------------------------------------- launchers
-template <typename T, bool LN>
+template <typename T, bool LN, bool ADD = false>
 static void fwd_dispatch(const void* x, const void* w, const void* b, void* y, float* mean, float* rstd,
-                         int N, int d, float eps, long ldy, hipStream_t s) {
+                         int N, int d, float eps, long ldy, hipStream_t s, AddDrop ad = AddDrop{}) {
   constexpr int VEC = 16 / sizeof(T);
   const int nvec = d / VEC;
   const int nv = (nvec + 63) / 64;
   dim3 grid(ceil_div(N, ROWS_PER_WG)), block(256);
-#define L(NVV) hipLaunchKernelGGL((norm_fwd_k<T, NVV, LN>), grid, block, 0, s, (const T*)x, (const T*)w, \
-                                  (const T*)b, (T*)y, mean, rstd, N, d, eps, ldy)
+#define L(NVV) hipLaunchKernelGGL((norm_fwd_k<T, NVV, LN, ADD>), grid, block, 0, s, (const T*)x, (const T*)w, \
+                                  (const T*)b, (T*)y, mean, rstd, N, d, eps, ldy, ad)
   if (nv <= 1) L(1); else if (nv <= 2) L(2); else if (nv <= 4) L(4); else if (nv <= 8) L(8); else L(16);
 #undef L
 }
@@ -288,6 +314,19 @@ void layernorm_bwd(DType dt, const void* dy, const void* x, const void* w, const
                    bool accumulate, int N, int d, int nwg, hipStream_t s) {
   BLLM_DISPATCH(dt, T, (bwd_dispatch<T, true>(dy, x, w, mean, rstd, dx_acc, dx, part_w, part_b, odt, dw, db,
                                               accumulate, N, d, nwg, s)));
+}
+
+void dropout_add_layernorm_fwd(DType dt, const void* x, const void* a, void* xs, const void* w, const void* b, void* y,
+                               float* mean, float* rstd, int N, int d, float eps, float p, uint64_t seed,
+                               uint64_t offset, hipStream_t s) {
+  AddDrop ad;
+  ad.a = a;
+  ad.xs = xs;
+  ad.seed = seed;
+  ad.offset = offset;
+  ad.thr = drop_threshold16(p);
+  ad.inv_keep = drop_inv_keep(p);
+  BLLM_DISPATCH(dt, T, (fwd_dispatch<T, true, true>(x, w, b, y, mean, rstd, N, d, eps, (long)d, s, ad)));
 }
 
 }  // namespace bllm

@@ -436,6 +436,26 @@ def test_bwd_bias_grad_fused(dt, N, F, acc):
             _ulps(db3, db4, dt, 1, name="gelu act db")
 
 
+@pytest.mark.parametrize("dt", DTYPES)
+@pytest.mark.parametrize("N,d", [(4096, 1280), (53, 768), (37, 64)])
+def test_dropout_add_layernorm_fused(dt, N, d):
+    """GPT-2's attention residual: dropout-add + LayerNorm forward in one pass, bitwise the two
+    kernels, and against the fp32 oracle."""
+    p, seed, off = 0.1, 4321, 1001
+    x = (torch.randn(N, d, device=DEV) + 0.5).to(dt)
+    a = torch.randn(N, d, device=DEV).to(dt)
+    w = (1 + 0.1 * torch.randn(d, device=DEV)).to(dt)
+    b = (0.1 * torch.randn(d, device=DEV)).to(dt)
+    x2, y, m, r = ops.dropout_add_layernorm(x, a, w, b, 1e-5, p, seed, off)
+    x2s = ops.dropout_add(x, a, p, seed, off)
+    ys, ms, rs = ops.layernorm_fwd(x2s, w, b, 1e-5)
+    assert torch.equal(x2, x2s) and torch.equal(y, ys) and torch.equal(m, ms) and torch.equal(r, rs)
+    x20 = ref.dropout_add(x.cpu().float(), a.cpu().float(), p, seed, off)
+    y0, _, _ = ref.layernorm_fwd(x20, w.cpu().float(), b.cpu().float(), 1e-5)
+    _close(x2, x20, dt, name="x2")
+    _close(y, y0, dt, 2, name="y")
+
+
 # ------------------------------------------------------------------ LoRA (csrc/lora.hip)
 def _up_only(t, Bs, c0, offs, s, N, M):
     out = torch.zeros(N, M, device=DEV)
@@ -558,6 +578,40 @@ def test_swiglu_bwd_lowrank(dt, N):
     _close(got, want, dt, 2, name="swiglu_bwd_lowrank")
     ref_dact = (base.float() + 0.5 * u.float() @ P.float()).to(dt)
     _close(got, ops.swiglu_bwd(gu, ref_dact), dt, 2, name="swiglu_bwd_lowrank vs fp32 dact")
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("N,F", [(1000, 1024), (4096, 512), (77, 192)])
+@pytest.mark.parametrize("accumulate", [False, True])
+def test_swiglu_bwd_lowrank_wgrad(dt, N, F, accumulate):
+    """SwiGLU backward of a LoRA MLP with the gate/up dB and the down dA summed in the same pass
+    (column-slab MFMA reductions) vs swiglu_bwd_lowrank + the separate lora_wgrad passes: dgu
+    bitwise, the gradients to a few fp32 summation-order ulps; and vs an fp32 matmul oracle."""
+    r, Rp = 16, 64
+    gu = torch.randn(N, 2 * F, device=DEV).to(dt)
+    dxa = torch.randn(N, F + Rp, device=DEV).to(dt)
+    P = (0.1 * torch.randn(r, F, device=DEV)).to(dt)
+    base, u = dxa[:, :F], dxa[:, F:F + r]
+    sta = torch.randn(N, 64 + 32, device=DEV).to(dt)      # [x part | s t (gate 16, up 16)] rows
+    st = sta[:, 64:96]
+    gdA = torch.randn(F, r, device=DEV).to(dt)
+    g0 = [torch.randn(r, F, device=DEV).to(dt), torch.randn(r, F, device=DEV).to(dt), gdA.t()]
+    g1 = [g.clone() for g in g0[:2]] + [gdA.clone().t()]
+    got = ops.swiglu_bwd_lowrank_wgrad(gu, base, u, P, 0.5, st, g1[0], g1[1], g1[2], accumulate)
+    want = ops.swiglu_bwd_lowrank(gu, base, u, P, 0.5)
+    assert torch.equal(got, want)
+    g2 = [g.clone() for g in g0[:2]] + [gdA.clone().t()]
+    ops.lora_wgrad(st, want, [g2[0], g2[1]], [0, 16], [0, F], 1.0, accumulate)
+    act = ops.swiglu_fwd(gu)
+    ops.lora_wgrad(u, act, [g2[2]], [0], [0], 0.5, accumulate)
+    for a, b, name in zip(g1, g2, ("dB gate", "dB up", "dA down")):
+        _ulps(a, b, dt, 1, name=name)
+    # fp32 oracle of the three reductions over the kernel's own (rounded) dg / du and act
+    F_ = F
+    for a, L, R, sc, g in ((g1[0], st[:, :16], want[:, :F_], 1.0, g0[0]), (g1[1], st[:, 16:], want[:, F_:], 1.0, g0[1]),
+                           (g1[2], u, act, 0.5, g0[2])):
+        ref32 = sc * (L.float().t() @ R.float()) + (g.float() if accumulate else 0)
+        _close(a, ref32.cpu(), dt, 4, name="vs fp32")
 
 
 def test_lora_model_uses_kernels_and_matches_gemm_path(monkeypatch):

@@ -333,3 +333,63 @@ def test_gemm_nt_kernel_in_model(monkeypatch):
     assert abs(l0 - l1) < 1e-2 * abs(l0)
     for k in g0:
         assert _rel(g1[k], g0[k]) < 2e-2, (k, _rel(g1[k], g0[k]))
+
+
+@pytest.mark.parametrize("ckpt", ["none", "selective", "full"])
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
+def test_fused_layernorm_dropout_in_model(ckpt, dt, monkeypatch):
+    """GPT-2 with dropout: the attention residual's dropout-add + norm2 as one row pass gives the
+    separate kernels' loss and gradients bitwise."""
+    from building_llm_from_scratch_amd.models import gpt2
+    ops.load_ext(required=True)
+    cfg = _cfgs()["gpt2"].replace(dtype=dt, drop_rate=0.1)
+    idx = torch.randint(0, cfg.vocab_size, (2, 257), device="cuda")
+    res, calls = {}, []
+    orig = ops.dropout_add_layernorm
+    monkeypatch.setattr(ops, "dropout_add_layernorm", lambda *a, **k: (calls.append(1), orig(*a, **k))[1])
+    for fused in (False, True):
+        monkeypatch.setattr(gpt2, "FUSED_LN_DROPOUT", fused)
+        torch.manual_seed(0)
+        m = build_model(cfg, use_actv_ckpt=ckpt, device="cuda")
+        m.flatten()
+        loss = m(idx[:, :-1], idx[:, 1:])
+        loss.backward()
+        res[fused] = (loss.item(), {k: p.grad.float().clone() for k, p in m.named_parameters()})
+    assert calls, "fused dropout-add + LayerNorm not used"
+    (l0, g0), (l1, g1) = res[False], res[True]
+    assert l0 == l1
+    for k in g0:
+        assert torch.equal(g1[k], g0[k]), (k, _rel(g1[k], g0[k]))
+
+
+def test_lora_swiglu_wgrad_fusion_in_model(monkeypatch):
+    """A LoRA Llama step with the MLP's gate/up dB and down dA summed inside the SwiGLU backward
+    (ops.swiglu_bwd_lowrank_wgrad) gives the separate lora_wgrad passes' loss and gradients."""
+    from building_llm_from_scratch_amd.models import llama
+    ops.load_ext(required=True)
+    cfg = get_config("llama3_2", "1B").replace(context_length=128, emb_dim=256, n_heads=4, n_kv_groups=2,
+                                               hidden_dim=512, n_layers=2, vocab_size=512, dtype=torch.bfloat16)
+    res, calls = {}, []
+    orig = ops.swiglu_bwd_lowrank_wgrad
+    monkeypatch.setattr(ops, "swiglu_bwd_lowrank_wgrad", lambda *a, **k: (calls.append(1), orig(*a, **k))[1])
+    for fused in (False, True):
+        monkeypatch.setattr(llama, "LORA_SWIGLU_WGRAD", fused)
+        torch.manual_seed(0)
+        m = build_model(cfg, device="cuda")
+        for p in m.parameters():
+            p.requires_grad = False
+        replace_linear_with_lora(m, rank=16, alpha=32)
+        for mod in m.modules():
+            if hasattr(mod, "B") and isinstance(mod.B, torch.nn.Parameter):
+                torch.nn.init.normal_(mod.B, std=0.05)
+        m.flatten(device="cuda")
+        idx = torch.randint(0, cfg.vocab_size, (2, 128), device="cuda", generator=torch.Generator("cuda").manual_seed(1))
+        for step in range(2):   # the second backward accumulates into the first's gradients
+            loss = m(idx, idx)
+            loss.backward()
+        res[fused] = (loss.item(), {n: p.grad.float().clone() for n, p in m.named_parameters() if p.requires_grad})
+    assert len(calls) == 4, calls     # 2 blocks x 2 steps
+    (l0, g0), (l1, g1) = res[False], res[True]
+    assert l0 == l1
+    for k in g0:
+        assert _rel(g1[k], g0[k]) < 1e-2, (k, _rel(g1[k], g0[k]))
