@@ -63,6 +63,12 @@ __device__ __forceinline__ void stv(T* p, const VecN<T, N>& r) {
   }
 }
 
+// SiLU gate sigma(a) = 1 / (1 + e^-a) on v_rcp_f32 (1 ulp): the IEEE division sequence (~10 VALU
+// instructions, two per element) made the SwiGLU passes VALU-bound.  Every SwiGLU kernel and the
+// GEMM epilogue form act = (a * sigma) * up from this one helper, so act is bitwise the same
+// wherever it is (re)computed.
+__device__ __forceinline__ float silu_sig(float a) { return __builtin_amdgcn_rcpf(1.f + __expf(-a)); }
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

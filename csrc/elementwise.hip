@@ -29,7 +29,7 @@ __global__ __launch_bounds__(256) void swiglu_fwd_k(const T* __restrict__ gu, T*
 #pragma unroll
     for (int j = 0; j < VEC; ++j) {
       const float a = to_f(g.v[j]);
-      o.v[j] = from_f<T>(a / (1.f + __expf(-a)) * to_f(u.v[j]));
+      o.v[j] = from_f<T>(a * silu_sig(a) * to_f(u.v[j]));
     }
     stv<T, VEC>(act + r * lda + c, o);
   }
@@ -48,10 +48,10 @@ __global__ __launch_bounds__(256) void swiglu_bwd_k(const T* __restrict__ gu, co
 #pragma unroll
     for (int j = 0; j < VEC; ++j) {
       const float a = to_f(g.v[j]), b = to_f(u.v[j]), dd = to_f(d.v[j]);
-      const float sg = 1.f / (1.f + __expf(-a));
+      const float sg = silu_sig(a);
       dg.v[j] = from_f<T>(dd * b * sg * (1.f + a * (1.f - sg)));
       du.v[j] = from_f<T>(dd * a * sg);
-      o.v[j] = from_f<T>(a / (1.f + __expf(-a)) * b);  // bitwise as swiglu_fwd
+      o.v[j] = from_f<T>(a * sg * b);  // bitwise as swiglu_fwd
     }
     stv<T, VEC>(dgu + r * 2 * F + c, dg);
     stv<T, VEC>(dgu + r * 2 * F + F + c, du);
@@ -108,7 +108,7 @@ __global__ __launch_bounds__(256) void swiglu_bwd_lr_k(const T* __restrict__ gu,
         // rounded to T like the lora_up output it replaces
         const float dd = to_f(from_f<T>(to_f(bs.v[e]) + s * corr[e]));
         const float a = to_f(g.v[e]), b = to_f(up.v[e]);
-        const float sg = 1.f / (1.f + __expf(-a));
+        const float sg = silu_sig(a);
         dg.v[e] = from_f<T>(dd * b * sg * (1.f + a * (1.f - sg)));
         du.v[e] = from_f<T>(dd * a * sg);
       }
@@ -163,7 +163,7 @@ __device__ __forceinline__ v8 lrw_frag(const char* tile, int stride, int col_byt
 }
 
 template <typename T>
-__global__ __launch_bounds__(256) void swiglu_bwd_lr_wg_k(const T* __restrict__ gu, const T* __restrict__ base,
+__global__ __launch_bounds__(256, 2) void swiglu_bwd_lr_wg_k(const T* __restrict__ gu, const T* __restrict__ base,
                                                           long ldb, const T* __restrict__ u, long ldu,
                                                           const T* __restrict__ P, const T* __restrict__ st,
                                                           long ldst, float s, T* __restrict__ dgu,
@@ -192,15 +192,21 @@ __global__ __launch_bounds__(256) void swiglu_bwd_lr_wg_k(const T* __restrict__ 
 
   Vec16<T> g, up, bs;
   uint4 lreg = make_uint4(0, 0, 0, 0);
+  // per-thread row pointers, advanced by one chunk per load (no 64-bit multiplies in the loop)
+  const T* pg = gu + (r0 + rr) * 2 * F + c;
+  const T* pb = base + (r0 + rr) * ldb + c;
+  const T* pl = lsrc + (r0 + lrow) * lld;
+  T* pd = dgu + (r0 + rr) * 2 * F + c;
+  const long step_g = (long)LRW_CH * 2 * F, step_b = (long)LRW_CH * ldb, step_l = (long)LRW_CH * lld;
   auto load = [&](long row) {
     if (row + rr < r1) {
-      const long rw = row + rr;
-      g = ld16(gu + rw * 2 * F + c);
-      up = ld16(gu + rw * 2 * F + F + c);
-      bs = ld16(base + rw * ldb + c);
+      g = ld16(pg);
+      up = ld16(pg + F);
+      bs = ld16(pb);
     }
     lreg = make_uint4(0, 0, 0, 0);
-    if (lq < 3 && row + lrow < r1) lreg = *reinterpret_cast<const uint4*>(lsrc + (row + lrow) * lld);
+    if (lq < 3 && row + lrow < r1) lreg = *reinterpret_cast<const uint4*>(pl);
+    pg += step_g, pb += step_b, pl += step_l;
   };
   lrw_f32x4 acc[3];
 #pragma unroll
@@ -229,15 +235,16 @@ __global__ __launch_bounds__(256) void swiglu_bwd_lr_wg_k(const T* __restrict__ 
       // rounded to T like the lora_up output it replaces (as swiglu_bwd_lr_k)
       const float dd = to_f(from_f<T>(to_f(cb.v[e]) + s * corr));
       const float a = to_f(cg.v[e]), b = to_f(cu.v[e]);
-      const float sg = 1.f / (1.f + __expf(-a));
+      const float sg = silu_sig(a);
       dg.v[e] = valid ? from_f<T>(dd * b * sg * (1.f + a * (1.f - sg))) : from_f<T>(0.f);
       du.v[e] = valid ? from_f<T>(dd * a * sg) : from_f<T>(0.f);
-      act.v[e] = valid ? from_f<T>(a / (1.f + __expf(-a)) * b) : from_f<T>(0.f);  // bitwise as swiglu_fwd
+      act.v[e] = valid ? from_f<T>(a * sg * b) : from_f<T>(0.f);  // bitwise as swiglu_fwd
     }
     if (valid) {
-      st16(dgu + (row + rr) * 2 * F + c, dg);
-      st16(dgu + (row + rr) * 2 * F + F + c, du);
+      st16(pd, dg);
+      st16(pd + F, du);
     }
+    pd += step_g;
     st16(reinterpret_cast<T*>(Rt[par][0] + rr * LRW_RS + cv * 16), dg);
     st16(reinterpret_cast<T*>(Rt[par][1] + rr * LRW_RS + cv * 16), du);
     st16(reinterpret_cast<T*>(Rt[par][2] + rr * LRW_RS + cv * 16), act);
@@ -288,7 +295,7 @@ __global__ __launch_bounds__(256) void swiglu_fwd_rows_k(const T* __restrict__ g
 #pragma unroll
         for (int j = 0; j < VEC; ++j) {
           const float a = to_f(g[k].v[j]);
-          o.v[j] = from_f<T>(a / (1.f + __expf(-a)) * to_f(u[k].v[j]));
+          o.v[j] = from_f<T>(a * silu_sig(a) * to_f(u[k].v[j]));
         }
         stv<T, VEC>(o0 + c * VEC, o);
       }
@@ -326,10 +333,10 @@ __global__ __launch_bounds__(256) void swiglu_bwd_rows_k(const T* __restrict__ g
 #pragma unroll
         for (int j = 0; j < VEC; ++j) {
           const float a = to_f(g[k].v[j]), b = to_f(u[k].v[j]), dd = to_f(d[k].v[j]);
-          const float sg = 1.f / (1.f + __expf(-a));
+          const float sg = silu_sig(a);
           dg.v[j] = from_f<T>(dd * b * sg * (1.f + a * (1.f - sg)));
           du.v[j] = from_f<T>(dd * a * sg);
-          o.v[j] = from_f<T>(a / (1.f + __expf(-a)) * b);  // bitwise as swiglu_fwd
+          o.v[j] = from_f<T>(a * sg * b);  // bitwise as swiglu_fwd
         }
         stv<T, VEC>(dg0 + c * VEC, dg);
         stv<T, VEC>(du0 + c * VEC, du);

@@ -164,7 +164,7 @@ __device__ __forceinline__ void epilogue4(f32x4 (&acc)[8][8], char* smem, int wm
 #pragma unroll
           for (int k = 0; k < EPT; ++k) {
             const float a = to_f(from_f<OT>(g[k])), b = to_f(from_f<OT>(u[k]));
-            w.e[k] = from_f<OT>(a / (1.f + __expf(-a)) * b);
+            w.e[k] = from_f<OT>(a * silu_sig(a) * b);
           }
           *(V16*)(act + (m0 + pass * 128 + lr) * (long)F + g0 + it * EPT) = w;
         }

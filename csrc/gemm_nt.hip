@@ -344,7 +344,7 @@ __global__ __launch_bounds__(THREADS4, 1) void gemm_nt4p_k(const T* __restrict__
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             const float a = to_f(gb[e]), b = to_f(ub[e]);
-            w[e] = from_f<OT>(a / (1.f + __expf(-a)) * b);
+            w[e] = from_f<OT>(a * silu_sig(a) * b);
           }
           *(o4*)(act + r * (long)F + col) = w;
         }

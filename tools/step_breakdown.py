@@ -24,6 +24,7 @@ BLLM_CLASSES = {
     "attn_fwd_naive_k": "attn (naive path)", "attn_bwd_dkv_naive_k": "attn (naive path)", "attn_bwd_dq_naive_k": "attn (naive path)",
     "swiglu_fwd_k": "swiglu_fwd", "swiglu_fwd_rows_k": "swiglu_fwd", "swiglu_bwd_k": "swiglu_bwd", "swiglu_bwd_rows_k": "swiglu_bwd",
     "swiglu_bwd_lr_k": "swiglu_bwd (+ LoRA dX of the down projection)",
+    "swiglu_bwd_lr_wg_k": "swiglu_bwd (+ LoRA dX of the down projection, gate/up dB, down dA)",
     "gelu_fwd_k": "gelu_fwd", "gelu_bwd_k": "gelu_bwd",
     "bwd_colsum_k": "bwd_colsum (GELU / dropout backward + bias column sums, csrc/elementwise.hip)",
     "col_reduce_k": "col_reduce",
