@@ -998,11 +998,7 @@ hipblasLtHandle_t lt_handle(int dev) {
   if (!h[dev]) LT_CHECK(hipblasLtCreate(&h[dev]));
   return h[dev];
 }
-struct LtOperands {
-  const void *W, *x, *C;
-  void *D, *ws;
-};
-const LtPlan& lt_plan(int dev, hipDataType dt, int64_t N, int64_t K, int64_t O, const LtOperands* tune_ops) {
+const LtPlan& lt_plan(int dev, hipDataType dt, int64_t N, int64_t K, int64_t O) {
   static std::map<std::tuple<int, int, int64_t, int64_t, int64_t>, LtPlan> cache;
   const auto key = std::make_tuple(dev, (int)dt, N, K, O);
   {
@@ -1023,44 +1019,14 @@ const LtPlan& lt_plan(int dev, hipDataType dt, int64_t N, int64_t K, int64_t O, 
   LT_CHECK(hipblasLtMatmulPreferenceCreate(&pref));
   uint64_t ws = kLtWorkspace;
   LT_CHECK(hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &ws, sizeof(ws)));
-  constexpr int kMaxCand = 16;
-  hipblasLtMatmulHeuristicResult_t res[kMaxCand];
+  // heuristic top-1: timing the top 16 on the real operands measured 0.4 % slower end to end
+  // (profiles/r5/lt_tune/) and made the choice process-dependent; removed in round 5
+  hipblasLtMatmulHeuristicResult_t res[1];
   int n = 0;
-  const char* tune_env = getenv("BLLM_LT_TUNE");
-  const bool tune = tune_env && tune_env[0] == '1' && tune_ops != nullptr;
-  LT_CHECK(hipblasLtMatmulAlgoGetHeuristic(h, p.op, p.a, p.b, p.c, p.c, pref, tune ? kMaxCand : 1, res, &n));
+  LT_CHECK(hipblasLtMatmulAlgoGetHeuristic(h, p.op, p.a, p.b, p.c, p.c, pref, 1, res, &n));
   hipblasLtMatmulPreferenceDestroy(pref);
   TORCH_CHECK(n > 0, "hipBLASLt: no solution for residual GEMM N=", N, " K=", K, " O=", O);
   p.algo = res[0].algo;
-  if (tune && n > 1) {
-    // opt-in (BLLM_LT_TUNE=1): time every heuristic candidate on the real operands (D is a scratch
-    // output, C is only read) and keep the fastest.  Timing-based, so the choice (and the bits)
-    // can differ between processes: off by default for reproducibility.
-    const float alpha = 1.f, beta = 1.f;
-    hipStream_t st = stream();
-    hipEvent_t e0, e1;
-    (void)hipEventCreate(&e0);
-    (void)hipEventCreate(&e1);
-    float best = 1e30f;
-    int besti = 0;
-    for (int i = 0; i < n; ++i) {
-      float ms = 0.f;
-      bool ok = true;
-      for (int rep = 0; rep < 4 && ok; ++rep) {
-        if (rep == 1) (void)hipEventRecord(e0, st);
-        ok = hipblasLtMatmul(h, p.op, &alpha, tune_ops->W, p.a, tune_ops->x, p.b, &beta, tune_ops->C, p.c,
-                             tune_ops->D, p.c, &res[i].algo, tune_ops->ws, kLtWorkspace, st) == HIPBLAS_STATUS_SUCCESS;
-      }
-      if (!ok) continue;
-      (void)hipEventRecord(e1, st);
-      (void)hipEventSynchronize(e1);
-      (void)hipEventElapsedTime(&ms, e0, e1);
-      if (ms < best) { best = ms; besti = i; }
-    }
-    (void)hipEventDestroy(e0);
-    (void)hipEventDestroy(e1);
-    p.algo = res[besti].algo;
-  }
   std::lock_guard<std::mutex> g(lt_mu);
   return cache.emplace(key, p).first->second;
 }
@@ -1080,8 +1046,7 @@ Tensor linear_residual(const Tensor& x, const Tensor& W, const Tensor& C) {
   const hipDataType dt = x.scalar_type() == at::kBFloat16 ? HIP_R_16BF : HIP_R_16F;
   auto D = at::empty({N, O}, x.options());
   auto ws = at::empty({(int64_t)kLtWorkspace}, x.options().dtype(at::kByte));
-  const LtOperands ops{W.data_ptr(), x.data_ptr(), C.data_ptr(), D.data_ptr(), ws.data_ptr()};
-  const LtPlan& p = lt_plan(dev, dt, N, K, O, &ops);
+  const LtPlan& p = lt_plan(dev, dt, N, K, O);
   const float alpha = 1.f, beta = 1.f;
   LT_CHECK(hipblasLtMatmul(lt_handle(dev), p.op, &alpha, W.data_ptr(), p.a, x.data_ptr(), p.b, &beta, C.data_ptr(),
                            p.c, D.data_ptr(), p.c, &p.algo, ws.data_ptr(), kLtWorkspace, stream()));
