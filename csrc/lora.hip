@@ -55,79 +55,91 @@ template <typename T> __device__ __forceinline__ float from_bits(short b) {
 }
 
 // --------------------------------------------------------------------------- lora_down
-// Block = 8 waves on 16 rows; the K loop is split over the waves (wave w takes k-steps
-// w, w+8, ...; eight, then four, per trip: that many 16-B x loads in flight per lane) and the
-// eight partial 16 x (16*NT) tiles are summed through LDS.
-// MFMA: A = X rows (lane: X[row l&15][k 8(l>>4)..+8], one 16-B load), B[k][col] = W[col][k]
-// (W rows are k-contiguous -> one 16-B load per column tile).
-template <typename T>
-__global__ __launch_bounds__(512) void lora_down_k(LoraDownArgs a, int N) {
-  constexpr int NW = 8;
-  __shared__ float red[NW][16][4 * 16 + 1];
+// Block = 4 waves on 64 rows; the waves split K (wave w takes k-steps w, w+4, ...; two per trip:
+// 8 x loads in flight per lane) and each runs the block's 4 row tiles against ONE W fragment per
+// column tile and k-step, so W (the packed A^T / B, nt*16 columns) crosses L2 -> CU once per 64
+// rows.  (Round 4's kernel did 16 rows per block: at nt = 2-3 (gate/up, QKV) it moved 2-3x more
+// W than x bytes and ran at 2.2-2.9 TB/s of x; this one 3.2-5.2 TB/s, tools/bench_lora.py,
+// profiles/r5/lora_kernels/.)  MFMA: A = X rows (lane: X[row l&15][k 8(l>>4)..+8], one 16-B load),
+// B[k][col] = W[col][k] (W rows are k-contiguous -> one 16-B load per column tile).  The four
+// partial [64 x cols] tiles meet in (dynamic) LDS and are summed in a fixed order.
+template <typename T, int NTM>
+__global__ __launch_bounds__(256) void lora_down4_k(LoraDownArgs a, int N) {
+  constexpr int NW = 4, RT = 4, ROWS = 16 * RT;  // NTM: max column tiles over the launch's chunks
+  extern __shared__ float red4[];  // [NW][ROWS][cols + 1]
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int ch = blockIdx.y;
-  const int nt = a.nt[ch];
-  const long row0 = (long)blockIdx.x * 16;
-  // rows past the token count (last block of an N % 16 != 0 batch) read row N-1, never stored
-  const long xr = row0 + (lane & 15) < N ? row0 + (lane & 15) : N - 1;
-  const T* x = (const T*)a.x + xr * a.ldx + a.c0[ch] + 8 * (lane >> 4);
+  const int nt = a.nt[ch], cols = nt * 16, ldr = cols + 1;
+  const long row0 = (long)blockIdx.x * ROWS;
+  const T* xs[RT];
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt) {
+    // rows past the token count read row N-1 (never stored)
+    const long xr = row0 + rt * 16 + (lane & 15) < N ? row0 + rt * 16 + (lane & 15) : N - 1;
+    xs[rt] = (const T*)a.x + xr * a.ldx + a.c0[ch] + 8 * (lane >> 4);
+  }
   const T* w = (const T*)a.w[ch] + (long)(lane & 15) * a.ldw[ch] + 8 * (lane >> 4);
   const long wstep = 16 * a.ldw[ch];
-  f32x4 acc[4];
+  f32x4 acc[RT][NTM];
 #pragma unroll
-  for (int t = 0; t < 4; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+    for (int t = 0; t < NTM; ++t) acc[rt][t] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int nks = a.len[ch] >> 5;
   int ks = wave;
-  for (; ks + 7 * NW < nks; ks += 8 * NW) {  // eight 16-B x loads in flight per lane
-    s16x8 xa[8];
+  for (; ks + NW < nks; ks += 2 * NW) {  // two k-steps per trip: 8 x loads in flight per lane
+    s16x8 xa[2][RT];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) xa[u] = ld8(x + (ks + u * NW) * 32);
+    for (int u = 0; u < 2; ++u)
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
+      for (int rt = 0; rt < RT; ++rt) xa[u][rt] = ld8(xs[rt] + (ks + u * NW) * 32);
+#pragma unroll
+    for (int t = 0; t < NTM; ++t) {
       if (t < nt) {
 #pragma unroll
-        for (int u = 0; u < 8; ++u) acc[t] = MF16<T>::mma(xa[u], ld8(w + t * wstep + (ks + u * NW) * 32), acc[t]);
-      }
-    }
-  }
-  for (; ks + 3 * NW < nks; ks += 4 * NW) {
-    s16x8 xa[4];
+        for (int u = 0; u < 2; ++u) {
+          const s16x8 wb = ld8(w + t * wstep + (ks + u * NW) * 32);
 #pragma unroll
-    for (int u = 0; u < 4; ++u) xa[u] = ld8(x + (ks + u * NW) * 32);
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      if (t < nt) {
-#pragma unroll
-        for (int u = 0; u < 4; ++u) acc[t] = MF16<T>::mma(xa[u], ld8(w + t * wstep + (ks + u * NW) * 32), acc[t]);
+          for (int rt = 0; rt < RT; ++rt) acc[rt][t] = MF16<T>::mma(xa[u][rt], wb, acc[rt][t]);
+        }
       }
     }
   }
   for (; ks < nks; ks += NW) {
-    const s16x8 xa0 = ld8(x + ks * 32);
+    s16x8 xa[RT];
 #pragma unroll
-    for (int t = 0; t < 4; ++t)
-      if (t < nt) acc[t] = MF16<T>::mma(xa0, ld8(w + t * wstep + ks * 32), acc[t]);
+    for (int rt = 0; rt < RT; ++rt) xa[rt] = ld8(xs[rt] + ks * 32);
+#pragma unroll
+    for (int t = 0; t < NTM; ++t) {
+      if (t < nt) {
+        const s16x8 wb = ld8(w + t * wstep + ks * 32);
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) acc[rt][t] = MF16<T>::mma(xa[rt], wb, acc[rt][t]);
+      }
+    }
   }
-  // C layout: lane holds C[row 4(l>>4)+i][col l&15]
+  // C layout: lane holds C[row 4(l>>4)+i][col l&15] of each 16 x 16 tile
 #pragma unroll
-  for (int t = 0; t < 4; ++t)
-    if (t < nt)
+  for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) red[wave][4 * (lane >> 4) + i][t * 16 + (lane & 15)] = acc[t][i];
+    for (int t = 0; t < NTM; ++t)
+      if (t < nt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          red4[(wave * ROWS + rt * 16 + 4 * (lane >> 4) + i) * ldr + t * 16 + (lane & 15)] = acc[rt][t][i];
   __syncthreads();
-  const int cols = nt * 16;
   T* out = (T*)a.out + row0 * a.ldo + a.ocol[ch];
-  for (int e = threadIdx.x; e < 16 * cols; e += NW * 64) {
+  for (int e = threadIdx.x; e < ROWS * cols; e += NW * 64) {
     const int r = e / cols, c = e - r * cols;
     if (row0 + r >= N) continue;
     float v = 0.f;
 #pragma unroll
-    for (int q = 0; q < NW; ++q) v += red[q][r][c];
+    for (int q = 0; q < NW; ++q) v += red4[(q * ROWS + r) * ldr + c];
     out[(long)r * a.ldo + c] = from_f<T>(v * a.scale);
   }
   if (ch == 0 && a.zpad > 0) {  // zero columns [R, R + zpad): the alignment pad of a K-augmented row
     T* pad = (T*)a.out + row0 * a.ldo + a.R;
-    for (int e = threadIdx.x; e < 16 * a.zpad; e += NW * 64) {
+    for (int e = threadIdx.x; e < ROWS * a.zpad; e += NW * 64) {
       const int r = e / a.zpad, c = e - r * a.zpad;
       if (row0 + r < N) pad[(long)r * a.ldo + c] = from_f<T>(0.f);
     }
@@ -182,11 +194,27 @@ __global__ __launch_bounds__(256) void lora_up_k(LoraUpArgs a, int rows, int N) 
       }
     }
     __syncthreads();
+    // the base (or, in a later rank pass, y) rows of a tile are loaded one tile ahead (register
+    // double buffer): loaded inside the epilogue, one 4-row group at a time, they left the
+    // kernel latency-bound at ~3 TB/s
+    VecN<T, 8> bsv[4], bsn[4];
+    auto load_base = [&](long r0_, VecN<T, 8> (&dst)[4]) {
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        const int row = (lane >> 4) + 4 * p;
+        if (col_ok && r0_ + row < N) {
+          if (j0) dst[p] = ldv<T, 8>((const T*)a.y + (r0_ + row) * a.ldy + a.c0[m] + cb + c8);
+          else if (a.base) dst[p] = ldv<T, 8>((const T*)a.base + (r0_ + row) * a.ldb + a.c0[m] + cb + c8);
+        }
+      }
+    };
+    load_base((long)blockIdx.x * rows + wave * 16, bsv);
     for (int rt = 0; rt < rows / 64; ++rt) {
       const long row0 = (long)blockIdx.x * rows + rt * 64 + wave * 16;
       if (row0 >= N) break;  // wave-uniform: this wave's remaining tiles are past the tokens
       const long tr = row0 + (lane & 15) < N ? row0 + (lane & 15) : N - 1;
       const T* t = (const T*)a.t + tr * a.ldt + a.toff[m] + j0;
+      if (rt + 1 < rows / 64 && row0 + 64 < N) load_base(row0 + 64, bsn);
       f32x4 acc[8];
 #pragma unroll
       for (int q = 0; q < 8; ++q) acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -214,11 +242,9 @@ __global__ __launch_bounds__(256) void lora_up_k(LoraUpArgs a, int rows, int N) 
         const f32x4 v0 = *reinterpret_cast<const f32x4*>(&ep[row * EP + c8]);
         const f32x4 v1 = *reinterpret_cast<const f32x4*>(&ep[row * EP + c8 + 4]);
         const float v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
-        VecN<T, 8> bs, o;
-        if (a.base) bs = ldv<T, 8>((const T*)a.base + (row0 + row) * a.ldb + a.c0[m] + cb + c8);
-        if (j0) {  // later rank pass: accumulate onto what the first pass wrote
-          bs = ldv<T, 8>((const T*)a.y + g);
-        }
+        // later rank pass: bsv holds what the first pass wrote (y)
+        const VecN<T, 8> bs = bsv[p];
+        VecN<T, 8> o;
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
           float z = a.scale * v[i];
@@ -228,6 +254,8 @@ __global__ __launch_bounds__(256) void lora_up_k(LoraUpArgs a, int rows, int N) 
         }
         stv<T, 8>((T*)a.y + g, o);
       }
+#pragma unroll
+      for (int p = 0; p < 4; ++p) bsv[p] = bsn[p];
       __builtin_amdgcn_wave_barrier();  // tile reads done before the next tile's writes
     }
   }
@@ -387,9 +415,25 @@ void lora_block(DType dt, const LoraBlockArgs& a, hipStream_t s) {
 }
 
 void lora_down(DType dt, const LoraDownArgs& a, int N, hipStream_t s) {
-  dim3 grid(ceil_div(N, 16), a.n);
-  if (dt == DType::BF16) hipLaunchKernelGGL(lora_down_k<bf16_t>, grid, dim3(512), 0, s, a, N);
-  else hipLaunchKernelGGL(lora_down_k<f16_t>, grid, dim3(512), 0, s, a, N);
+  int max_cols = 16;
+  for (int c = 0; c < a.n; ++c) max_cols = max_cols > a.nt[c] * 16 ? max_cols : a.nt[c] * 16;
+  const size_t lds = (size_t)4 * 64 * (max_cols + 1) * sizeof(float);
+  dim3 grid(ceil_div(N, 64), a.n);
+#define LD4(TT, NTM)                                                                                            \
+  do {                                                                                                          \
+    static const bool attr = hipFuncSetAttribute((const void*)lora_down4_k<TT, NTM>,                           \
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, 4 * 64 * 65 * 4) == \
+                             hipSuccess;                                                                        \
+    (void)attr;                                                                                                 \
+    hipLaunchKernelGGL((lora_down4_k<TT, NTM>), grid, dim3(256), lds, s, a, N);                                 \
+  } while (0)
+  const int ntm = max_cols / 16;
+  if (dt == DType::BF16) {
+    if (ntm == 1) LD4(bf16_t, 1); else if (ntm == 2) LD4(bf16_t, 2); else if (ntm == 3) LD4(bf16_t, 3); else LD4(bf16_t, 4);
+  } else {
+    if (ntm == 1) LD4(f16_t, 1); else if (ntm == 2) LD4(f16_t, 2); else if (ntm == 3) LD4(f16_t, 3); else LD4(f16_t, 4);
+  }
+#undef LD4
 }
 
 void lora_up(DType dt, const LoraUpArgs& a, int N, int max_len, hipStream_t s) {

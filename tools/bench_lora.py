@@ -33,6 +33,10 @@ def main():
     ap.add_argument("--tokens", type=int, default=38400, help="default: the LoRA preset's ~38k tokens per step")
     ap.add_argument("--rank", type=int, default=16)
     ap.add_argument("--iters", type=int, default=50)
+    ap.add_argument("--only", default=None, help="comma-separated case-name prefixes")
+    ap.add_argument("--env_ab", default=None,
+                    help="'|'-separated arms of KEY=VALUE[+KEY=VALUE] environment settings read per launch "
+                         "(e.g. 'BLLM_LORA_DOWN=16|'), each case timed under every arm")
     a = ap.parse_args()
     ops.load_ext(required=True)
     N, r, dt = a.tokens, a.rank, torch.bfloat16
@@ -70,9 +74,17 @@ def main():
             "wgrad_A": (lambda: ops.lora_wgrad(u, x, [g.t() for g in gA], offs, [0] * len(outs), 2.0), N * K * 2),
         }
         for k, (fn, nbytes) in cases.items():
-            us = timeit(fn, a.iters)
-            res[k] = {"us": round(us, 1), "roofline_us": round(nbytes / HBM * 1e6, 1),
-                      "TB/s": round(nbytes / us / 1e6, 2)}
+            if a.only and not any(k.startswith(o) for o in a.only.split(",")):
+                continue
+            for env in (a.env_ab.split("|") if a.env_ab else [""]):
+                for kv in env.split("+") if env else []:   # KEY=VALUE[+KEY=VALUE] set for this arm
+                    key, val = kv.split("=", 1)
+                    os.environ[key] = val
+                us = timeit(fn, a.iters)
+                for kv in env.split("+") if env else []:
+                    os.environ.pop(kv.split("=", 1)[0], None)
+                res[k + (f"[{env}]" if env else "")] = {"us": round(us, 1), "roofline_us": round(nbytes / HBM * 1e6, 1),
+                                                        "TB/s": round(nbytes / us / 1e6, 2)}
         print(json.dumps(res), flush=True)
         del x, dy, y, dx, t, u, xa
         torch.cuda.empty_cache()
