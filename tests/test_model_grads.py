@@ -305,3 +305,26 @@ def test_reference_gpt_model_smoke_shape():
         logits = m(idx)
     assert logits.shape == (2, 128, 50257)
     assert torch.isfinite(logits).all()
+
+
+def test_swiglu_bwd_lowrank_wgrad_reference_semantics():
+    """The CPU path of ops.swiglu_bwd_lowrank_wgrad (the contract its HIP kernel is tested
+    against on the GPU): dgu = swiglu_bwd(gu, base + s u P), gB_gate/up (+)= st^T dg / du,
+    gA_down^T (+)= s u^T swiglu_fwd(gu)."""
+    import torch
+    from building_llm_from_scratch_amd import ops
+    from building_llm_from_scratch_amd.ops import reference as ref
+    torch.manual_seed(0)
+    N, F, r, s = 37, 64, 16, 0.5
+    gu, base = torch.randn(N, 2 * F), torch.randn(N, F)
+    u, P, st = torch.randn(N, r), 0.1 * torch.randn(r, F), torch.randn(N, 32)
+    for acc in (False, True):
+        g0 = [torch.randn(r, F), torch.randn(r, F), torch.randn(F, r).t()]
+        g = [x.clone() for x in g0]
+        dgu = ops.swiglu_bwd_lowrank_wgrad(gu, base, u, P, s, st, g[0], g[1], g[2], acc)
+        want = ref.swiglu_bwd(gu, base + s * u @ P)
+        assert torch.allclose(dgu, want, atol=1e-5)
+        act = ref.swiglu_fwd(gu)
+        exp = [st[:, :16].t() @ want[:, :F], st[:, 16:].t() @ want[:, F:], s * u.t() @ act]
+        for a, e, b in zip(g, exp, g0):
+            assert torch.allclose(a, e + (b if acc else 0), atol=1e-4)
