@@ -100,7 +100,9 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
 // exp(-x^2 / 2) with phi.  libm's erff branches by range (divergent in a wave) and made the GELU
 // backward passes VALU-bound (~100 instructions per element); this is ~15, all full-rate but one
 // v_exp and one v_rcp.
-__device__ __forceinline__ float gelu_grad(float x) {
+// Phi(x) (standard normal CDF) and phi(x) on the A&S 7.1.26 erfc form (abs. error 1.5e-7):
+// branch-free, ~15 full-rate instructions
+__device__ __forceinline__ float norm_cdf_pdf(float x, float& pdf) {
   const float z = fabsf(x) * 0.70710678118654752f;
   // v_rcp_f32 (1 ulp): __frcp_rn lowers to the IEEE division sequence (div_scale / div_fmas /
   // div_fixup, ~10 instructions), more than the rest of the function; A&S 7.1.26 is 1.5e-7 anyway
@@ -108,8 +110,27 @@ __device__ __forceinline__ float gelu_grad(float x) {
   const float poly = t * (0.254829592f + t * (-0.284496736f + t * (1.421413741f + t * (-1.453152027f + t * 1.061405429f))));
   const float e = __expf(-0.5f * x * x);
   const float tail = 0.5f * poly * e;                  // 1 - Phi(|x|)
-  const float cdf = x >= 0.f ? 1.f - tail : tail;
-  return cdf + x * (e * 0.39894228040143268f);
+  pdf = e * 0.39894228040143268f;
+  return x >= 0.f ? 1.f - tail : tail;
+}
+__device__ __forceinline__ float gelu_grad(float x) {
+  float pdf;
+  const float cdf = norm_cdf_pdf(x, pdf);
+  return cdf + x * pdf;
+}
+// exact-erf GELU x Phi(x).  16-bit outputs use the A&S form above (its 1.5e-7 is far below a
+// bf16 / fp16 rounding unit, and libm's range-branching erff cost ~100 VALU instructions per
+// element -- the reason the fused c_fc + bias + GELU GEMM epilogue lost to the separate pass);
+// fp32 keeps libm's erff.  Every GELU forward (the elementwise kernel, the GEMM epilogue and the
+// GELU backward's rebuild of g) goes through this one function, so g is bitwise the same
+// wherever it is (re)computed.
+template <typename T> __device__ __forceinline__ float gelu_fwd_f(float x) {
+  if constexpr (sizeof(T) == 2) {
+    float pdf;
+    return x * norm_cdf_pdf(x, pdf);
+  } else {
+    return 0.5f * x * (1.f + erff(x * 0.70710678118654752f));
+  }
 }
 
 // ---------------------------------------------------------------- dropout RNG

@@ -354,7 +354,7 @@ __global__ __launch_bounds__(256) void gelu_fwd_k(const T* __restrict__ f, T* __
 #pragma unroll
     for (int j = 0; j < VEC; ++j) {
       const float x = to_f(a.v[j]);
-      o.v[j] = from_f<T>(0.5f * x * (1.f + erff(x * 0.70710678118654752f)));
+      o.v[j] = from_f<T>(gelu_fwd_f<T>(x));
     }
     stv<T, VEC>(g + i * VEC, o);
   }
@@ -529,7 +529,7 @@ __global__ __launch_bounds__(256) void bwd_colsum_k(const T* src, const T* __res
       for (int j = 0; j < VEC; ++j) {
         const float x = to_f(a.v[j]);
         o.v[j] = from_f<T>(to_f(v.v[j]) * gelu_grad(x));
-        if constexpr (OP == 2) g.v[j] = from_f<T>(0.5f * x * (1.f + erff(x * 0.70710678118654752f)));   // = gelu_fwd
+        if constexpr (OP == 2) g.v[j] = from_f<T>(gelu_fwd_f<T>(x));   // = gelu_fwd
       }
       if constexpr (OP == 2) st16(act + e, g);
     }

@@ -294,7 +294,7 @@ __global__ __launch_bounds__(THREADS4, 1) void gemm_nt4p_k(const T* __restrict__
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             const float x = to_f(fb[e]);
-            gb[e] = from_f<OT>(0.5f * x * (1.f + erff(x * 0.70710678118654752f)));
+            gb[e] = from_f<OT>(gelu_fwd_f<OT>(x));
           }
           *(o4*)(act + off) = gb;
         }
