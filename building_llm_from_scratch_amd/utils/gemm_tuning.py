@@ -37,7 +37,11 @@ def resolve_table(spec: Optional[str], model: str = "", size: str = "") -> Optio
         if spec is None:
             return None
     path = spec if os.path.isabs(spec) else os.path.join(ROOT, spec)
-    return path if os.path.exists(path) else None
+    if not os.path.exists(path):
+        import warnings
+        warnings.warn(f"TunableOp table {spec!r} not found: GEMMs use the libraries' heuristics")
+        return None
+    return path
 
 
 def install_table(path: Optional[str], local_rank: int = 0) -> Optional[str]:

@@ -419,7 +419,8 @@ def test_tunableop_table_resolution(tmp_path, monkeypatch):
     assert gt.resolve_table("auto", "GPT2", "774M").endswith("tunableop_gpt2_774m_b64_mi355x.csv")
     assert gt.resolve_table("auto", "llama3_2", "1B") is None
     assert gt.resolve_table("none", "llama3", "8B") is None and gt.resolve_table(None) is None
-    assert gt.resolve_table(str(tmp_path / "missing.csv")) is None
+    with pytest.warns(UserWarning, match="not found"):
+        assert gt.resolve_table(str(tmp_path / "missing.csv")) is None
     for k in ("PYTORCH_TUNABLEOP_ENABLED", "PYTORCH_TUNABLEOP_TUNING", "PYTORCH_TUNABLEOP_FILENAME"):
         monkeypatch.delenv(k, raising=False)
     assert gt.install_table(None) is None and "PYTORCH_TUNABLEOP_ENABLED" not in os.environ

@@ -79,6 +79,15 @@ def main():
     ):
         us = _time(fn)
         res[name] = {"us": round(us, 1), "GBps": round(nbytes / us / 1e3, 1)}
+    del gu, da
+    # fused AdamW on a 1 G-parameter slot (bf16 param + grad, fp32 master / m / v): 28 B per parameter
+    n = 1 << 30
+    p_ = torch.zeros(n, device=dev, dtype=dt)
+    g_ = torch.full((n,), 1e-3, device=dev, dtype=dt)
+    mst = torch.zeros(n, device=dev, dtype=torch.float32)
+    m1, m2 = torch.zeros_like(mst), torch.zeros_like(mst)
+    us = _time(lambda: ops.adamw_step_(p_, mst, g_, m1, m2, 1e-4, 0.9, 0.95, 1e-8, 0.1, 1), iters=5)
+    res["adamw_1g_params"] = {"us": round(us, 1), "GBps": round(28 * n / us / 1e3, 1)}
     print(json.dumps(res), flush=True)
 
 

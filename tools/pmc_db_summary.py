@@ -14,6 +14,7 @@ def main():
     ap.add_argument("--filter", default="")
     a = ap.parse_args()
     agg = collections.defaultdict(lambda: collections.defaultdict(float))
+    rows = collections.defaultdict(lambda: collections.defaultdict(int))
     for path in a.db:
         con = sqlite3.connect(path)
         for name, cname, val in con.execute("select name, counter_name, counter_value from pmc_events"):
@@ -21,10 +22,12 @@ def main():
                 continue
             k = re.sub(r"\(.*", "", name)[:100]
             agg[k][cname] += float(val)
+            rows[k][cname] += 1
     for k, d in agg.items():
         print(k)
         for c, v in sorted(d.items()):
-            print(f"    {c:32s} {v:12.4g}")
+            # rows: pmc_events records of this counter (one per dispatch for a derived counter)
+            print(f"    {c:32s} {v:12.4g}   rows {rows[k][c]}")
         wc = d.get("SQ_WAVE_CYCLES")
         if wc:
             for c in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_LDS",
