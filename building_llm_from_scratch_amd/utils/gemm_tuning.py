@@ -15,6 +15,7 @@ from __future__ import annotations
 import os
 import shutil
 import tempfile
+import warnings
 from typing import Optional
 
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -38,7 +39,6 @@ def resolve_table(spec: Optional[str], model: str = "", size: str = "") -> Optio
             return None
     path = spec if os.path.isabs(spec) else os.path.join(ROOT, spec)
     if not os.path.exists(path):
-        import warnings
         warnings.warn(f"TunableOp table {spec!r} not found: GEMMs use the libraries' heuristics")
         return None
     return path
