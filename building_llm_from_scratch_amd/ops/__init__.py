@@ -296,11 +296,47 @@ def wgrad_splits(M: int, N: int, K: int, n_cu: int = 256) -> int:
     return best
 
 
+# BLLM_WGRAD_TAIL=0: a ragged last wave is always handled by splitting every tile (A/B)
+WGRAD_TAIL = os.environ.get("BLLM_WGRAD_TAIL", "1") != "0"
+
+
+def wgrad_plan(M: int, N: int, K: int, n_cu: int = 256):
+    """("split", S) or ("tail", full, St) for the dW kernel.  Splitting EVERY tile S ways evens out a
+    ragged last wave but round-trips S fp32 copies of the whole [M, N] through HBM (Llama-3-8B
+    down projection: 896 tiles = 3.5 waves, S = 2 moves 1.2 GB).  The tail plan runs the whole
+    waves [0, full) at full K straight into the output and splits only the ragged tail St ways into
+    compact fp32 partials: the same wave count, 1/7 of the partial traffic there."""
+    tiles = (M // WGRAD_TILE) * (N // WGRAD_TILE)
+    S = wgrad_splits(M, N, K, n_cu)
+    if S == 1 or not WGRAD_TAIL:
+        return ("split", S)
+    base = 2.0 * M * N * K / 1.3e15                         # s, every CU busy
+    wave_t = base * n_cu / tiles                            # one wave of whole-K tiles
+    util = tiles * S / (n_cu * -(-(tiles * S) // n_cu))
+    best, best_t = ("split", S), base / util + (S * M * N * 8 + M * N * 4) / 4.5e12 + 6e-6
+    full = tiles // n_cu * n_cu
+    tail = tiles - full
+    if full == 0 or tail == 0:
+        return best
+    for St in range(2, 9):
+        if St > K // WGRAD_KGRAN or K // St < 1024:
+            break
+        t = (full // n_cu) * wave_t + -(-(tail * St) // n_cu) * wave_t / St
+        t += (St * tail * WGRAD_TILE * WGRAD_TILE * 8 + tail * WGRAD_TILE * WGRAD_TILE * 4) / 4.5e12 + 12e-6
+        if t < best_t * 0.99:
+            best, best_t = ("tail", full, St), t
+    return best
+
+
 def wgrad_gemm_(a, b, c, accumulate: bool = False, splits: Optional[int] = None):
     """c (+)= a^T b with a [K, M], b [K, N] token-major (dW = dY^T X), fp32 accumulation."""
     if _hip(a):
-        S = wgrad_splits(a.shape[1], b.shape[1], a.shape[0]) if splits is None else int(splits)
-        _k().wgrad_gemm_(a, b, c, bool(accumulate), S)
+        plan = wgrad_plan(a.shape[1], b.shape[1], a.shape[0]) if splits is None else ("split", int(splits))
+        if plan[0] == "tail" and c.stride(1) == 1 and c.stride(0) % 8 == 0 and c.data_ptr() % 16 == 0:
+            _k().wgrad_gemm_tail_(a, b, c, bool(accumulate), plan[1], plan[2])
+        else:
+            S = plan[1] if plan[0] == "split" else wgrad_splits(a.shape[1], b.shape[1], a.shape[0])
+            _k().wgrad_gemm_(a, b, c, bool(accumulate), S)
         return c
     r = a.float().t() @ b.float()
     if accumulate:

@@ -183,6 +183,10 @@ void lora_pack_t(DType dt, const LoraPackArgs& a, int K, int max_r, hipStream_t 
 // gemm_wgrad.hip — C[M, N] (+)= A^T B with A [K, M], B [K, N] row-major (dW = dY^T X).
 // S > 1: split s writes fp32 partial C + s * c_split (accumulate must be false).
 bool wgrad_gemm_supported(int M, int N, int K, int S);
+bool wgrad_tail_supported(int M, int N, int K, int full, int St);
+// tiles [0, full) whole-K into c, the rest split St ways into compact fp32 partials (part) + a sum
+void wgrad_gemm_tail(DType dt, DType odt, const void* a, long lda, const void* b, long ldb, void* c, long ldc, int M,
+                     int N, int K, int full, int St, float* part, bool accumulate, hipStream_t s);
 void wgrad_gemm(DType dt, DType odt, const void* a, long lda, const void* b, long ldb, void* c, long ldc,
                 long c_split, int M, int N, int K, int S, bool accumulate, hipStream_t s);
 // same kernel with a K-contiguous A: C[M, N] (+)= A[M, K] B[K, N] (dX = dY W)

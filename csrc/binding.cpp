@@ -447,6 +447,31 @@ void wgrad_gemm_(const Tensor& a, const Tensor& b, Tensor& c, bool accumulate, i
                           stream());
 }
 
+// c (+)= a^T b with the grouped tile order in two launches: tiles [0, full) whole-K straight into c,
+// the remaining tiles split St ways over K into compact fp32 partials summed into c afterwards
+void wgrad_gemm_tail_(const Tensor& a, const Tensor& b, Tensor& c, bool accumulate, int64_t full, int64_t St) {
+  TORCH_CHECK(a.is_cuda() && b.is_cuda() && c.is_cuda(), "wgrad_gemm_tail: GPU tensors");
+  c10::DeviceGuard g(a.device());
+  TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && c.dim() == 2, "wgrad_gemm_tail: 2-D operands");
+  const int64_t K = a.size(0), M = a.size(1), N = b.size(1);
+  TORCH_CHECK(b.size(0) == K && c.size(0) == M && c.size(1) == N, "wgrad_gemm_tail: shapes");
+  TORCH_CHECK(a.scalar_type() == b.scalar_type() &&
+                  (a.scalar_type() == at::kBFloat16 || a.scalar_type() == at::kHalf), "wgrad_gemm_tail: bf16/fp16 operands");
+  TORCH_CHECK(a.stride(1) == 1 && b.stride(1) == 1 && c.stride(1) == 1, "wgrad_gemm_tail: unit column strides");
+  TORCH_CHECK(a.stride(0) % 8 == 0 && b.stride(0) % 8 == 0 && c.stride(0) % 8 == 0, "wgrad_gemm_tail: 16-B aligned rows");
+  TORCH_CHECK((reinterpret_cast<uintptr_t>(a.data_ptr()) | reinterpret_cast<uintptr_t>(b.data_ptr()) |
+               reinterpret_cast<uintptr_t>(c.data_ptr())) % 16 == 0, "wgrad_gemm_tail: 16-B aligned operands");
+  TORCH_CHECK(a.stride(0) < (int64_t(1) << 26) && b.stride(0) < (int64_t(1) << 26), "wgrad_gemm_tail: row stride too large");
+  TORCH_CHECK(K < (int64_t(1) << 31) && M < (int64_t(1) << 31) && N < (int64_t(1) << 31));
+  TORCH_CHECK(bllm::wgrad_tail_supported((int)M, (int)N, (int)K, (int)full, (int)St), "wgrad_gemm_tail: unsupported ",
+              K, "x", M, "x", N, " full ", full, " splits ", St);
+  const int64_t tail = (M / 256) * (N / 256) - full;
+  auto part = at::empty({St * tail * 256 * 256}, a.options().dtype(at::kFloat));
+  bllm::wgrad_gemm_tail(dt_of(a), dt_of(c), a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0), c.data_ptr(),
+                        c.stride(0), (int)M, (int)N, (int)K, (int)full, (int)St, part.data_ptr<float>(), accumulate,
+                        stream());
+}
+
 // c [M, N] (+)= a [M, K] . b [K, N], all row-major (input gradient dX = dY W of a Linear)
 void gemm_nn_(const Tensor& a, const Tensor& b, Tensor& c, bool accumulate) {
   TORCH_CHECK(a.is_cuda() && b.is_cuda() && c.is_cuda(), "gemm_nn: GPU tensors");
@@ -1097,6 +1122,7 @@ TORCH_LIBRARY(bllm, m) {
   m.def("bias_grad_(Tensor dy, Tensor(a!) db, bool accumulate) -> ()");
   m.def("sum_partials_(Tensor part, Tensor(a!) out, bool accumulate) -> ()");
   m.def("wgrad_gemm_(Tensor a, Tensor b, Tensor(a!) c, bool accumulate, int splits) -> ()");
+  m.def("wgrad_gemm_tail_(Tensor a, Tensor b, Tensor(a!) c, bool accumulate, int full, int St) -> ()");
   m.def("gemm_nn_(Tensor a, Tensor b, Tensor(a!) c, bool accumulate) -> ()");
   m.def("gemm_nt_(Tensor a, Tensor b, Tensor(a!) c, bool accumulate) -> ()");
   m.def("gemm_nt_swiglu_(Tensor a, Tensor w, Tensor(a!) gu, Tensor(b!) act) -> ()");
@@ -1148,6 +1174,7 @@ TORCH_LIBRARY_IMPL(bllm, CUDA, m) {
   m.impl("rope_dev_", &rope_dev_);
   m.impl("sum_partials_", &sum_partials_);
   m.impl("wgrad_gemm_", &wgrad_gemm_);
+  m.impl("wgrad_gemm_tail_", &wgrad_gemm_tail_);
   m.impl("gemm_nn_", &gemm_nn_);
   m.impl("gemm_nt_", &gemm_nt_);
   m.impl("gemm_nt_swiglu_", &gemm_nt_swiglu_);

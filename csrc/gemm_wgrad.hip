@@ -371,19 +371,9 @@ __global__ __launch_bounds__(Geo::THREADS) void wgrad_gemm_k(const T* __restrict
 // tile maps (``map``, experiment knob BLLM_WG_MAP): 0 = XCD-contiguous over GROUP_M-deep column-major
 // groups (each XCD an M-band), 1 = plain bid order, 2 = the same over the transposed grid (each XCD
 // an N-band); ``group_m`` = group depth (BLLM_WG_GM)
-template <typename T, typename OT>
-__global__ __launch_bounds__(g4::THREADS4, 1) void wgrad4_k(const T* __restrict__ A, long lda,
-                                                            const T* __restrict__ B, long ldb, OT* __restrict__ C,
-                                                            long ldc, long c_split, int M, int N, int K,
-                                                            int accumulate, int wide, int map = 0,
-                                                            int group_m = GROUP_M) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-  const int wm = wave >> 1, wn = wave & 1;
-
-  const int nbm = M / BM, nbn = N / BN, nblk = nbm * nbn;
-  const int bid = blockIdx.x, xcd = bid & 7, q8 = nblk >> 3, r8 = nblk & 7;
-  const int wid = map == 1 ? bid : (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+// grouped tile order -> (tm, tn): GROUP_M-deep column-major groups (map 2: over the transposed
+// grid); shared by wgrad4_k and the split-tail reduction
+__device__ __forceinline__ void wg_tile(int wid, int nbm, int nbn, int map, int group_m, int& tm, int& tn) {
   const bool trg = map == 2;
   const int gmaj = trg ? nbn : nbm, gmin = trg ? nbm : nbn;
   const int per_group = group_m * gmin;
@@ -392,7 +382,31 @@ __global__ __launch_bounds__(g4::THREADS4, 1) void wgrad4_k(const T* __restrict_
   const int gm = gmaj - first_m < group_m ? gmaj - first_m : group_m;
   const int in_g = wid - grp * per_group;
   const int ta = first_m + in_g % gm, tb = in_g / gm;
-  const int tm = trg ? tb : ta, tn = trg ? ta : tb;
+  tm = trg ? tb : ta;
+  tn = trg ? ta : tb;
+}
+
+// tile0 / ntile: this launch covers tiles [tile0, tile0 + ntile) of the grouped order (the
+// XCD-contiguous deal is over those ntile).  compact (split tails): split sp of the launch's local
+// tile t writes its fp32 256 x 256 partial at C + ((sp * ntile + t) * 256 * 256), row stride 256.
+template <typename T, typename OT>
+__global__ __launch_bounds__(g4::THREADS4, 1) void wgrad4_k(const T* __restrict__ A, long lda,
+                                                            const T* __restrict__ B, long ldb, OT* __restrict__ C,
+                                                            long ldc, long c_split, int M, int N, int K,
+                                                            int accumulate, int wide, int map = 0,
+                                                            int group_m = GROUP_M, int tile0 = 0, int ntile = -1,
+                                                            int compact = 0) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int wm = wave >> 1, wn = wave & 1;
+
+  const int nbm = M / BM, nbn = N / BN;
+  const int cnt = ntile < 0 ? nbm * nbn : ntile;
+  const int bid = blockIdx.x, xcd = bid & 7, q8 = cnt >> 3, r8 = cnt & 7;
+  const int local = map == 1 ? bid : (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int wid = tile0 + local;
+  int tm, tn;
+  wg_tile(wid, nbm, nbn, map, group_m, tm, tn);
   const long m0 = (long)tm * BM, n0 = (long)tn * BN;
 
   const int S = gridDim.y, sp = blockIdx.y, nch = K / KCH;
@@ -495,25 +509,61 @@ __global__ __launch_bounds__(g4::THREADS4, 1) void wgrad4_k(const T* __restrict_
   for (int i = 0; i < 8; ++i)
 #pragma unroll
     for (int j = 0; j < 8; ++j) asm volatile("" : "+a"(acc[i][j]));
-  g4::epilogue4<T, OT, g4::EPI_NONE>(acc, smem, wm, wn, lane, C + sp * c_split, ldc, m0, n0, 0, 0, accumulate, wide,
-                                     (OT*)nullptr, 0);
+  if (compact)
+    g4::epilogue4<T, OT, g4::EPI_NONE>(acc, smem, wm, wn, lane, C + ((long)sp * cnt + local) * BM * BN, BN, 0, 0, 0,
+                                       0, 0, 1, (OT*)nullptr, 0);
+  else
+    g4::epilogue4<T, OT, g4::EPI_NONE>(acc, smem, wm, wn, lane, C + sp * c_split, ldc, m0, n0, 0, 0, accumulate, wide,
+                                       (OT*)nullptr, 0);
+}
+
+// c[tile] (+)= sum_s part[s][t] over the split-tail tiles t < ntile (fixed order: deterministic);
+// 8 consecutive outputs per thread
+template <typename OT>
+__global__ __launch_bounds__(256) void wg_tail_sum_k(const float* __restrict__ part, OT* __restrict__ C, long ldc,
+                                                     int M, int N, int tile0, int ntile, int S, int map, int group_m,
+                                                     int accumulate) {
+  const long per_tile = (long)BM * BN / 8;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < per_tile * ntile; i += (long)gridDim.x * 256) {
+    const int t = (int)(i / per_tile);
+    const int e = (int)(i - (long)t * per_tile) * 8;
+    const int r = e / BN, c = e - r * BN;
+    int tm, tn;
+    wg_tile(tile0 + t, M / BM, N / BN, map, group_m, tm, tn);
+    float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int sp = 0; sp < S; ++sp) {
+      const float* p = part + ((long)sp * ntile + t) * BM * BN + e;
+      const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+      v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w; v[4] += b.x; v[5] += b.y; v[6] += b.z; v[7] += b.w;
+    }
+    OT* o = C + ((long)tm * BM + r) * ldc + (long)tn * BN + c;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = from_f<OT>(accumulate ? to_f(o[j]) + v[j] : v[j]);
+  }
+}
+
+// experiment knobs, read per launch (A/B in one process): tile map and group depth
+static void wg_knobs(int& map, int& gm) {
+  const char* em = getenv("BLLM_WG_MAP");
+  const char* eg = getenv("BLLM_WG_GM");
+  map = em ? atoi(em) : 0;
+  gm = eg && atoi(eg) > 0 ? atoi(eg) : GROUP_M;
 }
 
 template <typename T, typename OT>
 void launch4(const void* a, long lda, const void* b, long ldb, void* c, long ldc, long c_split, int M, int N, int K,
-             int S, bool accumulate, hipStream_t s) {
+             int S, bool accumulate, hipStream_t s, int tile0 = 0, int ntile = -1, int compact = 0) {
   static const bool attr = hipFuncSetAttribute((const void*)wgrad4_k<T, OT>,
                                                hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES) == hipSuccess;
   (void)attr;
-  const dim3 grid((M / BM) * (N / BN), S);
+  const int cnt = ntile < 0 ? (M / BM) * (N / BN) : ntile;
+  const dim3 grid(cnt, S);
   const bool wide = reinterpret_cast<uintptr_t>(c) % 16 == 0 && (ldc * (long)sizeof(OT)) % 16 == 0 &&
                     (c_split * (long)sizeof(OT)) % 16 == 0;
-  // experiment knobs, read per launch (A/B in one process): tile map and group depth
-  const char* em = getenv("BLLM_WG_MAP");
-  const char* eg = getenv("BLLM_WG_GM");
-  const int map = em ? atoi(em) : 0, gm = eg && atoi(eg) > 0 ? atoi(eg) : GROUP_M;
+  int map, gm;
+  wg_knobs(map, gm);
   hipLaunchKernelGGL((wgrad4_k<T, OT>), grid, dim3(g4::THREADS4), LDS_BYTES, s, (const T*)a, lda, (const T*)b, ldb,
-                     (OT*)c, ldc, c_split, M, N, K, (int)accumulate, (int)wide, map, gm);
+                     (OT*)c, ldc, c_split, M, N, K, (int)accumulate, (int)wide, map, gm, tile0, ntile, compact);
 }
 
 template <typename T, typename OT, bool AK = false>
@@ -553,6 +603,34 @@ void gemm_nn(DType dt, DType odt, const void* a, long lda, const void* b, long l
 
 bool wgrad_gemm_supported(int M, int N, int K, int S) {
   return M > 0 && N > 0 && M % BM == 0 && N % BN == 0 && K >= KCH && K % KCH == 0 && S >= 1 && S <= K / KCH;
+}
+
+bool wgrad_tail_supported(int M, int N, int K, int full, int St) {
+  const int tiles = M > 0 && N > 0 && M % BM == 0 && N % BN == 0 ? (M / BM) * (N / BN) : 0;
+  return tiles > 0 && full >= 0 && full < tiles && K >= KCH && K % KCH == 0 && St >= 2 && St <= K / KCH;
+}
+
+// dW with the grouped tile order split in two launches: tiles [0, full) whole-K straight into c
+// (full = whole waves of workgroups), the tail [full, tiles) split St ways over K into compact
+// fp32 partials (part: St * (tiles - full) * 256 * 256 floats), summed into c by wg_tail_sum_k.
+// Same wave count as splitting every tile, ~1/St of its partial traffic when the tail is short.
+void wgrad_gemm_tail(DType dt, DType odt, const void* a, long lda, const void* b, long ldb, void* c, long ldc, int M,
+                     int N, int K, int full, int St, float* part, bool accumulate, hipStream_t s) {
+  const int tail = (M / BM) * (N / BN) - full;
+  int map, gm;
+  wg_knobs(map, gm);
+  BLLM_DISPATCH(odt, OT, {
+    if (full > 0) {
+      if (dt == DType::BF16) launch4<bf16_t, OT>(a, lda, b, ldb, c, ldc, 0, M, N, K, 1, accumulate, s, 0, full, 0);
+      else launch4<f16_t, OT>(a, lda, b, ldb, c, ldc, 0, M, N, K, 1, accumulate, s, 0, full, 0);
+    }
+    if (dt == DType::BF16) launch4<bf16_t, float>(a, lda, b, ldb, part, BN, 0, M, N, K, St, false, s, full, tail, 1);
+    else launch4<f16_t, float>(a, lda, b, ldb, part, BN, 0, M, N, K, St, false, s, full, tail, 1);
+    const long work = (long)tail * BM * BN / 8;
+    const int g = (int)((work + 255) / 256 < 2048 ? (work + 255) / 256 : 2048);
+    hipLaunchKernelGGL((wg_tail_sum_k<OT>), dim3(g), dim3(256), 0, s, (const float*)part, (OT*)c, ldc, M, N, full, tail,
+                       St, map, gm, (int)accumulate);
+  });
 }
 
 void wgrad_gemm(DType dt, DType odt, const void* a, long lda, const void* b, long ldb, void* c, long ldc,

@@ -684,6 +684,35 @@ def test_wgrad_gemm(dt, odt, K, M, N, S, accumulate):
     check_close(c, expect, odt, k=3.0, name="wgrad")
 
 
+@pytest.mark.parametrize("odt", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("M,N,K,full,St", [(768, 512, 1024, 4, 2), (768, 512, 1536, 2, 3), (512, 1280, 2048, 8, 2),
+                                           (1536, 256, 1024, 3, 4)])
+@pytest.mark.parametrize("accumulate", [False, True])
+@pytest.mark.parametrize("wmap", ["0", "2"])
+def test_wgrad_gemm_split_tail(odt, M, N, K, full, St, accumulate, wmap, monkeypatch):
+    """dW with the grouped tile order in two launches -- tiles [0, full) whole-K into c, the rest
+    split St ways into compact fp32 partials and summed -- vs an fp32 matmul (both tile maps: the
+    sum kernel must place every tail tile where the GEMM's map put it)."""
+    monkeypatch.setenv("BLLM_WG_MAP", wmap)
+    a_full = torch.randn(K, M + 64, device=DEV).to(torch.bfloat16)
+    a = a_full[:, 32:32 + M]
+    b = torch.randn(K, N, device=DEV).to(torch.bfloat16)
+    c = torch.randn(M, N, device=DEV).to(odt)
+    expect = a.float().t() @ b.float() + (c.float() if accumulate else 0)
+    torch.ops.bllm.wgrad_gemm_tail_(a, b, c, accumulate, full, St)
+    check_close(c, expect, odt, k=3.0, name="wgrad split tail")
+
+
+def test_wgrad_plan_routes_headline_tails():
+    """The planner keeps whole-K waves and splits only the ragged tail of the Llama-3-8B QKV / down
+    weight gradients; the library shapes that fill whole waves stay unsplit."""
+    assert ops.wgrad_plan(4096, 14336, 40960) == ("tail", 768, 2)
+    assert ops.wgrad_plan(6144, 4096, 40960) == ("tail", 256, 2)
+    assert ops.wgrad_plan(28672, 4096, 40960) == ("split", 1)
+    assert ops.wgrad_plan(4096, 4096, 40960) == ("split", 1)
+    assert ops.wgrad_plan(1280, 1280, 65536)[0] == "split"     # GPT-2: no whole wave to keep
+
+
 def test_wgrad_gemm_in_weight_grad_path():
     """_weight_grad routes eligible dW through the MFMA kernel; result == hipBLASLt path."""
     from building_llm_from_scratch_amd.models.linear import _weight_grad
