@@ -469,7 +469,9 @@ class HeadComputeMixin:
         (an augmented [N, d + r] output made hipBLASLt fall back from 1.64 to 0.66-0.75 PF at
         V = 128k, tools/bench_head_k.py); u = dl B^T is a skinny hipBLASLt GEMM over each dlogits
         chunk (355 us vs 610 us for lora_down, tools/bench_head_u.py), dB = (s t)^T dl runs on
-        lora_wgrad, then dh = dh_W + s u A^T and dA = s h^T u on the LoRA kernels."""
+        lora_wgrad, then dh = dh_W + s u A^T and dA = s h^T u on the LoRA kernels.  With
+        BLLM_LORA_HEAD_FUSED (default) u and dB come from one kernel reading each dl chunk once
+        (``ops.lora_head_bwd_``)."""
         hd, u_ = self.head, self.head.unit
         spec = hd.specs[0]
         A, Bm, sc = u_.data(spec.lora_A), u_.data(spec.lora_B), float(spec.scaling)   # [d, r], [r, V]
@@ -497,6 +499,7 @@ class HeadComputeMixin:
         gB = torch.empty(r, V, dtype=torch.float32, device=h.device) if u_.trainable(spec.lora_B) else None
         scale = (self.rctx.loss_scale / nvalid).reshape(1)
         total = torch.zeros(1, dtype=torch.float32, device=h.device)
+        fused_bwd = ops.lora_head_bwd_ok(V, r) and Bm.is_contiguous()
         for s0 in range(0, N, rows):
             hc, tc = ha[s0:s0 + rows], targets[s0:s0 + rows]
             logits = mm_nt(hc, Wa)
@@ -507,6 +510,10 @@ class HeadComputeMixin:
                 mm_nt(dl, Wd.t(), out=dh[s0:s0 + rows])                   # dh_W = dl . W
             else:
                 torch.mm(dl, Wd, out=dh[s0:s0 + rows])
+            if gB is not None and fused_bwd:                              # u and dB in one pass over dl
+                ops.lora_head_bwd_(dl, st[s0:s0 + rows], Bm, ub[s0:s0 + rows], gB, accumulate=s0 > 0)
+                del logits, dl
+                continue
             torch.mm(dl, Bm.t(), out=ub[s0:s0 + rows])            # u = dl B^T (hipBLASLt: 5.9 TB/s here)
             if gB is not None:                                            # dB = (s t)^T dl
                 ops.lora_wgrad(st[s0:s0 + rows], dl, [gB], [0], [0], 1.0, accumulate=s0 > 0)

@@ -709,6 +709,23 @@ def lora_wgrad(p, q, gs, pa, qb, scale: float, accumulate: bool = False):
     ref.lora_wgrad(p, q, gs, pa, qb, scale, accumulate)
 
 
+LORA_HEAD_FUSED = os.environ.get("BLLM_LORA_HEAD_FUSED", "1") != "0"
+
+
+def lora_head_bwd_ok(V: int, r: int) -> bool:
+    return LORA_HEAD_FUSED and r == 16 and V % 64 == 0
+
+
+def lora_head_bwd_(dl, st, B, u, gB, accumulate: bool = False):
+    """The LoRA head's two rank-16 products of a logits-gradient chunk dl [R, V] in one pass over
+    it: u = dl B^T (into u [R, 16]) and gB (+)= st^T dl (st [R, 16], B and gB [16, V])."""
+    if _hip(dl):
+        _k().lora_head_bwd_(dl, st, B, u, gB, bool(accumulate))
+        return
+    u.copy_((dl.float() @ B.float().t()).to(u.dtype))
+    _vec_into(gB, st.float().t() @ dl.float(), accumulate)
+
+
 def lora_pack_t(As):
     """[sum r_i, K] = concat_i A_i^T (A_i [K, r_i])"""
     if _hip(As[0]):

@@ -178,6 +178,12 @@ int lora_wgrad_splits(int blocks, int N);
 void lora_wgrad(DType dt, DType odt, const LoraWgradArgs& a, int N, int S, hipStream_t s);
 // g_m (+)= sum_s part[s][part_off_m + a * len_m + b] (a.part, a.part_ld, a.part_off set; scale not applied)
 void lora_reduce(DType odt, const LoraWgradArgs& a, int S, hipStream_t s);
+// the LoRA head's u = dl B^T (written to u [R, 16] via partials per 1,024-column slab, upart
+// [slabs][R][16]) and dB = st^T dl (partials per row range: gpart [S][16][V], summed by the caller
+// with lora_reduce) in one pass over dl (V % 64 == 0, r = 16)
+int lora_head_bwd_splits(int R, int V, long ldl);
+void lora_head_bwd(DType dt, const void* dl, long ldl, const void* st, long ldst, const void* B, long ldb,
+                   float* gpart, float* upart, void* u, int R, int V, int S, hipStream_t s);
 void lora_pack_t(DType dt, const LoraPackArgs& a, int K, int max_r, hipStream_t s);
 
 // gemm_wgrad.hip — C[M, N] (+)= A^T B with A [K, M], B [K, N] row-major (dW = dY^T X).

@@ -311,6 +311,44 @@ Tensor swiglu_bwd_lowrank_wgrad(const Tensor& gu, const Tensor& base, const Tens
   return dgu;
 }
 
+// LoRA head backward of one logits-gradient chunk dl [R, V]: u = dl B^T (written to u [R, 16]) and
+// gB (+)= st^T dl (gB [16, V], or a transposed view of a [V, 16] block) in one pass over dl
+void lora_head_bwd_(const Tensor& dl, const Tensor& st, const Tensor& B, Tensor& u, Tensor& gB, bool accumulate) {
+  check_gpu(dl, "dl"); check_gpu(B, "B");
+  c10::DeviceGuard g(dl.device());
+  const int64_t R = dl.size(0), V = dl.size(1);
+  TORCH_CHECK(dl.scalar_type() == at::kBFloat16 || dl.scalar_type() == at::kHalf, "lora_head_bwd: bf16 / fp16");
+  TORCH_CHECK(V % 64 == 0 && B.dim() == 2 && B.size(0) == 16 && B.size(1) == V, "lora_head_bwd: B is [16, V], V % 64");
+  auto rows16 = [&](const Tensor& t, int64_t rows, int64_t cols, const char* name) {
+    TORCH_CHECK(t.is_cuda() && t.dim() == 2 && t.size(0) == rows && t.size(1) == cols && t.stride(1) == 1 &&
+                    (t.stride(0) * t.element_size()) % 16 == 0 && (uintptr_t)t.data_ptr() % 16 == 0 &&
+                    t.scalar_type() == dl.scalar_type(),
+                "lora_head_bwd: ", name, " must be a 16-B aligned row-strided [", rows, ", ", cols, "] view");
+  };
+  rows16(dl, R, V, "dl");
+  rows16(B, 16, V, "B");
+  rows16(st, R, 16, "st");
+  TORCH_CHECK(u.is_cuda() && u.is_contiguous() && u.size(0) == R && u.size(1) == 16 &&
+                  u.scalar_type() == dl.scalar_type(), "lora_head_bwd: u is a contiguous [R, 16] of dl's dtype");
+  TORCH_CHECK(gB.is_cuda() && gB.dim() == 2 && gB.size(0) == 16 && gB.size(1) == V &&
+                  (gB.is_contiguous() || gB.t().is_contiguous()),
+              "lora_head_bwd: gB is a [16, V] (transposed) contiguous block");
+  const int S = bllm::lora_head_bwd_splits((int)R, (int)V, dl.stride(0));
+  const int64_t slabs = (V + 1023) / 1024;
+  auto gpart = at::empty({S, 16 * V}, dl.options().dtype(at::kFloat));
+  auto upart = at::empty({slabs, R * 16}, dl.options().dtype(at::kFloat));
+  bllm::lora_head_bwd(dt_of(dl), dl.data_ptr(), dl.stride(0), st.data_ptr(), st.stride(0), B.data_ptr(), B.stride(0),
+                      gpart.data_ptr<float>(), upart.data_ptr<float>(), u.data_ptr(), (int)R, (int)V, S, stream());
+  bllm::LoraWgradArgs a{};
+  a.accumulate = accumulate;
+  a.n = 1;
+  a.r[0] = 16; a.len[0] = (int)V; a.sa[0] = gB.stride(0); a.sb[0] = gB.stride(1);
+  a.gt[0][0] = gB.data_ptr();
+  a.part_off[0] = 0;
+  a.part = gpart.data_ptr<float>(); a.part_ld = 16 * V;
+  bllm::lora_reduce(dt_of(gB), a, S, stream());
+}
+
 // dgu as swiglu_bwd, and dact is overwritten in place by act = silu(g) * u
 Tensor swiglu_bwd_act(const Tensor& gu, Tensor& dact) {
   check_gpu(gu, "gu"); check_gpu(dact, "dact");
@@ -1114,6 +1152,7 @@ TORCH_LIBRARY(bllm, m) {
   m.def("swiglu_fwd_into_(Tensor gu, Tensor(a!) act) -> ()");
   m.def("swiglu_bwd_lowrank(Tensor gu, Tensor base, Tensor u, Tensor P, float scale) -> Tensor");
   m.def("swiglu_bwd_lowrank_wgrad(Tensor gu, Tensor base, Tensor u, Tensor P, float scale, Tensor st, Tensor(a!) gB_gate, Tensor(b!) gB_up, Tensor(c!) gA_down_t, bool accumulate) -> Tensor");
+  m.def("lora_head_bwd_(Tensor dl, Tensor st, Tensor B, Tensor(a!) u, Tensor(b!) gB, bool accumulate) -> ()");
   m.def("swiglu_bwd(Tensor gu, Tensor dact) -> Tensor");
   m.def("swiglu_bwd_act(Tensor gu, Tensor(a!) dact) -> Tensor");
   m.def("gelu_fwd(Tensor f) -> Tensor");
@@ -1163,6 +1202,7 @@ TORCH_LIBRARY_IMPL(bllm, CUDA, m) {
   m.impl("swiglu_fwd_into_", &swiglu_fwd_into_);
   m.impl("swiglu_bwd_lowrank", &swiglu_bwd_lowrank);
   m.impl("swiglu_bwd_lowrank_wgrad", &swiglu_bwd_lowrank_wgrad);
+  m.impl("lora_head_bwd_", &lora_head_bwd_);
   m.impl("swiglu_bwd", &swiglu_bwd);
   m.impl("swiglu_bwd_act", &swiglu_bwd_act);
   m.impl("gelu_fwd", &gelu_fwd);

@@ -20,6 +20,9 @@
 //
 // All three are HBM-bound (the rank is 8-64): x / dy / y are streamed exactly once per kernel
 // with 16-byte lane accesses; the small operands (A, B, t, u) stay L2-resident.
+#include <cstdlib>
+#include <type_traits>
+
 #include "api.h"
 
 namespace bllm {
@@ -406,6 +409,171 @@ __global__ __launch_bounds__(256) void lora_block_k(LoraBlockArgs a) {
 
 }  // namespace
 
+// --------------------------------------------------------------------------- lora_head_bwd
+// The LoRA head's two rank-16 products of one logits-gradient chunk dl [R, V] in ONE pass over dl
+// (both used to stream it: u = dl B^T on hipBLASLt, dB = (s t)^T dl on lora_wgrad):
+//   gpart[ry][j][c] = sum_{n in rows of ry} st[n][j] dl[n][c]      (dB partial per row range)
+//   upart[cx][n][j] = sum_{c in slab cx} dl[n][c] B[j][c]          (u partial per column slab)
+// A workgroup owns a slab of up to 1,024 columns (16 sub-slabs of 64) and a row range, walked in
+// 64-row chunks; per (chunk, sub-slab) the dl tile [64 x 64] and B's [16 x 64] slice are staged in
+// LDS (double-buffered, one barrier), then wave w adds its 16 columns of dB (A = st^T, B = dl,
+// both transposed reads, K = rows) and its 16 rows of u (A = dl rows, B = B rows, K = columns).
+// lora_reduce / sum_partials_into finish both sums in a fixed order (deterministic).
+constexpr int LHB_SUB = 64, LHB_NSUB = 16, LHB_ROWS = 64;
+constexpr int LHB_DS = LHB_SUB * 2 + 16;  // bytes per row of a dl / B tile (padded)
+constexpr int LHB_SS = 32;                // bytes per row of the st tile
+
+__device__ __forceinline__ s16x8 lhb_tr(const char* tile, int stride, int col_byte, int lane) {
+  const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+  const char* a = tile + (8 * g + q) * stride + col_byte + 8 * p;
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a));
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a + 4 * stride));
+  return s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+
+template <typename T, int D>
+__global__ __launch_bounds__(256) void lora_head_bwd_k(const T* __restrict__ dl, long ldl, const T* __restrict__ st,
+                                                       long ldst, const T* __restrict__ Bm, long ldb,
+                                                       float* __restrict__ gpart, float* __restrict__ upart, int R,
+                                                       int V, int rows_per) {
+  __shared__ __attribute__((aligned(16))) char Dt[2][LHB_ROWS * LHB_DS];
+  __shared__ __attribute__((aligned(16))) char Bt[2][16 * LHB_DS];
+  __shared__ __attribute__((aligned(16))) char St[LHB_ROWS * LHB_SS];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int c0 = blockIdx.x * LHB_SUB * LHB_NSUB;
+  const int nsub = (V - c0) / LHB_SUB < LHB_NSUB ? (V - c0) / LHB_SUB : LHB_NSUB;
+  // every slab runs all 16 sub-slabs (the last slab's missing ones on zero tiles: its dB columns are
+  // not stored, its u terms are 0): no data-dependent control flow around the MFMA accumulators, and
+  // the register set of iteration (chunk, sub) is sub % D at compile time
+  constexpr int nsubP = LHB_NSUB;
+  const int r0 = blockIdx.y * rows_per, r1 = r0 + rows_per < R ? r0 + rows_per : R;
+  const s16x8 zero = {0, 0, 0, 0, 0, 0, 0, 0};
+  // staging roles: dl tile rows dr, dr + 32 at 16-B chunk dc; B row bj (threads < 128); st row sr half sh
+  const int dr = tid >> 3, dc = (tid & 7) * 8, bj = tid >> 3, sr = tid >> 1, sh = tid & 1;
+  f32x4 accB[LHB_NSUB];
+#pragma unroll
+  for (int k = 0; k < LHB_NSUB; ++k) accB[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+  s16x8 pd0[D], pd1[D], pb[D], ps = zero;
+  // Loads are raw buffer loads on descriptors bounded to this workgroup's rows: a row past r1 (and
+  // a padded sub-slab, sent to an offset past every bound) reads as 0 with no branch, so the
+  // compiler can keep the D pieces in flight (exec-masked loads made it drain vmcnt to 0).
+  constexpr int OOB = 0x7ffffff0;
+  const int nrow = r1 > r0 ? r1 - r0 : 0;
+  const __amdgpu_buffer_rsrc_t rd =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(dl + (long)r0 * ldl), (short)0, (int)((long)nrow * ldl * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb =
+      __builtin_amdgcn_make_buffer_rsrc((void*)Bm, (short)0, (int)(16L * ldb * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(st + (long)r0 * ldst), (short)0, (int)((long)nrow * ldst * 2), 0x00020000);
+  const int half_off = (int)(32L * ldl * 2);  // rows dr + 32
+  // load cursor: (lrow, lsub) of the next piece to fetch, D iterations ahead of the MFMAs, as
+  // running byte offsets (not per-sub addresses, which the unrolled loop would keep live)
+  int lsub = 0;
+  int od = (int)(((long)dr * ldl + c0 + dc) * 2), ob = (int)(((long)bj * ldb + c0 + dc) * 2);
+  const int dstep = (int)(((long)LHB_ROWS * ldl - (long)nsubP * LHB_SUB) * 2);
+  auto bld = [](const __amdgpu_buffer_rsrc_t& r, int off, int soff) {
+    return __builtin_bit_cast(s16x8, __builtin_amdgcn_raw_buffer_load_b128(r, off, soff, 0));
+  };
+  auto load = [&](int k) {  // this thread's pieces of the cursor's (chunk, sub-slab) into register set k
+    const bool in = lsub < nsub;
+    pd0[k] = bld(rd, in ? od : OOB, 0);
+    pd1[k] = bld(rd, in ? od + half_off : OOB, 0);
+    if (tid < 128) pb[k] = bld(rb, in ? ob : OOB, 0);
+    od += LHB_SUB * 2; ob += LHB_SUB * 2;
+    if (++lsub == nsubP) { lsub = 0; od += dstep; ob -= nsubP * LHB_SUB * 2; }
+  };
+  auto load_st = [&](int row) {
+    if (tid < 128) ps = bld(rs, (int)(((long)(row - r0 + sr) * ldst + 8 * sh) * 2), 0);
+  };
+#pragma unroll
+  for (int k = 0; k < D; ++k) load(k);
+  load_st(r0);
+  int par = 0;
+  for (int row = r0; row < r1; row += LHB_ROWS) {
+    // st rows of this chunk (the previous chunk's readers are past its closing barrier)
+    if (tid < 128) *reinterpret_cast<s16x8*>(St + sr * LHB_SS + 16 * sh) = ps;
+    load_st(row + LHB_ROWS);
+    f32x4 accU = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int sub = 0; sub < LHB_NSUB; ++sub) {
+      {
+        const int k = sub % D;
+        {
+          *reinterpret_cast<s16x8*>(Dt[par] + dr * LHB_DS + dc * 2) = pd0[k];
+          *reinterpret_cast<s16x8*>(Dt[par] + (32 + dr) * LHB_DS + dc * 2) = pd1[k];
+          if (tid < 128) *reinterpret_cast<s16x8*>(Bt[par] + bj * LHB_DS + dc * 2) = pb[k];
+          __syncthreads();
+        }
+        load(k);
+        {
+#pragma unroll
+          for (int ks = 0; ks < 2; ++ks) {
+            // dB: [16 j x 16 cols of wave w] += st^T [16 x 32 rows] . dl [32 rows x 16 cols]
+            const s16x8 a = lhb_tr(St + ks * 32 * LHB_SS, LHB_SS, 0, lane);
+            const s16x8 b = lhb_tr(Dt[par] + ks * 32 * LHB_DS, LHB_DS, 32 * w, lane);
+            accB[sub] = MF16<T>::mma(a, b, accB[sub]);
+            // u: [16 rows of wave w x 16 j] += dl [16 rows x 32 cols] . B^T [32 cols x 16 j]
+            const int k8 = 32 * ks + 8 * (lane >> 4);
+            const s16x8 ua = *reinterpret_cast<const s16x8*>(Dt[par] + (16 * w + (lane & 15)) * LHB_DS + 2 * k8);
+            const s16x8 ub = *reinterpret_cast<const s16x8*>(Bt[par] + (lane & 15) * LHB_DS + 2 * k8);
+            accU = MF16<T>::mma(ua, ub, accU);
+          }
+          par ^= 1;
+        }
+      }
+    }
+    // u partial of this slab: lane holds C[row 16w + 4(l>>4) + i][j = l&15]
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int rr = row + 16 * w + 4 * (lane >> 4) + i;
+      if (rr < r1) upart[((long)blockIdx.x * R + rr) * 16 + (lane & 15)] = accU[i];
+    }
+    __syncthreads();  // St is rewritten by the next chunk
+  }
+  // dB partial of this row range: lane holds C[j = 4(l>>4) + i][col = 16w + (l&15)] per sub-slab
+#pragma unroll
+  for (int sub = 0; sub < LHB_NSUB; ++sub)
+    if (sub < nsub)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        gpart[((long)blockIdx.y * 16 + 4 * (lane >> 4) + i) * V + c0 + sub * LHB_SUB + 16 * w + (lane & 15)] = accB[sub][i];
+}
+
+// u[e] = sum over the column slabs of upart[slab][e] (fp32, fixed order), for the ~126 slabs of a
+// 128k vocabulary: a workgroup owns 256 outputs, wave w sums slabs w, w + 4, ... (4 loads in flight
+// per lane), then wave 0 adds the 4 wave sums in order.
+template <typename T>
+__global__ __launch_bounds__(256) void lhb_usum_k(const float* __restrict__ upart, T* __restrict__ u, long n,
+                                                  int slabs) {
+  __shared__ f32x4 red[4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const long e = (long)blockIdx.x * 256 + 4 * lane;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  if (e < n) {
+    int q = w;
+    for (; q + 12 < slabs; q += 16) {
+      const f32x4 a = *reinterpret_cast<const f32x4*>(upart + (long)q * n + e);
+      const f32x4 b = *reinterpret_cast<const f32x4*>(upart + (long)(q + 4) * n + e);
+      const f32x4 c = *reinterpret_cast<const f32x4*>(upart + (long)(q + 8) * n + e);
+      const f32x4 d = *reinterpret_cast<const f32x4*>(upart + (long)(q + 12) * n + e);
+      acc = acc + a;
+      acc = acc + b;
+      acc = acc + c;
+      acc = acc + d;
+    }
+    for (; q < slabs; q += 4) acc = acc + *reinterpret_cast<const f32x4*>(upart + (long)q * n + e);
+  }
+  red[w][lane] = acc;
+  __syncthreads();
+  if (w == 0 && e < n) {
+    const f32x4 t = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
+    s16x4 o;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) o[i] = bits_of<T>(t[i]);
+    *reinterpret_cast<s16x4*>(u + e) = o;
+  }
+}
+
 // ----------------------------------------------------------------------------- launchers
 void lora_block(DType dt, const LoraBlockArgs& a, hipStream_t s) {
   const long total = (long)a.rows * a.R;
@@ -476,6 +644,52 @@ void lora_reduce(DType odt, const LoraWgradArgs& a, int S, hipStream_t s) {
     const int g = (int)((total + 255) / 256 < 2048 ? (total + 255) / 256 : 2048);
     hipLaunchKernelGGL(lora_reduce_k<OT>, dim3(g), dim3(256), 0, s, a, S, total);
   });
+}
+
+static int lhb_env(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e && *e ? atoi(e) : dflt;
+}
+int lora_head_bwd_splits(int R, int V, long ldl) {
+  const int slabs = (V + LHB_SUB * LHB_NSUB - 1) / (LHB_SUB * LHB_NSUB);
+  // whole waves of resident workgroups (2 per CU at this kernel's register count): a partial last
+  // wave of workgroups leaves most CUs idle while it streams its row ranges
+  static const int target = lhb_env("BLLM_LHB_WG", 512);
+  int S = target / slabs;
+  const int max_s = (R + 4 * LHB_ROWS - 1) / (4 * LHB_ROWS);  // >= 4 chunks per row range
+  if (S > max_s) S = max_s;
+  if (S < 1) S = 1;
+  // the kernel's buffer offsets are 32-bit: a row range (plus the prefetch overrun) stays < 2 GB
+  while (((long)(R + S - 1) / S + 4 * LHB_ROWS) * ldl * 2 >= 0x7ff00000L) ++S;
+  return S;
+}
+void lora_head_bwd(DType dt, const void* dl, long ldl, const void* st, long ldst, const void* B, long ldb,
+                   float* gpart, float* upart, void* u, int R, int V, int S, hipStream_t s) {
+  const int slabs = (V + LHB_SUB * LHB_NSUB - 1) / (LHB_SUB * LHB_NSUB);
+  const int rows_per = ((R + S - 1) / S + LHB_ROWS - 1) / LHB_ROWS * LHB_ROWS;
+  const dim3 grid(slabs, S);
+  static const int depth = lhb_env("BLLM_LHB_DEPTH", 4);
+  auto go = [&](auto tag, auto dtag) {
+    using T = decltype(tag);
+    constexpr int D = decltype(dtag)::value;
+    hipLaunchKernelGGL((lora_head_bwd_k<T, D>), grid, dim3(256), 0, s, (const T*)dl, ldl, (const T*)st, ldst,
+                       (const T*)B, ldb, gpart, upart, R, V, rows_per);
+  };
+  auto usum = [&](auto tag) {
+    using T = decltype(tag);
+    const long n = (long)R * 16;
+    hipLaunchKernelGGL(lhb_usum_k<T>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, upart, (T*)u, n, slabs);
+  };
+  using D1 = std::integral_constant<int, 1>;
+  using D2 = std::integral_constant<int, 2>;
+  using D4 = std::integral_constant<int, 4>;
+  if (dt == DType::BF16) {
+    if (depth >= 4) go(bf16_t{}, D4{}); else if (depth == 2) go(bf16_t{}, D2{}); else go(bf16_t{}, D1{});
+    usum(bf16_t{});
+  } else {
+    if (depth >= 4) go(f16_t{}, D4{}); else if (depth == 2) go(f16_t{}, D2{}); else go(f16_t{}, D1{});
+    usum(f16_t{});
+  }
 }
 
 void lora_pack_t(DType dt, const LoraPackArgs& a, int K, int max_r, hipStream_t s) {

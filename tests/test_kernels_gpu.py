@@ -614,6 +614,30 @@ def test_swiglu_bwd_lowrank_wgrad(dt, N, F, accumulate):
         _close(a, ref32.cpu(), dt, 4, name="vs fp32")
 
 
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("R,V", [(4096, 128256), (1000, 640), (77, 1088), (300, 2048)])
+@pytest.mark.parametrize("accumulate", [False, True])
+def test_lora_head_bwd(dt, R, V, accumulate):
+    """The LoRA head's u = dl B^T and dB (+)= st^T dl from one pass over dl (column-slab MFMA
+    tiles, fixed-order partial sums) vs an fp32 matmul oracle; ragged rows and a partial last
+    column slab (V not a multiple of 1,024) included; gB as a transposed view; deterministic."""
+    r = 16
+    dl = (0.01 * torch.randn(R, V, device=DEV)).to(dt)
+    sta = torch.randn(R, 4160, device=DEV).to(dt)           # s t as a column view of a wider row
+    st = sta[:, 4096:4096 + r]
+    B = (0.1 * torch.randn(r, V, device=DEV)).to(dt)
+    g0 = torch.randn(V, r, device=DEV)                       # fp32 [V, 16], passed as its [16, V] view
+    gB = g0.clone().t()
+    u = torch.empty(R, r, dtype=dt, device=DEV)
+    ops.lora_head_bwd_(dl, st, B, u, gB, accumulate)
+    _close(u, (dl.float() @ B.float().t()).cpu(), dt, 4, name="u")
+    ref = st.float().t() @ dl.float() + (g0.t() if accumulate else 0)
+    check_elem(gB, ref, rtol=1e-4, atol=1e-4 * ref.abs().max().item(), name="gB")
+    u2, gB2 = torch.empty_like(u), g0.clone().t()
+    ops.lora_head_bwd_(dl, st, B, u2, gB2, accumulate)
+    assert torch.equal(u, u2) and torch.equal(gB, gB2)
+
+
 def test_lora_model_uses_kernels_and_matches_gemm_path(monkeypatch):
     """A LoRA Llama step on the fused kernels (K-augmented QKV / gate-up / down, grouped o, the
     fused LoRA head: V = 512) gives the same loss / LoRA grads as the per-member hipBLASLt path."""

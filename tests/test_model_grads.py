@@ -328,3 +328,17 @@ def test_swiglu_bwd_lowrank_wgrad_reference_semantics():
         exp = [st[:, :16].t() @ want[:, :F], st[:, 16:].t() @ want[:, F:], s * u.t() @ act]
         for a, e, b in zip(g, exp, g0):
             assert torch.allclose(a, e + (b if acc else 0), atol=1e-4)
+
+
+def test_lora_head_bwd_cpu_contract():
+    """ops.lora_head_bwd_ (CPU path): u = dl B^T and gB (+)= st^T dl into a transposed view."""
+    torch.manual_seed(0)
+    R, V = 70, 192
+    dl, st, B = torch.randn(R, V), torch.randn(R, 16), torch.randn(16, V)
+    u = torch.empty(R, 16)
+    g0 = torch.randn(V, 16)
+    for acc in (False, True):
+        gB = g0.clone().t()
+        ops.lora_head_bwd_(dl, st, B, u, gB, acc)
+        torch.testing.assert_close(u, dl @ B.t())
+        torch.testing.assert_close(gB, st.t() @ dl + (g0.t() if acc else 0))

@@ -1,0 +1,9 @@
+# lora_head_bwd_ prefetch depth x grid sweep on the one-chunk microbench, then the numerics
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"; export TMPDIR=/tmp; O=gpurun_out/lorahead; mkdir -p $O
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -p no:cacheprovider \
+  tests/test_kernels_gpu.py -k "lora_head" > $O/tests2.log 2>&1 || { tail -40 $O/tests2.log; exit 3; }
+tail -1 $O/tests2.log
+for d in 2 4; do for wg in 512 1024 1536; do
+  echo "depth=$d wg=$wg $(BLLM_LHB_DEPTH=$d BLLM_LHB_WG=$wg timeout -k 10 120 python -u tools/bench_head_u.py 2>/dev/null | tail -1)" || exit 4
+done; done | tee $O/sweep.txt

@@ -32,7 +32,7 @@ BLLM_CLASSES = {
     "norm_fwd_k": "norm_fwd", "norm_bwd_k": "norm_bwd", "norm_bwd_wave_k": "norm_bwd",
     "ce_fwd_k": "ce_fwd", "ce_bwd_k": "ce_bwd",
     "emb_fwd_k": "emb_", "emb_bwd_tok_k": "emb_", "emb_bwd_pos_k": "emb_",
-    "lora_down_k": "lora (csrc/lora.hip)", "lora_down4_k": "lora (csrc/lora.hip)", "lora_up_k": "lora (csrc/lora.hip)", "lora_wgrad_k": "lora (csrc/lora.hip)",
+    "lora_down_k": "lora (csrc/lora.hip)", "lora_down4_k": "lora (csrc/lora.hip)", "lora_head_bwd_k": "lora (csrc/lora.hip)", "lhb_usum_k": "lora (csrc/lora.hip)", "lora_up_k": "lora (csrc/lora.hip)", "lora_wgrad_k": "lora (csrc/lora.hip)",
     "lora_reduce_k": "lora (csrc/lora.hip)", "lora_pack_t_k": "lora (csrc/lora.hip)",
 }
 _MANGLED = re.compile(r"_ZN4bllm(?:12_GLOBAL__N_1)?(\d+)([A-Za-z_][A-Za-z0-9_]*)")
