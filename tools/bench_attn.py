@@ -38,6 +38,9 @@ def main():
     ap.add_argument("--variants", default="",
                     help="forward A/B arms 'name:VAR=v+VAR2=v;name2:...' (kernel knobs read per launch), "
                          "timed interleaved with the default; outputs compared with the default's")
+    ap.add_argument("--bwd_env_ab", default="",
+                    help="NAME=v1,v2,...: time the backward under each value of env NAME (a kernel knob read per "
+                         "launch), interleaved, and report dqkv's max difference from the first value's")
     ap.add_argument("--no_mask", action="store_true",
                     help="dropout shapes: re-hash the keep bits in backward instead of reading the forward's mask")
     a = ap.parse_args()
@@ -98,6 +101,21 @@ def main():
                                   tflops_0=round(flop / med["0"] / 1e9, 1), tflops_1=round(flop / med["1"] / 1e9, 1),
                                   max_abs_o=float((o0.float() - o1.float()).abs().max()),
                                   max_abs_lse=float((l0 - l1).abs().max()))), flush=True)
+        if a.bwd_env_ab:
+            nm, vals = a.bwd_env_ab.split("=", 1)
+            vals = vals.split(",")
+            tt, outs = {}, {}
+            for rnd in range(3):
+                for v in vals:
+                    os.environ[nm] = v
+                    tt.setdefault(v, []).append(timeit(
+                        lambda: ops.flash_attn_bwd(qkv, o, lse, do, B, T, H, G, hd, causal, p, 1, 0, keep_mask=km), a.iters))
+                    outs[v] = ops.flash_attn_bwd(qkv, o, lse, do, B, T, H, G, hd, causal, p, 1, 0, keep_mask=km)
+            os.environ.pop(nm)
+            ref0 = outs[vals[0]].float()
+            print(json.dumps(dict(shape=name, ab=nm, bwd_ms={v: round(sorted(ts)[1], 4) for v, ts in tt.items()},
+                                  max_abs_dqkv={v: float((x.float() - ref0).abs().max()) for v, x in outs.items()})),
+                  flush=True)
         res.append(dict(shape=name, B=B, T=T, causal=causal, keep_mask=km is not None, fwd_ms=round(tf, 4), bwd_ms=round(tb, 4),
                         fwd_tflops=round(flop / tf / 1e9, 1), bwd_tflops_5mm=round(2.5 * flop / tb / 1e9, 1)))
     for r in res:
