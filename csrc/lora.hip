@@ -422,6 +422,7 @@ __global__ __launch_bounds__(256) void lora_block_k(LoraBlockArgs a) {
 constexpr int LHB_SUB = 64, LHB_NSUB = 16, LHB_ROWS = 64;
 constexpr int LHB_DS = LHB_SUB * 2 + 16;  // bytes per row of a dl / B tile (padded)
 constexpr int LHB_SS = 32;                // bytes per row of the st tile
+constexpr int LHB_BS = LHB_SUB * LHB_NSUB * 2 + 16;  // bytes per row of the staged B slab (padded)
 
 __device__ __forceinline__ s16x8 lhb_tr(const char* tile, int stride, int col_byte, int lane) {
   const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
@@ -437,7 +438,8 @@ __global__ __launch_bounds__(256) void lora_head_bwd_k(const T* __restrict__ dl,
                                                        float* __restrict__ gpart, float* __restrict__ upart, int R,
                                                        int V, int rows_per) {
   __shared__ __attribute__((aligned(16))) char Dt[2][LHB_ROWS * LHB_DS];
-  __shared__ __attribute__((aligned(16))) char Bt[2][16 * LHB_DS];
+  // the slab's B [16 x 1,024] stays in LDS for the whole row range (staged once)
+  __shared__ __attribute__((aligned(16))) char Bs[16 * LHB_BS];
   __shared__ __attribute__((aligned(16))) char St[LHB_ROWS * LHB_SS];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int c0 = blockIdx.x * LHB_SUB * LHB_NSUB;
@@ -448,12 +450,16 @@ __global__ __launch_bounds__(256) void lora_head_bwd_k(const T* __restrict__ dl,
   constexpr int nsubP = LHB_NSUB;
   const int r0 = blockIdx.y * rows_per, r1 = r0 + rows_per < R ? r0 + rows_per : R;
   const s16x8 zero = {0, 0, 0, 0, 0, 0, 0, 0};
-  // staging roles: dl tile rows dr, dr + 32 at 16-B chunk dc; B row bj (threads < 128); st row sr half sh
-  const int dr = tid >> 3, dc = (tid & 7) * 8, bj = tid >> 3, sr = tid >> 1, sh = tid & 1;
+  // staging roles: dl tile rows dr, dr + 32 at 16-B chunk dc; st row sr half sh (threads < 128)
+  const int dr = tid >> 3, dc = (tid & 7) * 8, sr = tid >> 1, sh = tid & 1;
   f32x4 accB[LHB_NSUB];
 #pragma unroll
   for (int k = 0; k < LHB_NSUB; ++k) accB[k] = f32x4{0.f, 0.f, 0.f, 0.f};
-  s16x8 pd0[D], pd1[D], pb[D], ps = zero;
+  s16x8 pd0[D], pd1[D], ps = zero;
+  for (int e = tid; e < 16 * LHB_NSUB * (LHB_SUB / 8); e += 256) {
+    const int j = e / (LHB_NSUB * LHB_SUB / 8), c = (e - j * (LHB_NSUB * LHB_SUB / 8)) * 8;
+    *reinterpret_cast<s16x8*>(Bs + j * LHB_BS + 2 * c) = c < nsub * LHB_SUB ? ld8(Bm + (long)j * ldb + c0 + c) : zero;
+  }
   // Loads are raw buffer loads on descriptors bounded to this workgroup's rows: a row past r1 (and
   // a padded sub-slab, sent to an offset past every bound) reads as 0 with no branch, so the
   // compiler can keep the D pieces in flight (exec-masked loads made it drain vmcnt to 0).
@@ -461,15 +467,13 @@ __global__ __launch_bounds__(256) void lora_head_bwd_k(const T* __restrict__ dl,
   const int nrow = r1 > r0 ? r1 - r0 : 0;
   const __amdgpu_buffer_rsrc_t rd =
       __builtin_amdgcn_make_buffer_rsrc((void*)(dl + (long)r0 * ldl), (short)0, (int)((long)nrow * ldl * 2), 0x00020000);
-  const __amdgpu_buffer_rsrc_t rb =
-      __builtin_amdgcn_make_buffer_rsrc((void*)Bm, (short)0, (int)(16L * ldb * 2), 0x00020000);
   const __amdgpu_buffer_rsrc_t rs =
       __builtin_amdgcn_make_buffer_rsrc((void*)(st + (long)r0 * ldst), (short)0, (int)((long)nrow * ldst * 2), 0x00020000);
   const int half_off = (int)(32L * ldl * 2);  // rows dr + 32
   // load cursor: (lrow, lsub) of the next piece to fetch, D iterations ahead of the MFMAs, as
   // running byte offsets (not per-sub addresses, which the unrolled loop would keep live)
   int lsub = 0;
-  int od = (int)(((long)dr * ldl + c0 + dc) * 2), ob = (int)(((long)bj * ldb + c0 + dc) * 2);
+  int od = (int)(((long)dr * ldl + c0 + dc) * 2);
   const int dstep = (int)(((long)LHB_ROWS * ldl - (long)nsubP * LHB_SUB) * 2);
   auto bld = [](const __amdgpu_buffer_rsrc_t& r, int off, int soff) {
     return __builtin_bit_cast(s16x8, __builtin_amdgcn_raw_buffer_load_b128(r, off, soff, 0));
@@ -478,9 +482,8 @@ __global__ __launch_bounds__(256) void lora_head_bwd_k(const T* __restrict__ dl,
     const bool in = lsub < nsub;
     pd0[k] = bld(rd, in ? od : OOB, 0);
     pd1[k] = bld(rd, in ? od + half_off : OOB, 0);
-    if (tid < 128) pb[k] = bld(rb, in ? ob : OOB, 0);
-    od += LHB_SUB * 2; ob += LHB_SUB * 2;
-    if (++lsub == nsubP) { lsub = 0; od += dstep; ob -= nsubP * LHB_SUB * 2; }
+    od += LHB_SUB * 2;
+    if (++lsub == nsubP) { lsub = 0; od += dstep; }
   };
   auto load_st = [&](int row) {
     if (tid < 128) ps = bld(rs, (int)(((long)(row - r0 + sr) * ldst + 8 * sh) * 2), 0);
@@ -501,7 +504,6 @@ __global__ __launch_bounds__(256) void lora_head_bwd_k(const T* __restrict__ dl,
         {
           *reinterpret_cast<s16x8*>(Dt[par] + dr * LHB_DS + dc * 2) = pd0[k];
           *reinterpret_cast<s16x8*>(Dt[par] + (32 + dr) * LHB_DS + dc * 2) = pd1[k];
-          if (tid < 128) *reinterpret_cast<s16x8*>(Bt[par] + bj * LHB_DS + dc * 2) = pb[k];
           __syncthreads();
         }
         load(k);
@@ -515,7 +517,7 @@ __global__ __launch_bounds__(256) void lora_head_bwd_k(const T* __restrict__ dl,
             // u: [16 rows of wave w x 16 j] += dl [16 rows x 32 cols] . B^T [32 cols x 16 j]
             const int k8 = 32 * ks + 8 * (lane >> 4);
             const s16x8 ua = *reinterpret_cast<const s16x8*>(Dt[par] + (16 * w + (lane & 15)) * LHB_DS + 2 * k8);
-            const s16x8 ub = *reinterpret_cast<const s16x8*>(Bt[par] + (lane & 15) * LHB_DS + 2 * k8);
+            const s16x8 ub = *reinterpret_cast<const s16x8*>(Bs + (lane & 15) * LHB_BS + 2 * (sub * LHB_SUB + k8));
             accU = MF16<T>::mma(ua, ub, accU);
           }
           par ^= 1;

@@ -6,6 +6,6 @@ timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method threa
   tests/test_kernels_gpu.py -k "lora_head" > $O/tests.log 2>&1 || { tail -40 $O/tests.log; exit 3; }
 tail -1 $O/tests.log
 timeout -k 10 180 rocprofv3 --kernel-trace --stats -d $O -o run -- python3 tools/prof_lora_head.py > $O/log.txt 2>&1 || { tail -20 $O/log.txt; exit 4; }
-for d in 2 4; do for wg in 512 1024; do
+for d in 2 4; do for wg in 512 768; do
   echo "depth=$d wg=$wg $(BLLM_LHB_DEPTH=$d BLLM_LHB_WG=$wg timeout -k 10 120 python -u tools/bench_head_u.py 2>/dev/null | tail -1)" || exit 5
 done; done | tee $O/sweep.txt
