@@ -20,9 +20,6 @@
 //
 // All three are HBM-bound (the rank is 8-64): x / dy / y are streamed exactly once per kernel
 // with 16-byte lane accesses; the small operands (A, B, t, u) stay L2-resident.
-#include <cstdlib>
-#include <type_traits>
-
 #include "api.h"
 
 namespace bllm {
@@ -648,16 +645,12 @@ void lora_reduce(DType odt, const LoraWgradArgs& a, int S, hipStream_t s) {
   });
 }
 
-static int lhb_env(const char* name, int dflt) {
-  const char* e = getenv(name);
-  return e && *e ? atoi(e) : dflt;
-}
 int lora_head_bwd_splits(int R, int V, long ldl) {
   const int slabs = (V + LHB_SUB * LHB_NSUB - 1) / (LHB_SUB * LHB_NSUB);
-  // whole waves of resident workgroups (2 per CU at this kernel's register count): a partial last
-  // wave of workgroups leaves most CUs idle while it streams its row ranges
-  static const int target = lhb_env("BLLM_LHB_WG", 512);
-  int S = target / slabs;
+  // one whole wave of resident workgroups (2 per CU: LDS-bound): a partial last wave of
+  // workgroups leaves most CUs idle while it streams its row ranges (512 measured best of
+  // 512 / 768 / 1,024 / 1,536 / 2,048, profiles/r5/lora_head/)
+  int S = 512 / slabs;
   const int max_s = (R + 4 * LHB_ROWS - 1) / (4 * LHB_ROWS);  // >= 4 chunks per row range
   if (S > max_s) S = max_s;
   if (S < 1) S = 1;
@@ -670,27 +663,18 @@ void lora_head_bwd(DType dt, const void* dl, long ldl, const void* st, long ldst
   const int slabs = (V + LHB_SUB * LHB_NSUB - 1) / (LHB_SUB * LHB_NSUB);
   const int rows_per = ((R + S - 1) / S + LHB_ROWS - 1) / LHB_ROWS * LHB_ROWS;
   const dim3 grid(slabs, S);
-  static const int depth = lhb_env("BLLM_LHB_DEPTH", 4);
-  auto go = [&](auto tag, auto dtag) {
-    using T = decltype(tag);
-    constexpr int D = decltype(dtag)::value;
-    hipLaunchKernelGGL((lora_head_bwd_k<T, D>), grid, dim3(256), 0, s, (const T*)dl, ldl, (const T*)st, ldst,
-                       (const T*)B, ldb, gpart, upart, R, V, rows_per);
-  };
-  auto usum = [&](auto tag) {
-    using T = decltype(tag);
-    const long n = (long)R * 16;
-    hipLaunchKernelGGL(lhb_usum_k<T>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, upart, (T*)u, n, slabs);
-  };
-  using D1 = std::integral_constant<int, 1>;
-  using D2 = std::integral_constant<int, 2>;
-  using D4 = std::integral_constant<int, 4>;
+  const long n = (long)R * 16;
+  // prefetch depth 4 (measured against 1 and 2, profiles/r5/lora_head/sweep*.txt)
   if (dt == DType::BF16) {
-    if (depth >= 4) go(bf16_t{}, D4{}); else if (depth == 2) go(bf16_t{}, D2{}); else go(bf16_t{}, D1{});
-    usum(bf16_t{});
+    hipLaunchKernelGGL((lora_head_bwd_k<bf16_t, 4>), grid, dim3(256), 0, s, (const bf16_t*)dl, ldl,
+                       (const bf16_t*)st, ldst, (const bf16_t*)B, ldb, gpart, upart, R, V, rows_per);
+    hipLaunchKernelGGL(lhb_usum_k<bf16_t>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, upart, (bf16_t*)u, n,
+                       slabs);
   } else {
-    if (depth >= 4) go(f16_t{}, D4{}); else if (depth == 2) go(f16_t{}, D2{}); else go(f16_t{}, D1{});
-    usum(f16_t{});
+    hipLaunchKernelGGL((lora_head_bwd_k<f16_t, 4>), grid, dim3(256), 0, s, (const f16_t*)dl, ldl,
+                       (const f16_t*)st, ldst, (const f16_t*)B, ldb, gpart, upart, R, V, rows_per);
+    hipLaunchKernelGGL(lhb_usum_k<f16_t>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, upart, (f16_t*)u, n,
+                       slabs);
   }
 }
 

@@ -1,4 +1,6 @@
 # lora_head_bwd_ numerics, then per-kernel time (main kernel + the two fixed-order partial sums)
+# (historical: the BLLM_LHB_DEPTH / BLLM_LHB_WG knobs this sweeps were removed after it; depth 4 and
+# 512 workgroups are fixed in csrc/lora.hip -- the script documents how profiles/r5/lora_head/sweep*.txt were made)
 # and the one-chunk microbench per prefetch depth
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"; export TMPDIR=/tmp; O=gpurun_out/lorahead/prof; mkdir -p $O

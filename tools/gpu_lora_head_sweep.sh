@@ -1,4 +1,6 @@
 # lora_head_bwd_ prefetch depth x grid sweep on the one-chunk microbench, then the numerics
+# (historical: the BLLM_LHB_DEPTH / BLLM_LHB_WG knobs this sweeps were removed after it; depth 4 and
+# 512 workgroups are fixed in csrc/lora.hip -- the script documents how profiles/r5/lora_head/sweep*.txt were made)
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"; export TMPDIR=/tmp; O=gpurun_out/lorahead; mkdir -p $O
 timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -p no:cacheprovider \
