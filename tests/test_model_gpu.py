@@ -393,3 +393,37 @@ def test_lora_swiglu_wgrad_fusion_in_model(monkeypatch):
     assert l0 == l1
     for k in g0:
         assert _rel(g1[k], g0[k]) < 1e-2, (k, _rel(g1[k], g0[k]))
+
+
+def test_lora_head_fusion_in_model(monkeypatch):
+    """A LoRA Llama step with the head's u = dl B^T and dB = (s t)^T dl from one pass over each
+    logits-gradient chunk (ops.lora_head_bwd_) gives the hipBLASLt + lora_wgrad path's loss and
+    gradients, and two runs of the fused path are bitwise equal (fixed-order partial sums)."""
+    ops.load_ext(required=True)
+    cfg = get_config("llama3_2", "1B").replace(context_length=128, emb_dim=256, n_heads=4, n_kv_groups=2,
+                                               hidden_dim=512, n_layers=2, vocab_size=1088, dtype=torch.bfloat16)
+    res, calls = {}, []
+    orig = ops.lora_head_bwd_
+    monkeypatch.setattr(ops, "lora_head_bwd_", lambda *a, **k: (calls.append(1), orig(*a, **k))[1])
+    for run, fused in ((0, False), (1, True), (2, True)):
+        monkeypatch.setattr(ops, "LORA_HEAD_FUSED", fused)
+        torch.manual_seed(0)
+        m = build_model(cfg, device="cuda")
+        for p in m.parameters():
+            p.requires_grad = False
+        replace_linear_with_lora(m, rank=16, alpha=32)
+        for mod in m.modules():
+            if hasattr(mod, "B") and isinstance(mod.B, torch.nn.Parameter):
+                torch.nn.init.normal_(mod.B, std=0.05)
+        m.flatten(device="cuda")
+        idx = torch.randint(0, cfg.vocab_size, (2, 128), device="cuda", generator=torch.Generator("cuda").manual_seed(1))
+        for step in range(2):   # the second backward accumulates into the first's gradients
+            loss = m(idx, idx)
+            loss.backward()
+        res[run] = (loss.item(), {n: p.grad.float().clone() for n, p in m.named_parameters() if p.requires_grad})
+    assert len(calls) >= 4, calls     # fused runs: >= 1 chunk x 2 steps each
+    (l0, g0), (l1, g1), (l2, g2) = res[0], res[1], res[2]
+    assert l0 == l1 == l2
+    for k in g0:
+        assert _rel(g1[k], g0[k]) < 1e-2, (k, _rel(g1[k], g0[k]))
+        assert torch.equal(g1[k], g2[k]), k
