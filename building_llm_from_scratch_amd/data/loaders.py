@@ -16,7 +16,7 @@ from __future__ import annotations
 from functools import partial
 
 import torch
-from torch.utils.data import DataLoader
+from torch.utils.data import DataLoader, RandomSampler
 from torch.utils.data.distributed import DistributedSampler
 
 from ..utils.misc import read_json_file, read_text_file
@@ -28,7 +28,9 @@ def _is_dist() -> bool:
 
 
 def _make_loader(owner, ds, shuffle, drop_last, num_workers, generator):
-    workers = dict(num_workers=num_workers, persistent_workers=False)
+    # persistent workers: the trainer re-uses a file's loaders across epochs (reseeding the shuffle
+    # generator / set_epoch), so their worker processes are forked once instead of per epoch
+    workers = dict(num_workers=num_workers, persistent_workers=num_workers > 0)
     if num_workers > 0:
         workers["prefetch_factor"] = 4
     if owner.run_type == "multi_gpu" and _is_dist():
@@ -39,9 +41,13 @@ def _make_loader(owner, ds, shuffle, drop_last, num_workers, generator):
         return DataLoader(ds, batch_size=owner.batch_size, pin_memory=owner.pin_memory, shuffle=False,
                           drop_last=drop_last, sampler=DistributedSampler(ds, shuffle=True),
                           collate_fn=owner.collate_func, **workers)
-    return DataLoader(ds, batch_size=owner.batch_size, pin_memory=owner.pin_memory, shuffle=shuffle,
+    # the shuffle draws only from ``generator`` (its own sampler): the DataLoader's worker base
+    # seed comes from a separate fixed generator, so a loader re-used with ``generator`` reseeded
+    # (persistent workers skip that draw) yields the order a fresh loader with that seed yields
+    sampler = RandomSampler(ds, generator=generator) if shuffle else None
+    return DataLoader(ds, batch_size=owner.batch_size, pin_memory=owner.pin_memory, sampler=sampler,
                       drop_last=drop_last, collate_fn=owner.collate_func,
-                      generator=generator if shuffle else None, **workers)
+                      generator=torch.Generator().manual_seed(0), **workers)
 
 
 def first_batches(loader, n):

@@ -33,6 +33,9 @@ from .generate import generate_cached
 
 logger = setup_logger("train")
 
+# data files whose loaders the trainer keeps across epochs (read / tokenised / workers forked once)
+MAX_CACHED_FILES = 4
+
 ALPACA_CONTEXT = ("Below is an instruction that describes a task. Write a response that appropriately "
                   "completes the request.\n\n### Instruction:\nWhat is an antonym of 'complicated'?")
 
@@ -112,6 +115,9 @@ class Trainer:
         self._data_wait = 0.0
         # steps 1..comm_adapt_steps feed the engine's warm-up adaptation (parallel/ fsdp, ddp)
         self.comm_adapt_steps = comm_adapt_steps
+        # file index -> (train loader, val loader, shuffle generator), kept across epochs when there
+        # are few files: the data is read and tokenised once and the persistent workers forked once
+        self._loaders = {}
 
     # ------------------------------------------------------------------ helpers
     def _sync(self):
@@ -324,9 +330,19 @@ class Trainer:
                     skip = start[2] if (epoch, fi) == start[:2] else 0
                     # per-(epoch, file) shuffle seed: the order does not depend on how many
                     # random numbers were drawn before (sampling, dropout), so resume replays it
-                    g = torch.Generator().manual_seed(self.seed * 1_000_003 + epoch * 1009 + fi)
-                    train_loader, val_loader = self.loaderObj.create_dataloaders(
-                        read(fp), num_workers=self.num_workers, generator=g)
+                    shuffle_seed = self.seed * 1_000_003 + epoch * 1009 + fi
+                    cached = self._loaders.get(fi)
+                    if cached is not None:
+                        # the same loaders with the generator reseeded: the order a fresh
+                        # generator with this seed gives (the sampler draws at iter())
+                        train_loader, val_loader, g = cached
+                        g.manual_seed(shuffle_seed)
+                    else:
+                        g = torch.Generator().manual_seed(shuffle_seed)
+                        train_loader, val_loader = self.loaderObj.create_dataloaders(
+                            read(fp), num_workers=self.num_workers, generator=g)
+                        if len(self.data_files) <= MAX_CACHED_FILES:
+                            self._loaders[fi] = (train_loader, val_loader, g)
                     if hasattr(train_loader.sampler, "set_epoch"):
                         train_loader.sampler.set_epoch(epoch)
                     self.train_epoch(epoch, train_loader, val_loader, start_context=start_context,

@@ -431,3 +431,34 @@ def test_tunableop_table_resolution(tmp_path, monkeypatch):
     assert os.path.dirname(cp) == d and open(cp).read() == open(src).read()
     assert not os.path.islink(cp)
     assert cli.build_parser().parse_args([]).tunableop == "auto"
+
+
+def test_trainer_reuses_loaders_across_epochs(tmp_path):
+    """With few data files the trainer builds a file's loaders once and, each later epoch,
+    reseeds their shuffle generator (persistent workers are forked once): every epoch sees the
+    batch order that fresh loaders seeded for that (epoch, file) give."""
+    import json
+    from building_llm_from_scratch_amd.data.loaders import DataloaderIF
+    from building_llm_from_scratch_amd.data.tokenizer import ByteTokenizer
+    from building_llm_from_scratch_amd.utils.misc import read_json_file
+    tok = ByteTokenizer({"<|endoftext|>": 256})
+    recs = [{"instruction": f"say {i}", "input": "", "output": f"{i}" * (1 + i % 5)} for i in range(40)]
+    fp = tmp_path / "a.json"
+    fp.write_text(json.dumps(recs))
+    collate = __import__("functools").partial(custom_collate_fn, pad_token_id=256, allowed_max_length=256)
+    dif = DataloaderIF(tok, batch_size=4, max_length=256, collate_func=collate)
+    made = []
+    orig = dif.create_dataloaders
+    dif.create_dataloaders = lambda *a, **k: (made.append(1), orig(*a, **k))[1]
+    tr = Trainer(model=None, optimizer=_Opt(5e-4), config={}, data_files=[str(fp)], loaderObj=dif,
+                 save_dir=str(tmp_path), num_workers=2, seed=123)
+    seen = []
+    tr.train_epoch = lambda epoch, tl, vl, **kw: seen.append([x.clone() for x, _ in tl])
+    tr._loop(3, read_json_file, "ctx")
+    assert len(made) == 1 + 1        # get_total_steps_epoch's + the first epoch's; epochs 2-3 reuse
+    for epoch, got in enumerate(seen):
+        g = torch.Generator().manual_seed(123 * 1_000_003 + epoch * 1009)
+        ref = [x for x, _ in orig(recs, num_workers=0, generator=g)[0]]
+        assert len(got) == len(ref) == 9
+        assert all(torch.equal(a, b) for a, b in zip(got, ref)), epoch
+    assert not all(a.shape == b.shape and torch.equal(a, b) for a, b in zip(seen[0], seen[1]))   # reshuffled
