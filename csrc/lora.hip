@@ -412,12 +412,13 @@ __global__ __launch_bounds__(256) void lora_block_k(LoraBlockArgs a) {
 //   gpart[ry][j][c] = sum_{n in rows of ry} st[n][j] dl[n][c]      (dB partial per row range)
 //   upart[cx][n][j] = sum_{c in slab cx} dl[n][c] B[j][c]          (u partial per column slab)
 // A workgroup owns a slab of up to 1,024 columns (16 sub-slabs of 64) and a row range, walked in
-// 64-row chunks; per (chunk, sub-slab) the dl tile [64 x 64] and B's [16 x 64] slice are staged in
-// LDS (double-buffered, one barrier), then wave w adds its 16 columns of dB (A = st^T, B = dl,
-// both transposed reads, K = rows) and its 16 rows of u (A = dl rows, B = B rows, K = columns).
-// lora_reduce / sum_partials_into finish both sums in a fixed order (deterministic).
+// 64-row chunks; B's [16 x 1,024] slab is staged in LDS once, and per (chunk, sub-slab) the dl tile
+// [64 x 64] (4 tiles in flight in registers) is staged in LDS (double-buffered, one barrier), then
+// wave w adds its 16 columns of dB (A = st^T, B = dl, both transposed reads, K = rows) and its 16
+// rows of u (A = dl rows, B = B rows, K = columns).  lhb_usum_k / lora_reduce finish both sums in
+// a fixed order (deterministic).
 constexpr int LHB_SUB = 64, LHB_NSUB = 16, LHB_ROWS = 64;
-constexpr int LHB_DS = LHB_SUB * 2 + 16;  // bytes per row of a dl / B tile (padded)
+constexpr int LHB_DS = LHB_SUB * 2 + 16;  // bytes per row of a dl tile (padded)
 constexpr int LHB_SS = 32;                // bytes per row of the st tile
 constexpr int LHB_BS = LHB_SUB * LHB_NSUB * 2 + 16;  // bytes per row of the staged B slab (padded)
 
