@@ -208,24 +208,40 @@ __global__ __launch_bounds__(256) void lora_up_k(LoraUpArgs a, int rows, int N) 
         }
       }
     };
+    // the tile's t rows (the MFMA B fragments, rc <= 64: at most two 32-deep k-steps) are
+    // prefetched a tile ahead too: loaded in front of the MFMAs they left every tile waiting a
+    // full load latency
+    s16x8 tbv[2], tbn[2];
+    auto load_t = [&](long r0_, s16x8 (&dst)[2]) {
+      const long tr = r0_ + (lane & 15) < N ? r0_ + (lane & 15) : N - 1;
+      const T* t = (const T*)a.t + tr * a.ldt + a.toff[m] + j0;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int kk = 32 * ks + 8 * (lane >> 4);
+        dst[ks] = kk < rc ? ld8(t + kk) : zero;  // r % 16 == 0: the upper half of a step may be padding
+      }
+    };
     load_base((long)blockIdx.x * rows + wave * 16, bsv);
+    load_t((long)blockIdx.x * rows + wave * 16, tbv);
     for (int rt = 0; rt < rows / 64; ++rt) {
       const long row0 = (long)blockIdx.x * rows + rt * 64 + wave * 16;
       if (row0 >= N) break;  // wave-uniform: this wave's remaining tiles are past the tokens
-      const long tr = row0 + (lane & 15) < N ? row0 + (lane & 15) : N - 1;
-      const T* t = (const T*)a.t + tr * a.ldt + a.toff[m] + j0;
-      if (rt + 1 < rows / 64 && row0 + 64 < N) load_base(row0 + 64, bsn);
+      if (rt + 1 < rows / 64 && row0 + 64 < N) {
+        load_base(row0 + 64, bsn);
+        load_t(row0 + 64, tbn);
+      }
       f32x4 acc[8];
 #pragma unroll
       for (int q = 0; q < 8; ++q) acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
-      for (int k0 = 0; k0 < rc; k0 += 32) {
-        const int kk = k0 + 8 * (lane >> 4);
-        const bool live = kk < rc;  // r % 16 == 0: the upper half of the last step may be padding
-        const s16x8 tb = live ? ld8(t + kk) : zero;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        if (32 * ks >= rc) break;
+        const int kk = 32 * ks + 8 * (lane >> 4);
+        const bool live = kk < rc;
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
           const s16x8 ua = live ? *reinterpret_cast<const s16x8*>(&us[(q * 16 + (lane & 15)) * RP + kk]) : zero;
-          acc[q] = MF16<T>::mma(ua, tb, acc[q]);
+          acc[q] = MF16<T>::mma(ua, tbv[ks], acc[q]);
         }
       }
       // lane holds Y^T[col q*16 + 4(l>>4) + i][row l&15] -> per-wave [16 rows][128 cols] fp32 tile
@@ -256,6 +272,8 @@ __global__ __launch_bounds__(256) void lora_up_k(LoraUpArgs a, int rows, int N) 
       }
 #pragma unroll
       for (int p = 0; p < 4; ++p) bsv[p] = bsn[p];
+      tbv[0] = tbn[0];
+      tbv[1] = tbn[1];
       __builtin_amdgcn_wave_barrier();  // tile reads done before the next tile's writes
     }
   }
