@@ -1,6 +1,6 @@
 # lora_up with its t rows prefetched a tile ahead: numerics, then the microbench new vs previous
-# (needs building_llm_from_scratch_amd/_C_prev.so: the previous build, copied in by hand for the run)
-# build (the previous .so swapped in on the box's scratch copy)
+# build (the previous .so swapped in on the box's scratch copy; needs
+# building_llm_from_scratch_amd/_C_prev.so, the previous build, copied in by hand for the run)
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"; export TMPDIR=/tmp; O=gpurun_out/loraup; mkdir -p $O
 timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -p no:cacheprovider \
