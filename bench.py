@@ -174,10 +174,14 @@ def init_dist(a):
     # per-collective start / end events on RCCL's stream (Work._get_duration: the bandwidth
     # account of parallel/commstats.py); read by ProcessGroupNCCL at construction
     os.environ.setdefault("TORCH_NCCL_ENABLE_TIMING", "1")
+    a.rccl_log = None
     if rccl:
         from building_llm_from_scratch_amd.parallel import nccl_pg_options
+        if world > 1 or a.force_comm:   # RCCL's channel / algorithm choices -> "rccl_topology"
+            from building_llm_from_scratch_amd.utils.telemetry import rccl_debug_env
+            a.rccl_log = rccl_debug_env(rank)
         kw["device_id"] = dev
-        kw["pg_options"] = nccl_pg_options()
+        kw["pg_options"] = nccl_pg_options(kw["timeout"])
     backend = "nccl" if rccl else "gloo"
     if launched:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -432,12 +436,20 @@ def main(argv=None):
     probe_peak = None
     comm = getattr(engine, "comm", None)
     adapt_hist = []
+    # every warm-up step's collectives (op, bytes, dtype) compared across ranks over the
+    # rendezvous store right after the step is issued, before anything waits on them: a divergent
+    # order raises naming the first differing call instead of hanging until the PG timeout
+    from building_llm_from_scratch_amd.parallel.seqcheck import CollectiveSequence
+    seq = CollectiveSequence(enabled=world > 1 or a.force_comm)
+    seq_checked = 0
     for i in range(a.warmup):
         if comm is not None:
             comm.reset(enabled=True)      # this warm-up step's exposed waits (adaptation input)
         sync()
         tw = time.perf_counter()
-        loss = step(i)
+        with seq.recording(f"warmup{i}"):
+            loss = step(i)
+        seq_checked += seq.verify(f"warmup{i}")
         if i == 0 and plan is not None and cuda:
             # memory probe: the first step's measured peak (max over ranks) checks the plan
             sync()
@@ -604,8 +616,14 @@ def main(argv=None):
                      "adapted": adapt_hist,
                      "per_rank_fsdp_prefetch": [k[0] for k in knobs_all] if a.parallel == "fsdp" else None,
                      "per_rank_bucket_mib": [k[1] for k in knobs_all],
-                     "deferred_init": bool(getattr(engine, "deferred_init", False))},
+                     "deferred_init": bool(getattr(engine, "deferred_init", False)),
+                     # warm-up steps' collectives compared across ranks (parallel/seqcheck.py)
+                     "order_check": {"enabled": seq.enabled, "calls_checked_rank0": seq_checked,
+                                     "steps": a.warmup}},
         }
+        if a.rccl_log:
+            from building_llm_from_scratch_amd.utils.telemetry import rccl_topology
+            out["rccl_topology"] = rccl_topology(a.rccl_log)
         # what the box did during the timed steps (clocks, power, temperature, throttle residency)
         # and whether the GEMM tuning table was taken: box-to-box differences become readable
         out["telemetry"] = {"rank0": telem_all[0],

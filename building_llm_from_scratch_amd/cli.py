@@ -152,11 +152,10 @@ def ddp_setup(rank: int, world_size: int, args):
     device = _device_for(args, int(os.environ.get("LOCAL_RANK", rank)))
     backend = args.backend or ("nccl" if device.type == "cuda" else "gloo")
     timeout = timedelta(minutes=getattr(args, "pg_timeout_min", 30.0))
-    os.environ.setdefault("TORCH_NCCL_ENABLE_TIMING", "1")   # per-collective bandwidth account
     if backend == "nccl":
         from .parallel import nccl_pg_options
         dist.init_process_group("nccl", rank=rank, world_size=world_size, device_id=device, timeout=timeout,
-                                pg_options=nccl_pg_options())
+                                pg_options=nccl_pg_options(timeout))
     else:
         dist.init_process_group("gloo", rank=rank, world_size=world_size, timeout=timeout)
     return device

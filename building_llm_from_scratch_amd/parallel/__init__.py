@@ -18,14 +18,18 @@ import torch
 from ..models.base import LocalEngine
 
 
-def nccl_pg_options():
+def nccl_pg_options(timeout=None):
     """RCCL process-group options: collectives on HIGH-priority HIP streams, so a prefetched
     all-gather / reduce-scatter kernel is scheduled ahead of queued compute kernels instead of
-    waiting behind them (the overlap FSDP / DDP rely on)."""
+    waiting behind them (the overlap FSDP / DDP rely on).  ``timeout`` (the same timedelta
+    passed to ``init_process_group``) is stored in the options too: torch warns on every RCCL
+    init when the two differ."""
     import torch.distributed as dist
     try:
         opts = dist.ProcessGroupNCCL.Options()
         opts.is_high_priority_stream = True
+        if timeout is not None:
+            opts._timeout = timeout
         return opts
     except (AttributeError, RuntimeError):  # torch built without NCCL/RCCL
         return None

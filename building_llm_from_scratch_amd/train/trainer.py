@@ -16,6 +16,7 @@ loss guard, optional ``max_steps`` and resume state.
 """
 from __future__ import annotations
 
+import contextlib
 import itertools
 import math
 import time
@@ -30,6 +31,8 @@ from ..utils.misc import read_json_file, read_text_file, text_to_token_ids, toke
 from ..data.loaders import first_batches
 from .checkpoint import resume_state_path, save_model, save_resume_state
 from .generate import generate_cached
+
+IGNORE_INDEX = -100   # the instruction collate's masked-target id (data/datasets.py)
 
 logger = setup_logger("train")
 
@@ -91,6 +94,10 @@ class Trainer:
         self.save_resume = save_resume
         self.global_step = -1
         self.tokens_seen = 0
+        # this rank's tokens since the last exact all-rank sum (_flush_tokens); instruction data
+        # counts its real (non-ignored) targets, pretraining every input position
+        self._tokens_pending = 0
+        self.count_target_tokens = False
         self.train_losses, self.val_losses, self.track_lrs, self.track_tokens_seen = [], [], [], []
         self.metrics = MetricsWriter(metrics_file if rank == 0 else None)
         self._t_last = None
@@ -118,6 +125,8 @@ class Trainer:
         # file index -> (train loader, val loader, shuffle generator), kept across epochs when there
         # are few files: the data is read and tokenised once and the persistent workers forked once
         self._loaders = {}
+        self._seq = None              # parallel/seqcheck.CollectiveSequence (warm-up steps)
+        self._seq_timeout_s = 120.0
 
     # ------------------------------------------------------------------ helpers
     def _sync(self):
@@ -133,6 +142,17 @@ class Trainer:
         t = torch.tensor([x], dtype=torch.float64, device=self.device)
         dist.all_reduce(t)
         return t.item() / self.world_size
+
+    def _flush_tokens(self):
+        """Add every rank's tokens since the last flush to ``tokens_seen`` (one int64 SUM
+        all-reduce; called at the same steps on all ranks: eval points and checkpoint saves)."""
+        n = self._tokens_pending
+        self._tokens_pending = 0
+        if self._dist():
+            t = torch.tensor([n], dtype=torch.int64, device=self.device)
+            dist.all_reduce(t)
+            n = int(t.item())
+        self.tokens_seen += n
 
     def lr_at(self, step: int) -> float:
         if step < self.warmup_steps:
@@ -169,6 +189,32 @@ class Trainer:
                 logger.info(f"profiler trace written: {path}")
             self._prof = None
 
+    def _order_check(self):
+        """The collective-order checker for this step (None when not distributed or past warm-up)."""
+        if not self._dist() or self.global_step > self.comm_adapt_steps:
+            return None
+        if self._seq is None:
+            from ..parallel.seqcheck import CollectiveSequence
+            self._seq = CollectiveSequence(timeout_s=self._seq_timeout_s)
+        return self._seq
+
+    def _step_body(self, input_batch, target_batch):
+        loss = self.calc_loss_batch(input_batch, target_batch)
+        if self.loss_scaler is not None:
+            (loss * self.loss_scaler.scale).backward()
+            inv = torch.tensor([1.0 / self.loss_scaler.scale], device=self.device)
+            norm = self.optimizer.clip_grad_norm_(self.max_grad_norm, extra_scale=inv)
+            overflow = not bool(torch.isfinite(norm).item())
+            if self.loss_scaler.update(overflow):
+                self.optimizer.step()
+            elif self.rank == 0:
+                logger.warning(f"fp16 overflow at step {self.global_step}; loss scale -> {self.loss_scaler.scale}")
+        else:
+            loss.backward()
+            self.optimizer.clip_grad_norm_(self.max_grad_norm)
+            self.optimizer.step()
+        return loss
+
     def train_batch(self, input_batch, target_batch):
         self.optimizer.zero_grad()
         self.global_step += 1
@@ -188,21 +234,21 @@ class Trainer:
             # the fused head takes the logit gradient inside its forward: tell it the dloss that
             # backward will bring, so fp16 softmax tails are scaled before they are rounded
             rc.loss_scale = float(self.loss_scaler.scale)
-        loss = self.calc_loss_batch(input_batch, target_batch)
-        if self.loss_scaler is not None:
-            (loss * self.loss_scaler.scale).backward()
-            inv = torch.tensor([1.0 / self.loss_scaler.scale], device=self.device)
-            norm = self.optimizer.clip_grad_norm_(self.max_grad_norm, extra_scale=inv)
-            overflow = not bool(torch.isfinite(norm).item())
-            if self.loss_scaler.update(overflow):
-                self.optimizer.step()
-            elif self.rank == 0:
-                logger.warning(f"fp16 overflow at step {self.global_step}; loss scale -> {self.loss_scaler.scale}")
+        # warm-up steps 0..comm_adapt_steps: the step's collectives are recorded and compared
+        # across ranks right after they are issued (parallel/seqcheck.py) -- a divergent order
+        # raises naming the first differing call instead of hanging until the PG timeout
+        seq = self._order_check()
+        with seq.recording(f"step{self.global_step}") if seq is not None else contextlib.nullcontext():
+            loss = self._step_body(input_batch, target_batch)
+        if seq is not None:
+            seq.verify(f"step{self.global_step}")
+        # this rank's own count (reference train.py:123 counts per rank); padded instruction
+        # batches differ in length across ranks, so the node total is an exact sum
+        # (_flush_tokens) at every eval / checkpoint point, never numel x world_size
+        if self.count_target_tokens:
+            self._tokens_pending += int((target_batch != IGNORE_INDEX).sum())
         else:
-            loss.backward()
-            self.optimizer.clip_grad_norm_(self.max_grad_norm)
-            self.optimizer.step()
-        self.tokens_seen += input_batch.numel() * self.world_size
+            self._tokens_pending += input_batch.numel()
         if adapting:
             self._sync()
             rec = self.engine.adapt(1e3 * (time.perf_counter() - t_step))
@@ -262,6 +308,7 @@ class Trainer:
                 now = time.perf_counter()
                 if not math.isfinite(lv):
                     raise FloatingPointError(f"non-finite training loss at step {self.global_step}")
+                self._flush_tokens()
                 train_loss, val_loss = self.evaluate_model(train_loader, val_loader, self.eval_iter)
                 self.train_losses.append(train_loss)
                 self.val_losses.append(val_loss)
@@ -360,9 +407,11 @@ class Trainer:
         return self._loop(n_epochs, lambda fp: read_text_file(fp) + " " + eos + " ", "Every effort moves you")
 
     def finetune_model(self, n_epochs):
+        self.count_target_tokens = True   # padded instruction batches: count real targets
         return self._loop(n_epochs, read_json_file, ALPACA_CONTEXT)
 
     def _results(self):
+        self._flush_tokens()
         return self.train_losses, self.val_losses, self.track_tokens_seen, self.track_lrs
 
     # ------------------------------------------------------------------ eval / sample / ckpt
@@ -380,6 +429,7 @@ class Trainer:
         return decoded
 
     def save_checkpoint(self, file_name):
+        self._flush_tokens()   # the resume state carries the exact all-rank count
         if self._dist():
             dist.barrier()
         path = self.save_dir / file_name

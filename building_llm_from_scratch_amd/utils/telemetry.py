@@ -211,3 +211,46 @@ def tunableop_status(path: Optional[str]) -> Optional[Dict[str, Any]]:
         out["validators_match"] = None
         out["error"] = type(e).__name__
     return out
+
+
+def rccl_debug_env(rank: int, directory: Optional[str] = None) -> Optional[str]:
+    """Ask RCCL to log its init-time topology decisions (``NCCL_DEBUG=INFO``, subsystems INIT and
+    GRAPH only: no per-collective lines) to a per-rank file; returns the path.  Must run before
+    the process group is created.  Leaves a user's own NCCL_DEBUG settings alone."""
+    import os
+    import tempfile
+    if "NCCL_DEBUG" in os.environ:
+        return os.environ.get("NCCL_DEBUG_FILE")
+    path = os.path.join(directory or tempfile.gettempdir(), f"bllm_rccl_{os.getuid()}_{os.getpid()}_r{rank}.log")
+    os.environ.update(NCCL_DEBUG="INFO", NCCL_DEBUG_SUBSYS="INIT,GRAPH", NCCL_DEBUG_FILE=path)
+    return path
+
+
+def rccl_topology(path: Optional[str], max_lines: int = 24) -> Optional[Dict[str, Any]]:
+    """What RCCL chose at init, from its INIT/GRAPH log: ranks / nodes, the channel counts per
+    kind, the ring and tree orders of the first channels, and the algorithm/protocol threshold
+    lines (the per-collective choice RCCL's tuner makes from them)."""
+    import os
+    import re
+    if not path or not os.path.exists(path):
+        return None
+    lines = [ln.rstrip() for ln in open(path, errors="replace") if "NCCL INFO" in ln]
+    out: Dict[str, Any] = {"log": path, "lines": len(lines)}
+    keep = []
+    for ln in lines:
+        msg = ln.split("NCCL INFO", 1)[1].strip()
+        m = re.search(r"nRanks (\d+) nNodes (\d+) localRanks (\d+)", msg)
+        if m:
+            out.update(n_ranks=int(m.group(1)), n_nodes=int(m.group(2)), local_ranks=int(m.group(3)))
+        m = re.search(r"(\d+) coll channels, (?:(\d+) collnet channels, )?(?:(\d+) nvls channels, )?(\d+) p2p channels", msg)
+        if m:
+            out.update(coll_channels=int(m.group(1)), p2p_channels=int(m.group(4)))
+        if re.match(r"Channel \d+/\d+ :", msg):
+            out["channels"] = max(out.get("channels", 0), int(msg.split()[1].split("/")[1]))
+            if len(out.setdefault("rings", [])) < 4:
+                out["rings"].append(msg)
+        elif re.search(r"Trees|Tree \d|threadThresholds|Algo|algorithm|Protocol|Usable|Connected all|NET/|P2P|xGMI|XGMI",
+                       msg) and len(keep) < max_lines:
+            keep.append(msg)
+    out["decisions"] = keep
+    return out

@@ -83,6 +83,13 @@ def test_bench_headline_path_world2_one_gpu_matches_world1():
     for kind in ("all_gather", "reduce_scatter"):
         assert bw[kind]["count"] > 0 and bw[kind]["algbw_gbps"] > 0, bw
         assert bw[kind]["timing"] == "rccl events", bw
+    # warm-up collectives compared across ranks (parallel/seqcheck.py): the gloo pair and the
+    # forced RCCL path both checked something; RCCL's init-time choices are in the JSON
+    assert two["comm"]["order_check"]["enabled"] and two["comm"]["order_check"]["calls_checked_rank0"] > 0
+    assert forced["comm"]["order_check"]["calls_checked_rank0"] > 0, forced["comm"]
+    topo = forced["rccl_topology"]
+    assert topo is not None and topo["lines"] > 0, topo
+    assert topo.get("n_ranks") == 1, topo
     os.makedirs("gpurun_out", exist_ok=True)
     with open(os.path.join("gpurun_out", "bench_world2_one_gpu.json"), "w") as f:
         json.dump({"world1": one, "world2_one_gpu": two, "world1_forced_comm": forced}, f, indent=1)
