@@ -118,6 +118,9 @@ def parse(argv=None):
                     help="FSDP units all-gathered ahead (0 = auto: gather time over xGMI vs unit compute)")
     ap.add_argument("--layers", type=int, default=None, help="(debug only) override n_layers; invalidates the metric")
     ap.add_argument("--profile", action="store_true", help="print a per-phase timing breakdown to stderr")
+    ap.add_argument("--gemm_epilogues", action="store_true",
+                    help="gate/up + SwiGLU, QKV + RoPE, c_fc + bias + GELU on csrc/gemm_nt.hip's fused-epilogue "
+                         "kernel instead of the library GEMM + a separate pass (measured slower, A/B)")
     ap.add_argument("--overlap_optimizer", action="store_true",
                     help="run AdamW on a side HIP stream under the next forward")
     ap.add_argument("--data", default=None, choices=["pretrain", "random_ids", "fixed_ids", "alpaca"],
@@ -358,6 +361,9 @@ def main(argv=None):
     sync = torch.cuda.synchronize if cuda else (lambda: None)
 
     cfg = build_config(a, dev)
+    if a.gemm_epilogues:
+        from building_llm_from_scratch_amd.models.linear import use_gemm_epilogues
+        use_gemm_epilogues(True)
     torch.manual_seed(123)
     plan = None
     ckpt_mode = "selective" if a.actv_ckpt == "auto" else a.actv_ckpt
@@ -436,6 +442,22 @@ def main(argv=None):
     probe_peak = None
     comm = getattr(engine, "comm", None)
     adapt_hist = []
+    reprobe = False
+
+    def reprobe_plan(prev):
+        """The last step's measured peak (max over ranks) against the checkpoint plan; adds fully
+        recomputed blocks if it was over budget.  Returns the peak."""
+        nonlocal plan
+        sync()
+        pk = torch.tensor([float(torch.cuda.max_memory_allocated(dev))], device=dev)
+        dist.all_reduce(pk, op=dist.ReduceOp.MAX)
+        new = memplan.replan_after_probe(plan, cfg, B, T, pk.item(),
+                                         elt=torch.empty((), dtype=cfg.dtype).element_size())
+        if new is not plan:
+            plan = new
+            model.set_block_modes(plan.modes)
+            torch.cuda.reset_peak_memory_stats(dev)
+        return pk.item() if prev is None else max(prev, pk.item())
     # every warm-up step's collectives (op, bytes, dtype) compared across ranks over the
     # rendezvous store right after the step is issued, before anything waits on them: a divergent
     # order raises naming the first differing call instead of hanging until the PG timeout
@@ -452,23 +474,20 @@ def main(argv=None):
         seq_checked += seq.verify(f"warmup{i}")
         if i == 0 and plan is not None and cuda:
             # memory probe: the first step's measured peak (max over ranks) checks the plan
-            sync()
-            pk = torch.tensor([float(torch.cuda.max_memory_allocated(dev))], device=dev)
-            dist.all_reduce(pk, op=dist.ReduceOp.MAX)
-            probe_peak = pk.item()
-            new = memplan.replan_after_probe(plan, cfg, B, T, probe_peak,
-                                             elt=torch.empty((), dtype=cfg.dtype).element_size())
-            if new is not plan:
-                plan = new
-                model.set_block_modes(plan.modes)
-                torch.cuda.reset_peak_memory_stats(dev)
+            probe_peak = reprobe_plan(probe_peak)
         # warm-up adaptation (after the cold first step): FSDP prefetch depth / DDP bucket
         # size grown while a collective wait shows in the step (MAX over ranks, parallel/)
         if i >= 1 and hasattr(engine, "adapt"):
             sync()
+            if reprobe:   # the step after a prefetch change: its peak checks the plan again
+                probe_peak = reprobe_plan(probe_peak)
+                reprobe = False
             rec = engine.adapt(1e3 * (time.perf_counter() - tw))
             if rec is not None:
                 adapt_hist.append(rec)
+                if plan is not None and cuda and any(k.endswith("_new") for k in rec):
+                    torch.cuda.reset_peak_memory_stats(dev)
+                    reprobe = True
     sync()
     dist.barrier()
     sync()
@@ -590,6 +609,7 @@ def main(argv=None):
                 "optimizer": "AdamW fp32 master, wd 0.1, clip 1.0",
                 "gemm_tuning": (os.path.relpath(a.tunableop, os.path.dirname(os.path.abspath(__file__)))
                                 if a.tunableop else None),
+                "gemm_epilogues": bool(a.gemm_epilogues),
             },
             "mfu": round(mfu, 4),
             "hfu": round(mfu * recompute, 4),

@@ -43,6 +43,12 @@ def perform_checks(args):
         raise EnvironmentError("FSDP requires GPU devices (or --backend gloo for CPU testing).")
     if not args.use_fsdp and args.mixed_precision:
         raise ValueError("Mixed precision can only be enabled with FSDP.")
+    if getattr(args, "actv_ckpt_mode", None) == "auto" and getattr(args, "actv_ckpt_segments", None):
+        # the planner's per-block modes ARE the segmentation; a segment count would replace them
+        # with plain selective checkpointing while the log and the first-step probe still
+        # reasoned about the plan
+        raise ValueError("--actv_ckpt_mode auto chooses the recomputed blocks itself; "
+                         "it cannot be combined with --actv_ckpt_segments.")
 
 
 def build_parser() -> argparse.ArgumentParser:
@@ -86,6 +92,9 @@ def build_parser() -> argparse.ArgumentParser:
                         "measured peak) -- the headline bench's policy")
     x.add_argument("--ckpt_budget_gib", type=float, default=None,
                    help="auto mode: per-rank peak-memory ceiling (default 250 GiB, capped at device - 18 GiB)")
+    x.add_argument("--gemm_epilogues", action="store_true",
+                   help="gate/up + SwiGLU, QKV + RoPE and c_fc + bias + GELU on the fused-epilogue GEMM kernel "
+                        "(csrc/gemm_nt.hip) instead of the library GEMM + a separate pass; measured slower on MI355X")
     x.add_argument("--actv_ckpt_segments", type=int, default=None,
                    help="full mode: checkpoint_sequential segments (default n_layers = reference); "
                         "fewer segments recompute fewer blocks for more memory")

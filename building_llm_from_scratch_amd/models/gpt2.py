@@ -16,7 +16,6 @@ in-kernel dropout[HIP MFMA] -> out-proj GEMM (+bias) -> dropout+residual[HIP] ->
 """
 from __future__ import annotations
 
-import os
 
 import torch
 import torch.nn as nn
@@ -113,11 +112,11 @@ def _ln_bwd(unit, norm, dy, x, mean, rstd, dx_acc, acc):
 # bias gradients ride along in the dropout / GELU backward passes (ops.*_bwd_bias); tests set
 # this to False to check them against the separate column-sum pass
 FUSED_BIAS = True
-# BLLM_RECOMPUTE_FUSED=0: the checkpoint recompute runs its GELU forward as a separate pass (A/B)
-RECOMPUTE_FUSED = os.environ.get("BLLM_RECOMPUTE_FUSED", "1") != "0"
+# False: the checkpoint recompute runs its GELU forward as a separate pass (A/B)
+RECOMPUTE_FUSED = True
 # the attention residual's dropout-add and norm2 as one row pass (ops.dropout_add_layernorm, bitwise
-# the two kernels); BLLM_FUSED_LN_DROPOUT=0: separate passes (A/B, profiles/r5/ln_dropout/)
-FUSED_LN_DROPOUT = os.environ.get("BLLM_FUSED_LN_DROPOUT", "1") != "0"
+# the two kernels); False: separate passes (A/B, profiles/r5/ln_dropout/)
+FUSED_LN_DROPOUT = True
 
 
 def _drop_bwd_bias(lin, dy, p, seed, offset, acc):

@@ -23,7 +23,6 @@ hipBLASLt GEMMs.
 """
 from __future__ import annotations
 
-import os
 from dataclasses import dataclass
 from typing import List, Optional, Sequence
 
@@ -126,13 +125,13 @@ def _dgrad_wt_ok(dy: torch.Tensor, W: torch.Tensor) -> bool:
 
 
 # The forward-layout GEMMs (y = x W^T, dX on the transposed weight copy, the fused head's logits
-# and dh).  BLLM_GEMM_NT: 0 = hipBLASLt / rocBLAS (default), 1 = csrc/gemm_nt.hip's persistent
-# kernel wherever its shape rules hold (an A/B switch).  Round 5 measured the library GEMMs
+# and dh).  GEMM_NT False = hipBLASLt / rocBLAS (default), True = csrc/gemm_nt.hip's persistent
+# kernel wherever its shape rules hold (tests / A/B).  Round 5 measured the library GEMMs
 # (TunableOp-picked per shape) 3-12 % faster on every Llama-3-8B and GPT-2 projection, and the
 # epilogue fusions built on this kernel lost end to end (profiles/r5/fused_epilogues_ab.md).  A
 # per-shape timed pick ("auto") was removed: a lazily timed pick differs between ranks whose
 # batch shapes differ, and settling it needed a collective inside a cache miss.
-GEMM_NT = os.environ.get("BLLM_GEMM_NT", "0") == "1"
+GEMM_NT = False
 
 
 def nt_choice(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None) -> bool:
@@ -181,12 +180,22 @@ def _input_grad(dy: torch.Tensor, W: torch.Tensor, dx_acc: Optional[torch.Tensor
 
 # tests set this to drive the grouped LoRA path through the CPU oracles of ops.reference
 FORCE_GROUPED_LORA = False
-# gate/up GEMM + SwiGLU epilogue (FusedLinear.forward_swiglu) and QKV GEMM + RoPE epilogue
-# (FusedLinear.forward_rope), both on csrc/gemm_nt.hip's persistent 4-wave kernel
-FUSED_SWIGLU = os.environ.get("BLLM_FUSED_SWIGLU", "0") != "0"
-FUSED_ROPE = os.environ.get("BLLM_FUSED_ROPE", "0") != "0"
-# GPT-2 c_fc GEMM + bias + GELU epilogue (FusedLinear.forward_bias_gelu)
-FUSED_GELU = os.environ.get("BLLM_FUSED_GELU", "0") != "0"
+LORA_KAUG = True   # zero-copy K-augmented LoRA projections (FusedLinear.forward_kaug)
+# The forward epilogue fusions on csrc/gemm_nt.hip's persistent 4-wave kernel: gate/up GEMM +
+# SwiGLU (FusedLinear.forward_swiglu), QKV GEMM + RoPE (forward_rope), GPT-2 c_fc GEMM + bias +
+# GELU (forward_bias_gelu).  Off by default: the HBM pass each removes is worth less than what the
+# kernel gives up against the TunableOp-picked library GEMM on MI355X (-0.8 / -0.17 / -3.8 % end
+# to end, profiles/r5/fused_epilogues_ab.md).  ``use_gemm_epilogues(True)`` (CLI / bench
+# ``--gemm_epilogues``) turns all three on.
+FUSED_SWIGLU = False
+FUSED_ROPE = False
+FUSED_GELU = False
+
+
+def use_gemm_epilogues(on: bool) -> None:
+    """Route the gate/up, QKV and c_fc projections through the fused-epilogue kernels."""
+    global FUSED_SWIGLU, FUSED_ROPE, FUSED_GELU
+    FUSED_SWIGLU = FUSED_ROPE = FUSED_GELU = bool(on)
 
 
 class FusedLinear:
@@ -238,11 +247,12 @@ class FusedLinear:
         """K-augmented LoRA (see forward_kaug) needs a frozen, bias-free base weight that is not
         sharded: the persistent [W | Bd^T] / [W^T ; Bd] copies would keep a full unsharded frozen
         weight per rank under a sharding FSDP engine (Llama-3-8B gate/up: ~7.5 GB regardless of
-        world size) and would be rebuilt after every re-gather.  BLLM_LORA_KAUG=0 turns it off."""
+        world size) and would be rebuilt after every re-gather.  ``LORA_KAUG = False`` turns it off
+        (tests / A/B)."""
         return (self.has_lora and self.b_params is None
                 and not self.unit.trainable(self.W_params[0])
                 and not self.unit.state.get("sharded", False)
-                and os.environ.get("BLLM_LORA_KAUG", "1") != "0")
+                and LORA_KAUG)
 
     def kaug_input(self, like: torch.Tensor, K: int) -> Optional[torch.Tensor]:
         """An [N, K + R] buffer for a zero-copy K-augmented forward, or None: the caller's
@@ -349,7 +359,7 @@ class FusedLinear:
     def forward_swiglu(self, x: torch.Tensor):
         """Gate/up projection with the SwiGLU forward in the GEMM epilogue (``[fc1; fc2]``, no
         bias, no LoRA): returns ``(gu, act)`` or None when the fused kernel does not apply
-        (csrc/gemm_nt.hip; BLLM_FUSED_SWIGLU=0 turns it off)."""
+        (csrc/gemm_nt.hip; only with ``use_gemm_epilogues(True)``)."""
         if self.has_lora or self.b_params is not None or len(self.specs) != 2 or not FUSED_SWIGLU:
             return None
         W = self.W()
@@ -360,7 +370,7 @@ class FusedLinear:
     def forward_bias_gelu(self, x: torch.Tensor):
         """c_fc with its bias and the exact GELU in the GEMM epilogue (K9; no LoRA): returns
         ``(f, g)`` = (pre-activation, activation) or None when the fused kernel does not apply
-        (BLLM_FUSED_GELU=0 turns it off) and the caller runs the GEMM + ``gelu_fwd``."""
+        (only with ``use_gemm_epilogues(True)``) and the caller runs the GEMM + ``gelu_fwd``."""
         if self.has_lora or self.b_params is None or not FUSED_GELU:
             return None
         W, b = self.W(), self.b()
@@ -371,7 +381,7 @@ class FusedLinear:
     def forward_rope(self, x: torch.Tensor, cos, sin, T: int, H: int, G: int, hd: int):
         """QKV projection with RoPE applied to the q and k heads in the GEMM epilogue (K4; no bias,
         no LoRA): returns the rotated qkv, or None when the fused kernel does not apply (head dim
-        128 only; BLLM_FUSED_ROPE=0 turns it off) and the caller runs the GEMM + ``rope_``."""
+        128 only; only with ``use_gemm_epilogues(True)``) and the caller runs the GEMM + ``rope_``."""
         if self.has_lora or self.b_params is not None or not FUSED_ROPE:
             return None
         W = self.W()

@@ -323,8 +323,8 @@ class LlamaBlockCompute(UnitCompute):
         return dx.view(B, T, d)
 
 
-# BLLM_LORA_SWIGLU_WGRAD=0: the gate/up dB and down dA of a LoRA MLP as separate lora_wgrad passes (A/B)
-LORA_SWIGLU_WGRAD = os.environ.get("BLLM_LORA_SWIGLU_WGRAD", "1") != "0"
+# False: the gate/up dB and down dA of a LoRA MLP as separate lora_wgrad passes (A/B)
+LORA_SWIGLU_WGRAD = True
 
 
 def _compact_kaug(xa):
@@ -334,8 +334,8 @@ def _compact_kaug(xa):
     return xa
 
 
-# BLLM_RECOMPUTE_FUSED=0: the checkpoint recompute runs its SwiGLU forward as a separate pass (A/B)
-RECOMPUTE_FUSED = os.environ.get("BLLM_RECOMPUTE_FUSED", "1") != "0"
+# False: the checkpoint recompute runs its SwiGLU forward as a separate pass (A/B)
+RECOMPUTE_FUSED = True
 
 # logits chunk budget of the fused head + CE (bytes of one [rows, V] chunk)
 LOGIT_CHUNK_BYTES = int(os.environ.get("BLLM_LOGIT_CHUNK_MB", "2048")) * 2 ** 20
@@ -470,7 +470,7 @@ class HeadComputeMixin:
         V = 128k, tools/bench_head_k.py); u = dl B^T is a skinny hipBLASLt GEMM over each dlogits
         chunk (355 us vs 610 us for lora_down, tools/bench_head_u.py), dB = (s t)^T dl runs on
         lora_wgrad, then dh = dh_W + s u A^T and dA = s h^T u on the LoRA kernels.  With
-        BLLM_LORA_HEAD_FUSED (default) u and dB come from one kernel reading each dl chunk once
+        ops.LORA_HEAD_FUSED (default) u and dB come from one kernel reading each dl chunk once
         (``ops.lora_head_bwd_``)."""
         hd, u_ = self.head, self.head.unit
         spec = hd.specs[0]

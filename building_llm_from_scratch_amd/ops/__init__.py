@@ -246,9 +246,13 @@ def bias_grad_(dy, db, accumulate: bool = False):
 WGRAD_TILE, WGRAD_KGRAN = 256, 128
 
 
+# weight gradients on the token-major MFMA dW kernel (1.28-1.44 PF vs hipBLASLt's 0.96-1.17 on
+# that layout, profiles/r5/gemm_pmc/README.md); False routes them to hipBLASLt (tests / A/B)
+WGRAD_GEMM = True
+
+
 def wgrad_gemm_enabled() -> bool:
-    """``BLLM_WGRAD_GEMM=0`` routes weight gradients back to hipBLASLt (A/B measurements)."""
-    return os.environ.get("BLLM_WGRAD_GEMM", "1") != "0"
+    return WGRAD_GEMM
 
 
 def wgrad_gemm_ok(a: torch.Tensor, b: torch.Tensor, c: torch.Tensor) -> bool:
@@ -296,8 +300,8 @@ def wgrad_splits(M: int, N: int, K: int, n_cu: int = 256) -> int:
     return best
 
 
-# BLLM_WGRAD_TAIL=0: a ragged last wave is always handled by splitting every tile (A/B)
-WGRAD_TAIL = os.environ.get("BLLM_WGRAD_TAIL", "1") != "0"
+# False: a ragged last wave is always handled by splitting every tile (A/B only)
+WGRAD_TAIL = True
 
 
 def wgrad_plan(M: int, N: int, K: int, n_cu: int = 256):
@@ -345,21 +349,24 @@ def wgrad_gemm_(a, b, c, accumulate: bool = False, splits: Optional[int] = None)
     return c
 
 
+# input gradients (dX = dY W) on the MFMA kernel (``gemm_nn_``) instead of hipBLASLt: off, measured
+# at parity on the benchmark shapes (0.95-1.05x, tools/bench_dgrad.py, profiles/r1_wgrad_kernel.md)
+# -- hipBLASLt's dX family is already at 1.25-1.38 PF, unlike its dW family the kernel was written
+# for.  The kernel stays a public op (``gemm_nn_``); tests flip this to route the backward through it.
+DGRAD_GEMM = False
+
+
 def dgrad_gemm_enabled() -> bool:
-    """``BLLM_DGRAD_GEMM=1`` routes input gradients (dX = dY W) through the MFMA kernel
-    (``gemm_nn_``).  Off by default: measured at parity with hipBLASLt on the benchmark shapes
-    (0.95-1.05x, tools/bench_dgrad.py, profiles/r1_wgrad_kernel.md) — hipBLASLt's dX family is
-    already at 1.25-1.38 PF, unlike its dW family the kernel was written for."""
-    return os.environ.get("BLLM_DGRAD_GEMM", "0") == "1"
+    return DGRAD_GEMM
 
 
-_LT_RESIDUAL = os.environ.get("BLLM_LT_RESIDUAL", "1") != "0"
+_LT_RESIDUAL = True   # False: torch.addmm instead of the C != D hipBLASLt epilogue (tests / A/B)
 
 
 def linear_residual(x: torch.Tensor, W: torch.Tensor, C: torch.Tensor) -> torch.Tensor:
     """``C + x @ W^T`` as one hipBLASLt matmul that reads C in its epilogue and writes a new D
     (csrc/binding.cpp linear_residual).  ``torch.addmm(C, x, W.t())`` copies C into the output
-    first (one extra HBM pass of C).  BLLM_LT_RESIDUAL=0 selects torch.addmm (A/B)."""
+    first (one extra HBM pass of C)."""
     if (_LT_RESIDUAL and _hip(x) and x.dtype in (torch.bfloat16, torch.float16) and W.dtype == x.dtype
             and C.dtype == x.dtype and x.is_contiguous() and W.is_contiguous() and C.is_contiguous()):
         return _k().linear_residual(x, W, C)
@@ -374,12 +381,14 @@ def transpose2d(a: torch.Tensor) -> torch.Tensor:
     return a.t().contiguous()
 
 
+# large input-gradient GEMMs dX = dY W first transpose W into a scratch copy so hipBLASLt runs
+# dX = dY (W^T)^T with both operands K-contiguous -- the same fast layout as the forward x W^T
+# (tools/bench_gemm.py: 1.52-1.59 PF vs 1.30-1.38 PF for the dY W layout)
+DGRAD_WT = True
+
+
 def dgrad_wt_enabled() -> bool:
-    """``BLLM_DGRAD_WT`` (default on): large input-gradient GEMMs dX = dY W first transpose W
-    into a scratch copy so hipBLASLt runs dX = dY (W^T)^T with both operands K-contiguous —
-    the same fast layout as the forward x W^T (tools/bench_gemm.py: 1.52-1.59 PF vs 1.30-1.38
-    PF for the dY W layout)."""
-    return os.environ.get("BLLM_DGRAD_WT", "1") == "1"
+    return DGRAD_WT
 
 
 def gemm_nn_ok(a: torch.Tensor, b: torch.Tensor, c: Optional[torch.Tensor] = None) -> bool:
@@ -523,7 +532,7 @@ def attn_decode(q, kcache, vcache, L: int):
 
 
 def flash_attn_bwd(qkv, o, lse, do, B, T, H, G, hd, causal=True, dropout_p=0.0, seed=0, offset=0,
-                   keep_mask=None, rope=None):
+                   keep_mask=None, rope=None, store_ds=False):
     """``keep_mask``: the buffer the matching forward filled (``attn_keep_mask``), or None to
     regenerate the dropout bits from the counter hash (identical result).  ``rope``: the
     (cos, sin) tables the forward rotated q/k with; the returned dq/dk are then already
@@ -532,7 +541,7 @@ def flash_attn_bwd(qkv, o, lse, do, B, T, H, G, hd, causal=True, dropout_p=0.0, 
         load_ext(required=True)
         rc, rs = rope if rope is not None else (None, None)
         return _k().flash_attn_bwd(qkv, o, lse, do, B, T, H, G, hd, causal, float(dropout_p),
-                                   int(seed), int(offset), keep_mask, rc, rs)
+                                   int(seed), int(offset), keep_mask, rc, rs, bool(store_ds))
     dqkv = ref.flash_attn_bwd(qkv, o, lse, do, B, T, H, G, hd, causal, dropout_p, seed, offset)
     if rope is not None:
         ref.rope_(dqkv, rope[0], rope[1], T, H, G, hd, inverse=True)
@@ -709,7 +718,7 @@ def lora_wgrad(p, q, gs, pa, qb, scale: float, accumulate: bool = False):
     ref.lora_wgrad(p, q, gs, pa, qb, scale, accumulate)
 
 
-LORA_HEAD_FUSED = os.environ.get("BLLM_LORA_HEAD_FUSED", "1") != "0"
+LORA_HEAD_FUSED = True   # the LoRA head's u and dB in one pass over each dlogits chunk
 
 
 def lora_head_bwd_ok(V: int, r: int) -> bool:

@@ -36,8 +36,19 @@ IGNORE_INDEX = -100   # the instruction collate's masked-target id (data/dataset
 
 logger = setup_logger("train")
 
-# data files whose loaders the trainer keeps across epochs (read / tokenised / workers forked once)
-MAX_CACHED_FILES = 4
+# loaders are kept across epochs (read / tokenised / workers forked once) only for a one-file run:
+# with several files, every file's dataset, persistent workers and prefetched batches would stay
+# resident for the whole run; those runs rebuild a file's loaders per epoch and shut the previous
+# file's workers down as soon as it is done
+MAX_CACHED_FILES = 1
+
+
+def _shutdown_loader(loader):
+    """Stop a DataLoader's persistent worker processes now instead of at garbage collection."""
+    it = getattr(loader, "_iterator", None)
+    if it is not None and hasattr(it, "_shutdown_workers"):
+        it._shutdown_workers()
+    loader._iterator = None
 
 ALPACA_CONTEXT = ("Below is an instruction that describes a task. Write a response that appropriately "
                   "completes the request.\n\n### Instruction:\nWhat is an antonym of 'complicated'?")
@@ -253,9 +264,15 @@ class Trainer:
             self._sync()
             rec = self.engine.adapt(1e3 * (time.perf_counter() - t_step))
             self.engine.comm.enabled = False
-            if rec is not None and self.rank == 0 and any(k.endswith("_new") for k in rec):
-                logger.info(f"comm adaptation at step {self.global_step}: {rec}")
-        if not self._probed:
+            if rec is not None and any(k.endswith("_new") for k in rec):
+                if self.rank == 0:
+                    logger.info(f"comm adaptation at step {self.global_step}: {rec}")
+                # a deeper FSDP prefetch holds more gathered units than the checkpoint plan was
+                # sized for (prefetch 2): measure the next step's peak and re-plan against it
+                if getattr(self.model, "ckpt_plan", None) is not None and torch.device(self.device).type == "cuda":
+                    torch.cuda.reset_peak_memory_stats(self.device)
+                    self._probed = False
+        if not self._probed and not adapting:
             self._probed = True
             self._probe_ckpt_plan()
         return loss
@@ -394,6 +411,10 @@ class Trainer:
                         train_loader.sampler.set_epoch(epoch)
                     self.train_epoch(epoch, train_loader, val_loader, start_context=start_context,
                                      file_index=fi, skip_batches=skip)
+                    if fi not in self._loaders:
+                        _shutdown_loader(train_loader)
+                        _shutdown_loader(val_loader)
+                        del train_loader, val_loader
                     if pbar is not None:
                         pbar.update(1)
                     if self.stop:
@@ -443,11 +464,17 @@ class Trainer:
             dist.barrier()
 
     _STATE_KEYS = ("global_step", "tokens_seen", "train_losses", "val_losses", "track_lrs", "track_tokens_seen")
+    # batch order for a given (seed, epoch, file): 2 = the shuffle drawn straight from the
+    # per-(epoch, file) generator by RandomSampler, worker seeds from a fixed generator
+    # (data/loaders.py); states without it were written by builds that drew the worker base seed
+    # from that generator first, so their skip-ahead replays a different order
+    DATA_ORDER_VERSION = 2
 
     def trainer_state(self) -> dict:
         st = {k: getattr(self, k) for k in self._STATE_KEYS}
         rc = self.model.rctx
         st.update(pos=list(self.pos), rng_seed=int(rc.seed), rng_offset=int(rc._offset),
+                  data_order_version=self.DATA_ORDER_VERSION,
                   loss_scale=(self.loss_scaler.scale if self.loss_scaler else None),
                   loss_scale_clean=(self.loss_scaler.clean if self.loss_scaler else None))
         return st
@@ -456,6 +483,10 @@ class Trainer:
         for k in self._STATE_KEYS:
             setattr(self, k, st[k])
         if "pos" in st:
+            if st.get("data_order_version") != self.DATA_ORDER_VERSION and self.rank == 0:
+                logger.warning(f"resume state has data-order version {st.get('data_order_version')} "
+                               f"(this build: {self.DATA_ORDER_VERSION}): the batches after the resume "
+                               "point follow this build's shuffle, not the interrupted run's")
             self.pos = tuple(st["pos"])
             self._resume_pos = self.pos
             rc = self.model.rctx

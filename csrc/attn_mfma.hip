@@ -83,7 +83,7 @@ template <typename T> __device__ __forceinline__ uint32_t pack2(float a, float b
 // per-lane offsets, 2x(LD) saddr DMA issues with precomputed per-lane source offsets, and
 // ~130 VALU of online softmax (scale folded into the exp2 FMA; the O rescale is skipped when
 // no lane's running max moved, which is the common case after the first tiles).
-template <typename T, int HD, bool DROP, int FWD_BK, int NBUF, int OCC>
+template <typename T, int HD, bool DROP, int FWD_BK, int NBUF, int OCC, bool PIPE = false>
 __global__ __launch_bounds__(256, OCC) void attn_fwd_mfma_k(const T* __restrict__ qkv, T* __restrict__ out,
                                                           float* __restrict__ lse, int T_, int H, int G, int B_,
                                                           bool causal, uint32_t thr, float inv_keep, uint64_t seed,
@@ -178,6 +178,9 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd_mfma_k(const T* __restrict_
     vc16 = c64 * 4 + (pc & 3);
   };
   const uint32_t smem_u = lds_u32(smem);
+  // K / V bases in SGPRs once (the per-piece row offsets are then scalar arithmetic)
+  const char* ksb = (const char*)sgpr_ptr(kbase);
+  const char* vsb = (const char*)sgpr_ptr(vbase);
 
   const int kend = causal ? min(T_, q0 + BQ) : T_;
   const int ntiles = (kend + FWD_BK - 1) / FWD_BK;
@@ -191,7 +194,31 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd_mfma_k(const T* __restrict_
     const uint32_t base = smem_u + buf * 2 * TILE_B;
     int ln = lane;
     asm volatile("" : "+v"(ln));
-    if (k0 + FWD_BK <= T_) {
+    if (PIPE && k0 + FWD_BK <= T_) {
+      // piece i of lane ln: row rb_i + lr (rb_i = (w LD + i) 64 / CH, wave-uniform, folded into the
+      // SGPR base), chunk pc = ln % CH; unsigned shifts, and the V chunk does not depend on i
+      const uint32_t lr = (uint32_t)ln / CH, pc = (uint32_t)ln % CH;
+      const uint32_t lro = lr * rs2;
+#pragma unroll
+      for (int i = 0; i < LD; ++i) {
+        const int rb = (w * LD + i) * (64 / CH);
+        const uint32_t r = (uint32_t)rb + lr;
+        uint32_t kc16, c64;
+        if constexpr (HD == 128) {
+          kc16 = pc ^ (r & 15u);
+          c64 = (pc >> 2) ^ (r & 3u);
+        } else {
+          kc16 = pc ^ ((r >> 1) & 7u);
+          c64 = (pc >> 2) ^ ((r >> 1) & 1u);
+        }
+        const uint32_t vc16 = c64 * 4u + (pc & 3u);
+        const void* ks = ksb + (long)(k0 + rb) * rs2;
+        const void* vs = vsb + (long)(k0 + rb) * rs2;
+        const uint32_t pd = (w * LD + i) * 1024;
+        glds16s(ks, lro + kc16 * 16u, base + pd);
+        glds16s(vs, lro + vc16 * 16u, base + TILE_B + pd);
+      }
+    } else if (k0 + FWD_BK <= T_) {
       const void* ks = sgpr_ptr(kbase + (long)k0 * rs);
       const void* vs = sgpr_ptr(vbase + (long)k0 * rs);
 #pragma unroll
@@ -263,15 +290,47 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd_mfma_k(const T* __restrict_
     constexpr bool EDGE = decltype(edge_c)::value;
     // ---- S^T = K Q^T for the visible 32-key sub-tiles; each K fragment feeds QB MFMAs
     f32x16 s[QB][NV];
+    if constexpr (PIPE) {
+      // the NV sub-tiles' chains interleaved, K fragments of step kk+1 read before the MFMAs of
+      // step kk: NV reads in flight under every MFMA pair instead of read -> wait -> MFMA
+      v8 cur[NV];
 #pragma unroll
-    for (int kt = 0; kt < NV; ++kt) {
+      for (int kt = 0; kt < NV; ++kt) {
+        cur[kt] = *reinterpret_cast<const v8*>(kb + kt * 32 * ROWB + koff[0]);
 #pragma unroll
-      for (int u = 0; u < QB; ++u) s[u][kt] = f32x16{};
+        for (int u = 0; u < QB; ++u) s[u][kt] = f32x16{};
+      }
 #pragma unroll
       for (int kk = 0; kk < KK; ++kk) {
-        const v8 kf = *reinterpret_cast<const v8*>(kb + kt * 32 * ROWB + koff[kk]);
+        v8 nxt[NV];
+        if (kk + 1 < KK) {
 #pragma unroll
-        for (int u = 0; u < QB; ++u) s[u][kt] = MF<T>::mma(kf, qf[u][kk], s[u][kt]);
+          for (int kt = 0; kt < NV; ++kt) nxt[kt] = *reinterpret_cast<const v8*>(kb + kt * 32 * ROWB + koff[kk + 1]);
+        }
+        // keep the next step's reads ahead of this step's MFMAs (the scheduler otherwise sinks
+        // them to just before their use and every MFMA pair waits on a fresh LDS read)
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int kt = 0; kt < NV; ++kt)
+#pragma unroll
+          for (int u = 0; u < QB; ++u) s[u][kt] = MF<T>::mma(cur[kt], qf[u][kk], s[u][kt]);
+        __builtin_amdgcn_sched_barrier(0);
+        if (kk + 1 < KK) {
+#pragma unroll
+          for (int kt = 0; kt < NV; ++kt) cur[kt] = nxt[kt];
+        }
+      }
+    } else {
+#pragma unroll
+      for (int kt = 0; kt < NV; ++kt) {
+#pragma unroll
+        for (int u = 0; u < QB; ++u) s[u][kt] = f32x16{};
+#pragma unroll
+        for (int kk = 0; kk < KK; ++kk) {
+          const v8 kf = *reinterpret_cast<const v8*>(kb + kt * 32 * ROWB + koff[kk]);
+#pragma unroll
+          for (int u = 0; u < QB; ++u) s[u][kt] = MF<T>::mma(kf, qf[u][kk], s[u][kt]);
+        }
       }
     }
 #pragma unroll
@@ -308,14 +367,27 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd_mfma_k(const T* __restrict_
         m[u] = mn;
       }
       float ls = 0.f;
+      if constexpr (PIPE) {  // four partial sums: no 32-deep dependent add chain
+        float l4[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int kt = 0; kt < NV; ++kt)
+        for (int kt = 0; kt < NV; ++kt)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const float pv = __builtin_amdgcn_exp2f(fmaf(s[u][kt][r], c, -m[u]));
-          ls += pv;
-          s[u][kt][r] = pv;
-        }
+          for (int r = 0; r < 16; ++r) {
+            const float pv = __builtin_amdgcn_exp2f(fmaf(s[u][kt][r], c, -m[u]));
+            l4[r & 3] += pv;
+            s[u][kt][r] = pv;
+          }
+        ls = (l4[0] + l4[1]) + (l4[2] + l4[3]);
+      } else {
+#pragma unroll
+        for (int kt = 0; kt < NV; ++kt)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const float pv = __builtin_amdgcn_exp2f(fmaf(s[u][kt][r], c, -m[u]));
+            ls += pv;
+            s[u][kt][r] = pv;
+          }
+      }
       l[u] += ls;
       if constexpr (DROP) {
         // keys (r, r+1) with r even are adjacent: one hash serves both when the row base is even.
@@ -375,28 +447,56 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd_mfma_k(const T* __restrict_
     }
     // ---- O^T += V^T P^T: P fragments packed from the accumulators, V^T by transposed reads
     //      (each V^T fragment feeds QB MFMAs)
+    auto vread = [&](int kt, int s2, int dt) {
+      const int off = voff[dt] + (kt * 32 + s2 * 16) * ROWB;
+      const s16x4 r1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(vb + off));
+      const s16x4 r2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(vb + off + 8 * ROWB));
+      return __builtin_bit_cast(v8, __builtin_shufflevector(r1, r2, 0, 1, 2, 3, 4, 5, 6, 7));
+    };
+    if constexpr (PIPE) {
+      // one flat sequence of (kt, s2, dt) MFMAs with the next V^T fragment read before each one
+      constexpr int NPV = NV * 2 * DT;
+      v8 vcur = vread(0, 0, 0);
+      v8 pf[QB];
 #pragma unroll
-    for (int kt = 0; kt < NV; ++kt)
+      for (int i = 0; i < NPV; ++i) {
+        const int kt = i / (2 * DT), s2 = (i / DT) & 1, dt = i % DT;
+        v8 vnxt;
+        if (i + 1 < NPV) vnxt = vread((i + 1) / (2 * DT), ((i + 1) / DT) & 1, (i + 1) % DT);
+        if (dt == 0) {
 #pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-        v8 pf[QB];
+          for (int u = 0; u < QB; ++u) {
+            uint32_t uu[4];
 #pragma unroll
-        for (int u = 0; u < QB; ++u) {
-          uint32_t uu[4];
-#pragma unroll
-          for (int j = 0; j < 4; ++j) uu[j] = pack2<T>(s[u][kt][8 * s2 + 2 * j], s[u][kt][8 * s2 + 2 * j + 1]);
-          __builtin_memcpy(&pf[u], uu, 16);
+            for (int j = 0; j < 4; ++j) uu[j] = pack2<T>(s[u][kt][8 * s2 + 2 * j], s[u][kt][8 * s2 + 2 * j + 1]);
+            __builtin_memcpy(&pf[u], uu, 16);
+          }
         }
 #pragma unroll
-        for (int dt = 0; dt < DT; ++dt) {
-          const int off = voff[dt] + (kt * 32 + s2 * 16) * ROWB;
-          const s16x4 r1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(vb + off));
-          const s16x4 r2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(vb + off + 8 * ROWB));
-          const v8 va = __builtin_bit_cast(v8, __builtin_shufflevector(r1, r2, 0, 1, 2, 3, 4, 5, 6, 7));
-#pragma unroll
-          for (int u = 0; u < QB; ++u) o[u][dt] = MF<T>::mma(va, pf[u], o[u][dt]);
-        }
+        for (int u = 0; u < QB; ++u) o[u][dt] = MF<T>::mma(vcur, pf[u], o[u][dt]);
+        if (i + 1 < NPV) vcur = vnxt;
       }
+    } else {
+#pragma unroll
+      for (int kt = 0; kt < NV; ++kt)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          v8 pf[QB];
+#pragma unroll
+          for (int u = 0; u < QB; ++u) {
+            uint32_t uu[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) uu[j] = pack2<T>(s[u][kt][8 * s2 + 2 * j], s[u][kt][8 * s2 + 2 * j + 1]);
+            __builtin_memcpy(&pf[u], uu, 16);
+          }
+#pragma unroll
+          for (int dt = 0; dt < DT; ++dt) {
+            const v8 va = vread(kt, s2, dt);
+#pragma unroll
+            for (int u = 0; u < QB; ++u) o[u][dt] = MF<T>::mma(va, pf[u], o[u][dt]);
+          }
+        }
+    }
   };
   using Ic1 = std::integral_constant<int, 1>;
   using IcN = std::integral_constant<int, NKT>;
@@ -440,21 +540,28 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd_mfma_k(const T* __restrict_
 #pragma unroll
   for (int u = 0; u < QB; ++u) {
     const float lt = l[u] + __shfl_xor(l[u], 32, 64);
-    if (qi[u] < T_) {
-      const float inv = lt > 0.f ? 1.f / lt : 0.f;
-      T* orow = out + ((long)b * T_ + qi[u]) * (long)H * HD + (long)h * HD;
+    const float inv = lt > 0.f ? 1.f / lt : 0.f;
+    T* orow = out + ((long)b * T_ + min(qi[u], T_ - 1)) * (long)H * HD + (long)h * HD;
+    // 16-B stores: lane (q, half hh) holds d = 8 gq + 4 hh + 0..3 of each 32-column tile; one
+    // v_permlane32_swap per dword of a (gq, gq+1) pair leaves 8 contiguous d of group gq in the
+    // lower half and of gq+1 in the upper half (cdna_hip_programming.md T21: half the store
+    // instructions of the dwordx2 form, same bytes).  Every lane swaps (cross-lane); only the
+    // store is guarded.
 #pragma unroll
-      for (int dt = 0; dt < DT; ++dt)
+    for (int dt = 0; dt < DT; ++dt)
 #pragma unroll
-        for (int gq = 0; gq < 4; ++gq) {
-          const int d0 = dt * 32 + 8 * gq + 4 * hh;
-          uint2 v;
-          v.x = pack2<T>(o[u][dt][4 * gq + 0] * inv, o[u][dt][4 * gq + 1] * inv);
-          v.y = pack2<T>(o[u][dt][4 * gq + 2] * inv, o[u][dt][4 * gq + 3] * inv);
-          *reinterpret_cast<uint2*>(orow + d0) = v;
-        }
-      if (hh == 0) lse[((long)b * H + h) * T_ + qi[u]] = m[u] + log2f(lt);
-    }
+      for (int gq = 0; gq < 4; gq += 2) {
+        uint32_t ax = pack2<T>(o[u][dt][4 * gq + 0] * inv, o[u][dt][4 * gq + 1] * inv);
+        uint32_t ay = pack2<T>(o[u][dt][4 * gq + 2] * inv, o[u][dt][4 * gq + 3] * inv);
+        uint32_t bx = pack2<T>(o[u][dt][4 * gq + 4] * inv, o[u][dt][4 * gq + 5] * inv);
+        uint32_t by = pack2<T>(o[u][dt][4 * gq + 6] * inv, o[u][dt][4 * gq + 7] * inv);
+        const auto rx = __builtin_amdgcn_permlane32_swap(ax, bx, false, false);
+        const auto ry = __builtin_amdgcn_permlane32_swap(ay, by, false, false);
+        ax = rx[0]; bx = rx[1]; ay = ry[0]; by = ry[1];
+        if (qi[u] < T_)
+          *reinterpret_cast<uint4*>(orow + dt * 32 + 8 * gq + 8 * hh) = uint4{ax, ay, bx, by};
+      }
+    if (qi[u] < T_ && hh == 0) lse[((long)b * H + h) * T_ + qi[u]] = m[u] + log2f(lt);
   }
 }
 
@@ -471,16 +578,21 @@ void attn_fwd_mfma(DType dt, const void* qkv, void* o, float* lse, int B, int T_
   const uint32_t thr = drop_threshold16(p);
   const float ik = drop_inv_keep(p);
   const bool small = fwd_small_tiles(hd, p, (long)((T_ + FWD_BQ - 1) / FWD_BQ) * H * B);
-#define LAUNCH_V(TT, HDD, BK, NB, OC)                                                                      \
+  const bool pipe = getenv("BLLM_FWD_PIPE") && atoi(getenv("BLLM_FWD_PIPE")) != 0;  // A/B (temporary)
+#define LAUNCH_P(TT, HDD, BK, NB, OC, PP)                                                                      \
   do {                                                                                                        \
     const int lds = NB * 2 * BK * HDD * 2;                                                                    \
     const dim3 grid(((T_ + FWD_BQ - 1) / FWD_BQ) * H * B), block(256);                                        \
     if (p > 0.f)                                                                                              \
-      hipLaunchKernelGGL((attn_fwd_mfma_k<TT, HDD, true, BK, NB, OC>), grid, block, lds, s,          \
+      hipLaunchKernelGGL((attn_fwd_mfma_k<TT, HDD, true, BK, NB, OC, PP>), grid, block, lds, s,          \
                          (const TT*)qkv, (TT*)o, lse, T_, H, G, B, causal, thr, ik, seed, offset, keep_mask); \
     else                                                                                                      \
-      hipLaunchKernelGGL((attn_fwd_mfma_k<TT, HDD, false, BK, NB, OC>), grid, block, lds, s,         \
+      hipLaunchKernelGGL((attn_fwd_mfma_k<TT, HDD, false, BK, NB, OC, PP>), grid, block, lds, s,         \
                          (const TT*)qkv, (TT*)o, lse, T_, H, G, B, causal, thr, ik, seed, offset, nullptr); \
+  } while (0)
+#define LAUNCH_V(TT, HDD, BK, NB, OC)                                                                      \
+  do {                                                                                                        \
+    if (pipe) LAUNCH_P(TT, HDD, BK, NB, OC, true); else LAUNCH_P(TT, HDD, BK, NB, OC, false);             \
   } while (0)
 #define LAUNCH(TT, HDD)                                                                                       \
   do {                                                                                                        \
@@ -494,6 +606,7 @@ void attn_fwd_mfma(DType dt, const void* qkv, void* o, float* lse, int B, int T_
   }
 #undef LAUNCH
 #undef LAUNCH_V
+#undef LAUNCH_P
 }
 
 }  // namespace bllm

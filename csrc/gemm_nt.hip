@@ -408,16 +408,12 @@ void set_lds_attr() {
   (void)at;
 }
 
-// experiment knobs (read once): BLLM_NT_MAP (tile map, see the kernel), BLLM_NT_GM (group
-// depth) -- the round-5 placement A/B (profiles/r5/kernel_experiments.md); defaults ship
+// tile map (see the kernel) and group depth: the shipped defaults, changed only through
+// set_gemm_tile_maps (the round-5 placement A/B, profiles/r5/kernel_experiments.md)
 struct NtKnobs {
   int map = 0, gm = GROUP_M;
-  NtKnobs() {
-    if (const char* e = getenv("BLLM_NT_MAP")) map = atoi(e);
-    if (const char* e = getenv("BLLM_NT_GM")) gm = atoi(e) > 0 ? atoi(e) : GROUP_M;
-  }
 };
-static const NtKnobs& knobs() {
+static NtKnobs& knobs() {
   static NtKnobs k;
   return k;
 }
@@ -441,6 +437,11 @@ void launch(const void* a, long lda, const void* b, long ldb, void* c, long ldc,
 }
 
 }  // namespace
+
+void set_gemm_nt_tile_map(int map, int group_m) {
+  knobs().map = map;
+  knobs().gm = group_m > 0 ? group_m : GROUP_M;
+}
 
 bool gemm_nt_rope_supported(int M, int N, int K, long lda, long ldb, long ldc, int hd) {
   return hd == 128 && M > 0 && N > 0 && M % TM == 0 && N % TN == 0 && K % (2 * TK) == 0 && ldc % 4 == 0 &&

@@ -368,9 +368,9 @@ __global__ __launch_bounds__(Geo::THREADS) void wgrad_gemm_k(const T* __restrict
 //     t+1), then the reads of a0/b0 of tile t+1 over the last 16 MFMAs.
 // The body is branch-free for every tile (past the end the pieces re-load the last tile into a
 // buffer nothing reads again).  Pieces are buffer_load ... lds on a per-K-tile descriptor.
-// tile maps (``map``, experiment knob BLLM_WG_MAP): 0 = XCD-contiguous over GROUP_M-deep column-major
+// tile maps (``map``, set_gemm_tile_maps): 0 = XCD-contiguous over GROUP_M-deep column-major
 // groups (each XCD an M-band), 1 = plain bid order, 2 = the same over the transposed grid (each XCD
-// an N-band); ``group_m`` = group depth (BLLM_WG_GM)
+// an N-band); ``group_m`` = group depth
 // grouped tile order -> (tm, tn): GROUP_M-deep column-major groups (map 2: over the transposed
 // grid); shared by wgrad4_k and the split-tail reduction
 __device__ __forceinline__ void wg_tile(int wid, int nbm, int nbn, int map, int group_m, int& tm, int& tn) {
@@ -542,12 +542,12 @@ __global__ __launch_bounds__(256) void wg_tail_sum_k(const float* __restrict__ p
   }
 }
 
-// experiment knobs, read per launch (A/B in one process): tile map and group depth
+// tile map and group depth: the shipped defaults, changed only through set_gemm_tile_maps (the
+// placement A/B of profiles/r5/kernel_experiments.md and the map tests)
+static int g_wg_map = 0, g_wg_gm = GROUP_M;
 static void wg_knobs(int& map, int& gm) {
-  const char* em = getenv("BLLM_WG_MAP");
-  const char* eg = getenv("BLLM_WG_GM");
-  map = em ? atoi(em) : 0;
-  gm = eg && atoi(eg) > 0 ? atoi(eg) : GROUP_M;
+  map = g_wg_map;
+  gm = g_wg_gm;
 }
 
 template <typename T, typename OT>
@@ -590,6 +590,11 @@ void launch(const void* a, long lda, const void* b, long ldb, void* c, long ldc,
 }
 
 }  // namespace
+
+void set_wgrad_tile_map(int map, int group_m) {
+  g_wg_map = map;
+  g_wg_gm = group_m > 0 ? group_m : GROUP_M;
+}
 
 bool gemm_nn_supported(int M, int N, int K) { return M > 0 && N > 0 && M % BM == 0 && N % BN == 0 && K >= KCH && K % KCH == 0; }
 

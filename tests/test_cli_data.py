@@ -46,6 +46,8 @@ def test_reference_flags_and_defaults():
     (["--use_fsdp"], ValueError),                                        # FSDP needs multi_gpu
     (["--run_type", "multi_gpu", "--use_fsdp", "--use_zero_opt"], ValueError),
     (["--mixed_precision", "bf16"], ValueError),                         # needs FSDP
+    # the auto planner picks the recomputed blocks; a segment count would silently replace it
+    (["--use_actv_ckpt", "--actv_ckpt_mode", "auto", "--actv_ckpt_segments", "4"], ValueError),
 ])
 def test_perform_checks_rejects(tmp_path, extra, err):
     with pytest.raises(err):

@@ -358,6 +358,32 @@ def test_flash_attention_keep_mask_fused_gqa(hd):
     test_flash_attention_keep_mask(hd, 128, 128, 16, 8, True)
 
 
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("B,T,H,G,hd", [(2, 200, 4, 4, 128), (1, 300, 8, 2, 128), (2, 33, 4, 2, 64),
+                                         (3, 129, 4, 4, 64), (1, 1024, 8, 2, 128), (128, 128, 16, 8, 64)])
+@pytest.mark.parametrize("p", [0.0, 0.1])
+@pytest.mark.parametrize("causal", [True, False])
+def test_flash_attention_bwd_stored_ds(dt, B, T, H, G, hd, p, causal):
+    """The stored-dS backward: the dK/dV kernel stores dS^T and dQ = dS K reads it back
+    (csrc/attn_bwd_mfma.hip attn_bwd_dq_ds_k) instead of recomputing S and dP.  The dS^T workspace
+    comes from the caching allocator: a NaN-filled block is freed first so that any (key, q) the
+    dQ pass read without the dK/dV pass having written it would poison dQ.  Against the fp32
+    oracle, and against the recomputing dQ kernel (store_ds=False)."""
+    nan = torch.full((B * H * ((T + 63) // 64 * 64) * ((T + 127) // 128 * 128) + (1 << 20),), float("nan"),
+                     device=DEV, dtype=dt)
+    del nan
+    qkv = torch.randn(B * T, (H + 2 * G) * hd, device=DEV).to(dt)
+    do = torch.randn(B * T, H * hd, device=DEV).to(dt)
+    o, lse = ops.flash_attn_fwd(qkv, B, T, H, G, hd, causal, p, 5, 77)
+    d_ds = ops.flash_attn_bwd(qkv, o, lse, do, B, T, H, G, hd, causal, p, 5, 77, store_ds=True)
+    assert torch.isfinite(d_ds).all()
+    d_rc = ops.flash_attn_bwd(qkv, o, lse, do, B, T, H, G, hd, causal, p, 5, 77, store_ds=False)
+    want = ref.flash_attn_bwd(qkv.cpu().float(), o.cpu().float(), lse.cpu(), do.cpu().float(), B, T, H, G, hd,
+                              causal, p, 5, 77)
+    _close(d_ds, want, dt, 4, name="stored dS vs oracle")
+    _close(d_rc, want, dt, 4, name="recompute vs oracle")
+
+
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16, torch.float32])
 @pytest.mark.parametrize("B,T,H,G,hd", [(2, 200, 4, 4, 128),     # MHA: dK written by the dK/dV kernel
                                          (1, 300, 8, 2, 128),     # GQA: fp32 partials + reduce kernel
@@ -713,11 +739,12 @@ def test_wgrad_gemm(dt, odt, K, M, N, S, accumulate):
                                            (1536, 256, 1024, 3, 4)])
 @pytest.mark.parametrize("accumulate", [False, True])
 @pytest.mark.parametrize("wmap", ["0", "2"])
-def test_wgrad_gemm_split_tail(odt, M, N, K, full, St, accumulate, wmap, monkeypatch):
+def test_wgrad_gemm_split_tail(odt, M, N, K, full, St, accumulate, wmap, request):
     """dW with the grouped tile order in two launches -- tiles [0, full) whole-K into c, the rest
     split St ways into compact fp32 partials and summed -- vs an fp32 matmul (both tile maps: the
     sum kernel must place every tail tile where the GEMM's map put it)."""
-    monkeypatch.setenv("BLLM_WG_MAP", wmap)
+    torch.ops.bllm.set_gemm_tile_maps(int(wmap), 0, 0, 0)
+    request.addfinalizer(lambda: torch.ops.bllm.set_gemm_tile_maps(0, 0, 0, 0))
     a_full = torch.randn(K, M + 64, device=DEV).to(torch.bfloat16)
     a = a_full[:, 32:32 + M]
     b = torch.randn(K, N, device=DEV).to(torch.bfloat16)
@@ -816,9 +843,9 @@ def test_gemm_nn(dt, odt, M, K, N, accumulate):
 
 
 def test_dgrad_in_linear_backward(monkeypatch):
-    """With BLLM_DGRAD_GEMM=1 FusedLinear.backward routes dX through the MFMA kernel."""
+    """With ops.DGRAD_GEMM on, FusedLinear.backward routes dX through the MFMA kernel."""
     from building_llm_from_scratch_amd.models.linear import _input_grad
-    monkeypatch.setenv("BLLM_DGRAD_GEMM", "1")
+    monkeypatch.setattr(ops, "DGRAD_GEMM", True)
     dy = torch.randn(512, 768, device=DEV).to(torch.bfloat16)
     W = torch.randn(768, 1280, device=DEV).to(torch.bfloat16)
     assert ops.gemm_nn_ok(dy, W)
@@ -841,7 +868,7 @@ def test_transpose2d(dt, R, C):
 def test_dgrad_transposed_weight_path(monkeypatch):
     """Above DGRAD_WT_MIN_TOKENS the input gradient runs on a transposed weight copy."""
     from building_llm_from_scratch_amd.models import linear
-    monkeypatch.setenv("BLLM_DGRAD_GEMM", "0")
+    monkeypatch.setattr(ops, "DGRAD_GEMM", False)
     monkeypatch.setattr(linear, "DGRAD_WT_MIN_TOKENS", 256)
     calls = []
     orig = ops.transpose2d

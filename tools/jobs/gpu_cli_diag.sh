@@ -15,4 +15,4 @@ cli() {  # name, extra args...
 cli default
 cli workers0 --num_workers 0
 BLLM_DECODE_GRAPH=0 cli nograph
-bash tools/gpu_attn_pmc.sh
+bash tools/jobs/gpu_attn_pmc.sh

@@ -11,4 +11,4 @@ cat gpurun_out/cli2/gaps.txt
 rm -rf gpurun_out/cli2/tr
 timeout -k 10 400 python -u bench.py --steps 20 --warmup 5 > gpurun_out/cli2/bench.log 2>&1 || { tail -20 gpurun_out/cli2/bench.log; exit 5; }
 tail -1 gpurun_out/cli2/bench.log | grep -o '"value": [0-9.]*\|"sclk_mhz_avg": [0-9.]*'
-bash tools/gpu_gemm_pmc.sh
+bash tools/jobs/gpu_gemm_pmc.sh

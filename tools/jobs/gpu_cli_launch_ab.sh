@@ -10,4 +10,4 @@ timeout -k 10 400 python -u main.py $ARGS --metrics_file gpurun_out/clilaunch/sp
 echo "== spawn"; summ gpurun_out/clilaunch/spawn.jsonl
 timeout -k 10 400 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29562 main.py $ARGS --num_workers 0 --metrics_file gpurun_out/clilaunch/torchrun_w0.jsonl > gpurun_out/clilaunch/torchrun_w0.log 2>&1 || { tail -20 gpurun_out/clilaunch/torchrun_w0.log; exit 5; }
 echo "== torchrun workers0"; summ gpurun_out/clilaunch/torchrun_w0.jsonl
-bash tools/gpu_attn_cfg_ab.sh
+bash tools/jobs/gpu_attn_cfg_ab.sh

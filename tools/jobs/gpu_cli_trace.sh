@@ -8,5 +8,5 @@ timeout -k 10 400 python -u main.py --model llama3 --num_params 8B --run_type mu
   --profile_steps 6:7 > gpurun_out/clitrace/main.log 2>&1 || { tail -20 gpurun_out/clitrace/main.log; exit 3; }
 timeout -k 10 200 python tools/trace_top.py /tmp/bllm_cli_trace/trace_steps6-7_rank0.json --top 40 > gpurun_out/clitrace/top.txt 2>&1 || { tail gpurun_out/clitrace/top.txt; exit 4; }
 cat gpurun_out/clitrace/top.txt
-bash tools/gpu_wgrad_map_ab.sh
-bash tools/gpu_attn_cfg_ab.sh
+bash tools/jobs/gpu_wgrad_map_ab.sh
+bash tools/jobs/gpu_attn_cfg_ab.sh

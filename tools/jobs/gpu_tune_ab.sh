@@ -1,5 +1,5 @@
 # Interleaved A/B of a tuned TunableOp CSV against hipBLASLt's heuristic on a preset.
-# usage: bash tools/gpu_tune_ab.sh <preset> <csv>
+# usage: bash tools/jobs/gpu_tune_ab.sh <preset> <csv>
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"; export TMPDIR=/tmp; mkdir -p gpurun_out/tab
 for i in 1 2; do
