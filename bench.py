@@ -356,6 +356,7 @@ def main(argv=None):
         os.environ["BLLM_FORCE_COMM"] = "1"
     dist, dev, world, rank = init_dist(a)
     cuda = dev.type == "cuda"
+    rccl_on = cuda and not a.one_device and (world > 1 or a.force_comm)
     if cuda:
         ops.load_ext(required=True)
     sync = torch.cuda.synchronize if cuda else (lambda: None)
@@ -641,9 +642,9 @@ def main(argv=None):
                      "order_check": {"enabled": seq.enabled, "calls_checked_rank0": seq_checked,
                                      "steps": a.warmup}},
         }
-        if a.rccl_log:
+        if rccl_on:
             from building_llm_from_scratch_amd.utils.telemetry import rccl_topology
-            out["rccl_topology"] = rccl_topology(a.rccl_log)
+            out["rccl_topology"] = rccl_topology(a.rccl_log) or {"log": a.rccl_log, "lines": 0}
         # what the box did during the timed steps (clocks, power, temperature, throttle residency)
         # and whether the GEMM tuning table was taken: box-to-box differences become readable
         out["telemetry"] = {"rank0": telem_all[0],

@@ -532,7 +532,7 @@ def attn_decode(q, kcache, vcache, L: int):
 
 
 def flash_attn_bwd(qkv, o, lse, do, B, T, H, G, hd, causal=True, dropout_p=0.0, seed=0, offset=0,
-                   keep_mask=None, rope=None, store_ds=False):
+                   keep_mask=None, rope=None):
     """``keep_mask``: the buffer the matching forward filled (``attn_keep_mask``), or None to
     regenerate the dropout bits from the counter hash (identical result).  ``rope``: the
     (cos, sin) tables the forward rotated q/k with; the returned dq/dk are then already
@@ -541,7 +541,7 @@ def flash_attn_bwd(qkv, o, lse, do, B, T, H, G, hd, causal=True, dropout_p=0.0, 
         load_ext(required=True)
         rc, rs = rope if rope is not None else (None, None)
         return _k().flash_attn_bwd(qkv, o, lse, do, B, T, H, G, hd, causal, float(dropout_p),
-                                   int(seed), int(offset), keep_mask, rc, rs, bool(store_ds))
+                                   int(seed), int(offset), keep_mask, rc, rs)
     dqkv = ref.flash_attn_bwd(qkv, o, lse, do, B, T, H, G, hd, causal, dropout_p, seed, offset)
     if rope is not None:
         ref.rope_(dqkv, rope[0], rope[1], T, H, G, hd, inverse=True)

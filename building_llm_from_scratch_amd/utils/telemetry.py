@@ -216,11 +216,14 @@ def tunableop_status(path: Optional[str]) -> Optional[Dict[str, Any]]:
 def rccl_debug_env(rank: int, directory: Optional[str] = None) -> Optional[str]:
     """Ask RCCL to log its init-time topology decisions (``NCCL_DEBUG=INFO``, subsystems INIT and
     GRAPH only: no per-collective lines) to a per-rank file; returns the path.  Must run before
-    the process group is created.  Leaves a user's own NCCL_DEBUG settings alone."""
+    the process group is created.  A user's own ``NCCL_DEBUG_FILE`` is kept (and parsed); a
+    preset ``NCCL_DEBUG`` level (images often set WARN / VERSION) is raised to INFO into the file,
+    so RCCL's warnings land there too."""
     import os
     import tempfile
-    if "NCCL_DEBUG" in os.environ:
-        return os.environ.get("NCCL_DEBUG_FILE")
+    if os.environ.get("NCCL_DEBUG_FILE"):
+        os.environ.setdefault("NCCL_DEBUG", "INFO")
+        return os.environ["NCCL_DEBUG_FILE"]
     path = os.path.join(directory or tempfile.gettempdir(), f"bllm_rccl_{os.getuid()}_{os.getpid()}_r{rank}.log")
     os.environ.update(NCCL_DEBUG="INFO", NCCL_DEBUG_SUBSYS="INIT,GRAPH", NCCL_DEBUG_FILE=path)
     return path
@@ -249,7 +252,11 @@ def rccl_topology(path: Optional[str], max_lines: int = 24) -> Optional[Dict[str
             out["channels"] = max(out.get("channels", 0), int(msg.split()[1].split("/")[1]))
             if len(out.setdefault("rings", [])) < 4:
                 out["rings"].append(msg)
-        elif re.search(r"Trees|Tree \d|threadThresholds|Algo|algorithm|Protocol|Usable|Connected all|NET/|P2P|xGMI|XGMI",
+        elif re.match(r"Tree \d+ :", msg):
+            out["trees"] = out.get("trees", 0) + 1
+            if len(out.setdefault("tree_examples", [])) < 2:
+                out["tree_examples"].append(msg)
+        elif re.search(r"Trees|threadThresholds|Algo|algorithm|Protocol|Usable|Connected all|NET/|P2P|xGMI|XGMI",
                        msg) and len(keep) < max_lines:
             keep.append(msg)
     out["decisions"] = keep

@@ -60,19 +60,13 @@ bool attn_supported_head_dim(int hd);
 bool attn_keep_mask_ok(DType dt, int hd);
 void attn_fwd(DType dt, const void* qkv, void* o, float* lse, int B, int T, int H, int G, int hd, bool causal,
               float p, uint64_t seed, uint64_t offset, uint32_t* keep_mask, hipStream_t s);
-// ds_ws (bf16/fp16 MFMA path, else ignored): dS^T workspace of attn_ds_elems(B, T, H) elements -- the
-// dK/dV pass stores dS and dQ = dS K reads it back (no S / dP recompute); nullptr: the dQ kernel
-// recomputes S and dP instead
 void attn_bwd(DType dt, const void* qkv, const void* o, const float* lse, const void* dout, void* dqkv, float* delta,
               float* dq_acc, float* dkv_part, int B, int T, int H, int G, int hd, bool causal, float p, uint64_t seed,
-              uint64_t offset, const uint32_t* keep_mask, const float* rcos, const float* rsin, hipStream_t s,
-              void* ds_ws = nullptr);
-int attn_ds_tq_pad(int T);
+              uint64_t offset, const uint32_t* keep_mask, const float* rcos, const float* rsin, hipStream_t s);
 // GEMM tile -> workgroup placement (map 0 = XCD-contiguous M-bands, 1 = plain order, 2 = N-bands)
 // and group depth (<= 0: default) of the dW kernel and of the forward-layout kernel
 void set_wgrad_tile_map(int map, int group_m);
 void set_gemm_nt_tile_map(int map, int group_m);
-int attn_ds_tk_pad(int T);
 bool attn_mfma_head_dim(int hd);
 void attn_fwd_naive(DType dt, const void* qkv, void* o, float* lse, int B, int T, int H, int G, int hd, bool causal,
                     float p, uint64_t seed, uint64_t offset, hipStream_t s);

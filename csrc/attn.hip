@@ -10,7 +10,7 @@ void attn_fwd_mfma(DType dt, const void* qkv, void* o, float* lse, int B, int T,
 void attn_bwd_mfma(DType dt, const void* qkv, const void* o, const float* lse, const void* dout, void* dqkv,
                    float* delta, float* dq_acc, float* dkv_part, int B, int T, int H, int G, int hd, bool causal,
                    float p, uint64_t seed, uint64_t offset, const uint32_t* keep_mask, const float* rcos,
-                   const float* rsin, hipStream_t s, void* ds_ws);
+                   const float* rsin, hipStream_t s);
 
 bool attn_supported_head_dim(int hd) { return hd > 0 && hd <= 256; }
 bool attn_keep_mask_ok(DType dt, int hd) { return dt != DType::F32 && attn_mfma_head_dim(hd); }
@@ -27,11 +27,10 @@ void attn_fwd(DType dt, const void* qkv, void* o, float* lse, int B, int T, int 
 
 void attn_bwd(DType dt, const void* qkv, const void* o, const float* lse, const void* dout, void* dqkv, float* delta,
               float* dq_acc, float* dkv_part, int B, int T, int H, int G, int hd, bool causal, float p, uint64_t seed,
-              uint64_t offset, const uint32_t* keep_mask, const float* rcos, const float* rsin, hipStream_t s,
-              void* ds_ws) {
+              uint64_t offset, const uint32_t* keep_mask, const float* rcos, const float* rsin, hipStream_t s) {
   if (dt != DType::F32 && attn_mfma_head_dim(hd)) {  // inverse RoPE fused into the epilogues
     attn_bwd_mfma(dt, qkv, o, lse, dout, dqkv, delta, dq_acc, dkv_part, B, T, H, G, hd, causal, p, seed, offset,
-                  p > 0.f ? keep_mask : nullptr, rcos, rsin, s, ds_ws);
+                  p > 0.f ? keep_mask : nullptr, rcos, rsin, s);
     return;
   }
   if (dt == DType::F32 && attn_f32_head_dim(hd))

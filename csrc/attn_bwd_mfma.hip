@@ -23,7 +23,6 @@
 // reads (ds_read_b64_tr_b16).  Causal: only tiles at/below the diagonal; heaviest first.
 #include <float.h>
 #include <stdlib.h>
-#include <algorithm>
 #include <type_traits>
 
 #include "api.h"
@@ -105,12 +104,6 @@ template <typename v8> __device__ __forceinline__ v8 tr8(const char* base, int o
 }  // namespace
 
 constexpr int BWD_BKV = 128;  // keys per workgroup
-// 8-byte vector store, saddr form: wave-uniform SGPR base + per-lane 32-bit byte offset (+ an
-// immediate), so the dS^T stores hold no 64-bit per-lane address in VGPRs
-template <int IMM> __device__ __forceinline__ void gst8s(const void* sbase, uint32_t voff, uint32_t lo, uint32_t hi) {
-  const uint64_t d = (uint64_t)lo | ((uint64_t)hi << 32);
-  asm volatile("global_store_dwordx2 %0, %1, %2 offset:%3" ::"v"(voff), "v"(d), "s"(sbase), "n"(IMM) : "memory");
-}
 constexpr int BWD_BQ = 32;    // queries per step
 constexpr float kLog2eB = 1.4426950408889634f;
 
@@ -176,7 +169,7 @@ __device__ __forceinline__ void rope_bwd_store(const f32x16& lo, const f32x16& h
 }
 
 template <typename T, int HD, bool DROP, int NBUF, int OCC, bool FUSEG = false, bool DUAL = false, bool MASK = false,
-          bool VLDS = false, bool DSOUT = false, bool DS_DEFER = false, bool BPIPE = false>
+          bool VLDS = false>
 __global__ __launch_bounds__(256, OCC) void attn_bwd_mfma_k(const T* __restrict__ qkv, const T* __restrict__ dout,
                                                             const float* __restrict__ lse,
                                                             const float* __restrict__ delta, T* __restrict__ dqkv,
@@ -185,8 +178,7 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_mfma_k(const T* __restrict_
                                                             uint64_t seed, uint64_t doff,
                                                             const uint32_t* __restrict__ kmask,
                                                             const float* __restrict__ rcos,
-                                                            const float* __restrict__ rsin, T* __restrict__ dst,
-                                                            int tq_pad, int tk_pad) {
+                                                            const float* __restrict__ rsin) {
   typedef typename MFb<T>::v8 v8;
   constexpr int KK = HD / 16, DT = HD / 32, CH = HD / 8, ROWB = HD * 2;
   constexpr int IMG = BWD_BQ * ROWB;            // bytes of one [32][HD] image
@@ -276,36 +268,6 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_mfma_k(const T* __restrict_
   const float* lse_ = lse + ((long)b * H + h) * T_;
   const float* del_ = delta + ((long)b * H + h) * T_;
   const float* stat_src = (lane < 32 ? lse_ : del_);
-  // DSOUT: the step's dS (the bf16 values dK^T's MFMA consumes) goes to dS^T[b, h][key][q] for the
-  // dQ pass (attn_bwd_dq_ds_k).  Lane (key, half hh) holds queries q0 + 16 s2 + 8 e + 4 hh + 0..3 as
-  // two packed dwords per (s2, e): four 8-byte stores per step, held in registers and issued at the
-  // top of the next step BEFORE its DMA (vector memory completes in order, so the ring's counted
-  // waits are not lengthened by them).  Rows of keys >= T hold the masked zeros; every (key, q) the
-  // dQ pass reads is written (it skips 32-key sub-tiles above its waves' queries).
-  const T* dsbase = nullptr;  // dS^T rows of this wave's 32 keys (wave-uniform)
-  if constexpr (DSOUT) dsbase = dst + ((long)(b * H + h) * tk_pad + kw0) * tq_pad;
-  uint32_t dsp[2][4];
-  int ds_q0 = -1;
-  // lane (key l32, half hh): byte offset of (key, q0 + 4 hh) in the wave's rows; s2 / e add
-  // 32 / 16 bytes as immediates
-  auto ds_store = [&](int qs, const uint32_t (&v)[4], auto s2_c) {
-    constexpr int S2 = decltype(s2_c)::value;
-    int ln = lane;
-    asm volatile("" : "+v"(ln));
-    const uint32_t voff = ((uint32_t)(ln & 31) * (uint32_t)tq_pad + 4u * (uint32_t)(ln >> 5)) * 2u;
-    const void* sb = sgpr_ptr(dsbase + qs);
-    gst8s<32 * S2>(sb, voff, v[0], v[1]);
-    gst8s<32 * S2 + 16>(sb, voff, v[2], v[3]);
-  };
-  auto flush_ds = [&]() {
-    if constexpr (DSOUT && DS_DEFER) {
-      if (ds_q0 >= 0) {
-        ds_store(ds_q0, dsp[0], std::integral_constant<int, 0>{});
-        ds_store(ds_q0, dsp[1], std::integral_constant<int, 1>{});
-        ds_q0 = -1;
-      }
-    }
-  };
   DropSlab ds;
   uint64_t dslab = 0;
   if constexpr (DROP) {
@@ -353,16 +315,13 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_mfma_k(const T* __restrict_
             smem + slot * BUF + IMASK + w * 256);
   };
   // wait until step i+1's DMA landed, leaving the later issued steps (up to NBUF-2) in flight
-  // dS^T stores (issued after the step's DMA, so the youngest vector-memory ops of the step): the
-  // counted waits leave them in flight into the next step -- only the DMA has to have landed
-  constexpr int NST = DSOUT && !DS_DEFER ? 4 : 0;
   auto ring_wait = [&](int i, int nsteps) {
     if constexpr (NBUF == 4) {
-      if (i + 3 < nsteps) wait_vm<2 * NPW + NST>(); else if (i + 2 < nsteps) wait_vm<NPW + NST>(); else wait_vm<NST>();
+      if (i + 3 < nsteps) wait_vm<2 * NPW>(); else if (i + 2 < nsteps) wait_vm<NPW>(); else wait_vm0();
     } else if constexpr (NBUF == 3) {
-      if (i + 2 < nsteps) wait_vm<NPW + NST>(); else wait_vm<NST>();
+      if (i + 2 < nsteps) wait_vm<NPW>(); else wait_vm0();
     } else {
-      wait_vm<NST>();
+      wait_vm0();
     }
     __builtin_amdgcn_s_barrier();
   };
@@ -393,7 +352,6 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_mfma_k(const T* __restrict_
   }
   for (; i < nsteps; ++i) {
     const int q0 = qstart + i * BWD_BQ;
-    flush_ds();  // the previous step's dS^T (DSOUT)
     if (i + NBUF - 1 < nsteps) issue(q0 + (NBUF - 1) * BWD_BQ, slot == 0 ? NBUF - 1 : slot - 1);
     const char* S = smem + slot * BUF;
     // per-lane LDS offsets, recomputed each step from an opaque copy of the lane id (a few
@@ -461,53 +419,10 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_mfma_k(const T* __restrict_
         }
       }
       // dV^T += dO^T Pd ; dK^T += Q^T dS   (B operands straight from the accumulators)
-      auto tr_offs = [&](int s2, int dt, int& olo, int& ohi) {
-        if constexpr (DUAL) {
-          // lane 4q+p of a 16-lane group: row 4hh+q (+8), columns dt*32 + glb*16 + 4p .. +3
-          const int row = 4 * hh_ + qrow + s2 * 16, ch = dt * 4 + glb * 2 + (pcol >> 1);
-          olo = dual_off<HD>(row, ch) + 8 * (pcol & 1);
-          ohi = dual_off<HD>(row + 8, ch) + 8 * (pcol & 1);
-        } else {
-          olo = t_off<HD>(4 * hh_ + qrow, dt * 32 + glb * 16 + pcol * 4) + s2 * 16 * ROWB;
-          ohi = olo + 8 * ROWB;
-        }
-      };
-      // BPIPE: the (s2, dt) MFMA pairs as one sequence with the next pair's dO^T / Q^T fragments
-      // read before the current pair issues (else each pair waits on its own fresh reads)
-      v8 ao_c, aq_c;
-      if constexpr (BPIPE) {
-        int olo, ohi;
-        tr_offs(0, 0, olo, ohi);
-        ao_c = tr8<v8>(S + IOT, olo, ohi);
-        aq_c = tr8<v8>(S + IQT, olo, ohi);
-      }
-      // BPIPE: both k-steps' Pd / dS operands packed before the MFMAs (the 32 fp32 sacc / dpacc
-      // registers are dead from here on, which pays for the read-ahead fragments)
-      v8 pfa[2], dfa[2];
-      if constexpr (BPIPE) {
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) {
-          uint32_t u[4], v[4];
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            u[j] = pk2<T>(sacc[8 * s2 + 2 * j], sacc[8 * s2 + 2 * j + 1]);
-            v[j] = pk2<T>(dpacc[8 * s2 + 2 * j], dpacc[8 * s2 + 2 * j + 1]);
-          }
-          __builtin_memcpy(&pfa[s2], u, 16);
-          __builtin_memcpy(&dfa[s2], v, 16);
-          if constexpr (DSOUT) {
-            if (s2 == 0) ds_store(q0, v, std::integral_constant<int, 0>{});
-            else ds_store(q0, v, std::integral_constant<int, 1>{});
-          }
-        }
-      }
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) {
         v8 pf, df;
-        if constexpr (BPIPE) {
-          pf = pfa[s2];
-          df = dfa[s2];
-        } else {
+        {
           uint32_t u[4], v[4];
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
@@ -516,52 +431,29 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_mfma_k(const T* __restrict_
           }
           __builtin_memcpy(&pf, u, 16);
           __builtin_memcpy(&df, v, 16);
-          if constexpr (DSOUT) {
-            if constexpr (DS_DEFER) {
-#pragma unroll
-              for (int j = 0; j < 4; ++j) dsp[s2][j] = v[j];
-            } else if (s2 == 0) {
-              ds_store(q0, v, std::integral_constant<int, 0>{});
-            } else {
-              ds_store(q0, v, std::integral_constant<int, 1>{});
-            }
-          }
         }
 #pragma unroll
         for (int dt = 0; dt < DT; ++dt) {
-          if constexpr (BPIPE) {
-            const int n = s2 * DT + dt + 1;
-            v8 ao_n, aq_n;
-            if (n < 2 * DT) {
-              int olo, ohi;
-              tr_offs(n / DT, n % DT, olo, ohi);
-              ao_n = tr8<v8>(S + IOT, olo, ohi);
-              aq_n = tr8<v8>(S + IQT, olo, ohi);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-            dv[dt] = MFb<T>::mma(ao_c, pf, dv[dt]);
-            dk[dt] = MFb<T>::mma(aq_c, df, dk[dt]);
-            __builtin_amdgcn_sched_barrier(0);
-            if (n < 2 * DT) {
-              ao_c = ao_n;
-              aq_c = aq_n;
-            }
+          int olo, ohi;
+          if constexpr (DUAL) {
+            // lane 4q+p of a 16-lane group: row 4hh+q (+8), columns dt*32 + glb*16 + 4p .. +3
+            const int row = 4 * hh_ + qrow + s2 * 16, ch = dt * 4 + glb * 2 + (pcol >> 1);
+            olo = dual_off<HD>(row, ch) + 8 * (pcol & 1);
+            ohi = dual_off<HD>(row + 8, ch) + 8 * (pcol & 1);
           } else {
-            int olo, ohi;
-            tr_offs(s2, dt, olo, ohi);
-            const v8 ao = tr8<v8>(S + IOT, olo, ohi);
-            dv[dt] = MFb<T>::mma(ao, pf, dv[dt]);
-            const v8 aq = tr8<v8>(S + IQT, olo, ohi);
-            dk[dt] = MFb<T>::mma(aq, df, dk[dt]);
+            olo = t_off<HD>(4 * hh_ + qrow, dt * 32 + glb * 16 + pcol * 4) + s2 * 16 * ROWB;
+            ohi = olo + 8 * ROWB;
           }
+          const v8 ao = tr8<v8>(S + IOT, olo, ohi);
+          dv[dt] = MFb<T>::mma(ao, pf, dv[dt]);
+          const v8 aq = tr8<v8>(S + IQT, olo, ohi);
+          dk[dt] = MFb<T>::mma(aq, df, dk[dt]);
         }
       }
     }
-    if constexpr (DSOUT && DS_DEFER) ds_q0 = q0;
     ring_wait(i, nsteps);
     slot = slot == NBUF - 1 ? 0 : slot + 1;
   }
-  flush_ds();
 
   }  // heads
 
@@ -890,197 +782,6 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_dq_k(const T* __restrict__ 
   }
 }
 
-// ---------------------------------------------------------------------------------------
-// dQ from the stored dS (DSOUT path): dQ = (1/sqrt(d)) dS K, the one product of the five that
-// needs a sum over key blocks, without recomputing S and dP (the kernel above recomputes both:
-// 3 MFMA products per tile; this one: 1, reading dS^T once from HBM instead).  Workgroup = 4
-// waves x 32 queries of head h (as above); per key tile two DMA'd LDS images, K^T (64-B-chunk XOR,
-// hardware-transposed reads as the A operand, m = d) and dS^T [BK keys][128 q] (the same image
-// type with 128 columns, transposed reads as the B operand, n = q).  Both operands take the same
-// key permutation from the transposed read, so their product sums the right pairs.  32-key
-// sub-tiles above every query of a wave are skipped (the dK/dV pass never wrote them).
-template <int HD, int BK> constexpr int dqds_buf_bytes() { return BK * HD * 2 + BK * 256; }
-
-template <typename T, int HD, int BK, int NBUF, int OCC>
-__global__ __launch_bounds__(256, OCC) void attn_bwd_dq_ds_k(const T* __restrict__ qkv, const T* __restrict__ dst,
-                                                           T* __restrict__ dqkv, int T_, int H, int G, int B_,
-                                                           bool causal, int tq_pad, int tk_pad,
-                                                           const float* __restrict__ rcos,
-                                                           const float* __restrict__ rsin) {
-  typedef typename MFb<T>::v8 v8;
-  constexpr int DT = HD / 32, CH = HD / 8, ROWB = HD * 2;
-  constexpr int KIMG = BK * ROWB;               // K^T image bytes
-  constexpr int LDK = BK * CH / 256;            // 1-KiB pieces per wave: K^T image
-  constexpr int LDS_ = BK * 16 / 256;           // 1-KiB pieces per wave: dS^T image (256-B rows)
-  constexpr int BUF = dqds_buf_bytes<HD, BK>();
-  constexpr int NPW = LDK + LDS_;
-  constexpr int NKT = BK / 32;
-  static_assert(NBUF >= 2 && NBUF <= 4, "ring depth");
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-
-  const int nqb = (T_ + DQ_BQ - 1) / DQ_BQ;
-  const int lin = blockIdx.x, nbh = H * B_;
-  const int qbi = lin / nbh, bh = lin - qbi * nbh;
-  const int qb = causal ? nqb - 1 - qbi : qbi;
-  const int h = bh % H, b = bh / H;
-  const int g = h / (H / G);
-  const int tid = threadIdx.x, lane = tid & 63, hh = lane >> 5, l32 = lane & 31;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int gi = lane & 15, gl = (lane >> 4) & 1, qrow = gi >> 2, pcol = gi & 3;
-  const long rs = (long)(H + 2 * G) * HD;
-  const T* kb_ = qkv + (long)b * T_ * rs + (long)(H + g) * HD;
-  const int q0 = qb * DQ_BQ;
-  const T* db_ = dst + (long)(b * H + h) * tk_pad * tq_pad + q0;
-  const int wq_lo = q0 + w * 32, wq_hi = wq_lo + 31;
-  const int qi = wq_lo + l32;
-  const float scale = rsqrtf((float)HD);
-
-  f32x16 dq[DT];
-#pragma unroll
-  for (int i = 0; i < DT; ++i) dq[i] = f32x16{};
-  int troff[DT];
-#pragma unroll
-  for (int dt = 0; dt < DT; ++dt) troff[dt] = t_off<HD>(4 * hh + qrow, dt * 32 + gl * 16 + pcol * 4);
-  const int sboff = t_off<128>(4 * hh + qrow, w * 32 + gl * 16 + pcol * 4);
-  // DMA source offsets: K^T pieces (row stride rs) and dS^T pieces (row stride tq_pad), each the
-  // image's XOR applied to the source chunk so the lane-linear LDS write IS the swizzled image
-  uint32_t koffg[LDK], soffg[LDS_];
-  int prow[LDK], ptc[LDK];
-#pragma unroll
-  for (int i = 0; i < LDK; ++i) {
-    const int P = (w * LDK + i) * 64 + lane;
-    const int r = P / CH, pc = P % CH;
-    const int c64 = (pc >> 2) ^ (HD == 128 ? (r & 3) : ((r >> 1) & 1));
-    const int tc = c64 * 4 + (pc & 3);
-    prow[i] = r; ptc[i] = tc;
-    koffg[i] = (uint32_t)(r * rs * 2 + tc * 16);
-  }
-#pragma unroll
-  for (int i = 0; i < LDS_; ++i) {
-    const int P = (w * LDS_ + i) * 64 + lane;
-    const int r = P / 16, pc = P % 16;
-    const int tc = ((pc >> 2) ^ (r & 3)) * 4 + (pc & 3);
-    soffg[i] = (uint32_t)(r * tq_pad * 2 + tc * 16);
-  }
-  const uint32_t smem_u = lds_u32(smem);
-  auto issue = [&](int t, int slot) {
-    const int k0 = t * BK;
-    const uint32_t base = smem_u + slot * BUF;
-    const void* ss = sgpr_ptr(db_ + (long)k0 * tq_pad);  // rows < tk_pad: always in bounds
-#pragma unroll
-    for (int i = 0; i < LDS_; ++i) glds16s(ss, soffg[i], base + KIMG + (w * LDS_ + i) * 1024);
-    if (k0 + BK <= T_) {
-      const void* ks = sgpr_ptr(kb_ + (long)k0 * rs);
-#pragma unroll
-      for (int i = 0; i < LDK; ++i) glds16s(ks, koffg[i], base + (w * LDK + i) * 1024);
-    } else {  // sequence tail: clamp key rows (their dS is zero or the sub-tile is skipped)
-      char* lb = smem + slot * BUF;
-#pragma unroll
-      for (int i = 0; i < LDK; ++i) {
-        const int key = min(k0 + prow[i], T_ - 1);
-        glds16(kb_ + (long)key * rs + ptc[i] * 8, lb + (w * LDK + i) * 1024);
-      }
-    }
-  };
-  const int kend = causal ? min(T_, q0 + DQ_BQ) : T_;
-  const int ntiles = (kend + BK - 1) / BK;
-  const int nact = wq_lo >= T_ ? 0 : (causal ? min(ntiles, wq_hi / BK + 1) : ntiles);
-  const int klim = causal ? min(wq_hi, T_ - 1) : T_ - 1;  // last key any query of this wave sees
-  // wait until tile t+1 landed, leaving the later issued tiles (up to NBUF-2) in flight
-  auto ring_wait = [&](int t) {
-    if constexpr (NBUF == 4) {
-      if (t + 3 < ntiles) wait_vm<2 * NPW>(); else if (t + 2 < ntiles) wait_vm<NPW>(); else wait_vm0();
-    } else if constexpr (NBUF == 3) {
-      if (t + 2 < ntiles) wait_vm<NPW>(); else wait_vm0();
-    } else {
-      wait_vm0();
-    }
-    __builtin_amdgcn_s_barrier();
-  };
-#pragma unroll
-  for (int j = 0; j < NBUF - 1; ++j)
-    if (j < ntiles) issue(j, j);
-  if constexpr (NBUF == 4) {
-    if (ntiles > 2) wait_vm<2 * NPW>(); else if (ntiles > 1) wait_vm<NPW>(); else wait_vm0();
-  } else if constexpr (NBUF == 3) {
-    if (ntiles > 1) wait_vm<NPW>(); else wait_vm0();
-  } else {
-    wait_vm0();
-  }
-  __builtin_amdgcn_s_barrier();
-  int slot = 0, t = 0;
-  for (; t < nact; ++t) {
-    if (t + NBUF - 1 < ntiles) issue(t + NBUF - 1, slot == 0 ? NBUF - 1 : slot - 1);
-    const char* KT = smem + slot * BUF;
-    const char* SI = KT + KIMG;
-#pragma unroll
-    for (int kt = 0; kt < NKT; ++kt) {
-      if (t * BK + kt * 32 > klim) break;  // wave-uniform: sub-tile above every query / past T
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-        const int rb = kt * 32 + s2 * 16;
-        const v8 bq = tr8<v8>(SI, sboff + rb * 256, sboff + (rb + 8) * 256);
-#pragma unroll
-        for (int dt = 0; dt < DT; ++dt) {
-          const int o = troff[dt] + rb * ROWB;
-          dq[dt] = MFb<T>::mma(tr8<v8>(KT, o, o + 8 * ROWB), bq, dq[dt]);
-        }
-      }
-    }
-    ring_wait(t);
-    slot = slot == NBUF - 1 ? 0 : slot + 1;
-  }
-  for (; t < ntiles; ++t) {  // this wave is done; keep the ring and barriers going
-    if (t + NBUF - 1 < ntiles) issue(t + NBUF - 1, slot == 0 ? NBUF - 1 : slot - 1);
-    ring_wait(t);
-    slot = slot == NBUF - 1 ? 0 : slot + 1;
-  }
-  if (qi < T_) {
-    T* row = dqkv + ((long)b * T_ + qi) * rs + (long)h * HD;
-    if (rcos) {
-#pragma unroll
-      for (int dt = 0; dt < DT / 2; ++dt) rope_bwd_store<T, HD>(dq[dt], dq[dt + DT / 2], scale, hh, qi, dt * 32, rcos, rsin, row);
-      return;
-    }
-#pragma unroll
-    for (int dt = 0; dt < DT; ++dt)
-#pragma unroll
-      for (int gq = 0; gq < 4; ++gq) {
-        const int d0 = dt * 32 + 8 * gq + 4 * hh;
-        uint2 v;
-        v.x = pk2<T>(dq[dt][4 * gq] * scale, dq[dt][4 * gq + 1] * scale);
-        v.y = pk2<T>(dq[dt][4 * gq + 2] * scale, dq[dt][4 * gq + 3] * scale);
-        *reinterpret_cast<uint2*>(row + d0) = v;
-      }
-  }
-}
-
-// delta[b, h, t] = rowsum(dO * O) over one head's hd elements: 16-B loads, hd / 8 lanes per row
-template <typename T, int HD>
-__global__ __launch_bounds__(256) void attn_bwd_delta_k(const T* __restrict__ o, const T* __restrict__ dout,
-                                                        float* __restrict__ delta, long rows, int T_, int H) {
-  constexpr int LPR = HD / 8;  // lanes per (b, t, h) row
-  typedef typename MFb<T>::v8 v8;
-  const long nthr = (long)gridDim.x * 256;
-  for (long i = blockIdx.x * 256L + threadIdx.x; i < rows * LPR; i += nthr) {
-    const long row = i / LPR;  // (b T + t) H + h
-    const int part = (int)(i % LPR);
-    const v8 a = *reinterpret_cast<const v8*>(o + row * HD + part * 8);
-    const v8 c = *reinterpret_cast<const v8*>(dout + row * HD + part * 8);
-    float sacc = 0.f;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) sacc += (float)a[j] * (float)c[j];
-#pragma unroll
-    for (int m = LPR / 2; m >= 1; m >>= 1) sacc += __shfl_xor(sacc, m, 64);
-    if (part == 0) {
-      const long bt = row / H;
-      const int hd_ = (int)(row % H);
-      const long b = bt / T_, t = bt % T_;
-      delta[(b * H + hd_) * T_ + t] = sacc;
-    }
-  }
-}
-
 // GQA: dqkv[:, k/v part] = bf16(sum over the H/G query heads of each kv group)
 // With rcos: the inverse RoPE on dK as well (the thread of the first-half chunk d also sums the
 // chunk d + HD/2 and writes both; second-half threads of K have nothing to do).
@@ -1139,10 +840,6 @@ static bool fuse_gqa_heads(int B, int T_, int H, int G) {
 
 bool attn_bwd_kv_partials(int B, int T_, int H, int G) { return H != G && !fuse_gqa_heads(B, T_, H, G); }
 
-// dS^T workspace of the DSOUT backward: [B*H][attn_ds_tk_pad(T)][attn_ds_tq_pad(T)] elements
-int attn_ds_tq_pad(int T_) { return (T_ + DQ_BQ - 1) / DQ_BQ * DQ_BQ; }
-int attn_ds_tk_pad(int T_) { return (T_ + 63) / 64 * 64; }
-
 // launch helpers: one instantiation per (ring, occupancy, fused heads, dual images) and per
 // dropout form (none / counter hash / forward keep mask)
 struct BwdArgs {
@@ -1158,8 +855,6 @@ struct BwdArgs {
   const uint32_t* kmask;
   const float *rcos, *rsin;
   hipStream_t s;
-  void* dst;           // dS^T workspace (DSOUT path) or nullptr
-  int tq_pad, tk_pad;
 };
 template <typename TT, int HDD, bool DROP, int BK, int NB, int OC, bool MASK>
 static void launch_dq1(const BwdArgs& a, dim3 grid) {
@@ -1176,37 +871,9 @@ static void launch_dq(const BwdArgs& a, bool drop, dim3 grid) {
 template <typename TT, int HDD, bool DROP, int NB, int OC, bool FG, bool DU, bool MASK, bool VL>
 static void launch_kv1(const BwdArgs& a, dim3 grid) {
   constexpr int lds = NB * dkdv_buf_bytes<HDD, DU, MASK>() + (VL ? BWD_BKV * HDD * 2 : 0);
-  const bool defer = getenv("BLLM_DS_DEFER") && atoi(getenv("BLLM_DS_DEFER")) != 0;  // A/B (temporary)
-  const bool bpipe = getenv("BLLM_BWD_PIPE") && atoi(getenv("BLLM_BWD_PIPE")) != 0;  // A/B (temporary)
-  if (a.dst && bpipe)
-    hipLaunchKernelGGL((attn_bwd_mfma_k<TT, HDD, DROP, NB, OC, FG, DU, MASK, VL, true, false, true>), grid, dim3(256),
-                       lds, a.s, (const TT*)a.qkv, (const TT*)a.dout, a.lse, a.delta, (TT*)a.dqkv, a.dkv_part, a.T_,
-                       a.H, a.G, a.B, a.causal, a.thr, a.ik, a.seed, a.offset, a.kmask, a.rcos, a.rsin, (TT*)a.dst,
-                       a.tq_pad, a.tk_pad);
-  else if (!a.dst && bpipe)
-    hipLaunchKernelGGL((attn_bwd_mfma_k<TT, HDD, DROP, NB, OC, FG, DU, MASK, VL, false, false, true>), grid, dim3(256),
-                       lds, a.s, (const TT*)a.qkv, (const TT*)a.dout, a.lse, a.delta, (TT*)a.dqkv, a.dkv_part, a.T_,
-                       a.H, a.G, a.B, a.causal, a.thr, a.ik, a.seed, a.offset, a.kmask, a.rcos, a.rsin, nullptr, 0, 0);
-  else if (a.dst && defer)
-    hipLaunchKernelGGL((attn_bwd_mfma_k<TT, HDD, DROP, NB, OC, FG, DU, MASK, VL, true, true>), grid, dim3(256), lds, a.s,
-                       (const TT*)a.qkv, (const TT*)a.dout, a.lse, a.delta, (TT*)a.dqkv, a.dkv_part, a.T_, a.H, a.G,
-                       a.B, a.causal, a.thr, a.ik, a.seed, a.offset, a.kmask, a.rcos, a.rsin, (TT*)a.dst, a.tq_pad,
-                       a.tk_pad);
-  else if (a.dst)
-    hipLaunchKernelGGL((attn_bwd_mfma_k<TT, HDD, DROP, NB, OC, FG, DU, MASK, VL, true>), grid, dim3(256), lds, a.s,
-                       (const TT*)a.qkv, (const TT*)a.dout, a.lse, a.delta, (TT*)a.dqkv, a.dkv_part, a.T_, a.H, a.G,
-                       a.B, a.causal, a.thr, a.ik, a.seed, a.offset, a.kmask, a.rcos, a.rsin, (TT*)a.dst, a.tq_pad,
-                       a.tk_pad);
-  else
-    hipLaunchKernelGGL((attn_bwd_mfma_k<TT, HDD, DROP, NB, OC, FG, DU, MASK, VL>), grid, dim3(256), lds, a.s, (const TT*)a.qkv, (const TT*)a.dout, a.lse, a.delta,
-                       (TT*)a.dqkv, a.dkv_part, a.T_, a.H, a.G, a.B, a.causal, a.thr, a.ik, a.seed, a.offset, a.kmask,
-                       a.rcos, a.rsin, nullptr, 0, 0);
-}
-template <typename TT, int HDD, int BK, int NB, int OC>
-static void launch_dq_ds(const BwdArgs& a, dim3 grid) {
-  constexpr int lds = NB * dqds_buf_bytes<HDD, BK>();
-  hipLaunchKernelGGL((attn_bwd_dq_ds_k<TT, HDD, BK, NB, OC>), grid, dim3(256), lds, a.s, (const TT*)a.qkv,
-                     (const TT*)a.dst, (TT*)a.dqkv, a.T_, a.H, a.G, a.B, a.causal, a.tq_pad, a.tk_pad, a.rcos, a.rsin);
+  hipLaunchKernelGGL((attn_bwd_mfma_k<TT, HDD, DROP, NB, OC, FG, DU, MASK, VL>), grid, dim3(256), lds, a.s, (const TT*)a.qkv, (const TT*)a.dout, a.lse, a.delta,
+                     (TT*)a.dqkv, a.dkv_part, a.T_, a.H, a.G, a.B, a.causal, a.thr, a.ik, a.seed, a.offset, a.kmask,
+                     a.rcos, a.rsin);
 }
 template <typename TT, int HDD, int NB, int OC, bool FG, bool DU, bool VL = false>
 static void launch_kv(const BwdArgs& a, bool drop, dim3 grid) {
@@ -1221,15 +888,7 @@ static void launch_kv(const BwdArgs& a, bool drop, dim3 grid) {
 // profiles/r2_attn_hd64_dual.md), 4-slot ring; else separate row / transposed images, 2-slot ring
 template <typename TT, int HDD>
 static void launch_bwd(const BwdArgs& a, bool drop, bool fuseg, dim3 grid_q, dim3 grid_kv) {
-  if (a.dst) {  // delta pass, then dK/dV (+ dS^T), then dQ from dS^T
-    const long rows = (long)a.B * a.T_ * a.H;
-    const long thr = rows * (HDD / 8);
-    const int nb = (int)std::min<long>((thr + 255) / 256, 8192);
-    hipLaunchKernelGGL((attn_bwd_delta_k<TT, HDD>), dim3(nb), dim3(256), 0, a.s, (const TT*)a.o, (const TT*)a.dout,
-                       a.delta, rows, a.T_, a.H);
-  } else {
-    launch_dq<TT, HDD, 32, 3, 2>(a, drop, grid_q);
-  }
+  launch_dq<TT, HDD, 32, 3, 2>(a, drop, grid_q);
   if constexpr (HDD == 128) {
     if (fuseg) launch_kv<TT, HDD, 2, 2, true, true, true>(a, drop, grid_kv);
     else launch_kv<TT, HDD, 2, 2, false, true, true>(a, drop, grid_kv);
@@ -1238,26 +897,19 @@ static void launch_bwd(const BwdArgs& a, bool drop, bool fuseg, dim3 grid_q, dim
     else if (fuseg) launch_kv<TT, HDD, 2, 2, true, false>(a, drop, grid_kv);
     else launch_kv<TT, HDD, 2, 2, false, false>(a, drop, grid_kv);
   }
-  if (a.dst) {
-    const int v = getenv("BLLM_DQDS") ? atoi(getenv("BLLM_DQDS")) : 0;  // A/B (temporary)
-    if (v == 1) launch_dq_ds<TT, HDD, 64, 2, 2>(a, grid_q);
-    else if (v == 2) launch_dq_ds<TT, HDD, 32, 3, 3>(a, grid_q);
-    else launch_dq_ds<TT, HDD, 32, 4, 2>(a, grid_q);
-  }
 }
 
 void attn_bwd_mfma(DType dt, const void* qkv, const void* o, const float* lse, const void* dout, void* dqkv,
                    float* delta, float* dq_acc, float* dkv_part, int B, int T_, int H, int G, int hd, bool causal,
                    float p, uint64_t seed, uint64_t offset, const uint32_t* keep_mask, const float* rcos,
-                   const float* rsin, hipStream_t s, void* ds_ws) {
+                   const float* rsin, hipStream_t s) {
   (void)dq_acc;
   const int nkb = (T_ + BWD_BKV - 1) / BWD_BKV;
   const bool fuseg = fuse_gqa_heads(B, T_, H, G);
   dim3 grid_kv(nkb * (fuseg ? G : H) * B), grid_q(((T_ + DQ_BQ - 1) / DQ_BQ) * H * B);
   const bool drop = p > 0.f;
   const BwdArgs a{qkv, o, dout, lse, delta, dkv_part, dqkv, T_, H, G, B, causal, drop_threshold16(p),
-                  drop_inv_keep(p), seed, offset, drop ? keep_mask : nullptr, rcos, rsin, s, ds_ws,
-                  attn_ds_tq_pad(T_), attn_ds_tk_pad(T_)};
+                  drop_inv_keep(p), seed, offset, drop ? keep_mask : nullptr, rcos, rsin, s};
   if (dt == DType::BF16) {
     if (hd == 128) launch_bwd<bf16_t, 128>(a, drop, fuseg, grid_q, grid_kv);
     else launch_bwd<bf16_t, 64>(a, drop, fuseg, grid_q, grid_kv);

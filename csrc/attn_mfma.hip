@@ -82,8 +82,12 @@ template <typename T> __device__ __forceinline__ uint32_t pack2(float a, float b
 // Per 64-key tile and wave: 32 MFMAs, 16 b128 + 32 tr_b64 LDS reads at loop-invariant
 // per-lane offsets, 2x(LD) saddr DMA issues with precomputed per-lane source offsets, and
 // ~130 VALU of online softmax (scale folded into the exp2 FMA; the O rescale is skipped when
-// no lane's running max moved, which is the common case after the first tiles).
-template <typename T, int HD, bool DROP, int FWD_BK, int NBUF, int OCC, bool PIPE = false>
+// no lane's running max moved, which is the common case after the first tiles).  The LDS
+// fragment reads run one MFMA step ahead (QK^T: both 32-key sub-tiles' next K fragments before
+// this step's pair of MFMAs, pinned by sched_barrier; PV: the next V^T fragment before each
+// MFMA): hipcc's own schedule waited on every read right before its MFMA (round 6, headline
+// forward +1.5 % same process, profiles/r6/attn/).
+template <typename T, int HD, bool DROP, int FWD_BK, int NBUF, int OCC>
 __global__ __launch_bounds__(256, OCC) void attn_fwd_mfma_k(const T* __restrict__ qkv, T* __restrict__ out,
                                                           float* __restrict__ lse, int T_, int H, int G, int B_,
                                                           bool causal, uint32_t thr, float inv_keep, uint64_t seed,
@@ -166,8 +170,10 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd_mfma_k(const T* __restrict_
   for (int dt = 0; dt < DT; ++dt) voff[dt] = v_off<HD>(4 * hh + qrow, dt * 32 + gl * 16 + pcol * 4);
   // DMA piece i of this lane: row P / CH, physical 16-B chunk P % CH (P = (w LD + i) 64 + lane);
   // the source chunk carries the image's XOR swizzle.  Recomputed at every issue from an opaque
-  // copy of the lane id (a few full-rate VALU): kept in VGPRs across the loop they were spilled
-  // at hd 128, and each scratch reload's vmcnt(0) serialised the DMA pieces.
+  // copy of the lane id (kept in VGPRs across the loop they were spilled at hd 128, and each
+  // scratch reload's vmcnt(0) serialised the DMA pieces); the full-tile path below splits P into
+  // a wave-uniform row (SGPR base) and the lane's row / chunk with unsigned shifts (23 VALU per
+  // 8 pieces instead of 61), this general form serves the sequence-tail tile.
   const uint32_t rs2 = (uint32_t)rs * 2u;  // row stride in bytes (< 2^24 for every shape)
   auto piece = [&](int i, int ln, int& r, int& kc16, int& vc16) {
     const int P = (w * LD + i) * 64 + ln;
@@ -194,7 +200,7 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd_mfma_k(const T* __restrict_
     const uint32_t base = smem_u + buf * 2 * TILE_B;
     int ln = lane;
     asm volatile("" : "+v"(ln));
-    if (PIPE && k0 + FWD_BK <= T_) {
+    if (k0 + FWD_BK <= T_) {
       // piece i of lane ln: row rb_i + lr (rb_i = (w LD + i) 64 / CH, wave-uniform, folded into the
       // SGPR base), chunk pc = ln % CH; unsigned shifts, and the V chunk does not depend on i
       const uint32_t lr = (uint32_t)ln / CH, pc = (uint32_t)ln % CH;
@@ -217,18 +223,6 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd_mfma_k(const T* __restrict_
         const uint32_t pd = (w * LD + i) * 1024;
         glds16s(ks, lro + kc16 * 16u, base + pd);
         glds16s(vs, lro + vc16 * 16u, base + TILE_B + pd);
-      }
-    } else if (k0 + FWD_BK <= T_) {
-      const void* ks = sgpr_ptr(kbase + (long)k0 * rs);
-      const void* vs = sgpr_ptr(vbase + (long)k0 * rs);
-#pragma unroll
-      for (int i = 0; i < LD; ++i) {
-        int r, kc16, vc16;
-        piece(i, ln, r, kc16, vc16);
-        const uint32_t ro = __umul24((uint32_t)r, rs2);
-        const uint32_t pd = (w * LD + i) * 1024;
-        glds16s(ks, ro + kc16 * 16, base + pd);
-        glds16s(vs, ro + vc16 * 16, base + TILE_B + pd);
       }
     } else {  // sequence tail: clamp rows (masked / multiplied by P = 0 later)
       char* kb = smem + buf * 2 * TILE_B;
@@ -290,7 +284,7 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd_mfma_k(const T* __restrict_
     constexpr bool EDGE = decltype(edge_c)::value;
     // ---- S^T = K Q^T for the visible 32-key sub-tiles; each K fragment feeds QB MFMAs
     f32x16 s[QB][NV];
-    if constexpr (PIPE) {
+    {
       // the NV sub-tiles' chains interleaved, K fragments of step kk+1 read before the MFMAs of
       // step kk: NV reads in flight under every MFMA pair instead of read -> wait -> MFMA
       v8 cur[NV];
@@ -318,18 +312,6 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd_mfma_k(const T* __restrict_
         if (kk + 1 < KK) {
 #pragma unroll
           for (int kt = 0; kt < NV; ++kt) cur[kt] = nxt[kt];
-        }
-      }
-    } else {
-#pragma unroll
-      for (int kt = 0; kt < NV; ++kt) {
-#pragma unroll
-        for (int u = 0; u < QB; ++u) s[u][kt] = f32x16{};
-#pragma unroll
-        for (int kk = 0; kk < KK; ++kk) {
-          const v8 kf = *reinterpret_cast<const v8*>(kb + kt * 32 * ROWB + koff[kk]);
-#pragma unroll
-          for (int u = 0; u < QB; ++u) s[u][kt] = MF<T>::mma(kf, qf[u][kk], s[u][kt]);
         }
       }
     }
@@ -367,7 +349,7 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd_mfma_k(const T* __restrict_
         m[u] = mn;
       }
       float ls = 0.f;
-      if constexpr (PIPE) {  // four partial sums: no 32-deep dependent add chain
+      {  // four partial sums: no 32-deep dependent add chain
         float l4[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int kt = 0; kt < NV; ++kt)
@@ -378,15 +360,6 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd_mfma_k(const T* __restrict_
             s[u][kt][r] = pv;
           }
         ls = (l4[0] + l4[1]) + (l4[2] + l4[3]);
-      } else {
-#pragma unroll
-        for (int kt = 0; kt < NV; ++kt)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const float pv = __builtin_amdgcn_exp2f(fmaf(s[u][kt][r], c, -m[u]));
-            ls += pv;
-            s[u][kt][r] = pv;
-          }
       }
       l[u] += ls;
       if constexpr (DROP) {
@@ -453,7 +426,7 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd_mfma_k(const T* __restrict_
       const s16x4 r2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(vb + off + 8 * ROWB));
       return __builtin_bit_cast(v8, __builtin_shufflevector(r1, r2, 0, 1, 2, 3, 4, 5, 6, 7));
     };
-    if constexpr (PIPE) {
+    {
       // one flat sequence of (kt, s2, dt) MFMAs with the next V^T fragment read before each one
       constexpr int NPV = NV * 2 * DT;
       v8 vcur = vread(0, 0, 0);
@@ -476,26 +449,6 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd_mfma_k(const T* __restrict_
         for (int u = 0; u < QB; ++u) o[u][dt] = MF<T>::mma(vcur, pf[u], o[u][dt]);
         if (i + 1 < NPV) vcur = vnxt;
       }
-    } else {
-#pragma unroll
-      for (int kt = 0; kt < NV; ++kt)
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) {
-          v8 pf[QB];
-#pragma unroll
-          for (int u = 0; u < QB; ++u) {
-            uint32_t uu[4];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) uu[j] = pack2<T>(s[u][kt][8 * s2 + 2 * j], s[u][kt][8 * s2 + 2 * j + 1]);
-            __builtin_memcpy(&pf[u], uu, 16);
-          }
-#pragma unroll
-          for (int dt = 0; dt < DT; ++dt) {
-            const v8 va = vread(kt, s2, dt);
-#pragma unroll
-            for (int u = 0; u < QB; ++u) o[u][dt] = MF<T>::mma(va, pf[u], o[u][dt]);
-          }
-        }
     }
   };
   using Ic1 = std::integral_constant<int, 1>;
@@ -578,21 +531,16 @@ void attn_fwd_mfma(DType dt, const void* qkv, void* o, float* lse, int B, int T_
   const uint32_t thr = drop_threshold16(p);
   const float ik = drop_inv_keep(p);
   const bool small = fwd_small_tiles(hd, p, (long)((T_ + FWD_BQ - 1) / FWD_BQ) * H * B);
-  const bool pipe = getenv("BLLM_FWD_PIPE") && atoi(getenv("BLLM_FWD_PIPE")) != 0;  // A/B (temporary)
-#define LAUNCH_P(TT, HDD, BK, NB, OC, PP)                                                                      \
+#define LAUNCH_V(TT, HDD, BK, NB, OC)                                                                      \
   do {                                                                                                        \
     const int lds = NB * 2 * BK * HDD * 2;                                                                    \
     const dim3 grid(((T_ + FWD_BQ - 1) / FWD_BQ) * H * B), block(256);                                        \
     if (p > 0.f)                                                                                              \
-      hipLaunchKernelGGL((attn_fwd_mfma_k<TT, HDD, true, BK, NB, OC, PP>), grid, block, lds, s,          \
+      hipLaunchKernelGGL((attn_fwd_mfma_k<TT, HDD, true, BK, NB, OC>), grid, block, lds, s,          \
                          (const TT*)qkv, (TT*)o, lse, T_, H, G, B, causal, thr, ik, seed, offset, keep_mask); \
     else                                                                                                      \
-      hipLaunchKernelGGL((attn_fwd_mfma_k<TT, HDD, false, BK, NB, OC, PP>), grid, block, lds, s,         \
+      hipLaunchKernelGGL((attn_fwd_mfma_k<TT, HDD, false, BK, NB, OC>), grid, block, lds, s,         \
                          (const TT*)qkv, (TT*)o, lse, T_, H, G, B, causal, thr, ik, seed, offset, nullptr); \
-  } while (0)
-#define LAUNCH_V(TT, HDD, BK, NB, OC)                                                                      \
-  do {                                                                                                        \
-    if (pipe) LAUNCH_P(TT, HDD, BK, NB, OC, true); else LAUNCH_P(TT, HDD, BK, NB, OC, false);             \
   } while (0)
 #define LAUNCH(TT, HDD)                                                                                       \
   do {                                                                                                        \
@@ -606,7 +554,6 @@ void attn_fwd_mfma(DType dt, const void* qkv, void* o, float* lse, int B, int T_
   }
 #undef LAUNCH
 #undef LAUNCH_V
-#undef LAUNCH_P
 }
 
 }  // namespace bllm

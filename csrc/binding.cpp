@@ -706,7 +706,7 @@ void set_gemm_tile_maps(int64_t wg_map, int64_t wg_gm, int64_t nt_map, int64_t n
 Tensor flash_attn_bwd(const Tensor& qkv, const Tensor& o, const Tensor& lse, const Tensor& dout, int64_t B,
                       int64_t T, int64_t H, int64_t G, int64_t hd, bool causal, double p, int64_t seed,
                       int64_t offset, const optional<Tensor>& keep_mask, const optional<Tensor>& rope_cos,
-                      const optional<Tensor>& rope_sin, bool store_ds) {
+                      const optional<Tensor>& rope_sin) {
   check_gpu(qkv, "qkv"); check_gpu(o, "o"); check_gpu(lse, "lse"); check_gpu(dout, "dout");
   c10::DeviceGuard g(qkv.device());
   TORCH_CHECK(qkv.scalar_type() == at::kBFloat16 || qkv.scalar_type() == at::kHalf ||
@@ -721,14 +721,10 @@ Tensor flash_attn_bwd(const Tensor& qkv, const Tensor& o, const Tensor& lse, con
   const bool mfma = qkv.scalar_type() != at::kFloat && bllm::attn_mfma_head_dim((int)hd);
   // per-query-head dK/dV partials only for GQA (MHA writes dK/dV directly); dQ is atomic-free
   auto dkv_part = (mfma && bllm::attn_bwd_kv_partials((int)B, (int)T, (int)H, (int)G)) ? at::empty({2, B * T, H, hd}, qkv.options().dtype(at::kFloat)) : Tensor();
-  // dS^T [B*H][Tk][Tq] (16-bit, transient): the dK/dV pass stores dS, dQ = dS K reads it back
-  auto ds_ws = (mfma && store_ds) ? at::empty({B * H * (int64_t)bllm::attn_ds_tk_pad((int)T) * bllm::attn_ds_tq_pad((int)T)},
-                                              qkv.options()) : Tensor();
   bllm::attn_bwd(dt_of(qkv), qkv.data_ptr(), o.data_ptr(), lse.data_ptr<float>(), dout.data_ptr(), dqkv.data_ptr(),
                  delta.data_ptr<float>(), nullptr, dkv_part.defined() ? dkv_part.data_ptr<float>() : nullptr, (int)B, (int)T, (int)H, (int)G, (int)hd, causal,
                  (float)p, (uint64_t)seed, (uint64_t)offset, keep_mask_ptr(keep_mask, qkv, B, T, H, hd, p),
-                 rope_ptr(rope_cos, qkv, T, hd), rope_ptr(rope_sin, qkv, T, hd), stream(),
-                 ds_ws.defined() ? ds_ws.data_ptr() : nullptr);
+                 rope_ptr(rope_cos, qkv, T, hd), rope_ptr(rope_sin, qkv, T, hd), stream());
   return dqkv;
 }
 
@@ -1182,7 +1178,7 @@ TORCH_LIBRARY(bllm, m) {
   m.def("attn_decode_append(Tensor qkv, Tensor(a!) kcache, Tensor(b!) vcache, Tensor pos, int H, int G) -> Tensor");
   m.def("rope_dev_(Tensor(a!) qkv, Tensor cos, Tensor sin, int H, int G, int hd, Tensor pos) -> ()");
   m.def("flash_attn_fwd(Tensor qkv, int B, int T, int H, int G, int hd, bool causal, float p, int seed, int offset, Tensor(a!)? keep_mask=None) -> (Tensor, Tensor)");
-  m.def("flash_attn_bwd(Tensor qkv, Tensor o, Tensor lse, Tensor dout, int B, int T, int H, int G, int hd, bool causal, float p, int seed, int offset, Tensor? keep_mask=None, Tensor? rope_cos=None, Tensor? rope_sin=None, bool store_ds=True) -> Tensor");
+  m.def("flash_attn_bwd(Tensor qkv, Tensor o, Tensor lse, Tensor dout, int B, int T, int H, int G, int hd, bool causal, float p, int seed, int offset, Tensor? keep_mask=None, Tensor? rope_cos=None, Tensor? rope_sin=None) -> Tensor");
   m.def("ce_fwd(Tensor logits, Tensor targets, int ignore_index) -> (Tensor, Tensor)");
   m.def("ce_bwd_(Tensor(a!) logits, Tensor targets, Tensor lse, Tensor scale, int ignore_index) -> ()");
   m.def("embedding_fwd(Tensor idx, Tensor wte, Tensor? wpe, int T, float p, int seed, int offset) -> Tensor");

@@ -128,6 +128,10 @@ def test_bench_world8_self_diagnosing_fields(parallel):
     dc = out["data_check"]
     assert dc["sampler"] == "DistributedSampler" and dc["disjoint_across_ranks"] is True
     assert dc["windows_per_rank_used"] == 2 * 3    # micro-batch 2 x (1 warm-up + 2 timed steps)
+    # the warm-up step's collectives were compared across the 8 ranks (parallel/seqcheck.py)
+    oc = out["comm"]["order_check"]
+    assert oc["enabled"] and oc["calls_checked_rank0"] > 0 and oc["steps"] == 1
+    assert "rccl_topology" not in out       # gloo: nothing to capture
 
 
 def test_bench_random_ids_arm():

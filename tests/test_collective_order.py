@@ -99,3 +99,23 @@ def test_disabled_without_process_group():
     with seq.recording("x"):
         pass
     assert seq.verify("x") == 0
+
+
+def test_rccl_topology_parser(tmp_path):
+    """bench.py's ``rccl_topology``: RCCL's INIT/GRAPH log lines -> ranks, channel counts, ring /
+    tree examples and the algorithm-related lines."""
+    from building_llm_from_scratch_amd.utils.telemetry import rccl_topology
+    log = tmp_path / "r0.log"
+    log.write_text("h:1:1 [0] NCCL INFO comm 0x1 rank 0 nRanks 8 nNodes 1 localRanks 8 localRank 0 MNNVL 0\n"
+                   "h [0] NCCL INFO Channel 00/16 : 0 1 2 3 4 5 6 7\n"
+                   "h [0] NCCL INFO Channel 01/16 : 0 2 4 6 1 3 5 7\n"
+                   "h [0] NCCL INFO Tree 0 : -1 -> 0 -> 1/-1/-1\n"
+                   "h [0] NCCL INFO 16 coll channels, 16 collnet channels, 0 nvls channels, 16 p2p channels, "
+                   "2 p2p channels per peer\n"
+                   "h [0] NCCL INFO Connected all rings\n"
+                   "unrelated line\n")
+    t = rccl_topology(str(log))
+    assert t["n_ranks"] == 8 and t["local_ranks"] == 8 and t["channels"] == 16
+    assert t["coll_channels"] == 16 and t["p2p_channels"] == 16 and t["trees"] == 1
+    assert len(t["rings"]) == 2 and t["decisions"] == ["Connected all rings"]
+    assert rccl_topology(str(tmp_path / "missing.log")) is None

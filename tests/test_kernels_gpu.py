@@ -358,32 +358,6 @@ def test_flash_attention_keep_mask_fused_gqa(hd):
     test_flash_attention_keep_mask(hd, 128, 128, 16, 8, True)
 
 
-@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
-@pytest.mark.parametrize("B,T,H,G,hd", [(2, 200, 4, 4, 128), (1, 300, 8, 2, 128), (2, 33, 4, 2, 64),
-                                         (3, 129, 4, 4, 64), (1, 1024, 8, 2, 128), (128, 128, 16, 8, 64)])
-@pytest.mark.parametrize("p", [0.0, 0.1])
-@pytest.mark.parametrize("causal", [True, False])
-def test_flash_attention_bwd_stored_ds(dt, B, T, H, G, hd, p, causal):
-    """The stored-dS backward: the dK/dV kernel stores dS^T and dQ = dS K reads it back
-    (csrc/attn_bwd_mfma.hip attn_bwd_dq_ds_k) instead of recomputing S and dP.  The dS^T workspace
-    comes from the caching allocator: a NaN-filled block is freed first so that any (key, q) the
-    dQ pass read without the dK/dV pass having written it would poison dQ.  Against the fp32
-    oracle, and against the recomputing dQ kernel (store_ds=False)."""
-    nan = torch.full((B * H * ((T + 63) // 64 * 64) * ((T + 127) // 128 * 128) + (1 << 20),), float("nan"),
-                     device=DEV, dtype=dt)
-    del nan
-    qkv = torch.randn(B * T, (H + 2 * G) * hd, device=DEV).to(dt)
-    do = torch.randn(B * T, H * hd, device=DEV).to(dt)
-    o, lse = ops.flash_attn_fwd(qkv, B, T, H, G, hd, causal, p, 5, 77)
-    d_ds = ops.flash_attn_bwd(qkv, o, lse, do, B, T, H, G, hd, causal, p, 5, 77, store_ds=True)
-    assert torch.isfinite(d_ds).all()
-    d_rc = ops.flash_attn_bwd(qkv, o, lse, do, B, T, H, G, hd, causal, p, 5, 77, store_ds=False)
-    want = ref.flash_attn_bwd(qkv.cpu().float(), o.cpu().float(), lse.cpu(), do.cpu().float(), B, T, H, G, hd,
-                              causal, p, 5, 77)
-    _close(d_ds, want, dt, 4, name="stored dS vs oracle")
-    _close(d_rc, want, dt, 4, name="recompute vs oracle")
-
-
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16, torch.float32])
 @pytest.mark.parametrize("B,T,H,G,hd", [(2, 200, 4, 4, 128),     # MHA: dK written by the dK/dV kernel
                                          (1, 300, 8, 2, 128),     # GQA: fp32 partials + reduce kernel

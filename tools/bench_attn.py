@@ -41,9 +41,6 @@ def main():
     ap.add_argument("--bwd_env_ab", default="",
                     help="NAME=v1,v2,...: time the backward under each value of env NAME (a kernel knob read per "
                          "launch), interleaved, and report dqkv's max difference from the first value's")
-    ap.add_argument("--ds_ab", action="store_true",
-                    help="time the backward with the stored-dS dQ pass (default) and the recomputing dQ kernel, "
-                         "interleaved, and report dqkv's max difference")
     ap.add_argument("--no_mask", action="store_true",
                     help="dropout shapes: re-hash the keep bits in backward instead of reading the forward's mask")
     a = ap.parse_args()
@@ -69,8 +66,7 @@ def main():
         km = None if a.no_mask else ops.attn_keep_mask(qkv, B, T, H, hd, p)
         o, lse = ops.flash_attn_fwd(qkv, B, T, H, G, hd, causal, p, 1, 0, keep_mask=km)
         tf = timeit(lambda: ops.flash_attn_fwd(qkv, B, T, H, G, hd, causal, p, 1, 0, keep_mask=km), a.iters)
-        tb = timeit(lambda: ops.flash_attn_bwd(qkv, o, lse, do, B, T, H, G, hd, causal, p, 1, 0, keep_mask=km),
-                    a.iters)
+        tb = timeit(lambda: ops.flash_attn_bwd(qkv, o, lse, do, B, T, H, G, hd, causal, p, 1, 0, keep_mask=km), a.iters)
         flop = 2 * 2 * B * H * T * T * hd / (2 if causal else 1)  # two matmuls (causal: half the square)
         if a.variants:
             arms = [("default", {})] + [(vd.split(":", 1)[0], dict(e.split("=", 1) for e in vd.split(":", 1)[1].split("+") if e))
@@ -118,22 +114,6 @@ def main():
             ref0 = outs[vals[0]].float()
             print(json.dumps(dict(shape=name, ab=nm, bwd_ms={v: round(sorted(ts)[1], 4) for v, ts in tt.items()},
                                   max_abs_dqkv={v: float((x.float() - ref0).abs().max()) for v, x in outs.items()})),
-                  flush=True)
-        if a.ds_ab:
-            tt, outs = {}, {}
-            for rnd in range(3):
-                for arm in (True, False):
-                    tt.setdefault(arm, []).append(timeit(
-                        lambda: ops.flash_attn_bwd(qkv, o, lse, do, B, T, H, G, hd, causal, p, 1, 0, keep_mask=km,
-                                                   store_ds=arm), a.iters))
-                    outs[arm] = ops.flash_attn_bwd(qkv, o, lse, do, B, T, H, G, hd, causal, p, 1, 0, keep_mask=km,
-                                                   store_ds=arm)
-            med = {k: sorted(v)[1] for k, v in tt.items()}
-            print(json.dumps(dict(shape=name, ab="store_ds", bwd_ms_ds=round(med[True], 4),
-                                  bwd_ms_recompute=round(med[False], 4),
-                                  tflops_5mm_ds=round(2.5 * flop / med[True] / 1e9, 1),
-                                  tflops_5mm_recompute=round(2.5 * flop / med[False] / 1e9, 1),
-                                  max_abs_dqkv=float((outs[True].float() - outs[False].float()).abs().max()))),
                   flush=True)
         res.append(dict(shape=name, B=B, T=T, causal=causal, keep_mask=km is not None, fwd_ms=round(tf, 4), bwd_ms=round(tb, 4),
                         fwd_tflops=round(flop / tf / 1e9, 1), bwd_tflops_5mm=round(2.5 * flop / tb / 1e9, 1)))

@@ -9,7 +9,7 @@ tail -2 gpurun_out/r6ds2/tests_pipe.log
 S=llama3-8B-B40,gpt2-774M-B64,gpt2-774M-B64-nodrop,llama3.2-1B-B24
 timeout -k 10 300 python -u tools/bench_attn.py --shapes $S --env_ab BLLM_FWD_PIPE > gpurun_out/r6ds2/fwd_pipe.jsonl 2>&1 || { tail -5 gpurun_out/r6ds2/fwd_pipe.jsonl; exit 5; }
 grep '"ab"' gpurun_out/r6ds2/fwd_pipe.jsonl
-timeout -k 10 300 python -u tools/bench_attn.py --shapes $S --bwd_env_ab BLLM_DQDS=0,1,2 > gpurun_out/r6ds2/dqds.jsonl 2>&1 || { tail -5 gpurun_out/r6ds2/dqds.jsonl; exit 6; }
+timeout -k 10 300 python -u tools/bench_attn.py --shapes $S --bwd_env_ab BLLM_DQDS=0,1,2 --store_ds > gpurun_out/r6ds2/dqds.jsonl 2>&1 || { tail -5 gpurun_out/r6ds2/dqds.jsonl; exit 6; }
 grep '"ab"' gpurun_out/r6ds2/dqds.jsonl
 timeout -k 10 300 python -u tools/bench_attn.py --shapes $S --ds_ab > gpurun_out/r6ds2/ds_ab.jsonl 2>&1 || { tail -5 gpurun_out/r6ds2/ds_ab.jsonl; exit 7; }
 grep store_ds gpurun_out/r6ds2/ds_ab.jsonl
