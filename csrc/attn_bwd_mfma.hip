@@ -893,7 +893,10 @@ static void launch_bwd(const BwdArgs& a, bool drop, bool fuseg, dim3 grid_q, dim
     if (fuseg) launch_kv<TT, HDD, 2, 2, true, true, true>(a, drop, grid_kv);
     else launch_kv<TT, HDD, 2, 2, false, true, true>(a, drop, grid_kv);
   } else {
-    if (drop && a.kmask && !fuseg) launch_kv<TT, HDD, 4, 2, false, true>(a, drop, grid_kv);
+    // keep-mask dual-image variant at a launch bound of 3 workgroups per CU (168 VGPRs, 3 waves
+    // per SIMD instead of 2 at 170): GPT2-774M B=64 backward 1.260 -> 1.195 ms, B=24 0.448 ->
+    // 0.417 (profiles/r6/attn/occ_ab.jsonl)
+    if (drop && a.kmask && !fuseg) launch_kv<TT, HDD, 4, 3, false, true>(a, drop, grid_kv);
     else if (fuseg) launch_kv<TT, HDD, 2, 2, true, false>(a, drop, grid_kv);
     else launch_kv<TT, HDD, 2, 2, false, false>(a, drop, grid_kv);
   }
