@@ -1,9 +1,9 @@
 #!/usr/bin/env python3
 """One parametrised runner for GPU-box jobs (replaces the per-experiment shell scripts).
 
-    gpurun --timeout 900 -- python tools/jobs/gpu_job.py tests smoke bench
-    gpurun -- python tools/jobs/gpu_job.py bench --set batch=32 --tag b32
-    gpurun -- python tools/jobs/gpu_job.py prof --set preset=gpt2_774m_ddp
+    gpurun --timeout 900 -- python tools/gpu_job.py tests smoke bench
+    gpurun -- python tools/gpu_job.py bench --set batch=32 --tag b32
+    gpurun -- python tools/gpu_job.py prof --set preset=gpt2_774m_ddp
 
 Each recipe is a list of steps; every step runs under its own ``timeout -k 10 <s>``, its output
 goes to ``gpurun_out/<tag>/<step>.log`` and is streamed to stdout as it comes (so a long step

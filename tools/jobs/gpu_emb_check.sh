@@ -6,5 +6,5 @@ tail -2 gpurun_out/emb/tests.log
 timeout -k 10 300 python -u bench.py --preset gpt2_774m_ddp --steps 10 --warmup 3 > gpurun_out/emb/gpt2.log 2>&1 || exit 4
 timeout -k 10 300 python -u bench.py --steps 10 --warmup 3 > gpurun_out/emb/headline.log 2>&1 || exit 5
 grep -ho '"metric": "[^"]*", "value": [0-9.]*' gpurun_out/emb/*.log
-python tools/jobs/gpu_job.py prof --set preset=gpt2_774m_ddp --set kgrep=emb --tag emb_prof > /dev/null 2>&1 || exit 6
+python tools/gpu_job.py prof --set preset=gpt2_774m_ddp --set kgrep=emb --tag emb_prof > /dev/null 2>&1 || exit 6
 cat gpurun_out/emb_prof/kstats.log; head -16 gpurun_out/emb_prof/breakdown.log

@@ -6,5 +6,5 @@ tail -2 gpurun_out/head/tests.log
 timeout -k 10 300 python -u bench.py --preset gpt2_774m_ddp --steps 10 --warmup 3 > gpurun_out/head/gpt2_1.log 2>&1 || exit 4
 timeout -k 10 300 python -u bench.py --preset gpt2_774m_ddp --steps 10 --warmup 3 > gpurun_out/head/gpt2_2.log 2>&1 || exit 5
 grep -o '"value": [0-9.]*' gpurun_out/head/gpt2_*.log
-python tools/jobs/gpu_job.py prof --set preset=gpt2_774m_ddp --set kgrep=Cijk --tag head_prof > /dev/null 2>&1 || exit 6
+python tools/gpu_job.py prof --set preset=gpt2_774m_ddp --set kgrep=Cijk --tag head_prof > /dev/null 2>&1 || exit 6
 cat gpurun_out/head_prof/kstats.log; head -12 gpurun_out/head_prof/breakdown.log

@@ -9,5 +9,5 @@ timeout -k 10 300 python -u bench.py --preset llama32_1b_lora_alpaca --steps 10 
 BLLM_LORA_KAUG=0 timeout -k 10 300 python -u bench.py --preset llama32_1b_lora_alpaca --steps 10 --warmup 3 > gpurun_out/l2/lora_nokaug_$i.log 2>&1 || exit 6
 done
 grep -o '"value": [0-9.]*' gpurun_out/l2/lora_*.log
-python tools/jobs/gpu_job.py prof --set preset=llama32_1b_lora_alpaca --set kgrep=lora --tag l2_prof > /dev/null 2>&1 || exit 7
+python tools/gpu_job.py prof --set preset=llama32_1b_lora_alpaca --set kgrep=lora --tag l2_prof > /dev/null 2>&1 || exit 7
 cat gpurun_out/l2_prof/kstats.log; head -20 gpurun_out/l2_prof/breakdown.log

@@ -7,5 +7,5 @@ timeout -k 10 200 python tools/bench_lora.py --iters 20 > gpurun_out/l3/bench_lo
 timeout -k 10 300 python -u bench.py --preset llama32_1b_lora_alpaca --steps 10 --warmup 3 > gpurun_out/l3/lora_1.log 2>&1 || exit 5
 timeout -k 10 300 python -u bench.py --preset llama32_1b_lora_alpaca --steps 10 --warmup 3 > gpurun_out/l3/lora_2.log 2>&1 || exit 6
 grep -o '"value": [0-9.]*' gpurun_out/l3/lora_*.log
-python tools/jobs/gpu_job.py prof --set preset=llama32_1b_lora_alpaca --set kgrep=lora --tag l3_prof > /dev/null 2>&1 || exit 7
+python tools/gpu_job.py prof --set preset=llama32_1b_lora_alpaca --set kgrep=lora --tag l3_prof > /dev/null 2>&1 || exit 7
 cat gpurun_out/l3_prof/kstats.log; head -8 gpurun_out/l3_prof/breakdown.log

@@ -7,8 +7,8 @@ timeout -k 10 300 python -u bench.py --preset llama32_1b_lora_alpaca --steps 10 
 BLLM_LORA_KAUG=0 timeout -k 10 300 python -u bench.py --preset llama32_1b_lora_alpaca --steps 10 --warmup 3 > gpurun_out/ab/lora_nokaug_$i.log 2>&1 || exit 4
 done
 grep -o '"value": [0-9.]*' gpurun_out/ab/lora_*.log
-python tools/jobs/gpu_job.py prof --set preset=llama32_1b_lora_alpaca --tag ab_prof_lora > /dev/null 2>&1 || exit 5
-python tools/jobs/gpu_job.py prof --set preset=gpt2_774m_ddp --tag ab_prof_gpt2 > /dev/null 2>&1 || exit 6
+python tools/gpu_job.py prof --set preset=llama32_1b_lora_alpaca --tag ab_prof_lora > /dev/null 2>&1 || exit 5
+python tools/gpu_job.py prof --set preset=gpt2_774m_ddp --tag ab_prof_gpt2 > /dev/null 2>&1 || exit 6
 head -24 gpurun_out/ab_prof_lora/breakdown.log
 head -24 gpurun_out/ab_prof_gpt2/breakdown.log
 for i in 1 2; do

@@ -14,6 +14,6 @@ timeout -k 10 300 python -u bench.py --preset gpt2_774m_ddp --steps 10 --warmup 
 timeout -k 10 300 python -u bench.py --preset gpt2_774m_ddp --steps 10 --warmup 3 --tunableop gpurun_out/lk/gpt20.csv > gpurun_out/lk/gpt2_tuned_$i.log 2>&1 || exit 9
 done
 grep -o '"value": [0-9.]*' gpurun_out/lk/gpt2_*.log
-python tools/jobs/gpu_job.py prof --set preset=llama32_1b_lora_alpaca --tag lk_prof_lora > /dev/null 2>&1 || exit 10
-python tools/jobs/gpu_job.py prof --set preset=gpt2_774m_ddp --tag lk_prof_gpt2 > /dev/null 2>&1 || exit 11
+python tools/gpu_job.py prof --set preset=llama32_1b_lora_alpaca --tag lk_prof_lora > /dev/null 2>&1 || exit 10
+python tools/gpu_job.py prof --set preset=gpt2_774m_ddp --tag lk_prof_gpt2 > /dev/null 2>&1 || exit 11
 head -30 gpurun_out/lk_prof_lora/breakdown.log

@@ -11,6 +11,6 @@ for r in 1 2; do
     echo "down=$f round=$r $(tail -1 gpurun_out/lorak/lora_${f}_$r.log | grep -o '"value": [0-9.]*\|"sclk_mhz_avg": [0-9.]*' | tr '\n' ' ')"
   done
 done
-timeout -k 10 600 python tools/jobs/gpu_job.py prof --set preset=llama32_1b_lora_alpaca --tag lorak/prof > /dev/null 2>&1 || exit 6
+timeout -k 10 600 python tools/gpu_job.py prof --set preset=llama32_1b_lora_alpaca --tag lorak/prof > /dev/null 2>&1 || exit 6
 head -8 gpurun_out/lorak/prof/breakdown.log
 cat gpurun_out/lorak/micro.jsonl

@@ -12,6 +12,6 @@ for r in 1 2; do
     echo "fused=$f round=$r $(tail -1 gpurun_out/loraswi/b_${f}_$r.log | grep -o '"value": [0-9.]*\|"sclk_mhz_avg": [0-9.]*' | tr '\n' ' ')"
   done
 done
-timeout -k 10 900 python tools/jobs/gpu_job.py prof --set preset=llama32_1b_lora_alpaca --tag loraswi/prof > /dev/null 2>&1 || exit 5
+timeout -k 10 900 python tools/gpu_job.py prof --set preset=llama32_1b_lora_alpaca --tag loraswi/prof > /dev/null 2>&1 || exit 5
 grep -i "lora\|swiglu" gpurun_out/loraswi/prof/kstats.log
 head -20 gpurun_out/loraswi/prof/breakdown.log

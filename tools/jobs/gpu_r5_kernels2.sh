@@ -14,7 +14,7 @@ for r in 1 2; do
 done
 timeout -k 10 400 python -u bench.py --steps 20 --warmup 5 > gpurun_out/k2/headline.log 2>&1 || { tail -20 gpurun_out/k2/headline.log; exit 5; }
 echo "headline $(tail -1 gpurun_out/k2/headline.log | grep -o '"value": [0-9.]*\|"sclk_mhz_avg": [0-9.]*' | tr '\n' ' ')"
-timeout -k 10 600 python tools/jobs/gpu_job.py prof --set preset=llama32_1b_lora_alpaca --tag k2/prof_lora > /dev/null 2>&1 || exit 6
-timeout -k 10 600 python tools/jobs/gpu_job.py prof --tag k2/prof_llama > /dev/null 2>&1 || exit 7
+timeout -k 10 600 python tools/gpu_job.py prof --set preset=llama32_1b_lora_alpaca --tag k2/prof_lora > /dev/null 2>&1 || exit 6
+timeout -k 10 600 python tools/gpu_job.py prof --tag k2/prof_llama > /dev/null 2>&1 || exit 7
 grep -i "swiglu\|lora_wgrad" gpurun_out/k2/prof_lora/kstats.log gpurun_out/k2/prof_llama/kstats.log
 head -14 gpurun_out/k2/prof_llama/breakdown.log
