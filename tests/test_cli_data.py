@@ -464,3 +464,25 @@ def test_trainer_reuses_loaders_across_epochs(tmp_path):
         assert len(got) == len(ref) == 9
         assert all(torch.equal(a, b) for a, b in zip(got, ref)), epoch
     assert not all(a.shape == b.shape and torch.equal(a, b) for a, b in zip(seen[0], seen[1]))   # reshuffled
+
+
+def test_gemm_epilogues_flag(tmp_path, monkeypatch):
+    """``--gemm_epilogues`` turns on the three fused forward epilogues (gate/up + SwiGLU, QKV +
+    RoPE, c_fc + bias + GELU on csrc/gemm_nt.hip); off by default (measured slower, README)."""
+    import torch
+    from building_llm_from_scratch_amd.builder import build_model as build_model_
+    from building_llm_from_scratch_amd.config import get_config
+    from building_llm_from_scratch_amd.models import linear
+    for k in ("FUSED_SWIGLU", "FUSED_ROPE", "FUSED_GELU"):
+        monkeypatch.setattr(linear, k, False)
+    cfg = get_config("llama3_2", "1B").replace(context_length=16, emb_dim=32, n_heads=2, n_kv_groups=1,
+                                                hidden_dim=48, n_layers=1, vocab_size=97, dtype=torch.float32)
+    a = cli.get_args(["--data_dir", str(tmp_path), "--model", "llama3_2", "--num_params", "1B", "--device", "cpu"])
+    a.world_size = 1
+    build_model_(cfg, 0, torch.device("cpu"), a)
+    assert not (linear.FUSED_SWIGLU or linear.FUSED_ROPE or linear.FUSED_GELU)
+    a = cli.get_args(["--data_dir", str(tmp_path), "--model", "llama3_2", "--num_params", "1B", "--device", "cpu",
+                      "--gemm_epilogues"])
+    a.world_size = 1
+    build_model_(cfg, 0, torch.device("cpu"), a)
+    assert linear.FUSED_SWIGLU and linear.FUSED_ROPE and linear.FUSED_GELU
