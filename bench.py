@@ -118,9 +118,10 @@ def parse(argv=None):
                     help="FSDP units all-gathered ahead (0 = auto: gather time over xGMI vs unit compute)")
     ap.add_argument("--layers", type=int, default=None, help="(debug only) override n_layers; invalidates the metric")
     ap.add_argument("--profile", action="store_true", help="print a per-phase timing breakdown to stderr")
-    ap.add_argument("--gemm_epilogues", action="store_true",
+    ap.add_argument("--gemm_epilogues", nargs="?", const="swiglu,rope,gelu", default="",
                     help="gate/up + SwiGLU, QKV + RoPE, c_fc + bias + GELU on csrc/gemm_nt.hip's fused-epilogue "
-                         "kernel instead of the library GEMM + a separate pass (measured slower, A/B)")
+                         "kernel instead of the library GEMM + a separate pass (measured slower, A/B); "
+                         "bare flag = all three, or a comma list of swiglu,rope,gelu")
     ap.add_argument("--overlap_optimizer", action="store_true",
                     help="run AdamW on a side HIP stream under the next forward")
     ap.add_argument("--data", default=None, choices=["pretrain", "random_ids", "fixed_ids", "alpaca"],
@@ -364,7 +365,7 @@ def main(argv=None):
     cfg = build_config(a, dev)
     if a.gemm_epilogues:
         from building_llm_from_scratch_amd.models.linear import use_gemm_epilogues
-        use_gemm_epilogues(True)
+        use_gemm_epilogues([e for e in a.gemm_epilogues.split(",") if e])
     torch.manual_seed(123)
     plan = None
     ckpt_mode = "selective" if a.actv_ckpt == "auto" else a.actv_ckpt
@@ -610,7 +611,7 @@ def main(argv=None):
                 "optimizer": "AdamW fp32 master, wd 0.1, clip 1.0",
                 "gemm_tuning": (os.path.relpath(a.tunableop, os.path.dirname(os.path.abspath(__file__)))
                                 if a.tunableop else None),
-                "gemm_epilogues": bool(a.gemm_epilogues),
+                "gemm_epilogues": a.gemm_epilogues or None,
             },
             "mfu": round(mfu, 4),
             "hfu": round(mfu * recompute, 4),

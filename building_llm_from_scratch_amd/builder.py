@@ -80,9 +80,9 @@ def plan_checkpointing(config, args, device, world: int = 1):
 
 def build_model(config, rank, device, args):
     misc.start_memory_tracking()
-    if getattr(args, "gemm_epilogues", False):
+    if getattr(args, "gemm_epilogues", ""):
         from .models.linear import use_gemm_epilogues
-        use_gemm_epilogues(True)
+        use_gemm_epilogues([e for e in args.gemm_epilogues.split(",") if e])
     ckpt = getattr(args, "actv_ckpt_mode", None) or ("full" if args.use_actv_ckpt else "none")
     plan = None
     if ckpt == "auto":

@@ -92,9 +92,10 @@ def build_parser() -> argparse.ArgumentParser:
                         "measured peak) -- the headline bench's policy")
     x.add_argument("--ckpt_budget_gib", type=float, default=None,
                    help="auto mode: per-rank peak-memory ceiling (default 250 GiB, capped at device - 18 GiB)")
-    x.add_argument("--gemm_epilogues", action="store_true",
+    x.add_argument("--gemm_epilogues", nargs="?", const="swiglu,rope,gelu", default="",
                    help="gate/up + SwiGLU, QKV + RoPE and c_fc + bias + GELU on the fused-epilogue GEMM kernel "
-                        "(csrc/gemm_nt.hip) instead of the library GEMM + a separate pass; measured slower on MI355X")
+                        "(csrc/gemm_nt.hip) instead of the library GEMM + a separate pass; measured slower on "
+                        "MI355X; bare flag = all three, or a comma list of swiglu,rope,gelu")
     x.add_argument("--actv_ckpt_segments", type=int, default=None,
                    help="full mode: checkpoint_sequential segments (default n_layers = reference); "
                         "fewer segments recompute fewer blocks for more memory")

@@ -192,10 +192,18 @@ FUSED_ROPE = False
 FUSED_GELU = False
 
 
-def use_gemm_epilogues(on: bool) -> None:
-    """Route the gate/up, QKV and c_fc projections through the fused-epilogue kernels."""
+GEMM_EPILOGUES = ("swiglu", "rope", "gelu")
+
+
+def use_gemm_epilogues(on=True) -> None:
+    """Route the gate/up (``swiglu``), QKV (``rope``) and c_fc (``gelu``) projections through the
+    fused-epilogue kernels: ``True`` / ``False`` for all three, or an iterable of names."""
     global FUSED_SWIGLU, FUSED_ROPE, FUSED_GELU
-    FUSED_SWIGLU = FUSED_ROPE = FUSED_GELU = bool(on)
+    names = set(GEMM_EPILOGUES) if on is True else set() if on is False or on is None else set(on)
+    bad = names - set(GEMM_EPILOGUES)
+    if bad:
+        raise ValueError(f"unknown GEMM epilogue(s) {sorted(bad)}; choose from {GEMM_EPILOGUES}")
+    FUSED_SWIGLU, FUSED_ROPE, FUSED_GELU = "swiglu" in names, "rope" in names, "gelu" in names
 
 
 class FusedLinear:
