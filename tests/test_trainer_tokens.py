@@ -78,3 +78,41 @@ def test_world2_pretrain_tokens_exact():
     res = _run("pretrain")
     (m0, t0, _), (m1, t1, _) = res[0], res[1]
     assert t0 == t1 == m0 + m1, res
+
+
+def test_shutdown_loader_stops_persistent_workers():
+    """a multi-file run rebuilds each file's loaders per epoch; the finished file's
+    persistent workers are shut down at once instead of at garbage collection."""
+    from torch.utils.data import DataLoader
+    from building_llm_from_scratch_amd.train.trainer import _shutdown_loader
+    dl = DataLoader(list(range(32)), batch_size=4, num_workers=2, persistent_workers=True)
+    assert sum(1 for _ in dl) == 8
+    workers = list(dl._iterator._workers)
+    assert workers and all(w.is_alive() for w in workers)
+    _shutdown_loader(dl)
+    for w in workers:
+        w.join(timeout=10)
+    assert not any(w.is_alive() for w in workers)
+    assert dl._iterator is None
+
+
+def test_resume_state_records_data_order_version(caplog):
+    """the resume state carries the data-order version; a state written by an older
+    build (no version) still loads, with a warning that the batch order after it differs."""
+    import logging
+    from building_llm_from_scratch_amd.train.trainer import Trainer
+    cfg = get_config("llama3_2", "1B").replace(context_length=16, emb_dim=32, n_heads=2, n_kv_groups=1,
+                                                hidden_dim=48, n_layers=1, vocab_size=97, dtype=torch.float32)
+    m = build_model(cfg)
+    opt = FusedAdamW(m, lr=1e-3, weight_decay=0.0)
+    tr = Trainer(m, opt, cfg, [], SimpleNamespace(batch_size=2, tokenizer=None), "/tmp")
+    st = tr.trainer_state()
+    assert st["data_order_version"] == Trainer.DATA_ORDER_VERSION
+    old = dict(st)
+    old.pop("data_order_version")
+    tr2 = Trainer(m, opt, cfg, [], SimpleNamespace(batch_size=2, tokenizer=None), "/tmp")
+    logging.getLogger("train").propagate = True
+    with caplog.at_level(logging.WARNING):
+        tr2.load_trainer_state(old)
+    assert tr2.pos == tuple(st["pos"])
+    assert any("data-order version" in r.getMessage() for r in caplog.records)
