@@ -66,6 +66,12 @@ def _run(cmd, obj, flags):
     return obj, r.stderr
 
 
+# per-file compiler flags: the attention kernels' softmax must stay scalar f32 -- the SLP
+# vectorizer's v_pk_add / v_pk_mul beside MFMAs cost issue cycles (MI355X_MICROARCH.md, packed f32
+# VALU "an anti-lever beside MFMAs")
+FILE_FLAGS = {"attn_mfma.hip": ["-fno-slp-vectorize"]}
+
+
 def build(jobs: int = 8, clean: bool = False, debug: bool = False, verbose: bool = False) -> str:
     hipcc = _hipcc()
     tdir, tinc, tlib, abi = _torch_paths()
@@ -84,7 +90,7 @@ def build(jobs: int = 8, clean: bool = False, debug: bool = False, verbose: bool
         src = os.path.join(CSRC, f)
         if f.endswith(".hip"):
             obj = os.path.join(bdir, f + ".o")
-            cmd = [hipcc] + common + ["-c", src, "-o", obj]
+            cmd = [hipcc] + common + FILE_FLAGS.get(f, []) + ["-c", src, "-o", obj]
         elif f.endswith(".cpp"):
             obj = os.path.join(bdir, f + ".o")
             py_inc = sysconfig.get_paths()["include"]
