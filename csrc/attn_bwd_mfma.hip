@@ -178,7 +178,7 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_mfma_k(const T* __restrict_
                                                             uint64_t seed, uint64_t doff,
                                                             const uint32_t* __restrict__ kmask,
                                                             const float* __restrict__ rcos,
-                                                            const float* __restrict__ rsin) {
+                                                            const float* __restrict__ rsin, int xmap) {
   typedef typename MFb<T>::v8 v8;
   constexpr int KK = HD / 16, DT = HD / 32, CH = HD / 8, ROWB = HD * 2;
   constexpr int IMG = BWD_BQ * ROWB;            // bytes of one [32][HD] image
@@ -194,7 +194,8 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_mfma_k(const T* __restrict_
   // heaviest (lowest) key block first across the whole grid; all key blocks of one (b, h)
   // share lin % 8, i.e. one XCD and its L2 (Q / dO re-reads hit there)
   const int lin = blockIdx.x, nbh = (FUSEG ? G : H) * B_;
-  const int kb = lin / nbh, bh = lin - kb * nbh;
+  int kb, bh;
+  attn_wg_order(lin, nbh, 1, xmap, kb, bh);
   const int rep = H / G;
   const int b = FUSEG ? bh / G : bh / H;
   const int g = FUSEG ? bh % G : (bh % H) / rep;
@@ -524,7 +525,7 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_dq_k(const T* __restrict__ 
                                                         float inv_keep, uint64_t seed, uint64_t doff,
                                                         const uint32_t* __restrict__ kmask,
                                                         const float* __restrict__ rcos,
-                                                        const float* __restrict__ rsin) {
+                                                        const float* __restrict__ rsin, int xmap) {
   typedef typename MFb<T>::v8 v8;
   constexpr int KK = HD / 16, DT = HD / 32, CH = HD / 8, ROWB = HD * 2;
   constexpr int IMG = DQ_BK * ROWB;             // bytes of one [BK][HD] image
@@ -538,10 +539,12 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_dq_k(const T* __restrict__ 
   constexpr int MOFF = 3 * IMG;                 // per-wave keep-mask words (MASK)
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
-  // heaviest (last, for causal) query block first; one (b, h) per XCD residue
+  // heaviest (last, for causal) query block first; the query heads of one kv head on one XCD
+  // (xmap 1, common.h attn_wg_order: they share the K/V stream)
   const int nqb = (T_ + DQ_BQ - 1) / DQ_BQ;
   const int lin = blockIdx.x, nbh = H * B_;
-  const int qbi = lin / nbh, bh = lin - qbi * nbh;
+  int qbi, bh;
+  attn_wg_order(lin, nbh, H / G, xmap, qbi, bh);
   const int qb = causal ? nqb - 1 - qbi : qbi;
   const int h = bh % H, b = bh / H;
   const int g = h / (H / G);
@@ -855,12 +858,13 @@ struct BwdArgs {
   const uint32_t* kmask;
   const float *rcos, *rsin;
   hipStream_t s;
+  int xmap_q, xmap_kv;  // attn_wg_order modes of the dQ / dK-dV grids
 };
 template <typename TT, int HDD, bool DROP, int BK, int NB, int OC, bool MASK>
 static void launch_dq1(const BwdArgs& a, dim3 grid) {
   constexpr int lds = NB * dq_buf_bytes<HDD, BK, MASK>();
   hipLaunchKernelGGL((attn_bwd_dq_k<TT, HDD, DROP, BK, NB, OC, MASK>), grid, dim3(256), lds, a.s, (const TT*)a.qkv, (const TT*)a.o, (const TT*)a.dout, a.lse, a.delta, (TT*)a.dqkv, a.T_, a.H,
-                     a.G, a.B, a.causal, a.thr, a.ik, a.seed, a.offset, a.kmask, a.rcos, a.rsin);
+                     a.G, a.B, a.causal, a.thr, a.ik, a.seed, a.offset, a.kmask, a.rcos, a.rsin, a.xmap_q);
 }
 template <typename TT, int HDD, int BK, int NB, int OC>
 static void launch_dq(const BwdArgs& a, bool drop, dim3 grid) {
@@ -873,7 +877,7 @@ static void launch_kv1(const BwdArgs& a, dim3 grid) {
   constexpr int lds = NB * dkdv_buf_bytes<HDD, DU, MASK>() + (VL ? BWD_BKV * HDD * 2 : 0);
   hipLaunchKernelGGL((attn_bwd_mfma_k<TT, HDD, DROP, NB, OC, FG, DU, MASK, VL>), grid, dim3(256), lds, a.s, (const TT*)a.qkv, (const TT*)a.dout, a.lse, a.delta,
                      (TT*)a.dqkv, a.dkv_part, a.T_, a.H, a.G, a.B, a.causal, a.thr, a.ik, a.seed, a.offset, a.kmask,
-                     a.rcos, a.rsin);
+                     a.rcos, a.rsin, a.xmap_kv);
 }
 template <typename TT, int HDD, int NB, int OC, bool FG, bool DU, bool VL = false>
 static void launch_kv(const BwdArgs& a, bool drop, dim3 grid) {
@@ -911,8 +915,10 @@ void attn_bwd_mfma(DType dt, const void* qkv, const void* o, const float* lse, c
   const bool fuseg = fuse_gqa_heads(B, T_, H, G);
   dim3 grid_kv(nkb * (fuseg ? G : H) * B), grid_q(((T_ + DQ_BQ - 1) / DQ_BQ) * H * B);
   const bool drop = p > 0.f;
+  const int xq = attn_xcd_order_ok(B * H, H / G) ? 1 : 0;
+  const int xkv = attn_xcd_order_ok((fuseg ? G : H) * B, 1) ? 1 : 0;
   const BwdArgs a{qkv, o, dout, lse, delta, dkv_part, dqkv, T_, H, G, B, causal, drop_threshold16(p),
-                  drop_inv_keep(p), seed, offset, drop ? keep_mask : nullptr, rcos, rsin, s};
+                  drop_inv_keep(p), seed, offset, drop ? keep_mask : nullptr, rcos, rsin, s, xq, xkv};
   if (dt == DType::BF16) {
     if (hd == 128) launch_bwd<bf16_t, 128>(a, drop, fuseg, grid_q, grid_kv);
     else launch_bwd<bf16_t, 64>(a, drop, fuseg, grid_q, grid_kv);

@@ -243,6 +243,32 @@ __device__ __forceinline__ void glds16s(const void* sbase, uint32_t voff, uint32
 
 inline int ceil_div(long a, long b) { return (int)((a + b - 1) / b); }
 
+// Workgroup order of the attention kernels: a grid of nblk blocks (query or key blocks, heaviest
+// first) x nunit units ((batch, head) or (batch, kv head)); units come in groups of gsz that read
+// one K/V stream (the query heads of a kv head).  Workgroup lin runs on XCD lin % 8 (round-robin
+// dispatch).
+//   xmap 0: block-major over all units (unit = lin % nunit);
+//   xmap 1: XCD x owns the groups with index % 8 == x and runs them block-major, the units of a
+//           group back to back: the query heads that share a K/V stream read it through one L2
+//           (nunit / gsz must be a multiple of 8, attn_xcd_order_ok).  Round 6: Llama-3-8B B=40
+//           forward 658 -> 730 TF/s, Llama-3.2-1B 624 -> 675, backward 1.717 -> 1.660 ms (the dQ
+//           kernel; its K/V streams are shared the same way), MHA (GPT-2) unchanged
+//           (profiles/r6/attn/xcd/).  Measured and dropped: group-major order (each group's
+//           blocks back to back), worse on three of four shapes.
+__device__ __forceinline__ void attn_wg_order(int lin, int nunit, int gsz, int xmap, int& blk, int& unit) {
+  if (xmap == 0) {
+    blk = lin / nunit;
+    unit = lin - blk * nunit;
+    return;
+  }
+  const int x = lin & 7, k = lin >> 3;
+  const int per_blk = (nunit / gsz / 8) * gsz;
+  blk = k / per_blk;
+  const int rem = k - blk * per_blk, gl = rem / gsz;
+  unit = (gl * 8 + x) * gsz + (rem - gl * gsz);
+}
+inline bool attn_xcd_order_ok(int nunit, int gsz) { return gsz > 0 && nunit % gsz == 0 && (nunit / gsz) % 8 == 0; }
+
 // ---- kernel debug mode (tools/build_ext.py --debug -> _C_debug.so, loaded when
 // BLLM_KERNEL_DEBUG=1).  BLLM_DASSERT records the first failed check of a translation unit in a
 // device word with a vector atomic and lets the kernel run on (no trap: a fault would take the

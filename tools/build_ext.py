@@ -66,10 +66,10 @@ def _run(cmd, obj, flags):
     return obj, r.stderr
 
 
-# per-file compiler flags: the attention kernels' softmax must stay scalar f32 -- the SLP
-# vectorizer's v_pk_add / v_pk_mul beside MFMAs cost issue cycles (MI355X_MICROARCH.md, packed f32
-# VALU "an anti-lever beside MFMAs")
-FILE_FLAGS = {"attn_mfma.hip": ["-fno-slp-vectorize"]}
+# per-file compiler flags (none shipped: -fno-slp-vectorize on csrc/attn_mfma.hip, which keeps the
+# softmax's f32 adds scalar instead of v_pk_add beside the MFMAs, measured within noise of the
+# default on the shipped forward, profiles/r6/attn/pp/ab_pp_v3_*.jsonl)
+FILE_FLAGS = {}
 
 
 def build(jobs: int = 8, clean: bool = False, debug: bool = False, verbose: bool = False) -> str:
