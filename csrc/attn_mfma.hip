@@ -388,8 +388,8 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd_mfma_k(const T* __restrict_
             for (int r = 0; r < 16; r += 2) {
               const uint32_t hv = hash_at((uint32_t)(((r & 3) + 8 * (r >> 2)) >> 1));
               const bool k0b = (hv & 0xFFFFu) >= thr, k1b = (hv >> 16) >= thr;
-              s[u][kt][r] = k0b ? s[u][kt][r] * inv_keep : 0.f;
-              s[u][kt][r + 1] = k1b ? s[u][kt][r + 1] * inv_keep : 0.f;
+              s[u][kt][r] = k0b ? s[u][kt][r] : 0.f;
+              s[u][kt][r + 1] = k1b ? s[u][kt][r + 1] : 0.f;
               kbits |= ((uint32_t)k0b << ((r & 3) + 8 * (r >> 2))) |
                        ((uint32_t)k1b << (((r + 1) & 3) + 8 * (r >> 2)));
             }
@@ -406,7 +406,7 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd_mfma_k(const T* __restrict_
               const uint32_t h = par ? hv[r >> 2][(cr + 1) >> 1] : hv[r >> 2][cr >> 1];
               const bool hi = par ? ((cr + 1) & 1) : (cr & 1);
               const bool kb_ = (hi ? (h >> 16) : (h & 0xFFFFu)) >= thr;
-              s[u][kt][r] = kb_ ? s[u][kt][r] * inv_keep : 0.f;
+              s[u][kt][r] = kb_ ? s[u][kt][r] : 0.f;
               kbits |= (uint32_t)kb_ << ((r & 3) + 8 * (r >> 2));
             }
           }
@@ -494,7 +494,8 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd_mfma_k(const T* __restrict_
 #pragma unroll
   for (int u = 0; u < QB; ++u) {
     const float lt = l[u] + __shfl_xor(l[u], 32, 64);
-    const float inv = lt > 0.f ? 1.f / lt : 0.f;
+    // dropout's 1 / keep applied once here instead of to every kept probability
+    const float inv = lt > 0.f ? (DROP ? inv_keep : 1.f) / lt : 0.f;
     T* orow = out + ((long)b * T_ + min(qi[u], T_ - 1)) * (long)H * HD + (long)h * HD;
     // 16-B stores: lane (q, half hh) holds d = 8 gq + 4 hh + 0..3 of each 32-column tile; one
     // v_permlane32_swap per dword of a (gq, gq+1) pair leaves 8 contiguous d of group gq in the
