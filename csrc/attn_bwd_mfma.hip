@@ -138,6 +138,17 @@ template <int HD, bool DUAL = false, bool MASK = false> constexpr int dkdv_buf_b
 //   g1' = g1 c + g2 s,  g2' = g2 c - g1 s   (c, s = cos/sin [T, HD/2] fp32 at position pos).
 // Replaces a separate rope pass over dQ / dK (read + write of [N, (H + G) hd]).  ``row`` is the
 // head's first element.
+// One row-per-lane-pair 16-B store (cdna_hip_programming.md T21): this lane holds the packed
+// columns of groups gq (a) and gq+1 (b), 4 each, 4 hh + 0..3 within the group; one
+// v_permlane32_swap per dword leaves group gq's 8 columns in the lower lane half and gq+1's in the
+// upper, stored at dst = row + 8 gq + 8 hh.  Lanes l and l+32 must hold the same row.
+template <typename T>
+__device__ __forceinline__ void store16_pair(T* dst, const uint32_t (&a)[2], const uint32_t (&b)[2]) {
+  const auto rx = __builtin_amdgcn_permlane32_swap(a[0], b[0], false, false);
+  const auto ry = __builtin_amdgcn_permlane32_swap(a[1], b[1], false, false);
+  *reinterpret_cast<uint4*>(dst) = uint4{rx[0], ry[0], rx[1], ry[1]};
+}
+
 template <typename T, int HD>
 __device__ __forceinline__ void rope_bwd_store(const f32x16& lo, const f32x16& hi, float scale, int hh, int pos,
                                                int dc, const float* __restrict__ rcos,
@@ -145,6 +156,7 @@ __device__ __forceinline__ void rope_bwd_store(const f32x16& lo, const f32x16& h
   constexpr int HALF = HD / 2;
   const float* cp = rcos + (long)pos * HALF + dc + 4 * hh;
   const float* sp = rsin + (long)pos * HALF + dc + 4 * hh;
+  uint32_t w1[4][2], w2[4][2];  // packed (d, d+1), (d+2, d+3) of group gq, both halves
 #pragma unroll
   for (int gq = 0; gq < 4; ++gq) {
     const float4 c = *reinterpret_cast<const float4*>(cp + 8 * gq);
@@ -157,14 +169,16 @@ __device__ __forceinline__ void rope_bwd_store(const f32x16& lo, const f32x16& h
       o1[j] = g1 * cc[j] + g2 * ss[j];
       o2[j] = g2 * cc[j] - g1 * ss[j];
     }
-    const int d0 = dc + 8 * gq + 4 * hh;
-    uint2 v1, v2;
-    v1.x = pk2<T>(o1[0], o1[1]);
-    v1.y = pk2<T>(o1[2], o1[3]);
-    v2.x = pk2<T>(o2[0], o2[1]);
-    v2.y = pk2<T>(o2[2], o2[3]);
-    *reinterpret_cast<uint2*>(row + d0) = v1;
-    *reinterpret_cast<uint2*>(row + d0 + HALF) = v2;
+    w1[gq][0] = pk2<T>(o1[0], o1[1]);
+    w1[gq][1] = pk2<T>(o1[2], o1[3]);
+    w2[gq][0] = pk2<T>(o2[0], o2[1]);
+    w2[gq][1] = pk2<T>(o2[2], o2[3]);
+  }
+  // 16-B stores (T21, as attn_fwd_mfma_k's epilogue): lanes l and l+32 hold the same row
+#pragma unroll
+  for (int gq = 0; gq < 4; gq += 2) {
+    store16_pair<T>(row + dc + 8 * gq + 8 * hh, w1[gq], w1[gq + 1]);
+    store16_pair<T>(row + HALF + dc + 8 * gq + 8 * hh, w2[gq], w2[gq + 1]);
   }
 }
 
@@ -470,23 +484,21 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_mfma_k(const T* __restrict_
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt)
 #pragma unroll
-        for (int gq = 0; gq < 4; ++gq) {
-          const int d0 = dt * 32 + 8 * gq + 4 * hh;
-          uint2 a;
-          a.x = pk2<T>(dk[dt][4 * gq] * scale, dk[dt][4 * gq + 1] * scale);
-          a.y = pk2<T>(dk[dt][4 * gq + 2] * scale, dk[dt][4 * gq + 3] * scale);
-          *reinterpret_cast<uint2*>(pk + d0) = a;
+        for (int gq = 0; gq < 4; gq += 2) {
+          const uint32_t a[2] = {pk2<T>(dk[dt][4 * gq] * scale, dk[dt][4 * gq + 1] * scale),
+                                 pk2<T>(dk[dt][4 * gq + 2] * scale, dk[dt][4 * gq + 3] * scale)};
+          const uint32_t c[2] = {pk2<T>(dk[dt][4 * gq + 4] * scale, dk[dt][4 * gq + 5] * scale),
+                                 pk2<T>(dk[dt][4 * gq + 6] * scale, dk[dt][4 * gq + 7] * scale)};
+          store16_pair<T>(pk + dt * 32 + 8 * gq + 8 * hh, a, c);
         }
     }
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt)
 #pragma unroll
-      for (int gq = 0; gq < 4; ++gq) {
-        const int d0 = dt * 32 + 8 * gq + 4 * hh;
-        uint2 bb;
-        bb.x = pk2<T>(dv[dt][4 * gq], dv[dt][4 * gq + 1]);
-        bb.y = pk2<T>(dv[dt][4 * gq + 2], dv[dt][4 * gq + 3]);
-        *reinterpret_cast<uint2*>(pv + d0) = bb;
+      for (int gq = 0; gq < 4; gq += 2) {
+        const uint32_t a[2] = {pk2<T>(dv[dt][4 * gq], dv[dt][4 * gq + 1]), pk2<T>(dv[dt][4 * gq + 2], dv[dt][4 * gq + 3])};
+        const uint32_t c[2] = {pk2<T>(dv[dt][4 * gq + 4], dv[dt][4 * gq + 5]), pk2<T>(dv[dt][4 * gq + 6], dv[dt][4 * gq + 7])};
+        store16_pair<T>(pv + dt * 32 + 8 * gq + 8 * hh, a, c);
       }
   } else if (mykey < T_) {
     const long BT = (long)B_ * T_;
@@ -772,15 +784,16 @@ __global__ __launch_bounds__(256, OCC) void attn_bwd_dq_k(const T* __restrict__ 
       for (int dt = 0; dt < DT / 2; ++dt) rope_bwd_store<T, HD>(dq[dt], dq[dt + DT / 2], scale, hh, qi, dt * 32, rcos, rsin, row);
       return;
     }
+    // 16-B stores (store16_pair)
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt)
 #pragma unroll
-      for (int gq = 0; gq < 4; ++gq) {
-        const int d0 = dt * 32 + 8 * gq + 4 * hh;
-        uint2 v;
-        v.x = pk2<T>(dq[dt][4 * gq] * scale, dq[dt][4 * gq + 1] * scale);
-        v.y = pk2<T>(dq[dt][4 * gq + 2] * scale, dq[dt][4 * gq + 3] * scale);
-        *reinterpret_cast<uint2*>(row + d0) = v;
+      for (int gq = 0; gq < 4; gq += 2) {
+        const uint32_t a[2] = {pk2<T>(dq[dt][4 * gq] * scale, dq[dt][4 * gq + 1] * scale),
+                               pk2<T>(dq[dt][4 * gq + 2] * scale, dq[dt][4 * gq + 3] * scale)};
+        const uint32_t c[2] = {pk2<T>(dq[dt][4 * gq + 4] * scale, dq[dt][4 * gq + 5] * scale),
+                               pk2<T>(dq[dt][4 * gq + 6] * scale, dq[dt][4 * gq + 7] * scale)};
+        store16_pair<T>(row + dt * 32 + 8 * gq + 8 * hh, a, c);
       }
   }
 }

@@ -254,7 +254,8 @@ inline int ceil_div(long a, long b) { return (int)((a + b - 1) / b); }
 //           forward 658 -> 730 TF/s, Llama-3.2-1B 624 -> 675, backward 1.717 -> 1.660 ms (the dQ
 //           kernel; its K/V streams are shared the same way), MHA (GPT-2) unchanged
 //           (profiles/r6/attn/xcd/).  Measured and dropped: group-major order (each group's
-//           blocks back to back), worse on three of four shapes.
+//           blocks back to back), worse on three of four forward shapes and, for the dK/dV grid
+//           alone, on all five backward shapes (+5-17 %, profiles/r6/attn/xcd/kv_order.jsonl).
 __device__ __forceinline__ void attn_wg_order(int lin, int nunit, int gsz, int xmap, int& blk, int& unit) {
   if (xmap == 0) {
     blk = lin / nunit;
