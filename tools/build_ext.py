@@ -66,10 +66,6 @@ def _run(cmd, obj, flags):
     return obj, r.stderr
 
 
-# per-file compiler flags (none shipped: -fno-slp-vectorize on csrc/attn_mfma.hip, which keeps the
-# softmax's f32 adds scalar instead of v_pk_add beside the MFMAs, measured within noise of the
-# default on the shipped forward, profiles/r6/attn/pp/ab_pp_v3_*.jsonl)
-FILE_FLAGS = {}
 
 
 def build(jobs: int = 8, clean: bool = False, debug: bool = False, verbose: bool = False) -> str:
@@ -90,7 +86,7 @@ def build(jobs: int = 8, clean: bool = False, debug: bool = False, verbose: bool
         src = os.path.join(CSRC, f)
         if f.endswith(".hip"):
             obj = os.path.join(bdir, f + ".o")
-            cmd = [hipcc] + common + FILE_FLAGS.get(f, []) + ["-c", src, "-o", obj]
+            cmd = [hipcc] + common + ["-c", src, "-o", obj]
         elif f.endswith(".cpp"):
             obj = os.path.join(bdir, f + ".o")
             py_inc = sysconfig.get_paths()["include"]
