@@ -66,8 +66,6 @@ def _run(cmd, obj, flags):
     return obj, r.stderr
 
 
-
-
 def build(jobs: int = 8, clean: bool = False, debug: bool = False, verbose: bool = False) -> str:
     hipcc = _hipcc()
     tdir, tinc, tlib, abi = _torch_paths()
