@@ -115,7 +115,7 @@ __global__ __launch_bounds__(256) void norm_fwd_k(const T* __restrict__ x, const
 // cross the 4 waves through a parity-double-buffered LDS slot (one barrier per row).  Each
 // workgroup writes one fp32 partial row for dW (and dB); col_reduce_k sums them in a fixed
 // order (deterministic, no global atomics).
-template <typename T, int NV, bool LN>
+template <typename T, int NV, bool LN, bool PF>
 __global__ __launch_bounds__(256) void norm_bwd_k(const T* __restrict__ dy, const T* __restrict__ x,
                                                   const T* __restrict__ w, const float* __restrict__ mean,
                                                   const float* __restrict__ rstd, const T* __restrict__ dx_acc,
@@ -134,23 +134,49 @@ __global__ __launch_bounds__(256) void norm_bwd_k(const T* __restrict__ dy, cons
       aw[i][j] = 0.f;
       if (LN) ab[LN ? i : 0][j] = 0.f;
     }
-  int par = 0;
-  for (int row = blockIdx.x; row < N; row += gridDim.x, par ^= 1) {
-    const T* xr = x + (size_t)row * d;
-    const T* dyr = dy + (size_t)row * d;
-    const float rs = rstd[row];
-    const float mu = LN ? mean[row] : 0.f;
-    Vec16<T> xv[NV], dv[NV], wv[NV];
-    float sg = 0.f, sgx = 0.f;
+  // PF (rows shorter than 4 waves): the next row's x / dy / dx_acc are loaded before this row is
+  // reduced (register double buffer) -- with one row in flight per workgroup a GPT-2 row
+  // (d = 1280, 3 waves) kept too few loads outstanding: 170 -> 149 us per call (3.9 -> 4.5 TB/s).
+  // At d = 4096 the same prefetch measured 256 -> 284 us, so 4-wave rows keep the single-row
+  // form (profiles/r6/normpf/).  w is loaded once per workgroup.
+  Vec16<T> wv[NV], xv[NV], dv[NV], av[NV], nx[NV], nd[NV], na[NV];
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = tid + (int)blockDim.x * i;
+    if (c < nvec) wv[i] = ld16(w + c * VEC);
+  }
+  auto load_row = [&](int r, Vec16<T> (&lx)[NV], Vec16<T> (&ld)[NV], Vec16<T> (&la)[NV]) {
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
       const int c = tid + (int)blockDim.x * i;
       if (c < nvec) {
-        xv[i] = ld16(xr + c * VEC);
-        dv[i] = ld16(dyr + c * VEC);
-        wv[i] = ld16(w + c * VEC);
+        lx[i] = ld16(x + (size_t)r * d + c * VEC);
+        ld[i] = ld16(dy + (size_t)r * d + c * VEC);
+        if (dx_acc) la[i] = ld16(dx_acc + (size_t)r * d + c * VEC);
       }
     }
+  };
+  int par = 0;
+  if constexpr (PF) {
+    if ((int)blockIdx.x < N) load_row(blockIdx.x, xv, dv, av);
+  }
+  for (int row = blockIdx.x; row < N; row += gridDim.x, par ^= 1) {
+    if constexpr (PF) {
+      const int rn = row + (int)gridDim.x;
+      if (rn < N) load_row(rn, nx, nd, na);
+    } else {
+#pragma unroll
+      for (int i = 0; i < NV; ++i) {
+        const int c = tid + (int)blockDim.x * i;
+        if (c < nvec) {
+          xv[i] = ld16(x + (size_t)row * d + c * VEC);
+          dv[i] = ld16(dy + (size_t)row * d + c * VEC);
+        }
+      }
+    }
+    const float rs = rstd[row];
+    const float mu = LN ? mean[row] : 0.f;
+    float sg = 0.f, sgx = 0.f;
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
       const int c = tid + (int)blockDim.x * i;
@@ -183,22 +209,29 @@ __global__ __launch_bounds__(256) void norm_bwd_k(const T* __restrict__ dy, cons
     sgx /= d;
     sg /= d;
     T* dxr = dx + (size_t)row * d;
-    const T* ar = dx_acc ? dx_acc + (size_t)row * d : nullptr;
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
       const int c = tid + (int)blockDim.x * i;
       if (c < nvec) {
-        Vec16<T> o, av;
-        if (ar) av = ld16(ar + c * VEC);
+        Vec16<T> o;
+        if (!PF && dx_acc) av[i] = ld16(dx_acc + (size_t)row * d + c * VEC);
 #pragma unroll
         for (int j = 0; j < VEC; ++j) {
           const float xh = (to_f(xv[i].v[j]) - mu) * rs;
           const float gg = to_f(dv[i].v[j]) * to_f(wv[i].v[j]);
           float r = rs * (gg - (LN ? sg : 0.f) - xh * sgx);
-          if (ar) r += to_f(av.v[j]);
+          if (dx_acc) r += to_f(av[i].v[j]);
           o.v[j] = from_f<T>(r);
         }
         st16(dxr + c * VEC, o);
+      }
+    }
+    if constexpr (PF) {
+#pragma unroll
+      for (int i = 0; i < NV; ++i) {
+        xv[i] = nx[i];
+        dv[i] = nd[i];
+        if (dx_acc) av[i] = na[i];
       }
     }
   }
@@ -279,9 +312,9 @@ static void bwd_dispatch(const void* dy, const void* x, const void* w, const flo
   const int bt = nvec >= 256 ? 256 : ceil_div(nvec, 64) * 64;
   const int nv = ceil_div(nvec, bt);
   dim3 grid(nwg), block(bt);
-#define L(NVV) hipLaunchKernelGGL((norm_bwd_k<T, NVV, LN>), grid, block, 0, s, (const T*)dy, (const T*)x, \
-                                  (const T*)w, mean, rstd, (const T*)dx_acc, (T*)dx, part_w, part_b, N, d)
-  if (nv <= 1) L(1); else if (nv <= 2) L(2); else L(4);
+#define L(NVV, PF) hipLaunchKernelGGL((norm_bwd_k<T, NVV, LN, PF>), grid, block, 0, s, (const T*)dy, (const T*)x, \
+                                      (const T*)w, mean, rstd, (const T*)dx_acc, (T*)dx, part_w, part_b, N, d)
+  if (bt < 256) L(1, true); else if (nv <= 1) L(1, false); else if (nv <= 2) L(2, false); else L(4, false);
 #undef L
   col_reduce(part_w, odt, dw, nwg, d, accumulate, s);
   if (LN) col_reduce(part_b, odt, db, nwg, d, accumulate, s);
