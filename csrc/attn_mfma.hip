@@ -522,11 +522,16 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd_mfma_k(const T* __restrict_
 
 bool attn_mfma_head_dim(int hd) { return hd == 64 || hd == 128; }
 
-// forward tiling: 64-key tiles, 2-slot ring, 2 workgroups per CU; for hd 64 with dropout on grids
-// of >= 2048 workgroups 32-key tiles with up to 3 workgroups per CU (GPT2-774M B=24 0.179 ->
-// 0.163 ms: the hash work wants the third co-resident workgroup).  Dropped: 32-key tiles with a
-// 3-slot ring, two 32-query blocks per wave (slower on every shape, profiles/r3/attn_fwd_qb2.md).
-static bool fwd_small_tiles(int hd, float p, long nwg) { return hd == 64 && p > 0.f && nwg >= 2048; }
+// forward tiling: 64-key tiles, 2-slot ring, 2 workgroups per CU; for hd 64 on grids of >= 2048
+// workgroups 32-key tiles with up to 3 workgroups per CU (GPT2-774M B=24 with dropout 0.179 ->
+// 0.163 ms: the hash work wants the third co-resident workgroup; round 6, after the XCD order:
+// Llama-3.2-1B B=24 without dropout 658 -> 686 TF/s, GPT-2 without dropout unchanged,
+// profiles/r6/attn/smalltiles/).  Dropped: 32-key tiles with a 3-slot ring, two 32-query blocks
+// per wave (slower on every shape, profiles/r3/attn_fwd_qb2.md).
+static bool fwd_small_tiles(int hd, float p, long nwg) {
+  (void)p;
+  return hd == 64 && nwg >= 2048;
+}
 
 void attn_fwd_mfma(DType dt, const void* qkv, void* o, float* lse, int B, int T_, int H, int G, int hd, bool causal,
                    float p, uint64_t seed, uint64_t offset, uint32_t* keep_mask, hipStream_t s) {
